@@ -1,0 +1,170 @@
+/*
+ * aicp_hip.h — C-ABI of the MI355X-native ICP registration core (libaicp_hip.so).
+ *
+ * This is the drop-in boundary that replaces the in-process C++ virtual interfaces
+ * of aicp_core (reference paths relative to zbqq/aicp_mapping):
+ *
+ *   aicp::AbstractRegistrator   aicp_core/include/aicp_registration/abstract_registrator.hpp:8-19
+ *     registerClouds(ref, read, Matrix4f&)   -> aicp_hip_register / aicp_hip_register_batch
+ *     getOutputReading(cloud)                -> aicp_hip_transform
+ *     updateConfigParams(path)               -> aicp_hip_parse_pm_yaml
+ *   aicp::AbstractOverlapper    aicp_core/include/aicp_overlap/abstract_overlapper.hpp:13-19
+ *     computeOverlap(...) + getOverlap()     -> aicp_hip_overlap / aicp_hip_overlap_batch
+ *   App::computeRegistration ratio auto-tune aicp_core/src/registration/app.cpp:197-205
+ *     + replaceRatioConfigFile               aicp_core/src/utils/fileIO.cpp:179-214
+ *                                            -> aicp_hip_autotune_ratio,
+ *                                               aicp_hip_replace_ratio_config_file,
+ *                                               aicp_hip_align_batch (overlap -> ratio -> ICP on device)
+ *
+ * Conventions
+ *   - Plain C, no exceptions cross this boundary; every entry point returns an AICP_* code.
+ *   - Host memory is caller-owned. Point arrays are AoS float x,y,z at a byte stride, so a
+ *     pcl::PointXYZ array (16 B per point) passes zero-copy with stride = 16.
+ *   - Counts are explicit (the reference uses cloud.width, cloudIO.cpp:83).
+ *   - Transforms are column-major float[16], so Eigen::Matrix4f::data() passes through.
+ *   - A context owns one HIP stream and a device arena; use one context per host thread
+ *     (the reference calls its registrator from a single worker thread, app.cpp:528-550).
+ */
+#ifndef AICP_HIP_H_
+#define AICP_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes --------------------------------------------------------------------- */
+#define AICP_OK 0
+#define AICP_ERR_CONVERGENCE 1  /* maps PM::ConvergenceError ("no outlier to filter",
+                                   "no point to minimize", NaN in the differential checker) */
+#define AICP_ERR_INVALID 2      /* invalid argument / config (reference: exit(1),
+                                   pointmatcher_registration.cpp:60-64,96-100) */
+#define AICP_ERR_HIP 3          /* HIP runtime failure or extension unavailable */
+#define AICP_ERR_UNSUPPORTED 4  /* chain element or size not supported by this core */
+
+typedef struct aicp_hip_ctx aicp_hip_ctx;
+typedef struct aicp_hip_batch aicp_hip_batch;
+
+/* The libpointmatcher chain subset of icp_autotuned_default.yaml:9-51. */
+typedef struct {
+  int32_t knn_normals;    /* SurfaceNormalDataPointsFilter.knn            (20)   */
+  float nn_epsilon;       /* KDTreeMatcher.epsilon                        (3.16) */
+  float nn_max_dist;      /* KDTreeMatcher.maxDist                        (inf)  */
+  float trimmed_ratio;    /* TrimmedDistOutlierFilter.ratio               (0.70) */
+  int32_t max_iter;       /* CounterTransformationChecker.maxIterationCount (20) */
+  float min_diff_rot;     /* DifferentialTransformationChecker.minDiffRotErr (1e-3) */
+  float min_diff_trans;   /* DifferentialTransformationChecker.minDiffTransErr (1e-2) */
+  int32_t smooth_length;  /* DifferentialTransformationChecker.smoothLength (4) */
+  int32_t bucket_size;    /* libnabo kd-tree bucketSize                    (8)   */
+  int32_t knn_match;      /* KDTreeMatcher.knn; only 1 is supported        (1)   */
+} aicp_icp_config;
+
+typedef struct {
+  int32_t status;            /* AICP_* code of this pair                          */
+  int32_t iterations;        /* ICP iterations executed (IterationsCount)         */
+  int32_t converged;         /* 1: differential checker stopped, 0: counter limit */
+  int32_t degenerate_normals;/* SurfaceNormal rank-deficient points (reference)   */
+  float inlier_ratio;        /* weightedPointUsedRatio of the last iteration      */
+  float trimmed_ratio;       /* ratio actually used                               */
+  float overlap_percent;     /* octree-equivalent overlap, -1 if not computed     */
+  int32_t tree_depth;        /* depth of the matcher kd-tree                      */
+  uint64_t nn_points_touched;/* libnabo PointCountTouched over all iterations     */
+  uint64_t nn_nodes_touched; /* inner nodes descended over all iterations         */
+  uint64_t overlap_keys[3];  /* |S_ref|, |S_read|, |S_ref ∩ S_read|                */
+} aicp_icp_stats;
+
+typedef struct {
+  const float* ref;      /* reference cloud, x,y,z at ref_stride bytes            */
+  uint64_t n_ref;
+  uint64_t ref_stride;   /* bytes between points; 12 (packed) or 16 (PointXYZ)   */
+  const float* read;     /* reading cloud                                         */
+  uint64_t n_read;
+  uint64_t read_stride;
+  const float* init_T;   /* nullable = identity; column-major 4x4                 */
+  double ref_origin[3];  /* sensor origin of the reference (pose translation)     */
+  double read_origin[3]; /* sensor origin of the reading                          */
+} aicp_pair;
+
+/* flags for aicp_hip_align_batch / aicp_hip_batch_run */
+#define AICP_RUN_OVERLAP 1      /* compute overlap and auto-tune the trimmed ratio */
+#define AICP_RUN_ICP 2          /* run the ICP registration                        */
+#define AICP_RUN_TIME_NN 4      /* record HIP events around every NN launch        */
+
+/* ---- context ---------------------------------------------------------------------------- */
+int aicp_hip_create(int device, aicp_hip_ctx** out);
+void aicp_hip_destroy(aicp_hip_ctx* ctx);
+const char* aicp_hip_last_error(const aicp_hip_ctx* ctx);
+const char* aicp_hip_version(void);
+
+/* ---- configuration (host-only; the reference re-parses the chain per call) -------------- */
+void aicp_hip_default_config(aicp_icp_config* out);
+/* Parses the libpointmatcher chain subset (pointmatcher_registration.cpp:59-66).
+ * Unsupported chain elements yield AICP_ERR_UNSUPPORTED. */
+int aicp_hip_parse_pm_yaml(const char* path, aicp_icp_config* out);
+/* Text rewrite of "ratio: " + 4 chars, byte-for-byte as fileIO.cpp:179-214. */
+int aicp_hip_replace_ratio_config_file(const char* in_path, const char* out_path, float ratio);
+/* clamp(overlap/100, .25, .70) (app.cpp:197-202) then the 6-significant-digit text
+ * round trip of replaceRatioConfigFile + lexical_cast<float>. */
+float aicp_hip_autotune_ratio(float overlap_percent);
+
+/* ---- registration / overlap (host buffers) ---------------------------------------------- */
+int aicp_hip_register(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pair,
+                      float out_T[16], aicp_icp_stats* stats /* nullable */);
+int aicp_hip_register_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg,
+                            const aicp_pair* pairs, size_t n_pairs,
+                            float* out_T /* 16*n */, aicp_icp_stats* stats /* n, nullable */);
+int aicp_hip_overlap(aicp_hip_ctx* ctx, const aicp_pair* pair, double resolution,
+                     float* out_overlap_percent);
+int aicp_hip_overlap_batch(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs,
+                           double resolution, float* out_overlap_percent /* n */,
+                           aicp_icp_stats* stats /* n, nullable: overlap_keys */);
+/* App::runAicpPipeline hot path (app.cpp:218-247): overlap -> auto-tuned ratio -> ICP,
+ * all on device, one launch sequence for the whole batch. cfg->trimmed_ratio is ignored
+ * when flags has AICP_RUN_OVERLAP. */
+int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg,
+                         const aicp_pair* pairs, size_t n_pairs, double resolution, int flags,
+                         float* out_T /* 16*n */, aicp_icp_stats* stats /* n, nullable */);
+/* getOutputReading: out = T * in (float, pad row 1), pointmatcher_registration.cpp:128-131. */
+int aicp_hip_transform(aicp_hip_ctx* ctx, const float T[16], const float* in, size_t n,
+                       size_t stride, float* out /* packed xyz, 3*n */);
+
+/* ---- device-resident batches (inputs uploaded once, run many times) ----------------------- */
+int aicp_hip_batch_upload(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs,
+                          aicp_hip_batch** out);
+int aicp_hip_batch_run(aicp_hip_ctx* ctx, aicp_hip_batch* batch, const aicp_icp_config* cfg,
+                       double resolution, int flags, float* out_T /* 16*n */,
+                       aicp_icp_stats* stats /* n, nullable */);
+void aicp_hip_batch_free(aicp_hip_ctx* ctx, aicp_hip_batch* batch);
+/* Timing of the last batch_run with AICP_RUN_TIME_NN: NN launches, their total duration
+ * (HIP events on the context stream), and the algorithmic bytes they moved. */
+int aicp_hip_last_nn_timing(const aicp_hip_ctx* ctx, int* n_launches, double* total_ms,
+                            double* algorithmic_bytes, uint64_t* queries);
+/* Phase wall times (ms) of the last batch_run: [0] overlap, [1] centre+tree,
+ * [2] normals, [3] icp loop, [4] total. */
+int aicp_hip_last_phase_ms(const aicp_hip_ctx* ctx, double out_ms[5]);
+
+/* ---- kernel-level entry points (parity tests and diagnostics) --------------------------- */
+/* kd-tree over pts (as given, no centring) + k-NN of queries: libnabo
+ * KDTreeUnbalancedPtInLeavesImplicitBoundsStackOpt order, ALLOW_SELF_MATCH.
+ * ids are input indices of pts; unmatched = -1 with dist +inf. */
+int aicp_hip_knn(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride,
+                 const float* queries, size_t nq, size_t qstride, int k, float epsilon,
+                 float max_dist, int32_t* out_ids /* k*nq */, float* out_d2 /* k*nq */,
+                 uint64_t* out_touched /* nullable */);
+/* SurfaceNormal descriptor (knn, keepNormals) of pts in input order. */
+int aicp_hip_normals(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, int knn,
+                     float* out_normals /* 3*n */, int32_t* out_degenerate /* nullable */);
+/* Matches::getDistsQuantile on the device (radix select). */
+int aicp_hip_dists_quantile(aicp_hip_ctx* ctx, const float* d2, size_t n, float quantile,
+                            float* out_limit);
+/* solvePossiblyUnderdeterminedLinearSystem on the device (A row-major 6x6, double). */
+int aicp_hip_solve6(aicp_hip_ctx* ctx, const double* A, const double* b, double* out_x,
+                    int32_t* out_path /* 0 LLT, 1 QR min-norm, 2 eigen pseudo-inverse */);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AICP_HIP_H_ */
