@@ -1,0 +1,360 @@
+"""ctypes binding of libaicp_hip.so (include/aicp_hip.h).
+
+The HIP library is the product: importing this module loads it and raises if it is missing
+or does not export the declared entry points. There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libaicp_hip.so")
+
+AICP_OK = 0
+AICP_ERR_CONVERGENCE = 1
+AICP_ERR_INVALID = 2
+AICP_ERR_HIP = 3
+AICP_ERR_UNSUPPORTED = 4
+
+AICP_RUN_OVERLAP = 1
+AICP_RUN_ICP = 2
+AICP_RUN_TIME_NN = 4
+
+EXPORTS = [
+    "aicp_hip_create", "aicp_hip_destroy", "aicp_hip_last_error", "aicp_hip_version",
+    "aicp_hip_default_config", "aicp_hip_parse_pm_yaml", "aicp_hip_replace_ratio_config_file",
+    "aicp_hip_autotune_ratio", "aicp_hip_register", "aicp_hip_register_batch",
+    "aicp_hip_overlap", "aicp_hip_overlap_batch", "aicp_hip_align_batch", "aicp_hip_transform",
+    "aicp_hip_batch_upload", "aicp_hip_batch_run", "aicp_hip_batch_free",
+    "aicp_hip_last_nn_timing", "aicp_hip_last_phase_ms", "aicp_hip_knn", "aicp_hip_normals",
+    "aicp_hip_dists_quantile", "aicp_hip_solve6",
+]
+
+
+class IcpConfig(C.Structure):
+    _fields_ = [
+        ("knn_normals", C.c_int32),
+        ("nn_epsilon", C.c_float),
+        ("nn_max_dist", C.c_float),
+        ("trimmed_ratio", C.c_float),
+        ("max_iter", C.c_int32),
+        ("min_diff_rot", C.c_float),
+        ("min_diff_trans", C.c_float),
+        ("smooth_length", C.c_int32),
+        ("bucket_size", C.c_int32),
+        ("knn_match", C.c_int32),
+    ]
+
+
+class IcpStats(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("iterations", C.c_int32),
+        ("converged", C.c_int32),
+        ("degenerate_normals", C.c_int32),
+        ("inlier_ratio", C.c_float),
+        ("trimmed_ratio", C.c_float),
+        ("overlap_percent", C.c_float),
+        ("tree_depth", C.c_int32),
+        ("nn_points_touched", C.c_uint64),
+        ("nn_nodes_touched", C.c_uint64),
+        ("overlap_keys", C.c_uint64 * 3),
+    ]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "overlap_keys"}
+        d["overlap_keys"] = [int(x) for x in self.overlap_keys]
+        return d
+
+
+class Pair(C.Structure):
+    _fields_ = [
+        ("ref", C.POINTER(C.c_float)),
+        ("n_ref", C.c_uint64),
+        ("ref_stride", C.c_uint64),
+        ("read", C.POINTER(C.c_float)),
+        ("n_read", C.c_uint64),
+        ("read_stride", C.c_uint64),
+        ("init_T", C.POINTER(C.c_float)),
+        ("ref_origin", C.c_double * 3),
+        ("read_origin", C.c_double * 3),
+    ]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    L = C.CDLL(LIB_PATH)
+    for name in EXPORTS:
+        if not hasattr(L, name):
+            raise ImportError(f"{LIB_PATH} does not export {name}")
+    vp = C.c_void_p
+    fp = C.POINTER(C.c_float)
+    dp = C.POINTER(C.c_double)
+    ip = C.POINTER(C.c_int32)
+    up = C.POINTER(C.c_uint64)
+    cfgp = C.POINTER(IcpConfig)
+    stp = C.POINTER(IcpStats)
+    pp = C.POINTER(Pair)
+    sz = C.c_size_t
+    L.aicp_hip_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.aicp_hip_destroy.argtypes = [vp]
+    L.aicp_hip_destroy.restype = None
+    L.aicp_hip_last_error.argtypes = [vp]
+    L.aicp_hip_last_error.restype = C.c_char_p
+    L.aicp_hip_version.restype = C.c_char_p
+    L.aicp_hip_default_config.argtypes = [cfgp]
+    L.aicp_hip_default_config.restype = None
+    L.aicp_hip_parse_pm_yaml.argtypes = [C.c_char_p, cfgp]
+    L.aicp_hip_replace_ratio_config_file.argtypes = [C.c_char_p, C.c_char_p, C.c_float]
+    L.aicp_hip_autotune_ratio.argtypes = [C.c_float]
+    L.aicp_hip_autotune_ratio.restype = C.c_float
+    L.aicp_hip_register.argtypes = [vp, cfgp, pp, fp, stp]
+    L.aicp_hip_register_batch.argtypes = [vp, cfgp, pp, sz, fp, stp]
+    L.aicp_hip_overlap.argtypes = [vp, pp, C.c_double, fp]
+    L.aicp_hip_overlap_batch.argtypes = [vp, pp, sz, C.c_double, fp, stp]
+    L.aicp_hip_align_batch.argtypes = [vp, cfgp, pp, sz, C.c_double, C.c_int, fp, stp]
+    L.aicp_hip_transform.argtypes = [vp, fp, fp, sz, sz, fp]
+    L.aicp_hip_batch_upload.argtypes = [vp, pp, sz, C.POINTER(vp)]
+    L.aicp_hip_batch_run.argtypes = [vp, vp, cfgp, C.c_double, C.c_int, fp, stp]
+    L.aicp_hip_batch_free.argtypes = [vp, vp]
+    L.aicp_hip_batch_free.restype = None
+    L.aicp_hip_last_nn_timing.argtypes = [vp, C.POINTER(C.c_int), dp, dp, up]
+    L.aicp_hip_last_phase_ms.argtypes = [vp, dp]
+    L.aicp_hip_knn.argtypes = [vp, fp, sz, sz, fp, sz, sz, C.c_int, C.c_float, C.c_float, ip, fp, up]
+    L.aicp_hip_normals.argtypes = [vp, fp, sz, sz, C.c_int, fp, ip]
+    L.aicp_hip_dists_quantile.argtypes = [vp, fp, sz, C.c_float, fp]
+    L.aicp_hip_solve6.argtypes = [vp, dp, dp, dp, ip]
+    return L
+
+
+lib = _load()
+
+
+class AicpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"aicp_hip error {code}: {msg}")
+        self.code = code
+
+
+class ConvergenceError(AicpError):
+    """Maps PM::ConvergenceError (uncaught in the reference, app.cpp:210)."""
+
+
+def default_config(**kw) -> IcpConfig:
+    c = IcpConfig()
+    lib.aicp_hip_default_config(C.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def parse_pm_yaml(path: str):
+    c = IcpConfig()
+    rc = lib.aicp_hip_parse_pm_yaml(path.encode(), C.byref(c))
+    return rc, c
+
+
+def autotune_ratio(overlap_percent: float) -> float:
+    return float(lib.aicp_hip_autotune_ratio(overlap_percent))
+
+
+def replace_ratio_config_file(in_path: str, out_path: str, ratio: float) -> int:
+    return lib.aicp_hip_replace_ratio_config_file(in_path.encode(), out_path.encode(), ratio)
+
+
+def _fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def as_points(p) -> np.ndarray:
+    """float32 array of shape (N, 3) or (N, 4) (pcl::PointXYZ layout), C-contiguous."""
+    a = np.ascontiguousarray(p, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] not in (3, 4):
+        raise ValueError("points must be (N, 3) or (N, 4)")
+    return a
+
+
+def make_pair(ref, read, ref_origin=(0, 0, 0), read_origin=(0, 0, 0), init_T=None):
+    """Returns (Pair, keepalive). init_T: 4x4 row-major numpy -> column-major float[16]."""
+    ref = as_points(ref)
+    read = as_points(read)
+    keep = [ref, read]
+    p = Pair()
+    p.ref = _fptr(ref)
+    p.n_ref = ref.shape[0]
+    p.ref_stride = ref.shape[1] * 4
+    p.read = _fptr(read)
+    p.n_read = read.shape[0]
+    p.read_stride = read.shape[1] * 4
+    if init_T is not None:
+        t = np.ascontiguousarray(np.asarray(init_T, np.float32).reshape(4, 4).T.reshape(16))
+        keep.append(t)
+        p.init_T = _fptr(t)
+    for k in range(3):
+        p.ref_origin[k] = float(ref_origin[k])
+        p.read_origin[k] = float(read_origin[k])
+    return p, keep
+
+
+class Context:
+    """One aicp_hip_ctx: a HIP stream + device arena on one GPU."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        rc = lib.aicp_hip_create(int(device), C.byref(h))
+        if rc != AICP_OK:
+            raise AicpError(rc, f"aicp_hip_create(device={device}) failed (no HIP device?)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.aicp_hip_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def last_error(self) -> str:
+        return lib.aicp_hip_last_error(self.h).decode()
+
+    def check(self, rc):
+        if rc == AICP_ERR_CONVERGENCE:
+            raise ConvergenceError(rc, self.last_error())
+        if rc != AICP_OK:
+            raise AicpError(rc, self.last_error())
+
+    # -------------------------------------------------------------- batch pipeline ----------
+    def align_batch(self, pairs, cfg=None, resolution=0.2, flags=AICP_RUN_ICP, raise_on_error=True):
+        """pairs: list of dict(ref, read, ref_origin, read_origin, init_T). Returns (T[n,4,4]
+        row-major float32, list of stats dicts, rc)."""
+        cfg = cfg or default_config()
+        arr = (Pair * len(pairs))()
+        keep = []
+        for i, pr in enumerate(pairs):
+            p, k = make_pair(pr["ref"], pr["read"], pr.get("ref_origin", (0, 0, 0)),
+                             pr.get("read_origin", (0, 0, 0)), pr.get("init_T"))
+            arr[i] = p
+            keep.append(k)
+        outT = np.zeros((len(pairs), 16), np.float32)
+        st = (IcpStats * len(pairs))()
+        rc = lib.aicp_hip_align_batch(self.h, C.byref(cfg), arr, len(pairs), float(resolution),
+                                      int(flags), _fptr(outT), st)
+        if raise_on_error and rc != AICP_OK:
+            self.check(rc)
+        T = outT.reshape(-1, 4, 4).transpose(0, 2, 1).copy()
+        return T, [s.as_dict() for s in st], rc
+
+    def upload(self, pairs):
+        return ResidentBatch(self, pairs)
+
+    def last_nn_timing(self):
+        n = C.c_int()
+        ms = C.c_double()
+        by = C.c_double()
+        q = C.c_uint64()
+        lib.aicp_hip_last_nn_timing(self.h, C.byref(n), C.byref(ms), C.byref(by), C.byref(q))
+        return dict(launches=n.value, total_ms=ms.value, bytes=by.value, queries=q.value)
+
+    def last_phase_ms(self):
+        a = (C.c_double * 5)()
+        lib.aicp_hip_last_phase_ms(self.h, a)
+        return dict(overlap=a[0], tree_host=a[1], normals=a[2], icp_loop=a[3], total=a[4])
+
+    # -------------------------------------------------------------- kernel-level -----------
+    def knn(self, pts, queries, k=1, eps=0.0, max_dist=float("inf")):
+        pts = as_points(pts)
+        q = as_points(queries)
+        ids = np.zeros((q.shape[0], k), np.int32)
+        d2 = np.zeros((q.shape[0], k), np.float32)
+        touched = np.zeros(2, np.uint64)
+        rc = lib.aicp_hip_knn(self.h, _fptr(pts), pts.shape[0], pts.shape[1] * 4, _fptr(q), q.shape[0],
+                              q.shape[1] * 4, int(k), float(eps), float(max_dist),
+                              ids.ctypes.data_as(C.POINTER(C.c_int32)), _fptr(d2),
+                              touched.ctypes.data_as(C.POINTER(C.c_uint64)))
+        self.check(rc)
+        return ids, d2, int(touched[0]), int(touched[1])
+
+    def normals(self, pts, knn=20):
+        pts = as_points(pts)
+        out = np.zeros((pts.shape[0], 3), np.float32)
+        deg = C.c_int32()
+        rc = lib.aicp_hip_normals(self.h, _fptr(pts), pts.shape[0], pts.shape[1] * 4, int(knn), _fptr(out),
+                                  C.byref(deg))
+        self.check(rc)
+        return out, deg.value
+
+    def dists_quantile(self, d2, quantile):
+        d2 = np.ascontiguousarray(d2, np.float32).ravel()
+        out = C.c_float()
+        rc = lib.aicp_hip_dists_quantile(self.h, _fptr(d2), d2.size, float(quantile), C.byref(out))
+        self.check(rc)
+        return out.value
+
+    def solve6(self, A, b):
+        A = np.ascontiguousarray(A, np.float64).reshape(36)
+        b = np.ascontiguousarray(b, np.float64).reshape(6)
+        x = np.zeros(6, np.float64)
+        path = C.c_int32()
+        dp = C.POINTER(C.c_double)
+        rc = lib.aicp_hip_solve6(self.h, A.ctypes.data_as(dp), b.ctypes.data_as(dp), x.ctypes.data_as(dp),
+                                 C.byref(path))
+        self.check(rc)
+        return x, path.value
+
+    def transform(self, T, pts):
+        pts = as_points(pts)
+        t = np.ascontiguousarray(np.asarray(T, np.float32).reshape(4, 4).T.reshape(16))
+        out = np.zeros((pts.shape[0], 3), np.float32)
+        rc = lib.aicp_hip_transform(self.h, _fptr(t), _fptr(pts), pts.shape[0], pts.shape[1] * 4, _fptr(out))
+        self.check(rc)
+        return out
+
+
+class ResidentBatch:
+    """Pairs uploaded once to HBM (aicp_hip_batch_upload), run many times."""
+
+    def __init__(self, ctx: Context, pairs):
+        self.ctx = ctx
+        self.n = len(pairs)
+        arr = (Pair * self.n)()
+        keep = []
+        for i, pr in enumerate(pairs):
+            p, k = make_pair(pr["ref"], pr["read"], pr.get("ref_origin", (0, 0, 0)),
+                             pr.get("read_origin", (0, 0, 0)), pr.get("init_T"))
+            arr[i] = p
+            keep.append(k)
+        h = C.c_void_p()
+        rc = lib.aicp_hip_batch_upload(ctx.h, arr, self.n, C.byref(h))
+        ctx.check(rc)
+        self.h = h
+        self.outT = np.zeros((self.n, 16), np.float32)
+        self.stats = (IcpStats * self.n)()
+
+    def run(self, cfg=None, resolution=0.2, flags=AICP_RUN_ICP | AICP_RUN_OVERLAP, raise_on_error=True):
+        cfg = cfg or default_config()
+        rc = lib.aicp_hip_batch_run(self.ctx.h, self.h, C.byref(cfg), float(resolution), int(flags),
+                                    _fptr(self.outT), self.stats)
+        if raise_on_error and rc != AICP_OK:
+            self.ctx.check(rc)
+        return rc
+
+    def transforms(self):
+        return self.outT.reshape(-1, 4, 4).transpose(0, 2, 1).copy()
+
+    def stats_dicts(self):
+        return [s.as_dict() for s in self.stats]
+
+    def free(self):
+        if getattr(self, "h", None):
+            lib.aicp_hip_batch_free(self.ctx.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        self.free()

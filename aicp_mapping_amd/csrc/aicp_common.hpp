@@ -1,0 +1,80 @@
+// aicp_common.hpp — data layout shared by the host orchestrator and the HIP kernels.
+//
+// HBM layout (one batch = P pairs, every array concatenated over pairs, offsets in PairDesc):
+//   read_raw  float4[ΣN]  reading xyz as given (w unused)
+//   read_c    float4[ΣN]  reading in the reference-mean frame (T_refMean_dataIn applied once)
+//   ref_raw   float4[ΣM]  reference xyz as given (overlap input)
+//   bpts      float4[ΣM]  centred reference points in kd-tree bucket order, w = input id bits
+//   bnrm      float4[ΣM]  SurfaceNormal normals in bucket order (w = 0)
+//   nodes     uint2[ΣW]   kd-tree nodes, preorder (left child = n + 1):
+//                           inner: x = cut (float bits), y = cd | right << 2
+//                           leaf : x = bucket count,     y = 3  | bucket_start << 2
+//   parent    int32[ΣW]   parent node (-1 at the root), used to climb after a leaf
+//   match     int32[ΣN]   bucket position of the NN of each reading point
+//   d2        float[ΣN]   squared NN distance
+// Bucket positions are local to the pair (ref_off added by the kernels).
+#pragma once
+#include <stdint.h>
+
+namespace aicp {
+
+constexpr int kHistBins = 2048;     // radix-select digit 1/2 (11 bits)
+constexpr int kHist3Bins = 1024;    // digit 3 (10 bits)
+constexpr int kNNBlock = 256;       // NN / reduce kernel block
+constexpr int kReducePerThread = 4; // reading points per thread in the reduce kernel
+constexpr int kRedCols = 28;        // 21 unique A entries + 6 b + kept count
+constexpr int kFarStack = 48;       // max nested far descents (= max tree depth supported)
+constexpr int kHistRing = 32;       // differential checker history ring
+constexpr uint32_t kLeaf = 3;
+
+struct PairDesc {
+  uint32_t ref_off, n_ref;      // into ref arrays (ref_raw, bpts, bnrm)
+  uint32_t read_off, n_read;    // into reading arrays
+  uint32_t node_off, n_nodes;   // into nodes/parent
+  uint32_t red_blk_off, n_red_blk;  // reduce blocks of this pair (slab rows)
+  float Tinit[16];              // T_refMean_dataIn (column-major)
+  float Tmean[16];              // T_refIn_refMean
+  float mean[3];                // reference centroid (float)
+  float ratio;                  // configured trimmed ratio (overridden by overlap)
+  int32_t tree_depth;
+  // overlap bitmaps (AICP_RUN_OVERLAP): one bit per 0.2 m voxel of the padded key box
+  int32_t ovl_min[3];           // key of voxel (0,0,0)
+  int32_t ovl_dim[3];           // box extent in voxels
+  uint64_t ovl_word_off;        // into the bitmap arena (ref bitmap, then read bitmap)
+  uint64_t ovl_words;           // 32-bit words per bitmap
+  double ref_origin[3], read_origin[3];
+};
+
+struct PairState {
+  float T[16];          // T_iter, column-major
+  float limit;          // trimmed distance limit of the current iteration
+  float ratio;          // trimmed ratio in use
+  int32_t active;       // 1 while iterating
+  int32_t status;       // AICP_* code
+  int32_t iters;
+  int32_t converged;
+  int32_t kept;
+  int32_t n_finite;
+  int32_t hist_count;   // entries pushed into the checker ring
+  int32_t degenerate;
+  float inlier_ratio;
+  float overlap;        // percent, -1 if not computed
+  uint64_t touched_pts, touched_nodes;
+  uint64_t ovl_counts[3];
+  int32_t ovl_bbox[6];  // kmin[3], kmax[3] (union of both clouds)
+  int32_t ovl_err;
+  int32_t pad_;
+  double qh[kHistRing][4];
+  double th[kHistRing][3];
+};
+
+struct IcpParams {
+  float maxE2;     // (1 + eps)^2, float
+  float maxR2;     // maxDist^2
+  int32_t max_iter;
+  int32_t smooth;
+  float min_rot, min_trans;
+  int32_t knn_normals;
+};
+
+}  // namespace aicp

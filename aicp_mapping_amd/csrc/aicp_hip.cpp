@@ -1,0 +1,816 @@
+// aicp_hip.cpp — C-ABI of libaicp_hip.so: context, device arena, batch pipeline.
+//
+// One batch run (aicp_hip_batch_run) for P pairs, one HIP stream, no per-iteration host sync:
+//   1. [device] overlap: origin/endpoint key boxes (k_ovl_init, k_ovl_bbox) -> async D2H
+//   2. [host, overlapped with 1] per pair: centroid, centred reference, libnabo-order kd-tree
+//      (ICP::compute "matcher->init(reference)"), one std::thread per pair up to 16
+//   3. [device] bitmaps sized from the boxes; DDA ray marking, popcounts, overlap% and the
+//      auto-tuned ratio per pair (App::computeRegistration, app.cpp:197-205)
+//   4. [device] gather centred reference into bucket order, reading into the ref-mean
+//      frame, SurfaceNormal on the reference (k_normals)
+//   5. [device] max_iter x {NN, select, reduce, update}; converged pairs exit early
+//   6. [device] T = T_refIn_refMean * T_iter * T_refMean_dataIn; D2H of T and pair states
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/aicp_hip.h"
+#include "aicp_common.hpp"
+#include "icp_math.hpp"
+#include "kdtree_host.hpp"
+#include "kernels.hpp"
+
+using namespace aicp;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+hipError_t ensure(DevBuf& b, size_t bytes) {
+  if (bytes <= b.cap && b.p) return hipSuccess;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  const size_t nb = std::max<size_t>(256, bytes + bytes / 4);
+  const hipError_t e = hipMalloc(&b.p, nb);
+  if (e == hipSuccess) b.cap = nb;
+  return e;
+}
+hipError_t ensure(PinBuf& b, size_t bytes) {
+  if (bytes <= b.cap && b.p) return hipSuccess;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  const size_t nb = std::max<size_t>(256, bytes + bytes / 4);
+  const hipError_t e = hipHostMalloc(&b.p, nb, hipHostMallocDefault);
+  if (e == hipSuccess) b.cap = nb;
+  return e;
+}
+void release(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+void release(PinBuf& b) {
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
+struct Maps {  // block maps of one flat grid
+  std::vector<int32_t> pair;
+  std::vector<uint32_t> start;
+  void add(int p, uint32_t n, uint32_t per_block) {
+    for (uint32_t s = 0; s < n; s += per_block) {
+      pair.push_back(p);
+      start.push_back(s);
+    }
+  }
+};
+
+}  // namespace
+
+struct aicp_hip_batch {
+  size_t P = 0;
+  std::vector<PairDesc> desc;
+  std::vector<std::vector<float>> ref_host;  // packed xyz (tree build input)
+  std::vector<float> initT;                  // 16 per pair
+  uint64_t total_ref = 0, total_read = 0;
+  uint32_t n_red_total = 0;
+  DevBuf ref_raw, read_raw, maps;
+  BlockMap m_read{}, m_ref{}, m_red{};
+};
+
+struct aicp_hip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  DevBuf read_c, bpts, bnrm, nodes, parent, perm, match, d2, desc, state, hist, slab, bitmap,
+      outT, scratch;
+  PinBuf pin_desc, pin_tree, pin_state, pin_out, pin_io;
+  std::vector<HostTree> trees;
+  std::vector<hipEvent_t> nn_ev;
+  hipEvent_t ev[8] = {};
+  int last_nn_launches = 0;
+  double last_nn_ms = 0, last_nn_bytes = 0;
+  uint64_t last_queries = 0;
+  double last_phase[5] = {0, 0, 0, 0, 0};
+};
+
+#define HIPC(x)                                                                   \
+  do {                                                                            \
+    const hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess) {                                                       \
+      ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);                  \
+      return AICP_ERR_HIP;                                                        \
+    }                                                                             \
+  } while (0)
+
+#define FAIL(code, msg)   \
+  do {                    \
+    ctx->err = (msg);     \
+    return (code);        \
+  } while (0)
+
+namespace {
+
+bool valid_pair(const aicp_pair& p) {
+  if (!p.ref || !p.read || p.n_ref < 1 || p.n_read < 1) return false;
+  if (p.ref_stride < 12 || p.read_stride < 12 || (p.ref_stride % 4) || (p.read_stride % 4)) return false;
+  if (p.n_ref >= (1ull << 30) || p.n_read >= (1ull << 30)) return false;
+  return true;
+}
+
+void pack_xyz(const float* src, uint64_t n, uint64_t stride_bytes, float* dst3) {
+  const char* b = reinterpret_cast<const char*>(src);
+  for (uint64_t i = 0; i < n; ++i) {
+    const float* p = reinterpret_cast<const float*>(b + i * stride_bytes);
+    dst3[3 * i] = p[0];
+    dst3[3 * i + 1] = p[1];
+    dst3[3 * i + 2] = p[2];
+  }
+}
+void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4) {
+  const char* b = reinterpret_cast<const char*>(src);
+  for (uint64_t i = 0; i < n; ++i) {
+    const float* p = reinterpret_cast<const float*>(b + i * stride_bytes);
+    dst4[4 * i] = p[0];
+    dst4[4 * i + 1] = p[1];
+    dst4[4 * i + 2] = p[2];
+    dst4[4 * i + 3] = 1.f;
+  }
+}
+
+int check_cfg(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, int flags) {
+  if (!cfg) FAIL(AICP_ERR_INVALID, "null config");
+  if (cfg->knn_match != 1) FAIL(AICP_ERR_UNSUPPORTED, "KDTreeMatcher.knn != 1");
+  if (flags & AICP_RUN_ICP) {
+    if (cfg->knn_normals != 10 && cfg->knn_normals != 20 && cfg->knn_normals != 30)
+      FAIL(AICP_ERR_UNSUPPORTED, "SurfaceNormal knn must be 10, 20 or 30");
+    if (cfg->max_iter < 1 || cfg->max_iter > 1000) FAIL(AICP_ERR_INVALID, "maxIterationCount");
+    if (cfg->smooth_length < 1 || cfg->smooth_length >= kHistRing) FAIL(AICP_ERR_UNSUPPORTED, "smoothLength");
+    if (cfg->bucket_size < 1) FAIL(AICP_ERR_INVALID, "bucketSize");
+    if (!(flags & AICP_RUN_OVERLAP) && !(cfg->trimmed_ratio > 0.f && cfg->trimmed_ratio <= 1.f))
+      FAIL(AICP_ERR_INVALID, "TrimmedDistOutlierFilter.ratio");
+    if (!(cfg->nn_epsilon >= 0.f)) FAIL(AICP_ERR_INVALID, "epsilon");
+  }
+  return AICP_OK;
+}
+
+int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_batch* B) {
+  if (!pairs || n == 0) FAIL(AICP_ERR_INVALID, "no pairs");
+  B->P = n;
+  B->desc.assign(n, PairDesc{});
+  B->ref_host.resize(n);
+  B->initT.assign(16 * n, 0.f);
+  uint64_t ro = 0, wo = 0;
+  uint32_t red = 0;
+  Maps mr, mf, md;
+  for (size_t i = 0; i < n; ++i) {
+    const aicp_pair& p = pairs[i];
+    if (!valid_pair(p)) FAIL(AICP_ERR_INVALID, "invalid pair " + std::to_string(i));
+    PairDesc& d = B->desc[i];
+    d.ref_off = (uint32_t)ro;
+    d.n_ref = (uint32_t)p.n_ref;
+    d.read_off = (uint32_t)wo;
+    d.n_read = (uint32_t)p.n_read;
+    d.red_blk_off = red;
+    d.n_red_blk = (uint32_t)((p.n_read + kNNBlock * kReducePerThread - 1) / (kNNBlock * kReducePerThread));
+    for (int k = 0; k < 3; ++k) {
+      d.ref_origin[k] = p.ref_origin[k];
+      d.read_origin[k] = p.read_origin[k];
+    }
+    red += d.n_red_blk;
+    ro += p.n_ref;
+    wo += p.n_read;
+    if (ro >= (1ull << 31) || wo >= (1ull << 31)) FAIL(AICP_ERR_UNSUPPORTED, "batch too large");
+    if (p.init_T)
+      std::memcpy(&B->initT[16 * i], p.init_T, 64);
+    else
+      ident4(&B->initT[16 * i]);
+    B->ref_host[i].resize(3 * p.n_ref);
+    pack_xyz(p.ref, p.n_ref, p.ref_stride, B->ref_host[i].data());
+    mr.add((int)i, d.n_read, kNNBlock);
+    mf.add((int)i, d.n_ref, kNNBlock);
+    md.add((int)i, d.n_read, kNNBlock * kReducePerThread);
+  }
+  B->total_ref = ro;
+  B->total_read = wo;
+  B->n_red_total = red;
+  // raw clouds as float4
+  HIPC(ensure(B->ref_raw, ro * 16));
+  HIPC(ensure(B->read_raw, wo * 16));
+  HIPC(ensure(ctx->pin_io, std::max(ro, wo) * 16));
+  float* st = ctx->pin_io.as<float>();
+  for (size_t i = 0; i < n; ++i) {
+    const PairDesc& d = B->desc[i];
+    pack_xyz4(pairs[i].ref, d.n_ref, pairs[i].ref_stride, st + 4ull * d.ref_off);
+  }
+  HIPC(hipMemcpyAsync(B->ref_raw.p, st, ro * 16, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  for (size_t i = 0; i < n; ++i) {
+    const PairDesc& d = B->desc[i];
+    pack_xyz4(pairs[i].read, d.n_read, pairs[i].read_stride, st + 4ull * d.read_off);
+  }
+  HIPC(hipMemcpyAsync(B->read_raw.p, st, wo * 16, hipMemcpyHostToDevice, ctx->stream));
+  // block maps: [read pair][read start][ref pair][ref start][red pair][red start]
+  const size_t nr = mr.pair.size(), nf = mf.pair.size(), nd = md.pair.size();
+  const size_t words = 2 * (nr + nf + nd);
+  HIPC(ensure(B->maps, words * 4));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  uint32_t* mp = ctx->pin_io.as<uint32_t>();
+  size_t o = 0;
+  auto put = [&](const Maps& m, BlockMap& bm) {
+    const size_t cnt = m.pair.size();
+    std::memcpy(mp + o, m.pair.data(), cnt * 4);
+    std::memcpy(mp + o + cnt, m.start.data(), cnt * 4);
+    bm.pair = B->maps.as<int32_t>() + o;
+    bm.start = B->maps.as<uint32_t>() + o + cnt;
+    bm.n_blocks = (uint32_t)cnt;
+    o += 2 * cnt;
+  };
+  HIPC(ensure(ctx->pin_io, words * 4));
+  mp = ctx->pin_io.as<uint32_t>();
+  put(mr, B->m_read);
+  put(mf, B->m_ref);
+  put(md, B->m_red);
+  HIPC(hipMemcpyAsync(B->maps.p, mp, words * 4, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return AICP_OK;
+}
+
+void build_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, std::vector<float>& means) {
+  const size_t P = B->P;
+  ctx->trees.resize(P);
+  means.assign(3 * P, 0.f);
+  auto work = [&](size_t i) {
+    const std::vector<float>& ref = B->ref_host[i];
+    const size_t m = ref.size() / 3;
+    double acc[3] = {0, 0, 0};
+    for (size_t k = 0; k < m; ++k)
+      for (int d = 0; d < 3; ++d) acc[d] += (double)ref[3 * k + d];
+    float mu[3];
+    for (int d = 0; d < 3; ++d) mu[d] = (float)(acc[d] / (double)m);
+    std::vector<float> c(3 * m);
+    for (size_t k = 0; k < m; ++k)
+      for (int d = 0; d < 3; ++d) c[3 * k + d] = ref[3 * k + d] - mu[d];
+    build_kdtree_host(c.data(), (int64_t)m, bucket, ctx->trees[i]);
+    for (int d = 0; d < 3; ++d) means[3 * i + d] = mu[d];
+  };
+  const size_t nt = std::min<size_t>(P, std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())));
+  if (nt <= 1) {
+    for (size_t i = 0; i < P; ++i) work(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (size_t i = t; i < P; i += nt) work(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+double ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
+  return ms;
+}
+
+int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, double res,
+              int flags, float* outT, aicp_icp_stats* stats, float* out_overlap) {
+  const auto t_start = std::chrono::steady_clock::now();
+  int rc = check_cfg(ctx, cfg, flags);
+  if (rc) return rc;
+  const bool doOvl = flags & AICP_RUN_OVERLAP, doIcp = flags & AICP_RUN_ICP;
+  if (doOvl && !(res > 0)) FAIL(AICP_ERR_INVALID, "resolution");
+  const size_t P = B->P;
+  hipStream_t s = ctx->stream;
+  for (auto& e : ctx->ev)
+    if (!e) HIPC(hipEventCreate(&e));
+  const bool timeNN = (flags & AICP_RUN_TIME_NN) && doIcp;
+  if (timeNN)
+    while ((int)ctx->nn_ev.size() < 2 * cfg->max_iter) {
+      hipEvent_t e;
+      HIPC(hipEventCreate(&e));
+      ctx->nn_ev.push_back(e);
+    }
+  std::vector<PairDesc> desc = B->desc;
+  for (auto& d : desc) d.ratio = cfg->trimmed_ratio;
+  HIPC(ensure(ctx->desc, P * sizeof(PairDesc)));
+  HIPC(ensure(ctx->state, P * sizeof(PairState)));
+  HIPC(ensure(ctx->hist, P * kHistBins * 4));
+  HIPC(ensure(ctx->pin_desc, 2 * P * sizeof(PairDesc)));
+  HIPC(ensure(ctx->pin_state, P * sizeof(PairState)));
+  HIPC(ensure(ctx->outT, P * 64));
+  HIPC(ensure(ctx->pin_out, P * 64));
+  PairDesc* pdA = ctx->pin_desc.as<PairDesc>();
+  PairDesc* pdB = pdA + P;
+  PairDesc* dDesc = ctx->desc.as<PairDesc>();
+  PairState* dState = ctx->state.as<PairState>();
+  uint32_t* dHist = ctx->hist.as<uint32_t>();
+  std::memcpy(pdA, desc.data(), P * sizeof(PairDesc));
+  HIPC(hipEventRecord(ctx->ev[0], s));
+  HIPC(hipMemcpyAsync(dDesc, pdA, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+  launch_init_state(s, (int)P, dDesc, dState, dHist);
+  if (doOvl) {
+    launch_ovl_init(s, (int)P, dDesc, dState, res);
+    launch_ovl_bbox(s, B->m_ref, dDesc, dState, B->ref_raw.as<float4>(), 0, res);
+    launch_ovl_bbox(s, B->m_read, dDesc, dState, B->read_raw.as<float4>(), 1, res);
+    HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
+  }
+  HIPC(hipEventRecord(ctx->ev[1], s));
+  // host: kd-trees (overlaps the device work above)
+  std::vector<float> means;
+  double tree_ms = 0;
+  uint64_t total_nodes = 0;
+  if (doIcp) {
+    const auto t0 = std::chrono::steady_clock::now();
+    build_trees(ctx, B, cfg->bucket_size, means);
+    tree_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (size_t i = 0; i < P; ++i) {
+      const HostTree& t = ctx->trees[i];
+      if (t.depth >= kFarStack) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack");
+      PairDesc& d = desc[i];
+      d.node_off = (uint32_t)total_nodes;
+      d.n_nodes = (uint32_t)t.parent.size();
+      d.tree_depth = t.depth;
+      total_nodes += d.n_nodes;
+      for (int k = 0; k < 3; ++k) d.mean[k] = means[3 * i + k];
+      float Tm[16], Tmi[16];
+      ident4(Tm);
+      ident4(Tmi);
+      for (int k = 0; k < 3; ++k) {
+        Tm[12 + k] = d.mean[k];
+        Tmi[12 + k] = -d.mean[k];
+      }
+      std::memcpy(d.Tmean, Tm, 64);
+      mul4(Tmi, &B->initT[16 * i], d.Tinit);
+    }
+    if (total_nodes >= (1ull << 30)) FAIL(AICP_ERR_UNSUPPORTED, "too many kd-tree nodes");
+  }
+  uint64_t bm_words = 0;
+  if (doOvl) {
+    HIPC(hipEventSynchronize(ctx->ev[1]));
+    const PairState* hs = ctx->pin_state.as<PairState>();
+    for (size_t i = 0; i < P; ++i) {
+      PairDesc& d = desc[i];
+      uint64_t vox = 1;
+      for (int k = 0; k < 3; ++k) {
+        int lo = hs[i].ovl_bbox[k], hi = hs[i].ovl_bbox[3 + k];
+        if (lo > hi) lo = hi = 0;  // nothing inside the key range
+        d.ovl_min[k] = lo - 2;
+        d.ovl_dim[k] = (hi - lo) + 5;
+        vox *= (uint64_t)d.ovl_dim[k];
+      }
+      if (vox > (1ull << 36)) FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the bitmap grid");
+      d.ovl_words = (vox + 31) / 32;
+      d.ovl_word_off = bm_words;
+      bm_words += 2 * d.ovl_words;
+    }
+    HIPC(ensure(ctx->bitmap, bm_words * 4));
+  }
+  // second descriptor upload + kd-trees
+  std::memcpy(pdB, desc.data(), P * sizeof(PairDesc));
+  HIPC(hipMemcpyAsync(dDesc, pdB, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+  if (doIcp) {
+    const size_t permB = B->total_ref * 4, nodeB = total_nodes * 8, parB = total_nodes * 4;
+    HIPC(ensure(ctx->pin_tree, permB + nodeB + parB));
+    HIPC(ensure(ctx->perm, permB));
+    HIPC(ensure(ctx->nodes, nodeB));
+    HIPC(ensure(ctx->parent, parB));
+    char* base = ctx->pin_tree.as<char>();
+    for (size_t i = 0; i < P; ++i) {
+      const HostTree& t = ctx->trees[i];
+      const PairDesc& d = desc[i];
+      std::memcpy(base + 4ull * d.ref_off, t.perm.data(), 4ull * d.n_ref);
+      std::memcpy(base + permB + 8ull * d.node_off, t.nodes.data(), 8ull * d.n_nodes);
+      std::memcpy(base + permB + nodeB + 4ull * d.node_off, t.parent.data(), 4ull * d.n_nodes);
+    }
+    HIPC(hipMemcpyAsync(ctx->perm.p, base, permB, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(ctx->nodes.p, base + permB, nodeB, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(ctx->parent.p, base + permB + nodeB, parB, hipMemcpyHostToDevice, s));
+  }
+  HIPC(hipEventRecord(ctx->ev[2], s));
+  if (doOvl) {
+    uint32_t* bm = ctx->bitmap.as<uint32_t>();
+    HIPC(hipMemsetAsync(bm, 0, bm_words * 4, s));
+    launch_ovl_mark(s, B->m_ref, dDesc, dState, B->ref_raw.as<float4>(), 0, res, bm);
+    launch_ovl_mark(s, B->m_read, dDesc, dState, B->read_raw.as<float4>(), 1, res, bm);
+    launch_ovl_count(s, (int)P, dDesc, dState, bm);
+    launch_ovl_finish(s, (int)P, dState, doIcp ? 1 : 0);
+  }
+  HIPC(hipEventRecord(ctx->ev[3], s));
+  IcpParams prm{};
+  int nn_launches = 0;
+  if (doIcp) {
+    HIPC(ensure(ctx->read_c, B->total_read * 16));
+    HIPC(ensure(ctx->bpts, B->total_ref * 16));
+    HIPC(ensure(ctx->bnrm, B->total_ref * 16));
+    HIPC(ensure(ctx->match, B->total_read * 4));
+    HIPC(ensure(ctx->d2, B->total_read * 4));
+    HIPC(ensure(ctx->slab, (size_t)B->n_red_total * kRedCols * 8));
+    float4* bpts = ctx->bpts.as<float4>();
+    float4* bnrm = ctx->bnrm.as<float4>();
+    float4* readc = ctx->read_c.as<float4>();
+    const uint2* nodes = ctx->nodes.as<uint2>();
+    const int32_t* parent = ctx->parent.as<int32_t>();
+    launch_gather_ref(s, B->m_ref, dDesc, B->ref_raw.as<float4>(), ctx->perm.as<int32_t>(), bpts);
+    launch_prepare_read(s, B->m_read, dDesc, B->read_raw.as<float4>(), readc);
+    if (!launch_normals(s, B->m_ref, dDesc, dState, nodes, parent, bpts, bnrm, cfg->knn_normals))
+      FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
+    HIPC(hipEventRecord(ctx->ev[4], s));
+    prm.maxE2 = (1 + cfg->nn_epsilon) * (1 + cfg->nn_epsilon);
+    prm.maxR2 = cfg->nn_max_dist * cfg->nn_max_dist;
+    prm.max_iter = cfg->max_iter;
+    prm.smooth = cfg->smooth_length;
+    prm.min_rot = cfg->min_diff_rot;
+    prm.min_trans = cfg->min_diff_trans;
+    prm.knn_normals = cfg->knn_normals;
+    for (int it = 0; it < cfg->max_iter; ++it) {
+      if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it], s));
+      launch_icp_nn(s, B->m_read, dDesc, dState, readc, nodes, parent, bpts, ctx->match.as<int32_t>(),
+                    ctx->d2.as<float>(), dHist, prm);
+      if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it + 1], s));
+      ++nn_launches;
+      launch_icp_select(s, (int)P, dDesc, dState, ctx->d2.as<float>(), dHist);
+      launch_icp_reduce(s, B->m_red, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
+                        bpts, bnrm, ctx->slab.as<double>());
+      launch_icp_update(s, (int)P, dDesc, dState, ctx->slab.as<double>(), dHist, prm);
+    }
+    launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
+  } else {
+    HIPC(hipEventRecord(ctx->ev[4], s));
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(ctx->ev[5], s));
+  HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
+  if (doIcp) HIPC(hipMemcpyAsync(ctx->pin_out.p, ctx->outT.p, P * 64, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  // results
+  const PairState* hs = ctx->pin_state.as<PairState>();
+  int first_err = AICP_OK;
+  uint64_t queries = 0, tp = 0, tn = 0;
+  for (size_t i = 0; i < P; ++i) {
+    const PairState& st = hs[i];
+    int status = st.status;
+    if (doOvl && st.ovl_err && !status) status = AICP_ERR_HIP;
+    if (status && !first_err) first_err = status;
+    if (outT && doIcp) std::memcpy(outT + 16 * i, ctx->pin_out.as<float>() + 16 * i, 64);
+    if (out_overlap) out_overlap[i] = st.overlap;
+    queries += (uint64_t)st.iters * desc[i].n_read;
+    tp += st.touched_pts;
+    tn += st.touched_nodes;
+    if (stats) {
+      aicp_icp_stats& o = stats[i];
+      std::memset(&o, 0, sizeof(o));
+      o.status = status;
+      o.iterations = st.iters;
+      o.converged = st.converged;
+      o.degenerate_normals = st.degenerate;
+      o.inlier_ratio = st.inlier_ratio;
+      o.trimmed_ratio = st.ratio;
+      o.overlap_percent = st.overlap;
+      o.tree_depth = desc[i].tree_depth;
+      o.nn_points_touched = st.touched_pts;
+      o.nn_nodes_touched = st.touched_nodes;
+      for (int k = 0; k < 3; ++k) o.overlap_keys[k] = st.ovl_counts[k];
+    }
+  }
+  ctx->last_nn_launches = timeNN ? nn_launches : 0;
+  ctx->last_nn_ms = 0;
+  if (timeNN)
+    for (int it = 0; it < nn_launches; ++it) ctx->last_nn_ms += ev_ms(ctx->nn_ev[2 * it], ctx->nn_ev[2 * it + 1]);
+  // N*(12 B query + 8 B id/d2) + V*16 B + W*8 B
+  ctx->last_nn_bytes = (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0;
+  ctx->last_queries = queries;
+  ctx->last_phase[0] = doOvl ? ev_ms(ctx->ev[0], ctx->ev[1]) + ev_ms(ctx->ev[2], ctx->ev[3]) : 0;
+  ctx->last_phase[1] = tree_ms;
+  ctx->last_phase[2] = doIcp ? ev_ms(ctx->ev[3], ctx->ev[4]) : 0;
+  ctx->last_phase[3] = doIcp ? ev_ms(ctx->ev[4], ctx->ev[5]) : 0;
+  ctx->last_phase[4] =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  if (first_err) ctx->err = "pair status " + std::to_string(first_err);
+  return first_err;
+}
+
+void free_batch(aicp_hip_batch* B) {
+  if (!B) return;
+  release(B->ref_raw);
+  release(B->read_raw);
+  release(B->maps);
+  delete B;
+}
+
+// single-pair tree on arbitrary points for the kernel-level entry points
+int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, HostTree& t) {
+  std::vector<float> xyz(3 * n);
+  pack_xyz(pts, n, stride, xyz.data());
+  build_kdtree_host(xyz.data(), (int64_t)n, 8, t);
+  if (t.depth >= kFarStack) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack");
+  HIPC(ensure(ctx->bpts, n * 16));
+  HIPC(ensure(ctx->nodes, t.parent.size() * 8));
+  HIPC(ensure(ctx->parent, t.parent.size() * 4));
+  HIPC(ensure(ctx->pin_io, std::max(n * 16, t.parent.size() * 8)));
+  float* b = ctx->pin_io.as<float>();
+  for (size_t j = 0; j < n; ++j) {
+    const int32_t id = t.perm[j];
+    b[4 * j] = xyz[3 * id];
+    b[4 * j + 1] = xyz[3 * id + 1];
+    b[4 * j + 2] = xyz[3 * id + 2];
+    std::memcpy(&b[4 * j + 3], &id, 4);
+  }
+  HIPC(hipMemcpy(ctx->bpts.p, b, n * 16, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->nodes.p, t.nodes.data(), t.parent.size() * 8, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->parent.p, t.parent.data(), t.parent.size() * 4, hipMemcpyHostToDevice));
+  return AICP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* aicp_hip_version(void) { return "aicp_hip 0.1 (gfx950)"; }
+
+int aicp_hip_create(int device, aicp_hip_ctx** out) {
+  if (!out) return AICP_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return AICP_ERR_HIP;
+  if (device < 0 || device >= n) return AICP_ERR_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return AICP_ERR_HIP;
+  aicp_hip_ctx* c = new aicp_hip_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return AICP_ERR_HIP;
+  }
+  *out = c;
+  return AICP_OK;
+}
+
+void aicp_hip_destroy(aicp_hip_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->parent, &ctx->perm, &ctx->match,
+                    &ctx->d2, &ctx->desc, &ctx->state, &ctx->hist, &ctx->slab, &ctx->bitmap, &ctx->outT,
+                    &ctx->scratch})
+    release(*b);
+  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_tree, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io}) release(*b);
+  for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
+  for (auto e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* aicp_hip_last_error(const aicp_hip_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int aicp_hip_batch_upload(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs, aicp_hip_batch** out) {
+  if (!ctx || !out) return AICP_ERR_INVALID;
+  HIPC(hipSetDevice(ctx->device));
+  aicp_hip_batch* B = new aicp_hip_batch();
+  const int rc = upload_pairs(ctx, pairs, n_pairs, B);
+  if (rc) {
+    free_batch(B);
+    *out = nullptr;
+    return rc;
+  }
+  *out = B;
+  return AICP_OK;
+}
+
+void aicp_hip_batch_free(aicp_hip_ctx* ctx, aicp_hip_batch* batch) {
+  if (ctx) (void)hipStreamSynchronize(ctx->stream);
+  free_batch(batch);
+}
+
+int aicp_hip_batch_run(aicp_hip_ctx* ctx, aicp_hip_batch* batch, const aicp_icp_config* cfg, double resolution,
+                       int flags, float* out_T, aicp_icp_stats* stats) {
+  if (!ctx || !batch) return AICP_ERR_INVALID;
+  if (!(flags & (AICP_RUN_ICP | AICP_RUN_OVERLAP))) FAIL(AICP_ERR_INVALID, "nothing to run");
+  HIPC(hipSetDevice(ctx->device));
+  return run_batch(ctx, batch, cfg, resolution, flags, out_T, stats, nullptr);
+}
+
+int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
+                         double resolution, int flags, float* out_T, aicp_icp_stats* stats) {
+  aicp_hip_batch* B = nullptr;
+  int rc = aicp_hip_batch_upload(ctx, pairs, n_pairs, &B);
+  if (rc) return rc;
+  rc = aicp_hip_batch_run(ctx, B, cfg, resolution, flags, out_T, stats);
+  aicp_hip_batch_free(ctx, B);
+  return rc;
+}
+
+int aicp_hip_register_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
+                            float* out_T, aicp_icp_stats* stats) {
+  return aicp_hip_align_batch(ctx, cfg, pairs, n_pairs, 0.0, AICP_RUN_ICP, out_T, stats);
+}
+
+int aicp_hip_register(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pair, float out_T[16],
+                      aicp_icp_stats* stats) {
+  return aicp_hip_register_batch(ctx, cfg, pair, 1, out_T, stats);
+}
+
+int aicp_hip_overlap_batch(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs, double resolution,
+                           float* out_overlap_percent, aicp_icp_stats* stats) {
+  if (!ctx) return AICP_ERR_INVALID;
+  aicp_hip_batch* B = nullptr;
+  int rc = aicp_hip_batch_upload(ctx, pairs, n_pairs, &B);
+  if (rc) return rc;
+  aicp_icp_config cfg;
+  aicp_hip_default_config(&cfg);
+  rc = run_batch(ctx, B, &cfg, resolution, AICP_RUN_OVERLAP, nullptr, stats, out_overlap_percent);
+  aicp_hip_batch_free(ctx, B);
+  return rc;
+}
+
+int aicp_hip_overlap(aicp_hip_ctx* ctx, const aicp_pair* pair, double resolution, float* out) {
+  return aicp_hip_overlap_batch(ctx, pair, 1, resolution, out, nullptr);
+}
+
+int aicp_hip_transform(aicp_hip_ctx* ctx, const float T[16], const float* in, size_t n, size_t stride,
+                       float* out) {
+  if (!ctx || !T || !in || !out || stride < 12) return AICP_ERR_INVALID;
+  if (n == 0) return AICP_OK;
+  HIPC(hipSetDevice(ctx->device));
+  HIPC(ensure(ctx->scratch, 64 + 2 * n * 16));
+  HIPC(ensure(ctx->pin_io, n * 16));
+  float* h = ctx->pin_io.as<float>();
+  pack_xyz4(in, n, stride, h);
+  char* d = ctx->scratch.as<char>();
+  HIPC(hipMemcpy(d, T, 64, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(d + 64, h, n * 16, hipMemcpyHostToDevice));
+  launch_transform(ctx->stream, (int)n, (const float*)d, (const float4*)(d + 64), (float4*)(d + 64 + n * 16));
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  HIPC(hipMemcpy(h, d + 64 + n * 16, n * 16, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
+  return AICP_OK;
+}
+
+int aicp_hip_last_nn_timing(const aicp_hip_ctx* ctx, int* n_launches, double* total_ms, double* bytes,
+                            uint64_t* queries) {
+  if (!ctx) return AICP_ERR_INVALID;
+  if (n_launches) *n_launches = ctx->last_nn_launches;
+  if (total_ms) *total_ms = ctx->last_nn_ms;
+  if (bytes) *bytes = ctx->last_nn_bytes;
+  if (queries) *queries = ctx->last_queries;
+  return AICP_OK;
+}
+
+int aicp_hip_last_phase_ms(const aicp_hip_ctx* ctx, double out_ms[5]) {
+  if (!ctx || !out_ms) return AICP_ERR_INVALID;
+  for (int i = 0; i < 5; ++i) out_ms[i] = ctx->last_phase[i];
+  return AICP_OK;
+}
+
+int aicp_hip_knn(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, const float* queries, size_t nq,
+                 size_t qstride, int k, float epsilon, float max_dist, int32_t* out_ids, float* out_d2,
+                 uint64_t* out_touched) {
+  if (!ctx || !pts || !queries || !out_ids || !out_d2 || n == 0 || stride < 12 || qstride < 12) return AICP_ERR_INVALID;
+  HIPC(hipSetDevice(ctx->device));
+  HostTree t;
+  int rc = upload_tree(ctx, pts, n, stride, t);
+  if (rc) return rc;
+  HIPC(ensure(ctx->read_c, nq * 16 + 16));
+  HIPC(ensure(ctx->match, nq * (size_t)k * 4 + 4));
+  HIPC(ensure(ctx->d2, nq * (size_t)k * 4 + 4));
+  HIPC(ensure(ctx->scratch, 16));
+  HIPC(ensure(ctx->pin_io, std::max<size_t>(nq * 16, nq * (size_t)k * 4) + 16));
+  float* h = ctx->pin_io.as<float>();
+  pack_xyz4(queries, nq, qstride, h);
+  HIPC(hipMemcpy(ctx->read_c.p, h, nq * 16, hipMemcpyHostToDevice));
+  HIPC(hipMemset(ctx->scratch.p, 0, 16));
+  const float maxE2 = (1 + epsilon) * (1 + epsilon);
+  const float maxR2 = max_dist * max_dist;
+  if (!launch_knn_generic(ctx->stream, (int)nq, ctx->read_c.as<float4>(), ctx->nodes.as<uint2>(),
+                          ctx->parent.as<int32_t>(), ctx->bpts.as<float4>(), k, maxE2, maxR2,
+                          ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->scratch.as<unsigned long long>()))
+    FAIL(AICP_ERR_UNSUPPORTED, "k must be 1, 4, 10, 20 or 30");
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  HIPC(hipMemcpy(out_ids, ctx->match.p, nq * (size_t)k * 4, hipMemcpyDeviceToHost));
+  HIPC(hipMemcpy(out_d2, ctx->d2.p, nq * (size_t)k * 4, hipMemcpyDeviceToHost));
+  if (out_touched) HIPC(hipMemcpy(out_touched, ctx->scratch.p, 16, hipMemcpyDeviceToHost));
+  return AICP_OK;
+}
+
+int aicp_hip_normals(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, int knn, float* out_normals,
+                     int32_t* out_degenerate) {
+  if (!ctx || !pts || !out_normals || n == 0 || stride < 12) return AICP_ERR_INVALID;
+  HIPC(hipSetDevice(ctx->device));
+  HostTree t;
+  int rc = upload_tree(ctx, pts, n, stride, t);
+  if (rc) return rc;
+  PairDesc d{};
+  d.n_ref = (uint32_t)n;
+  d.n_nodes = (uint32_t)t.parent.size();
+  d.ratio = 0.5f;
+  Maps mf;
+  mf.add(0, (uint32_t)n, kNNBlock);
+  HIPC(ensure(ctx->desc, sizeof(PairDesc)));
+  HIPC(ensure(ctx->state, sizeof(PairState)));
+  HIPC(ensure(ctx->hist, kHistBins * 4));
+  HIPC(ensure(ctx->bnrm, n * 16));
+  HIPC(ensure(ctx->scratch, mf.pair.size() * 8));
+  HIPC(hipMemcpy(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->scratch.p, mf.pair.data(), mf.pair.size() * 4, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->scratch.as<char>() + mf.pair.size() * 4, mf.start.data(), mf.pair.size() * 4,
+                 hipMemcpyHostToDevice));
+  BlockMap m{ctx->scratch.as<int32_t>(), (const uint32_t*)(ctx->scratch.as<char>() + mf.pair.size() * 4),
+             (uint32_t)mf.pair.size()};
+  launch_init_state(ctx->stream, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->hist.as<uint32_t>());
+  if (!launch_normals(ctx->stream, m, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->nodes.as<uint2>(),
+                      ctx->parent.as<int32_t>(), ctx->bpts.as<float4>(), ctx->bnrm.as<float4>(), knn))
+    FAIL(AICP_ERR_UNSUPPORTED, "knn must be 10, 20 or 30");
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  std::vector<float> nb(4 * n);
+  HIPC(hipMemcpy(nb.data(), ctx->bnrm.p, n * 16, hipMemcpyDeviceToHost));
+  PairState st;
+  HIPC(hipMemcpy(&st, ctx->state.p, sizeof(st), hipMemcpyDeviceToHost));
+  for (size_t j = 0; j < n; ++j)
+    for (int k = 0; k < 3; ++k) out_normals[3 * (size_t)t.perm[j] + k] = nb[4 * j + k];
+  if (out_degenerate) *out_degenerate = st.degenerate;
+  return AICP_OK;
+}
+
+int aicp_hip_dists_quantile(aicp_hip_ctx* ctx, const float* d2, size_t n, float quantile, float* out_limit) {
+  if (!ctx || !d2 || !out_limit || n == 0 || n >= (1ull << 31)) return AICP_ERR_INVALID;
+  if (!(quantile >= 0.f && quantile <= 1.f)) return AICP_ERR_INVALID;  // "quantile must be between 0 and 1"
+  HIPC(hipSetDevice(ctx->device));
+  PairDesc d{};
+  d.n_read = (uint32_t)n;
+  d.ratio = quantile;
+  Maps mr;
+  mr.add(0, (uint32_t)n, kNNBlock);
+  HIPC(ensure(ctx->desc, sizeof(PairDesc)));
+  HIPC(ensure(ctx->state, sizeof(PairState)));
+  HIPC(ensure(ctx->hist, kHistBins * 4));
+  HIPC(ensure(ctx->d2, n * 4));
+  HIPC(ensure(ctx->scratch, mr.pair.size() * 8));
+  HIPC(hipMemcpy(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->d2.p, d2, n * 4, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->scratch.p, mr.pair.data(), mr.pair.size() * 4, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->scratch.as<char>() + mr.pair.size() * 4, mr.start.data(), mr.pair.size() * 4,
+                 hipMemcpyHostToDevice));
+  BlockMap m{ctx->scratch.as<int32_t>(), (const uint32_t*)(ctx->scratch.as<char>() + mr.pair.size() * 4),
+             (uint32_t)mr.pair.size()};
+  launch_init_state(ctx->stream, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->hist.as<uint32_t>());
+  launch_hist_d2(ctx->stream, m, ctx->desc.as<PairDesc>(), ctx->d2.as<float>(), ctx->hist.as<uint32_t>());
+  launch_icp_select(ctx->stream, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->d2.as<float>(),
+                    ctx->hist.as<uint32_t>());
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  PairState st;
+  HIPC(hipMemcpy(&st, ctx->state.p, sizeof(st), hipMemcpyDeviceToHost));
+  if (st.status) FAIL(st.status, "no outlier to filter");
+  *out_limit = st.limit;
+  return AICP_OK;
+}
+
+int aicp_hip_solve6(aicp_hip_ctx* ctx, const double* A, const double* b, double* out_x, int32_t* out_path) {
+  if (!ctx || !A || !b || !out_x) return AICP_ERR_INVALID;
+  HIPC(hipSetDevice(ctx->device));
+  HIPC(ensure(ctx->scratch, 8 * (36 + 6 + 6) + 8));
+  char* d = ctx->scratch.as<char>();
+  HIPC(hipMemcpy(d, A, 36 * 8, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(d + 288, b, 6 * 8, hipMemcpyHostToDevice));
+  launch_solve6(ctx->stream, (const double*)d, (const double*)(d + 288), (double*)(d + 336), (int32_t*)(d + 384));
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  HIPC(hipMemcpy(out_x, d + 336, 48, hipMemcpyDeviceToHost));
+  int32_t path = 0;
+  HIPC(hipMemcpy(&path, d + 384, 4, hipMemcpyDeviceToHost));
+  if (out_path) *out_path = path;
+  return AICP_OK;
+}
+
+}  // extern "C"

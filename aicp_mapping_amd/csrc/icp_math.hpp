@@ -1,0 +1,432 @@
+// icp_math.hpp — small fixed-size math of the ICP update, callable on host and device.
+//
+// Float point arithmetic follows the operation order of the reference (Eigen lazy/GEMM
+// products with a sequential k loop, no FMA: the library is compiled -ffp-contract=off).
+// Decompositions run in double with float-precision rank thresholds:
+//   solvePossiblyUnderdeterminedLinearSystem   (libpointmatcher ErrorMinimizer)
+//   Eigen::AngleAxis -> rotation               (PointToPlaneErrorMinimizer::compute)
+//   DifferentialTransformationChecker          (quaternion angular distance)
+//   SurfaceNormalDataPointsFilter rank test + smallest eigenvector
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#define AICP_HD __host__ __device__ inline
+
+namespace aicp {
+
+constexpr float kFltEps = 1.1920928955078125e-07f;
+constexpr double kDblEps = 2.220446049250313e-16;
+constexpr double kDblMin = 2.2250738585072014e-308;
+
+AICP_HD float m4(const float* m, int r, int c) { return m[c * 4 + r]; }
+
+AICP_HD void mul4(const float* A, const float* B, float* C) {
+  float t[16];
+  for (int c = 0; c < 4; ++c)
+    for (int r = 0; r < 4; ++r) {
+      float s = m4(A, r, 0) * m4(B, 0, c);
+      s += m4(A, r, 1) * m4(B, 1, c);
+      s += m4(A, r, 2) * m4(B, 2, c);
+      s += m4(A, r, 3) * m4(B, 3, c);
+      t[c * 4 + r] = s;
+    }
+  for (int i = 0; i < 16; ++i) C[i] = t[i];
+}
+
+// T * (x, y, z, 1), rows 0..2
+AICP_HD void apply4(const float* T, float x, float y, float z, float* o) {
+  for (int r = 0; r < 3; ++r) {
+    float s = m4(T, r, 0) * x;
+    s += m4(T, r, 1) * y;
+    s += m4(T, r, 2) * z;
+    s += m4(T, r, 3);
+    o[r] = s;
+  }
+}
+
+AICP_HD void ident4(float* T) {
+  for (int i = 0; i < 16; ++i) T[i] = (i % 5 == 0) ? 1.f : 0.f;
+}
+
+// ΔT from the solution x = (rotation vector, translation), Eigen::AngleAxis semantics.
+AICP_HD void delta_transform(const float* x, float* T) {
+  const float sq = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
+  const float angle = sqrtf(sq);
+  float axis[3] = {x[0], x[1], x[2]};
+  if (sq > 0.f) {
+    for (int i = 0; i < 3; ++i) axis[i] = x[i] / angle;
+  }
+  const float sa = (float)sin((double)angle);
+  const float c = (float)cos((double)angle);
+  float sin_axis[3], cos1_axis[3];
+  for (int i = 0; i < 3; ++i) {
+    sin_axis[i] = sa * axis[i];
+    cos1_axis[i] = (1.f - c) * axis[i];
+  }
+  float R[9];  // row-major
+  float tmp = cos1_axis[0] * axis[1];
+  R[0 * 3 + 1] = tmp - sin_axis[2];
+  R[1 * 3 + 0] = tmp + sin_axis[2];
+  tmp = cos1_axis[0] * axis[2];
+  R[0 * 3 + 2] = tmp + sin_axis[1];
+  R[2 * 3 + 0] = tmp - sin_axis[1];
+  tmp = cos1_axis[1] * axis[2];
+  R[1 * 3 + 2] = tmp - sin_axis[0];
+  R[2 * 3 + 1] = tmp + sin_axis[0];
+  for (int i = 0; i < 3; ++i) R[i * 3 + i] = cos1_axis[i] * axis[i] + c;
+  bool nan = false;
+  for (int r = 0; r < 3; ++r)
+    for (int cc = 0; cc < 3; ++cc) {
+      T[cc * 4 + r] = R[r * 3 + cc];
+      nan |= (R[r * 3 + cc] != R[r * 3 + cc]);
+    }
+  for (int r = 0; r < 3; ++r) {
+    T[12 + r] = x[3 + r];
+    nan |= (x[3 + r] != x[3 + r]);
+  }
+  T[3] = T[7] = T[11] = 0.f;
+  T[15] = 1.f;
+  if (nan)  // "mOut != mOut": degenerate rotation -> identity block
+    for (int r = 0; r < 3; ++r)
+      for (int cc = 0; cc < 3; ++cc) T[cc * 4 + r] = (r == cc) ? 1.f : 0.f;
+}
+
+// Quaternion (w, x, y, z) of the rotation block, Shoemake's method in double.
+AICP_HD void quat_from_T(const float* T, double* q) {
+  double m[3][3];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) m[r][c] = (double)m4(T, r, c);
+  double t = (m[0][0] + m[1][1]) + m[2][2];
+  if (t > 0) {
+    t = sqrt(t + 1.0);
+    q[0] = 0.5 * t;
+    t = 0.5 / t;
+    q[1] = (m[2][1] - m[1][2]) * t;
+    q[2] = (m[0][2] - m[2][0]) * t;
+    q[3] = (m[1][0] - m[0][1]) * t;
+  } else {
+    int i = 0;
+    if (m[1][1] > m[0][0]) i = 1;
+    if (m[2][2] > m[i][i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
+    double v[3];
+    v[i] = 0.5 * t;
+    t = 0.5 / t;
+    q[0] = (m[k][j] - m[j][k]) * t;
+    v[j] = (m[j][i] + m[i][j]) * t;
+    v[k] = (m[k][i] + m[i][k]) * t;
+    q[1] = v[0];
+    q[2] = v[1];
+    q[3] = v[2];
+  }
+}
+
+AICP_HD double quat_angdist(const double* a, const double* b) {
+  const double bw = b[0], bx = -b[1], by = -b[2], bz = -b[3];
+  const double w = a[0] * bw - a[1] * bx - a[2] * by - a[3] * bz;
+  const double x = a[0] * bx + a[1] * bw + a[2] * bz - a[3] * by;
+  const double y = a[0] * by + a[2] * bw + a[3] * bx - a[1] * bz;
+  const double z = a[0] * bz + a[3] * bw + a[1] * by - a[2] * bx;
+  return 2.0 * atan2(sqrt(x * x + y * y + z * z), fabs(w));
+}
+
+// ---- full-pivoting Householder QR (Eigen FullPivHouseholderQR semantics), n <= 6 --------
+struct PivQR {
+  int n, nonzero, rank;
+  double a[36];
+  double tau[6];
+  int rowT[6], colT[6];
+  double maxpivot;
+};
+
+AICP_HD void pivqr(const double* A, int n, PivQR& q) {
+  q.n = n;
+  for (int i = 0; i < n * n; ++i) q.a[i] = A[i];
+  const double prec = (double)kFltEps * n;
+  q.nonzero = n;
+  q.maxpivot = 0;
+  double biggest = 0;
+  for (int k = 0; k < n; ++k) {
+    int br = k, bc = k;
+    double bv = -1;
+    for (int c = k; c < n; ++c)
+      for (int r = k; r < n; ++r) {
+        const double v = fabs(q.a[r * n + c]);
+        if (v > bv) {
+          bv = v;
+          br = r;
+          bc = c;
+        }
+      }
+    if (k == 0) biggest = bv;
+    if (bv <= biggest * prec) {
+      q.nonzero = k;
+      for (int i = k; i < n; ++i) {
+        q.rowT[i] = i;
+        q.colT[i] = i;
+        q.tau[i] = 0;
+      }
+      break;
+    }
+    q.rowT[k] = br;
+    q.colT[k] = bc;
+    if (br != k)
+      for (int c = k; c < n; ++c) {
+        const double t = q.a[k * n + c];
+        q.a[k * n + c] = q.a[br * n + c];
+        q.a[br * n + c] = t;
+      }
+    if (bc != k)
+      for (int r = 0; r < n; ++r) {
+        const double t = q.a[r * n + k];
+        q.a[r * n + k] = q.a[r * n + bc];
+        q.a[r * n + bc] = t;
+      }
+    double tailSq = 0;
+    for (int r = k + 1; r < n; ++r) tailSq += q.a[r * n + k] * q.a[r * n + k];
+    const double c0 = q.a[k * n + k];
+    double beta, tau;
+    if (tailSq <= kDblMin) {
+      tau = 0;
+      beta = c0;
+      for (int r = k + 1; r < n; ++r) q.a[r * n + k] = 0;
+    } else {
+      beta = sqrt(c0 * c0 + tailSq);
+      if (c0 >= 0) beta = -beta;
+      const double den = c0 - beta;
+      for (int r = k + 1; r < n; ++r) q.a[r * n + k] /= den;
+      tau = (beta - c0) / beta;
+    }
+    q.tau[k] = tau;
+    q.a[k * n + k] = beta;
+    if (fabs(beta) > q.maxpivot) q.maxpivot = fabs(beta);
+    for (int c = k + 1; c < n; ++c) {
+      double s = q.a[k * n + c];
+      for (int r = k + 1; r < n; ++r) s += q.a[r * n + k] * q.a[r * n + c];
+      s *= tau;
+      q.a[k * n + c] -= s;
+      for (int r = k + 1; r < n; ++r) q.a[r * n + c] -= s * q.a[r * n + k];
+    }
+  }
+  const double thr = fabs(q.maxpivot) * ((double)kFltEps * n);
+  q.rank = 0;
+  for (int i = 0; i < q.nonzero; ++i) q.rank += (fabs(q.a[i * n + i]) > thr) ? 1 : 0;
+}
+
+// Q = P0 H0 P1 H1 ... (row-major n x n)
+AICP_HD void pivqr_Q(const PivQR& q, double* Q) {
+  const int n = q.n;
+  for (int i = 0; i < n * n; ++i) Q[i] = 0;
+  for (int i = 0; i < n; ++i) Q[i * n + i] = 1;
+  for (int k = n - 1; k >= 0; --k) {
+    const double tau = (k < q.nonzero) ? q.tau[k] : 0.0;
+    if (tau != 0) {
+      for (int c = k; c < n; ++c) {
+        double s = Q[k * n + c];
+        for (int r = k + 1; r < n; ++r) s += q.a[r * n + k] * Q[r * n + c];
+        s *= tau;
+        Q[k * n + c] -= s;
+        for (int r = k + 1; r < n; ++r) Q[r * n + c] -= s * q.a[r * n + k];
+      }
+    }
+    const int r = (k < q.nonzero) ? q.rowT[k] : k;
+    if (r != k)
+      for (int c = 0; c < n; ++c) {
+        const double t = Q[k * n + c];
+        Q[k * n + c] = Q[r * n + c];
+        Q[r * n + c] = t;
+      }
+  }
+}
+
+AICP_HD bool llt_solve(const double* M, int r, const double* b, double* x) {
+  double L[36];
+  for (int i = 0; i < 36; ++i) L[i] = 0;
+  for (int j = 0; j < r; ++j) {
+    double d = M[j * r + j];
+    for (int k = 0; k < j; ++k) d -= L[j * r + k] * L[j * r + k];
+    if (!(d > 0)) return false;
+    const double ljj = sqrt(d);
+    L[j * r + j] = ljj;
+    for (int i = j + 1; i < r; ++i) {
+      double s = M[i * r + j];
+      for (int k = 0; k < j; ++k) s -= L[i * r + k] * L[j * r + k];
+      L[i * r + j] = s / ljj;
+    }
+  }
+  double y[6];
+  for (int i = 0; i < r; ++i) {
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= L[i * r + k] * y[k];
+    y[i] = s / L[i * r + i];
+  }
+  for (int i = r - 1; i >= 0; --i) {
+    double s = y[i];
+    for (int k = i + 1; k < r; ++k) s -= L[k * r + i] * x[k];
+    x[i] = s / L[i * r + i];
+  }
+  return true;
+}
+
+// Cyclic Jacobi eigen-decomposition (symmetric, row-major), eigenvectors as columns of V.
+AICP_HD void jacobi_eig(const double* A, int n, double* w, double* V) {
+  double a[36];
+  for (int i = 0; i < n * n; ++i) a[i] = A[i];
+  for (int i = 0; i < n * n; ++i) V[i] = 0;
+  for (int i = 0; i < n; ++i) V[i * n + i] = 1;
+  for (int sweep = 0; sweep < 64; ++sweep) {
+    double offn = 0, diag = 0;
+    for (int p = 0; p < n; ++p) {
+      diag += a[p * n + p] * a[p * n + p];
+      for (int q = p + 1; q < n; ++q) offn += a[p * n + q] * a[p * n + q];
+    }
+    if (offn <= 1e-30 * diag || offn == 0) break;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = a[p * n + q];
+        if (apq == 0) continue;
+        const double app = a[p * n + p], aqq = a[q * n + q];
+        const double theta = (aqq - app) / (2 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+        const double c = 1 / sqrt(t * t + 1), s = t * c;
+        for (int k = 0; k < n; ++k) {
+          const double akp = a[k * n + p], akq = a[k * n + q];
+          a[k * n + p] = c * akp - s * akq;
+          a[k * n + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double apk = a[p * n + k], aqk = a[q * n + k];
+          a[p * n + k] = c * apk - s * aqk;
+          a[q * n + k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double vkp = V[k * n + p], vkq = V[k * n + q];
+          V[k * n + p] = c * vkp - s * vkq;
+          V[k * n + q] = s * vkp + c * vkq;
+        }
+      }
+  }
+  for (int i = 0; i < n; ++i) w[i] = a[i * n + i];
+}
+
+// solvePossiblyUnderdeterminedLinearSystem (A row-major 6x6). Returns the path taken:
+// 0 LLT (full rank), 1 rank-r minimal-norm QR, 2 pseudo-inverse (JacobiSVD fallback).
+AICP_HD int solve6(const double* A, const double* b, double* x) {
+  const int n = 6;
+  PivQR qr;
+  pivqr(A, n, qr);
+  if (qr.rank == n) {
+    if (llt_solve(A, n, b, x)) return 0;
+  } else if (qr.rank > 0) {
+    const int r = qr.rank;
+    double Q[36];
+    pivqr_Q(qr, Q);
+    int perm[6];
+    for (int i = 0; i < n; ++i) perm[i] = i;
+    for (int k = 0; k < n; ++k) {
+      const int c = (k < qr.nonzero) ? qr.colT[k] : k;
+      const int t = perm[k];
+      perm[k] = perm[c];
+      perm[c] = t;
+    }
+    double R1[36], RRt[36], qb[6], y[6];
+    for (int i = 0; i < r; ++i)
+      for (int j = 0; j < n; ++j) {
+        double s = 0;
+        for (int k = 0; k < n; ++k) s += Q[k * n + i] * A[k * n + perm[j]];
+        R1[i * n + j] = s;
+      }
+    for (int i = 0; i < r; ++i)
+      for (int j = 0; j < r; ++j) {
+        double s = 0;
+        for (int k = 0; k < n; ++k) s += R1[i * n + k] * R1[j * n + k];
+        RRt[i * r + j] = s;
+      }
+    for (int i = 0; i < r; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += Q[k * n + i] * b[k];
+      qb[i] = s;
+    }
+    if (llt_solve(RRt, r, qb, y)) {
+      double z[6];
+      for (int j = 0; j < n; ++j) {
+        double s = 0;
+        for (int i = 0; i < r; ++i)
+          if (j >= i) s += R1[i * n + j] * y[i];
+        z[j] = s;
+      }
+      for (int i = 0; i < n; ++i) x[perm[i]] = z[i];
+      double nb = 0, nax = 0, nd = 0;
+      for (int i = 0; i < n; ++i) {
+        double s = 0;
+        for (int k = 0; k < n; ++k) s += A[i * n + k] * x[k];
+        nb += b[i] * b[i];
+        nax += s * s;
+        nd += (b[i] - s) * (b[i] - s);
+      }
+      if (nd <= 1e-10 * (nb < nax ? nb : nax)) return 1;
+    }
+  }
+  double w[6], V[36];
+  jacobi_eig(A, n, w, V);
+  double wmax = 0;
+  for (int i = 0; i < n; ++i) wmax = fmax(wmax, fabs(w[i]));
+  double thr = wmax * (n * kDblEps);
+  if (thr < kDblMin) thr = kDblMin;
+  for (int i = 0; i < n; ++i) x[i] = 0;
+  for (int e = 0; e < n; ++e) {
+    if (fabs(w[e]) <= thr) continue;
+    double s = 0;
+    for (int k = 0; k < n; ++k) s += V[k * n + e] * b[k];
+    s /= w[e];
+    for (int k = 0; k < n; ++k) x[k] += V[k * n + e] * s;
+  }
+  return 2;
+}
+
+// SurfaceNormal: rank(fullPivQR(C)) + 1 >= 3 -> smallest eigenvector, else e_y.
+AICP_HD bool normal_from_cov(const double* C, float* nrm) {
+  PivQR qr;
+  pivqr(C, 3, qr);
+  if (qr.rank + 1 >= 3) {
+    double w[3], V[9];
+    jacobi_eig(C, 3, w, V);
+    int s = 0;
+    double sv = 1.79769313486231570e308;
+    for (int j = 0; j < 3; ++j)
+      if (w[j] < sv) {
+        sv = w[j];
+        s = j;
+      }
+    for (int r = 0; r < 3; ++r) nrm[r] = (float)V[r * 3 + s];
+    return false;
+  }
+  nrm[0] = 0.f;
+  nrm[1] = 1.f;
+  nrm[2] = 0.f;
+  return true;
+}
+
+// replaceRatioConfigFile text round trip for r in [0.1, 1): "%g" keeps 6 significant digits
+// = 1e-6 resolution; m = rint(r * 1e6) is exact in double and float(m / 1e6) is the
+// correctly rounded parse (no double-rounding hazard: m/1e6 is never within 2^-54 of a
+// float midpoint). tests/test_library_cpu.py checks it against snprintf + strtof.
+AICP_HD float quantize_ratio_fast(float r) {
+  const double m = rint((double)r * 1e6);
+  return (float)(m / 1e6);
+}
+
+AICP_HD float autotune_ratio_fast(float overlap_percent) {
+  float cur = (float)(overlap_percent / 100.0);
+  if (cur < 0.25)
+    cur = 0.25f;
+  else if (cur > 0.70)
+    cur = 0.70f;
+  if (cur != cur) return cur;
+  return quantize_ratio_fast(cur);
+}
+
+}  // namespace aicp

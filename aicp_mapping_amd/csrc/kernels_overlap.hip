@@ -1,0 +1,221 @@
+// kernels_overlap.hip — octree overlap of OctreesOverlap::computeOverlap on the device.
+//
+// Reference (aicp_core/src/overlap/octrees_overlap.cpp:29-72,113-241 + octomap):
+// each cloud's known-voxel set S = every key of computeRayKeys(origin, p) (Amanatides-Woo,
+// float direction, double tMax) plus every endpoint key; overlap% = min(|A∩B|/|A|,
+// |A∩B|/|B|) * 100. octomap stores S in an octree, prunes and expands it; only the set matters.
+//
+// Device form: one bit per voxel of the pair's padded key box (one bitmap per cloud),
+// each ray marks its keys with check-then-atomicOr, then popcounts give |A|, |B| and |A∩B|.
+// A 60 x 60 x 6 m scene at 0.2 m is ~2.7 M voxels = 340 KB per bitmap, so the sets stay
+// L2-resident while the rays are cast.
+#include <hip/hip_runtime.h>
+
+#include "aicp_common.hpp"
+#include "icp_math.hpp"
+#include "kernels.hpp"
+
+namespace aicp {
+
+constexpr int kTreeMaxVal = 32768;
+
+__device__ __forceinline__ bool key_checked(double rf, float c, int& key) {
+  const int sc = (int)floor(rf * (double)c) + kTreeMaxVal;
+  if (sc >= 0 && sc < 2 * kTreeMaxVal) {
+    key = sc;
+    return true;
+  }
+  return false;
+}
+
+__global__ void k_ovl_init(int n_pairs, const PairDesc* __restrict__ pd, PairState* st, double res) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  const double rf = 1.0 / res;
+  int lo[3] = {1 << 30, 1 << 30, 1 << 30}, hi[3] = {-(1 << 30), -(1 << 30), -(1 << 30)};
+  for (int side = 0; side < 2; ++side) {
+    const double* o = side ? pd[p].read_origin : pd[p].ref_origin;
+    int k[3];
+    bool ok = true;
+    for (int i = 0; i < 3; ++i) ok &= key_checked(rf, (float)o[i], k[i]);
+    if (!ok) continue;
+    for (int i = 0; i < 3; ++i) {
+      lo[i] = min(lo[i], k[i]);
+      hi[i] = max(hi[i], k[i]);
+    }
+  }
+  for (int i = 0; i < 3; ++i) {
+    st[p].ovl_bbox[i] = lo[i];
+    st[p].ovl_bbox[3 + i] = hi[i];
+    st[p].ovl_counts[i] = 0;
+  }
+  st[p].ovl_err = 0;
+}
+
+__global__ __launch_bounds__(256) void k_ovl_bbox(BlockMap m, const PairDesc* __restrict__ pd,
+                                                  PairState* st, const float4* __restrict__ pts,
+                                                  int side, double res) {
+  const int pair = m.pair[blockIdx.x];
+  const uint32_t j = m.start[blockIdx.x] + threadIdx.x;
+  const PairDesc& d = pd[pair];
+  const uint32_t n = side ? d.n_read : d.n_ref;
+  const uint32_t off = side ? d.read_off : d.ref_off;
+  const double rf = 1.0 / res;
+  int lo[3] = {1 << 30, 1 << 30, 1 << 30}, hi[3] = {-(1 << 30), -(1 << 30), -(1 << 30)};
+  if (j < n) {
+    const float4 p = pts[off + j];
+    int k[3];
+    if (key_checked(rf, p.x, k[0]) && key_checked(rf, p.y, k[1]) && key_checked(rf, p.z, k[2]))
+      for (int i = 0; i < 3; ++i) lo[i] = hi[i] = k[i];
+  }
+  for (int i = 0; i < 3; ++i) {
+    int a = lo[i], b = hi[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a = min(a, __shfl_xor(a, o, 64));
+      b = max(b, __shfl_xor(b, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0 && a <= b) {
+      atomicMin(&st[pair].ovl_bbox[i], a);
+      atomicMax(&st[pair].ovl_bbox[3 + i], b);
+    }
+  }
+}
+
+// computeRayKeys(origin, end) + endpoint key, marking bits of one bitmap.
+__global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __restrict__ pd,
+                                                  PairState* st, const float4* __restrict__ pts,
+                                                  int side, double res, uint32_t* bitmap) {
+  const int pair = m.pair[blockIdx.x];
+  const uint32_t j = m.start[blockIdx.x] + threadIdx.x;
+  const PairDesc& d = pd[pair];
+  const uint32_t n = side ? d.n_read : d.n_ref;
+  if (j >= n) return;
+  const uint32_t off = side ? d.read_off : d.ref_off;
+  uint32_t* bm = bitmap + d.ovl_word_off + (side ? d.ovl_words : 0);
+  const int mn0 = d.ovl_min[0], mn1 = d.ovl_min[1], mn2 = d.ovl_min[2];
+  const int dm0 = d.ovl_dim[0], dm1 = d.ovl_dim[1], dm2 = d.ovl_dim[2];
+  bool err = false;
+  auto mark = [&](int k0, int k1, int k2) {
+    const int a = k0 - mn0, b = k1 - mn1, c = k2 - mn2;
+    if ((unsigned)a >= (unsigned)dm0 || (unsigned)b >= (unsigned)dm1 || (unsigned)c >= (unsigned)dm2) {
+      err = true;
+      return;
+    }
+    const uint64_t idx = ((uint64_t)a * (uint64_t)dm1 + (uint64_t)b) * (uint64_t)dm2 + (uint64_t)c;
+    const uint32_t bit = 1u << (idx & 31);
+    uint32_t* w = bm + (idx >> 5);
+    if (!(*(volatile uint32_t*)w & bit)) atomicOr(w, bit);  // stale read -> one extra OR
+  };
+  const double* od = side ? d.read_origin : d.ref_origin;
+  const float o[3] = {(float)od[0], (float)od[1], (float)od[2]};
+  const float4 p4 = pts[off + j];
+  const float e[3] = {p4.x, p4.y, p4.z};
+  const double rf = 1.0 / res;
+  int ko[3], ke[3];
+  const bool okO = key_checked(rf, o[0], ko[0]) && key_checked(rf, o[1], ko[1]) &&
+                   key_checked(rf, o[2], ko[2]);
+  const bool okE = key_checked(rf, e[0], ke[0]) && key_checked(rf, e[1], ke[1]) &&
+                   key_checked(rf, e[2], ke[2]);
+  if (okO && okE && !(ko[0] == ke[0] && ko[1] == ke[1] && ko[2] == ke[2])) {
+    mark(ko[0], ko[1], ko[2]);
+    float dir[3] = {e[0] - o[0], e[1] - o[1], e[2] - o[2]};
+    const float nsq = dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2];
+    const float length = (float)sqrt((double)nsq);
+    for (int i = 0; i < 3; ++i) dir[i] /= length;
+    int step[3];
+    double tMax[3], tDelta[3];
+    int cur[3] = {ko[0], ko[1], ko[2]};
+    for (int i = 0; i < 3; ++i) {
+      step[i] = dir[i] > 0.0f ? 1 : (dir[i] < 0.0f ? -1 : 0);
+      if (step[i] != 0) {
+        double vb = (double(cur[i] - kTreeMaxVal) + 0.5) * res;
+        vb += (float)(step[i] * res * 0.5);
+        tMax[i] = (vb - (double)o[i]) / (double)dir[i];
+        tDelta[i] = res / (double)fabsf(dir[i]);
+      } else {
+        tMax[i] = 1.7976931348623157e308;
+        tDelta[i] = 1.7976931348623157e308;
+      }
+    }
+    const double len = (double)length;
+    for (;;) {
+      int dim;
+      if (tMax[0] < tMax[1])
+        dim = (tMax[0] < tMax[2]) ? 0 : 2;
+      else
+        dim = (tMax[1] < tMax[2]) ? 1 : 2;
+      cur[dim] = (cur[dim] + step[dim]) & 0xFFFF;
+      tMax[dim] += tDelta[dim];
+      if (cur[0] == ke[0] && cur[1] == ke[1] && cur[2] == ke[2]) break;
+      const double dfo = fmin(fmin(tMax[0], tMax[1]), tMax[2]);
+      if (dfo > len) break;
+      mark(cur[0], cur[1], cur[2]);
+    }
+  }
+  if (okE) mark(ke[0], ke[1], ke[2]);
+  if (err) atomicOr(&st[pair].ovl_err, 1);
+}
+
+// popcounts: |A|, |B|, |A & B| (64 workgroups per pair, integer atomics -> deterministic)
+constexpr int kCountBlocksPerPair = 64;
+__global__ __launch_bounds__(256) void k_ovl_count(const PairDesc* __restrict__ pd, PairState* st,
+                                                   const uint32_t* __restrict__ bitmap) {
+  const int pair = blockIdx.x / kCountBlocksPerPair;
+  const int sub = blockIdx.x % kCountBlocksPerPair;
+  const PairDesc& d = pd[pair];
+  const uint32_t* A = bitmap + d.ovl_word_off;
+  const uint32_t* B = A + d.ovl_words;
+  unsigned long long ca = 0, cb = 0, cab = 0;
+  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < d.ovl_words;
+       w += (uint64_t)kCountBlocksPerPair * 256) {
+    const uint32_t a = A[w], b = B[w];
+    ca += __popc(a);
+    cb += __popc(b);
+    cab += __popc(a & b);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ca += __shfl_xor(ca, o, 64);
+    cb += __shfl_xor(cb, o, 64);
+    cab += __shfl_xor(cab, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd((unsigned long long*)&st[pair].ovl_counts[0], ca);
+    atomicAdd((unsigned long long*)&st[pair].ovl_counts[1], cb);
+    atomicAdd((unsigned long long*)&st[pair].ovl_counts[2], cab);
+  }
+}
+
+__global__ void k_ovl_finish(int n_pairs, PairState* st, int set_ratio) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  PairState& s = st[p];
+  const float ov = (float)s.ovl_counts[2];
+  const float a = ov / (float)s.ovl_counts[0];
+  const float b = ov / (float)s.ovl_counts[1];
+  const float mn = (b < a) ? b : a;  // std::min
+  s.overlap = (float)(mn * 100.0);
+  if (set_ratio) s.ratio = autotune_ratio_fast(s.overlap);
+}
+
+void launch_ovl_init(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, double res) {
+  k_ovl_init<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, res);
+}
+void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
+                     const float4* pts, int side, double res) {
+  if (m.n_blocks) k_ovl_bbox<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res);
+}
+void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
+                     const float4* pts, int side, double res, uint32_t* bitmap) {
+  if (m.n_blocks) k_ovl_mark<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res, bitmap);
+}
+void launch_ovl_count(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
+                      const uint32_t* bitmap) {
+  k_ovl_count<<<n_pairs * kCountBlocksPerPair, 256, 0, s>>>(pd, st, bitmap);
+}
+void launch_ovl_finish(hipStream_t s, int n_pairs, PairState* st, int set_ratio) {
+  k_ovl_finish<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, st, set_ratio);
+}
+
+}  // namespace aicp
