@@ -6,10 +6,11 @@
 //   ref_raw   float4[ΣM]  reference xyz as given (overlap input)
 //   bpts      float4[ΣM]  centred reference points in kd-tree bucket order, w = input id bits
 //   bnrm      float4[ΣM]  SurfaceNormal normals in bucket order (w = 0)
-//   nodes     uint2[ΣW]   kd-tree nodes, preorder (left child = n + 1):
-//                           inner: x = cut (float bits), y = cd | right << 2
-//                           leaf : x = bucket count,     y = 3  | bucket_start << 2
-//   parent    int32[ΣW]   parent node (-1 at the root), used to climb after a leaf
+//   nodes     uint4[ΣW]   kd-tree node records, preorder (left child = n + 1):
+//                           inner: x = cut (float bits), y = cd | right << 2, z = parent
+//                           leaf : x = bucket count,     y = 3  | bucket_start << 2, z = parent
+//                         (16 B: a node record and a bucket point load with one instruction)
+//   parent    int32[ΣW]   parent node (-1 at the root), used by the kNN (normals) climb
 //   match     int32[ΣN]   bucket position of the NN of each reading point
 //   d2        float[ΣN]   squared NN distance
 // Bucket positions are local to the pair (ref_off added by the kernels).
@@ -22,10 +23,23 @@ constexpr int kHistBins = 2048;     // radix-select digit 1/2 (11 bits)
 constexpr int kHist3Bins = 1024;    // digit 3 (10 bits)
 constexpr int kNNBlock = 256;       // NN / reduce kernel block
 constexpr int kReducePerThread = 4; // reading points per thread in the reduce kernel
-constexpr int kRedCols = 28;        // 21 unique A entries + 6 b + kept count
+constexpr int kRedCols = 30;        // 21 unique A entries + 6 b + kept + NN touch counts (2)
 constexpr int kFarStack = 48;       // max nested far descents (= max tree depth supported)
 constexpr int kHistRing = 32;       // differential checker history ring
 constexpr uint32_t kLeaf = 3;
+constexpr int kMaxPairs = 4096;     // pairs per batch
+constexpr int kXcdGroups = 8;       // work groups of the persistent kernels (one per XCD)
+constexpr int kCtrStride = 16;      // words between the per-group work counters (64 B)
+constexpr int kCtrWords = 2 * kXcdGroups * kCtrStride;  // ICP NN counters, then normals kNN
+
+// Compacted list of the pairs still iterating (k_active_list), consumed by the persistent
+// NN kernel: slot s of the work space belongs to pair[e] with off[e] <= s < off[e+1].
+struct ActiveList {
+  uint32_t n;
+  uint32_t total;
+  uint32_t off[kMaxPairs + 1];
+  int32_t pair[kMaxPairs];
+};
 
 struct PairDesc {
   uint32_t ref_off, n_ref;      // into ref arrays (ref_raw, bpts, bnrm)
@@ -37,11 +51,11 @@ struct PairDesc {
   float mean[3];                // reference centroid (float)
   float ratio;                  // configured trimmed ratio (overridden by overlap)
   int32_t tree_depth;
-  // overlap bitmaps (AICP_RUN_OVERLAP): one bit per 0.2 m voxel of the padded key box
+  // overlap voxel maps (AICP_RUN_OVERLAP): one byte per voxel of the padded key box
   int32_t ovl_min[3];           // key of voxel (0,0,0)
   int32_t ovl_dim[3];           // box extent in voxels
-  uint64_t ovl_word_off;        // into the bitmap arena (ref bitmap, then read bitmap)
-  uint64_t ovl_words;           // 32-bit words per bitmap
+  uint64_t ovl_word_off;        // byte offset into the map arena (ref map, then read map)
+  uint64_t ovl_words;           // bytes per map (multiple of 16)
   double ref_origin[3], read_origin[3];
 };
 
@@ -59,7 +73,7 @@ struct PairState {
   int32_t degenerate;
   float inlier_ratio;
   float overlap;        // percent, -1 if not computed
-  uint64_t touched_pts, touched_nodes;
+  uint64_t touched_pts, touched_nodes;  // libnabo PointCountTouched / inner nodes, all iterations
   uint64_t ovl_counts[3];
   int32_t ovl_bbox[6];  // kmin[3], kmax[3] (union of both clouds)
   int32_t ovl_err;

@@ -4,7 +4,7 @@
 //   1. [device] overlap: origin/endpoint key boxes (k_ovl_init, k_ovl_bbox) -> async D2H
 //   2. [host, overlapped with 1] per pair: centroid, centred reference, libnabo-order kd-tree
 //      (ICP::compute "matcher->init(reference)"), one std::thread per pair up to 16
-//   3. [device] bitmaps sized from the boxes; DDA ray marking, popcounts, overlap% and the
+//   3. [device] voxel maps sized from the boxes; DDA ray marking, sums, overlap% and the
 //      auto-tuned ratio per pair (App::computeRegistration, app.cpp:197-205)
 //   4. [device] gather centred reference into bucket order, reading into the ref-mean
 //      frame, SurfaceNormal on the reference (k_normals)
@@ -109,8 +109,8 @@ struct aicp_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf read_c, bpts, bnrm, nodes, parent, perm, match, d2, desc, state, hist, slab, bitmap,
-      outT, scratch;
+  DevBuf read_c, bpts, bnrm, nodes, parent, perm, match, d2, desc, state, touch, slab, bitmap,
+      outT, scratch, active, ctrs, nbids;
   PinBuf pin_desc, pin_tree, pin_state, pin_out, pin_io;
   std::vector<HostTree> trees;
   std::vector<hipEvent_t> nn_ev;
@@ -322,20 +322,23 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   for (auto& d : desc) d.ratio = cfg->trimmed_ratio;
   HIPC(ensure(ctx->desc, P * sizeof(PairDesc)));
   HIPC(ensure(ctx->state, P * sizeof(PairState)));
-  HIPC(ensure(ctx->hist, P * kHistBins * 4));
-  HIPC(ensure(ctx->pin_desc, 2 * P * sizeof(PairDesc)));
+  if (P > (size_t)kMaxPairs) FAIL(AICP_ERR_UNSUPPORTED, "more than 4096 pairs in one batch");
+  HIPC(ensure(ctx->active, sizeof(ActiveList)));
+  HIPC(ensure(ctx->ctrs, kCtrWords * 4));
+  HIPC(ensure(ctx->pin_desc, 3 * P * sizeof(PairDesc)));
   HIPC(ensure(ctx->pin_state, P * sizeof(PairState)));
   HIPC(ensure(ctx->outT, P * 64));
   HIPC(ensure(ctx->pin_out, P * 64));
   PairDesc* pdA = ctx->pin_desc.as<PairDesc>();
   PairDesc* pdB = pdA + P;
+  PairDesc* pdC = pdB + P;
   PairDesc* dDesc = ctx->desc.as<PairDesc>();
   PairState* dState = ctx->state.as<PairState>();
-  uint32_t* dHist = ctx->hist.as<uint32_t>();
+  uint32_t* dCtr = ctx->ctrs.as<uint32_t>();
   std::memcpy(pdA, desc.data(), P * sizeof(PairDesc));
   HIPC(hipEventRecord(ctx->ev[0], s));
   HIPC(hipMemcpyAsync(dDesc, pdA, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
-  launch_init_state(s, (int)P, dDesc, dState, dHist);
+  launch_init_state(s, (int)P, dDesc, dState);
   if (doOvl) {
     launch_ovl_init(s, (int)P, dDesc, dState, res);
     launch_ovl_bbox(s, B->m_ref, dDesc, dState, B->ref_raw.as<float4>(), 0, res);
@@ -343,6 +346,39 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
   }
   HIPC(hipEventRecord(ctx->ev[1], s));
+  // overlap: size the voxel maps from the key boxes, then mark (device) while the host builds
+  // the kd-trees
+  uint64_t bm_bytes = 0;
+  if (doOvl) {
+    HIPC(hipEventSynchronize(ctx->ev[1]));
+    const PairState* hs = ctx->pin_state.as<PairState>();
+    for (size_t i = 0; i < P; ++i) {
+      PairDesc& d = desc[i];
+      uint64_t vox = 1;
+      for (int k = 0; k < 3; ++k) {
+        int lo = hs[i].ovl_bbox[k], hi = hs[i].ovl_bbox[3 + k];
+        if (lo > hi) lo = hi = 0;  // nothing inside the key range
+        d.ovl_min[k] = lo - 2;
+        d.ovl_dim[k] = (hi - lo) + 5;
+        vox *= (uint64_t)d.ovl_dim[k];
+      }
+      if (vox > (1ull << 34)) FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
+      d.ovl_words = (vox + 15) / 16 * 16;
+      d.ovl_word_off = bm_bytes;
+      bm_bytes += 2 * d.ovl_words;
+    }
+    HIPC(ensure(ctx->bitmap, bm_bytes));
+    std::memcpy(pdB, desc.data(), P * sizeof(PairDesc));
+    HIPC(hipMemcpyAsync(dDesc, pdB, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+    HIPC(hipEventRecord(ctx->ev[6], s));
+    uint8_t* bm = ctx->bitmap.as<uint8_t>();
+    HIPC(hipMemsetAsync(bm, 0, bm_bytes, s));
+    launch_ovl_mark(s, B->m_ref, dDesc, dState, B->ref_raw.as<float4>(), 0, res, bm);
+    launch_ovl_mark(s, B->m_read, dDesc, dState, B->read_raw.as<float4>(), 1, res, bm);
+    launch_ovl_count(s, (int)P, dDesc, dState, bm);
+    launch_ovl_finish(s, (int)P, dState, doIcp ? 1 : 0);
+  }
+  HIPC(hipEventRecord(ctx->ev[2], s));
   // host: kd-trees (overlaps the device work above)
   std::vector<float> means;
   double tree_ms = 0;
@@ -371,33 +407,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       mul4(Tmi, &B->initT[16 * i], d.Tinit);
     }
     if (total_nodes >= (1ull << 30)) FAIL(AICP_ERR_UNSUPPORTED, "too many kd-tree nodes");
-  }
-  uint64_t bm_words = 0;
-  if (doOvl) {
-    HIPC(hipEventSynchronize(ctx->ev[1]));
-    const PairState* hs = ctx->pin_state.as<PairState>();
-    for (size_t i = 0; i < P; ++i) {
-      PairDesc& d = desc[i];
-      uint64_t vox = 1;
-      for (int k = 0; k < 3; ++k) {
-        int lo = hs[i].ovl_bbox[k], hi = hs[i].ovl_bbox[3 + k];
-        if (lo > hi) lo = hi = 0;  // nothing inside the key range
-        d.ovl_min[k] = lo - 2;
-        d.ovl_dim[k] = (hi - lo) + 5;
-        vox *= (uint64_t)d.ovl_dim[k];
-      }
-      if (vox > (1ull << 36)) FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the bitmap grid");
-      d.ovl_words = (vox + 31) / 32;
-      d.ovl_word_off = bm_words;
-      bm_words += 2 * d.ovl_words;
-    }
-    HIPC(ensure(ctx->bitmap, bm_words * 4));
-  }
-  // second descriptor upload + kd-trees
-  std::memcpy(pdB, desc.data(), P * sizeof(PairDesc));
-  HIPC(hipMemcpyAsync(dDesc, pdB, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
-  if (doIcp) {
-    const size_t permB = B->total_ref * 4, nodeB = total_nodes * 8, parB = total_nodes * 4;
+    // full descriptor + kd-trees
+    std::memcpy(pdC, desc.data(), P * sizeof(PairDesc));
+    HIPC(hipMemcpyAsync(dDesc, pdC, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+    const size_t permB = B->total_ref * 4, nodeB = total_nodes * 16, parB = total_nodes * 4;
     HIPC(ensure(ctx->pin_tree, permB + nodeB + parB));
     HIPC(ensure(ctx->perm, permB));
     HIPC(ensure(ctx->nodes, nodeB));
@@ -407,21 +420,12 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       const HostTree& t = ctx->trees[i];
       const PairDesc& d = desc[i];
       std::memcpy(base + 4ull * d.ref_off, t.perm.data(), 4ull * d.n_ref);
-      std::memcpy(base + permB + 8ull * d.node_off, t.nodes.data(), 8ull * d.n_nodes);
+      std::memcpy(base + permB + 16ull * d.node_off, t.nodes.data(), 16ull * d.n_nodes);
       std::memcpy(base + permB + nodeB + 4ull * d.node_off, t.parent.data(), 4ull * d.n_nodes);
     }
     HIPC(hipMemcpyAsync(ctx->perm.p, base, permB, hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(ctx->nodes.p, base + permB, nodeB, hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(ctx->parent.p, base + permB + nodeB, parB, hipMemcpyHostToDevice, s));
-  }
-  HIPC(hipEventRecord(ctx->ev[2], s));
-  if (doOvl) {
-    uint32_t* bm = ctx->bitmap.as<uint32_t>();
-    HIPC(hipMemsetAsync(bm, 0, bm_words * 4, s));
-    launch_ovl_mark(s, B->m_ref, dDesc, dState, B->ref_raw.as<float4>(), 0, res, bm);
-    launch_ovl_mark(s, B->m_read, dDesc, dState, B->read_raw.as<float4>(), 1, res, bm);
-    launch_ovl_count(s, (int)P, dDesc, dState, bm);
-    launch_ovl_finish(s, (int)P, dState, doIcp ? 1 : 0);
   }
   HIPC(hipEventRecord(ctx->ev[3], s));
   IcpParams prm{};
@@ -432,15 +436,20 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(ensure(ctx->bnrm, B->total_ref * 16));
     HIPC(ensure(ctx->match, B->total_read * 4));
     HIPC(ensure(ctx->d2, B->total_read * 4));
+    HIPC(ensure(ctx->touch, B->total_read * 4));
     HIPC(ensure(ctx->slab, (size_t)B->n_red_total * kRedCols * 8));
     float4* bpts = ctx->bpts.as<float4>();
     float4* bnrm = ctx->bnrm.as<float4>();
     float4* readc = ctx->read_c.as<float4>();
-    const uint2* nodes = ctx->nodes.as<uint2>();
+    const uint4* nodes = ctx->nodes.as<uint4>();
     const int32_t* parent = ctx->parent.as<int32_t>();
     launch_gather_ref(s, B->m_ref, dDesc, B->ref_raw.as<float4>(), ctx->perm.as<int32_t>(), bpts);
     launch_prepare_read(s, B->m_read, dDesc, B->read_raw.as<float4>(), readc);
-    if (!launch_normals(s, B->m_ref, dDesc, dState, nodes, parent, bpts, bnrm, cfg->knn_normals))
+    HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
+    uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
+    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s));
+    if (!launch_normals(s, (int)P, (uint32_t)B->total_ref, dDesc, dState, nodes, parent, bpts, bnrm,
+                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
     HIPC(hipEventRecord(ctx->ev[4], s));
     prm.maxE2 = (1 + cfg->nn_epsilon) * (1 + cfg->nn_epsilon);
@@ -450,16 +459,18 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     prm.min_rot = cfg->min_diff_rot;
     prm.min_trans = cfg->min_diff_trans;
     prm.knn_normals = cfg->knn_normals;
+    ActiveList* dAl = ctx->active.as<ActiveList>();
     for (int it = 0; it < cfg->max_iter; ++it) {
+      launch_active_list(s, (int)P, dDesc, dState, dAl, dCtr);
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it], s));
-      launch_icp_nn(s, B->m_read, dDesc, dState, readc, nodes, parent, bpts, ctx->match.as<int32_t>(),
-                    ctx->d2.as<float>(), dHist, prm);
+      launch_icp_nn(s, (int)B->total_read, dDesc, dState, dAl, readc, nodes, parent, bpts,
+                    ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm);
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it + 1], s));
       ++nn_launches;
-      launch_icp_select(s, (int)P, dDesc, dState, ctx->d2.as<float>(), dHist);
+      launch_icp_select(s, (int)P, dDesc, dState, ctx->d2.as<float>());
       launch_icp_reduce(s, B->m_red, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
-                        bpts, bnrm, ctx->slab.as<double>());
-      launch_icp_update(s, (int)P, dDesc, dState, ctx->slab.as<double>(), dHist, prm);
+                        ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>());
+      launch_icp_update(s, (int)P, dDesc, dState, ctx->slab.as<double>(), prm);
     }
     launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
   } else {
@@ -482,8 +493,9 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     if (outT && doIcp) std::memcpy(outT + 16 * i, ctx->pin_out.as<float>() + 16 * i, 64);
     if (out_overlap) out_overlap[i] = st.overlap;
     queries += (uint64_t)st.iters * desc[i].n_read;
-    tp += st.touched_pts;
-    tn += st.touched_nodes;
+    const uint64_t ptp = st.touched_pts, ptn = st.touched_nodes;
+    tp += ptp;
+    tn += ptn;
     if (stats) {
       aicp_icp_stats& o = stats[i];
       std::memset(&o, 0, sizeof(o));
@@ -495,8 +507,8 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       o.trimmed_ratio = st.ratio;
       o.overlap_percent = st.overlap;
       o.tree_depth = desc[i].tree_depth;
-      o.nn_points_touched = st.touched_pts;
-      o.nn_nodes_touched = st.touched_nodes;
+      o.nn_points_touched = ptp;
+      o.nn_nodes_touched = ptn;
       for (int k = 0; k < 3; ++k) o.overlap_keys[k] = st.ovl_counts[k];
     }
   }
@@ -507,7 +519,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   // N*(12 B query + 8 B id/d2) + V*16 B + W*8 B
   ctx->last_nn_bytes = (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0;
   ctx->last_queries = queries;
-  ctx->last_phase[0] = doOvl ? ev_ms(ctx->ev[0], ctx->ev[1]) + ev_ms(ctx->ev[2], ctx->ev[3]) : 0;
+  ctx->last_phase[0] = doOvl ? ev_ms(ctx->ev[0], ctx->ev[1]) + ev_ms(ctx->ev[6], ctx->ev[2]) : 0;
   ctx->last_phase[1] = tree_ms;
   ctx->last_phase[2] = doIcp ? ev_ms(ctx->ev[3], ctx->ev[4]) : 0;
   ctx->last_phase[3] = doIcp ? ev_ms(ctx->ev[4], ctx->ev[5]) : 0;
@@ -532,9 +544,9 @@ int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, Ho
   build_kdtree_host(xyz.data(), (int64_t)n, 8, t);
   if (t.depth >= kFarStack) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack");
   HIPC(ensure(ctx->bpts, n * 16));
-  HIPC(ensure(ctx->nodes, t.parent.size() * 8));
+  HIPC(ensure(ctx->nodes, t.parent.size() * 16));
   HIPC(ensure(ctx->parent, t.parent.size() * 4));
-  HIPC(ensure(ctx->pin_io, std::max(n * 16, t.parent.size() * 8)));
+  HIPC(ensure(ctx->pin_io, std::max(n * 16, t.parent.size() * 16)));
   float* b = ctx->pin_io.as<float>();
   for (size_t j = 0; j < n; ++j) {
     const int32_t id = t.perm[j];
@@ -543,9 +555,10 @@ int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, Ho
     b[4 * j + 2] = xyz[3 * id + 2];
     std::memcpy(&b[4 * j + 3], &id, 4);
   }
-  HIPC(hipMemcpy(ctx->bpts.p, b, n * 16, hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->nodes.p, t.nodes.data(), t.parent.size() * 8, hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->parent.p, t.parent.data(), t.parent.size() * 4, hipMemcpyHostToDevice));
+  HIPC(hipMemcpyAsync(ctx->bpts.p, b, n * 16, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(hipMemcpyAsync(ctx->nodes.p, t.nodes.data(), t.parent.size() * 16, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(hipMemcpyAsync(ctx->parent.p, t.parent.data(), t.parent.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
   return AICP_OK;
 }
 
@@ -577,8 +590,8 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->parent, &ctx->perm, &ctx->match,
-                    &ctx->d2, &ctx->desc, &ctx->state, &ctx->hist, &ctx->slab, &ctx->bitmap, &ctx->outT,
-                    &ctx->scratch})
+                    &ctx->d2, &ctx->desc, &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT,
+                    &ctx->scratch, &ctx->active, &ctx->ctrs, &ctx->nbids})
     release(*b);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_tree, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io}) release(*b);
   for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
@@ -699,23 +712,25 @@ int aicp_hip_knn(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, c
   HostTree t;
   int rc = upload_tree(ctx, pts, n, stride, t);
   if (rc) return rc;
+  hipStream_t st_ = ctx->stream;
   HIPC(ensure(ctx->read_c, nq * 16 + 16));
   HIPC(ensure(ctx->match, nq * (size_t)k * 4 + 4));
   HIPC(ensure(ctx->d2, nq * (size_t)k * 4 + 4));
-  HIPC(ensure(ctx->scratch, 16));
+  HIPC(ensure(ctx->scratch, 16 + kCtrWords * 4));
   HIPC(ensure(ctx->pin_io, std::max<size_t>(nq * 16, nq * (size_t)k * 4) + 16));
   float* h = ctx->pin_io.as<float>();
   pack_xyz4(queries, nq, qstride, h);
-  HIPC(hipMemcpy(ctx->read_c.p, h, nq * 16, hipMemcpyHostToDevice));
-  HIPC(hipMemset(ctx->scratch.p, 0, 16));
+  HIPC(hipMemcpyAsync(ctx->read_c.p, h, nq * 16, hipMemcpyHostToDevice, st_));
+  HIPC(hipMemsetAsync(ctx->scratch.p, 0, 16 + kCtrWords * 4, st_));
   const float maxE2 = (1 + epsilon) * (1 + epsilon);
   const float maxR2 = max_dist * max_dist;
-  if (!launch_knn_generic(ctx->stream, (int)nq, ctx->read_c.as<float4>(), ctx->nodes.as<uint2>(),
+  if (!launch_knn_generic(st_, (uint32_t)nq, ctx->read_c.as<float4>(), ctx->nodes.as<uint4>(),
                           ctx->parent.as<int32_t>(), ctx->bpts.as<float4>(), k, maxE2, maxR2,
-                          ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->scratch.as<unsigned long long>()))
+                          ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->scratch.as<unsigned long long>(),
+                          (uint32_t*)(ctx->scratch.as<char>() + 16)))
     FAIL(AICP_ERR_UNSUPPORTED, "k must be 1, 4, 10, 20 or 30");
   HIPC(hipGetLastError());
-  HIPC(hipStreamSynchronize(ctx->stream));
+  HIPC(hipStreamSynchronize(st_));
   HIPC(hipMemcpy(out_ids, ctx->match.p, nq * (size_t)k * 4, hipMemcpyDeviceToHost));
   HIPC(hipMemcpy(out_d2, ctx->d2.p, nq * (size_t)k * 4, hipMemcpyDeviceToHost));
   if (out_touched) HIPC(hipMemcpy(out_touched, ctx->scratch.p, 16, hipMemcpyDeviceToHost));
@@ -729,29 +744,25 @@ int aicp_hip_normals(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t strid
   HostTree t;
   int rc = upload_tree(ctx, pts, n, stride, t);
   if (rc) return rc;
+  hipStream_t st_ = ctx->stream;
   PairDesc d{};
   d.n_ref = (uint32_t)n;
   d.n_nodes = (uint32_t)t.parent.size();
   d.ratio = 0.5f;
-  Maps mf;
-  mf.add(0, (uint32_t)n, kNNBlock);
   HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(ensure(ctx->state, sizeof(PairState)));
-  HIPC(ensure(ctx->hist, kHistBins * 4));
   HIPC(ensure(ctx->bnrm, n * 16));
-  HIPC(ensure(ctx->scratch, mf.pair.size() * 8));
-  HIPC(hipMemcpy(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->scratch.p, mf.pair.data(), mf.pair.size() * 4, hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->scratch.as<char>() + mf.pair.size() * 4, mf.start.data(), mf.pair.size() * 4,
-                 hipMemcpyHostToDevice));
-  BlockMap m{ctx->scratch.as<int32_t>(), (const uint32_t*)(ctx->scratch.as<char>() + mf.pair.size() * 4),
-             (uint32_t)mf.pair.size()};
-  launch_init_state(ctx->stream, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->hist.as<uint32_t>());
-  if (!launch_normals(ctx->stream, m, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->nodes.as<uint2>(),
-                      ctx->parent.as<int32_t>(), ctx->bpts.as<float4>(), ctx->bnrm.as<float4>(), knn))
+  HIPC(ensure(ctx->nbids, n * 4 * (size_t)std::max(knn, 1)));
+  HIPC(ensure(ctx->ctrs, kCtrWords * 4));
+  HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, st_));
+  HIPC(hipMemsetAsync(ctx->ctrs.p, 0, kCtrWords * 4, st_));
+  launch_init_state(st_, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>());
+  if (!launch_normals(st_, 1, (uint32_t)n, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(),
+                      ctx->nodes.as<uint4>(), ctx->parent.as<int32_t>(), ctx->bpts.as<float4>(),
+                      ctx->bnrm.as<float4>(), knn, ctx->nbids.as<int32_t>(), ctx->ctrs.as<uint32_t>()))
     FAIL(AICP_ERR_UNSUPPORTED, "knn must be 10, 20 or 30");
   HIPC(hipGetLastError());
-  HIPC(hipStreamSynchronize(ctx->stream));
+  HIPC(hipStreamSynchronize(st_));
   std::vector<float> nb(4 * n);
   HIPC(hipMemcpy(nb.data(), ctx->bnrm.p, n * 16, hipMemcpyDeviceToHost));
   PairState st;
@@ -766,29 +777,21 @@ int aicp_hip_dists_quantile(aicp_hip_ctx* ctx, const float* d2, size_t n, float 
   if (!ctx || !d2 || !out_limit || n == 0 || n >= (1ull << 31)) return AICP_ERR_INVALID;
   if (!(quantile >= 0.f && quantile <= 1.f)) return AICP_ERR_INVALID;  // "quantile must be between 0 and 1"
   HIPC(hipSetDevice(ctx->device));
+  hipStream_t st_ = ctx->stream;
   PairDesc d{};
   d.n_read = (uint32_t)n;
   d.ratio = quantile;
-  Maps mr;
-  mr.add(0, (uint32_t)n, kNNBlock);
   HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(ensure(ctx->state, sizeof(PairState)));
-  HIPC(ensure(ctx->hist, kHistBins * 4));
   HIPC(ensure(ctx->d2, n * 4));
-  HIPC(ensure(ctx->scratch, mr.pair.size() * 8));
-  HIPC(hipMemcpy(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->d2.p, d2, n * 4, hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->scratch.p, mr.pair.data(), mr.pair.size() * 4, hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->scratch.as<char>() + mr.pair.size() * 4, mr.start.data(), mr.pair.size() * 4,
-                 hipMemcpyHostToDevice));
-  BlockMap m{ctx->scratch.as<int32_t>(), (const uint32_t*)(ctx->scratch.as<char>() + mr.pair.size() * 4),
-             (uint32_t)mr.pair.size()};
-  launch_init_state(ctx->stream, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->hist.as<uint32_t>());
-  launch_hist_d2(ctx->stream, m, ctx->desc.as<PairDesc>(), ctx->d2.as<float>(), ctx->hist.as<uint32_t>());
-  launch_icp_select(ctx->stream, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->d2.as<float>(),
-                    ctx->hist.as<uint32_t>());
+  HIPC(ensure(ctx->pin_io, n * 4));
+  std::memcpy(ctx->pin_io.p, d2, n * 4);
+  HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, st_));
+  HIPC(hipMemcpyAsync(ctx->d2.p, ctx->pin_io.p, n * 4, hipMemcpyHostToDevice, st_));
+  launch_init_state(st_, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>());
+  launch_icp_select(st_, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->d2.as<float>());
   HIPC(hipGetLastError());
-  HIPC(hipStreamSynchronize(ctx->stream));
+  HIPC(hipStreamSynchronize(st_));
   PairState st;
   HIPC(hipMemcpy(&st, ctx->state.p, sizeof(st), hipMemcpyDeviceToHost));
   if (st.status) FAIL(st.status, "no outlier to filter");

@@ -22,6 +22,8 @@ struct Builder {
     const int32_t pos = (int32_t)t.parent.size();
     t.nodes.push_back(x);
     t.nodes.push_back(y);
+    t.nodes.push_back((uint32_t)par);
+    t.nodes.push_back(0u);
     t.parent.push_back(par);
     return pos;
   }
@@ -86,7 +88,7 @@ struct Builder {
     rmn[cd] = cut;
     build(first, first + left, mn, lmx, me, depth + 1);
     const int32_t right = build(first + left, last, rmn, mx, me, depth + 1);
-    t.nodes[2 * me + 1] = (uint32_t)cd | ((uint32_t)right << 2);
+    t.nodes[4 * me + 1] = (uint32_t)cd | ((uint32_t)right << 2);
     return me;
   }
 };
@@ -113,7 +115,7 @@ void build_kdtree_host(const float* xyz, int64_t n, int bucket, HostTree& out) {
   out.parent.clear();
   out.perm.clear();
   out.depth = 0;
-  out.nodes.reserve((size_t)(n / std::max(1, bucket / 2) + 4) * 2);
+  out.nodes.reserve((size_t)(n / std::max(1, bucket / 2) + 4) * 4);
   out.parent.reserve((size_t)(n / std::max(1, bucket / 2) + 4));
   out.perm.reserve((size_t)n);
   Builder b{pts, out, bucket};

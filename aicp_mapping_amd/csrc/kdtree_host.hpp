@@ -12,7 +12,7 @@
 namespace aicp {
 
 struct HostTree {
-  std::vector<uint32_t> nodes;   // 2 words per node (see aicp_common.hpp)
+  std::vector<uint32_t> nodes;   // 4 words per node (see aicp_common.hpp)
   std::vector<int32_t> parent;   // per node
   std::vector<int32_t> perm;     // bucket position -> input index
   int32_t depth = 0;

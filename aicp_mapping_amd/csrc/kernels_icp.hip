@@ -1,18 +1,24 @@
 // kernels_icp.hip — ICP hot path on CDNA4 (gfx950).
 //
 // Per ICP iteration (libpointmatcher ICP loop), for every pair of a
-// batch at once, four launches and no host synchronisation:
-//   k_icp_nn      transform (T_iter, fused) + libnabo-order approximate 1-NN + the first radix
-//                 digit histogram of d^2 (LDS, flushed with one atomic per non-empty bin)
-//   k_icp_select  exact k-th smallest d^2 (Matches::getDistsQuantile) by 3-digit radix select,
-//                 one 1024-thread workgroup per pair, candidates of digit 1 kept in LDS
-//   k_icp_reduce  TrimmedDist weights + getMatchedPoints gather + point-to-plane F, dot and the
-//                 27-entry normal-equation sums in double from exact float products; wave
-//                 butterfly + LDS, one deterministic partial row per workgroup (no atomics)
-//   k_icp_update  fixed-order sum of the partial rows, 6x6 solve, AngleAxis update of T_iter,
-//                 Counter + Differential checkers, per-pair active flag (early exit for the
-//                 remaining launches of converged pairs)
+// batch at once, five launches and no host synchronisation:
+//   k_active_list  compacts the pairs still iterating into the NN work space
+//   k_icp_nn       persistent waves: transform by T_iter (fused) + libnabo-order approximate
+//                  1-NN; a lane that finishes its query refills from a 64-query chunk of the
+//                  work space, so far-descent tails do not hold whole waves
+//   k_icp_select   exact k-th smallest d^2 (Matches::getDistsQuantile) by 3-digit radix select,
+//                  one 1024-thread workgroup per pair (per-wave LDS sub-histograms, digit-1
+//                  candidates kept in LDS)
+//   k_icp_reduce   TrimmedDist weights + getMatchedPoints gather + point-to-plane F, dot and the
+//                  27-entry normal-equation sums in double from exact float products; wave
+//                  butterfly + LDS, one deterministic partial row per workgroup (no atomics)
+//   k_icp_update   fixed-order sum of the partial rows, 6x6 solve, AngleAxis update of T_iter,
+//                  Counter + Differential checkers, per-pair active flag
+// SurfaceNormal: k_knn_ids (persistent kNN, eps 0, ids only) + k_normals_from_ids (uniform
+// covariance / eigen work per point).
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "aicp_common.hpp"
 #include "icp_math.hpp"
@@ -21,15 +27,15 @@
 namespace aicp {
 
 // ------------------------------------------------------------------------------------------
-// k-NN traversal in libnabo recurseKnn order
+// k-NN traversal in libnabo recurseKnn order, resumable in rounds
 // ------------------------------------------------------------------------------------------
 // recurseKnn visits the near child first, then the far child if rd' = rd - off[cd]^2 +
 // new_off^2 passes (rd' <= maxR2 && rd' * maxE2 < head). Along a run of near children rd and
-// off do not change, so the far test of every level of a descent can be evaluated during the
-// descent itself; after the leaf the climb (through parent[]) is skipped entirely when the
-// smallest such rd' already fails against the current head -- the common case with
-// epsilon = 3.16. Far descents push (far child, rd, off[cd], outer min, outer start) on a
-// bounded stack (nesting <= tree depth <= kFarStack, checked on the host).
+// off do not change, so the far test of every level of a descent is evaluated during the
+// descent itself; after the leaf the climb (through parent[]) is skipped when the smallest
+// such rd' already fails -- the common case with epsilon = 3.16. A round = one descent, its
+// bucket and the climb up to the next far child (or to the end of the query). Far descents
+// push (far child, rd, off[cd], outer min, outer start); nesting <= tree depth < kFarStack.
 template <int K>
 struct Best {
   float v[K];  // ascending, head = v[K-1] (IndexHeapBruteForceVector)
@@ -71,23 +77,47 @@ __device__ __forceinline__ float sel3(uint32_t cd, float a, float b, float c) {
   return cd == 0 ? a : (cd == 1 ? b : c);
 }
 
+// Far-descent stack: the only dynamically indexed state (private/scratch memory, touched only
+// on far descents); kept apart from Trav so the rest of the traversal stays in registers.
+struct FarStack {
+  int32_t F[kFarStack];
+  float rd[kFarStack], old[kFarStack], mn[kFarStack];
+  int32_t start[kFarStack];
+  int32_t P[kFarStack], PP[kFarStack];  // node whose far child began the frame, and its parent
+};
+
 template <int K>
-__device__ __forceinline__ void knn_traverse(const uint2* __restrict__ nodes,
-                                             const int32_t* __restrict__ parent,
-                                             const float4* __restrict__ pts, float q0, float q1,
-                                             float q2, float maxE2, float maxR2, Best<K>& best,
-                                             uint32_t& tpts, uint32_t& tnodes) {
-  float off0 = 0.f, off1 = 0.f, off2 = 0.f, rd = 0.f;
-  int32_t stF[kFarStack];
-  float stRd[kFarStack], stOld[kFarStack], stMin[kFarStack];
-  int32_t stStart[kFarStack];
-  int sp = 0;
-  int32_t n = 0, start = 0;
-  float minFar;
-  for (;;) {
-    // ---- descend along near children
+struct Trav {
+  const uint4* nodes;
+  const float4* pts;
+  float q0, q1, q2;
+  float off0, off1, off2, rd, minFar;
+  int32_t n, start, sp;
+  uint32_t tp, tn;
+  Best<K> best;
+
+  __device__ __forceinline__ void bind(const uint4* nb, const float4* pb, uint32_t node_off, uint32_t ref_off) {
+    nodes = nb + node_off;
+    pts = pb + ref_off;
+  }
+  __device__ __forceinline__ float res_d2() const { return best.v[0]; }
+  __device__ __forceinline__ int32_t res_id() const { return best.id[0]; }
+
+  __device__ __forceinline__ void reset(float a, float b, float c) {
+    q0 = a;
+    q1 = b;
+    q2 = c;
+    off0 = off1 = off2 = rd = 0.f;
+    n = start = sp = 0;
+    tp = tn = 0;
+    best_init<K>(best);
+  }
+
+  // one round (a descent, its bucket and the climb to the next far descent); true when done.
+  // The climb follows the parent index stored in each node record (one load per level).
+  __device__ __forceinline__ bool advance(FarStack& fs, float maxE2, float maxR2, const uint4*, const float4*) {
     minFar = __builtin_inff();
-    uint2 nd = nodes[n];
+    uint4 nd = nodes[n];
     while ((nd.y & 3u) != kLeaf) {
       const uint32_t cd = nd.y & 3u;
       const float no = sel3(cd, q0, q1, q2) - __uint_as_float(nd.x);
@@ -95,10 +125,9 @@ __device__ __forceinline__ void knn_traverse(const uint2* __restrict__ nodes,
       const float rdf = rd + (-oc * oc + no * no);
       minFar = fminf(minFar, rdf);
       n = (no > 0.f) ? (int32_t)(nd.y >> 2) : n + 1;
-      ++tnodes;
+      ++tn;
       nd = nodes[n];
     }
-    // ---- bucket
     {
       const uint32_t b0 = nd.y >> 2, cnt = nd.x;
       for (uint32_t i = 0; i < cnt; ++i) {
@@ -110,40 +139,42 @@ __device__ __forceinline__ void knn_traverse(const uint2* __restrict__ nodes,
         dist += d2 * d2;
         if (dist <= maxR2 && dist < best.v[K - 1]) best_replace<K>(best, (int32_t)(b0 + i), dist);
       }
-      tpts += cnt;
+      tp += cnt;
     }
-    // ---- climb
-    int32_t c = n;
+    int32_t c = n, pc = (int32_t)nd.z;
     if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
-    bool descend = false;
-    while (!descend) {
+    for (;;) {
       if (c == start) {
-        if (sp == 0) return;
+        if (sp == 0) return true;
         --sp;
-        const uint32_t pcd = (uint32_t)stF[sp] >> 30;
-        rd = stRd[sp];
-        if (pcd == 0) off0 = stOld[sp];
-        else if (pcd == 1) off1 = stOld[sp];
-        else off2 = stOld[sp];
-        minFar = stMin[sp];
-        start = stStart[sp];
-        c = parent[c];
+        const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
+        rd = fs.rd[sp];
+        const float old = fs.old[sp];
+        if (pcd == 0) off0 = old;
+        else if (pcd == 1) off1 = old;
+        else off2 = old;
+        minFar = fs.mn[sp];
+        start = fs.start[sp];
+        c = fs.P[sp];
+        pc = fs.PP[sp];
         if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
         continue;
       }
-      const int32_t p = parent[c];
-      const uint2 pn = nodes[p];
+      const int32_t p = pc;
+      const uint4 pn = nodes[p];
       const uint32_t cd = pn.y & 3u;
       const float no = sel3(cd, q0, q1, q2) - __uint_as_float(pn.x);
       const float oc = sel3(cd, off0, off1, off2);
       const float rdf = rd + (-oc * oc + no * no);
       if (rdf <= maxR2 && rdf * maxE2 < best.v[K - 1]) {
         const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
-        stF[sp] = (int32_t)((uint32_t)far | (cd << 30));
-        stRd[sp] = rd;
-        stOld[sp] = oc;
-        stMin[sp] = minFar;
-        stStart[sp] = start;
+        fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
+        fs.rd[sp] = rd;
+        fs.old[sp] = oc;
+        fs.mn[sp] = minFar;
+        fs.start[sp] = start;
+        fs.P[sp] = p;
+        fs.PP[sp] = (int32_t)pn.z;
         ++sp;
         if (cd == 0) off0 = no;
         else if (cd == 1) off1 = no;
@@ -151,22 +182,208 @@ __device__ __forceinline__ void knn_traverse(const uint2* __restrict__ nodes,
         rd = rdf;
         n = far;
         start = far;
-        descend = true;
-      } else {
-        c = p;
+        return false;
       }
+      c = p;
+      pc = (int32_t)pn.z;
     }
   }
-}
+};
 
-__device__ __forceinline__ void block_map(const BlockMap& m, int& pair, uint32_t& local) {
-  pair = m.pair[blockIdx.x];
-  local = m.start[blockIdx.x] + threadIdx.x;
+// 1-NN (the ICP matcher) as a one-load-per-step state machine: each iteration a lane issues
+// exactly one 16-byte load -- a node record or a bucket point, chosen per lane -- and then
+// advances its own phase (descent / bucket / climb), so lanes in different phases of their
+// traversals share every load instruction instead of serialising whole loops. Visit order,
+// far tests and results are those of Trav<1> (libnabo recurseKnn).
+enum : int32_t { kDesc = 0, kLeafScan = 1, kClimb = 2 };
+
+struct SM0 {
+  uint32_t nb, pb;  // node / bucket offsets of the query's pair
+  float q0, q1, q2;
+  float off0, off1, off2, rd, minFar;
+  int32_t n, start, sp, phase;
+  uint32_t b, cnt;
+  int32_t lp;  // parent of the leaf being scanned
+  float bestd;
+  int32_t bid;
+  uint32_t tp, tn;
+
+  __device__ __forceinline__ void bind(const uint4*, const float4*, uint32_t node_off, uint32_t ref_off) {
+    nb = node_off;
+    pb = ref_off;
+  }
+  __device__ __forceinline__ float res_d2() const { return bestd; }
+  __device__ __forceinline__ int32_t res_id() const { return bid; }
+
+  __device__ __forceinline__ void reset(float a, float bb, float cc) {
+    q0 = a;
+    q1 = bb;
+    q2 = cc;
+    off0 = off1 = off2 = rd = 0.f;
+    minFar = __builtin_inff();
+    n = start = sp = 0;
+    phase = kDesc;
+    bestd = __builtin_inff();
+    bid = -1;
+    tp = tn = 0;
+  }
+
+  // branch-free: a store through a selected member pointer would keep the struct in scratch
+  __device__ __forceinline__ void set_off(uint32_t cd, float v) {
+    off0 = (cd == 0) ? v : off0;
+    off1 = (cd == 1) ? v : off1;
+    off2 = (cd == 2) ? v : off2;
+  }
+
+  __device__ __forceinline__ bool advance(FarStack& fs, float E, float R, const uint4* __restrict__ nodes,
+                                          const float4* __restrict__ pts) {
+    const uint4 v = (phase == kLeafScan) ? *reinterpret_cast<const uint4*>(pts + pb + b) : nodes[nb + n];
+    int32_t c, pc;
+    if (phase == kDesc) {
+      if ((v.y & 3u) != kLeaf) {
+        const uint32_t cd = v.y & 3u;
+        const float no = sel3(cd, q0, q1, q2) - __uint_as_float(v.x);
+        const float oc = sel3(cd, off0, off1, off2);
+        minFar = fminf(minFar, rd + (-oc * oc + no * no));
+        n = (no > 0.f) ? (int32_t)(v.y >> 2) : n + 1;
+        ++tn;
+      } else {
+        b = v.y >> 2;
+        cnt = v.x;
+        lp = (int32_t)v.z;
+        phase = kLeafScan;
+      }
+      return false;
+    }
+    if (phase == kLeafScan) {
+      const float d0 = q0 - __uint_as_float(v.x), d1 = q1 - __uint_as_float(v.y), d2 = q2 - __uint_as_float(v.z);
+      float dist = 0.f;
+      dist += d0 * d0;
+      dist += d1 * d1;
+      dist += d2 * d2;
+      if (dist <= R && dist < bestd) {
+        bestd = dist;
+        bid = (int32_t)b;
+      }
+      ++tp;
+      ++b;
+      if (--cnt != 0) return false;
+      c = n;
+      pc = lp;
+      if (!(minFar <= R && minFar * E < bestd)) c = start;
+    } else {  // kClimb: v = record of node n, parent of the finished near child
+      const uint32_t cd = v.y & 3u;
+      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(v.x);
+      const float oc = sel3(cd, off0, off1, off2);
+      const float rdf = rd + (-oc * oc + no * no);
+      if (rdf <= R && rdf * E < bestd) {
+        const int32_t far = (no > 0.f) ? n + 1 : (int32_t)(v.y >> 2);
+        const int k = sp;
+        fs.F[k] = (int32_t)((uint32_t)far | (cd << 30));
+        fs.rd[k] = rd;
+        fs.old[k] = oc;
+        fs.mn[k] = minFar;
+        fs.start[k] = start;
+        fs.P[k] = n;
+        fs.PP[k] = (int32_t)v.z;
+        sp = k + 1;
+        set_off(cd, no);
+        rd = rdf;
+        start = far;
+        n = far;
+        minFar = __builtin_inff();
+        phase = kDesc;
+        return false;
+      }
+      c = n;
+      pc = (int32_t)v.z;
+    }
+    for (;;) {  // frame completions need no loads
+      if (c != start) {
+        n = pc;
+        phase = kClimb;
+        return false;
+      }
+      if (sp == 0) return true;
+      const int k = --sp;
+      rd = fs.rd[k];
+      set_off((uint32_t)fs.F[k] >> 30, fs.old[k]);
+      minFar = fs.mn[k];
+      start = fs.start[k];
+      c = fs.P[k];
+      pc = fs.PP[k];
+      if (!(minFar <= R && minFar * E < bestd)) c = start;
+    }
+  }
+};
+
+// Persistent waves with XCD-affine work: the slot space [0, total) is cut into kXcdGroups
+// contiguous ranges and group g is served only by blocks with blockIdx % 8 == g, which the
+// dispatcher places on one XCD (MI355X_MICROARCH.md, workgroup dispatch: speed only, never
+// correctness -- any placement still processes every slot exactly once). Consecutive slots
+// belong to the same pair, so each XCD's 4 MiB L2 holds the trees of ~P/8 pairs instead of
+// all P. Each group has its own counter (64-byte stride); slots are taken in 64-slot chunks
+// per wave and handed to the lanes that need work in lane order, so a lane starts a new query
+// as soon as its previous one completes. fetch(slot, eng) initialises a lane's query;
+// done(slot, eng) consumes the result.
+template <class Eng, class Fetch, class Done>
+__device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, float maxE2, float maxR2,
+                                               const uint4* __restrict__ nodes, const float4* __restrict__ pts,
+                                               Fetch&& fetch, Done&& done) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t g = blockIdx.x % kXcdGroups;
+  const uint32_t lo = (uint32_t)(((uint64_t)total * g) / kXcdGroups);
+  const uint32_t hi = (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups);
+  uint32_t* gctr = ctr + g * kCtrStride;
+  Eng t;
+  FarStack fs;
+  bool has = false, fresh = false;
+  uint32_t pool = 0, pool_end = 0, my = 0;
+  bool exhausted = false;
+  for (;;) {
+    for (;;) {
+      const uint64_t needm = __ballot(!has);
+      if (needm == 0 || exhausted) break;
+      if (pool >= pool_end) {
+        uint32_t base = 0;
+        if (lane == 0) base = lo + atomicAdd(gctr, 64u);
+        base = __shfl(base, 0, 64);
+        if (base >= hi) {
+          exhausted = true;
+          break;
+        }
+        pool = base;
+        pool_end = min(base + 64u, hi);
+      }
+      const uint32_t rank = (uint32_t)__popcll(needm & ((1ull << lane) - 1ull));
+      const uint32_t avail = pool_end - pool;
+      if (!has && rank < avail) {
+        my = pool + rank;
+        has = true;
+        fresh = true;
+      }
+      pool += min(avail, (uint32_t)__popcll(needm));
+    }
+    if (fresh) {
+      fetch(my, t);
+      fresh = false;
+    }
+    if (__ballot(has) == 0) break;
+    if (has && t.advance(fs, maxE2, maxR2, nodes, pts)) {
+      done(my, t);
+      has = false;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
 // setup kernels
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void block_map(const BlockMap& m, int& pair, uint32_t& local) {
+  pair = m.pair[blockIdx.x];
+  local = m.start[blockIdx.x] + threadIdx.x;
+}
+
 __global__ __launch_bounds__(256) void k_prepare_read(BlockMap m, const PairDesc* __restrict__ pd,
                                                       const float4* __restrict__ raw,
                                                       float4* __restrict__ out) {
@@ -221,125 +438,226 @@ __global__ void k_init_state(int n_pairs, const PairDesc* __restrict__ pd, PairS
   s.th[0][0] = s.th[0][1] = s.th[0][2] = 0.0;
 }
 
-__global__ void k_zero_hist(int n_pairs, uint32_t* hist1) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_pairs * kHistBins) hist1[i] = 0;
+// one workgroup: prefix of n_read over the pairs still active + zero the work counter
+__global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDesc* __restrict__ pd,
+                                                      const PairState* __restrict__ st,
+                                                      ActiveList* al, uint32_t* ctr) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t wcnt[16];
+  __shared__ uint32_t carry_off, carry_cnt;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) carry_off = carry_cnt = 0;
+  if (t < kXcdGroups) ctr[t * kCtrStride] = 0;
+  __syncthreads();
+  for (int base = 0; base < n_pairs; base += 1024) {
+    const int p = base + t;
+    const bool a = p < n_pairs && st[p].active;
+    const uint32_t v = a ? pd[p].n_read : 0u;
+    uint32_t x = v, c = a ? 1u : 0u;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64), z = __shfl_up(c, off, 64);
+      if (lane >= off) {
+        x += y;
+        c += z;
+      }
+    }
+    if (lane == 63) {
+      wsum[wave] = x;
+      wcnt[wave] = c;
+    }
+    __syncthreads();
+    uint32_t bo = carry_off, bc = carry_cnt;
+    for (int w = 0; w < wave; ++w) {
+      bo += wsum[w];
+      bc += wcnt[w];
+    }
+    if (a) {
+      const uint32_t e = bc + c - 1;
+      al->pair[e] = p;
+      al->off[e] = bo + x - v;
+    }
+    __syncthreads();
+    if (t == 1023) {
+      carry_off = bo + x;
+      carry_cnt = bc + c;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    al->n = carry_cnt;
+    al->total = carry_off;
+    al->off[carry_cnt] = carry_off;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
-// SurfaceNormal on the reference (bucket order queries: spatially coherent waves)
+// SurfaceNormal: persistent kNN (ids) + uniform covariance / eigen pass
 // ------------------------------------------------------------------------------------------
+// slot = global reference index (bucket order, concatenated over pairs); pair by search over
+// the pairs' ref_off (ascending).
+__device__ __forceinline__ int pair_of_ref(const PairDesc* __restrict__ pd, int n_pairs, uint32_t s) {
+  int lo = 0, hi = n_pairs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pd[mid].ref_off <= s) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 template <int K>
-__global__ __launch_bounds__(256) void k_normals(BlockMap m, const PairDesc* __restrict__ pd,
-                                                 PairState* st, const uint2* __restrict__ nodes,
+__global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
+                                                 const uint4* __restrict__ nodes,
                                                  const int32_t* __restrict__ parent,
                                                  const float4* __restrict__ bpts,
-                                                 float4* __restrict__ bnrm) {
-  int pair;
-  uint32_t j;
-  block_map(m, pair, j);
-  const PairDesc& d = pd[pair];
-  __shared__ uint32_t deg;
-  if (threadIdx.x == 0) deg = 0;
-  __syncthreads();
-  if (j < d.n_ref) {
-    const float4* P = bpts + d.ref_off;
-    const float4 q = P[j];
-    Best<K> best;
-    best_init<K>(best);
-    uint32_t tp = 0, tn = 0;
-    knn_traverse<K>(nodes + d.node_off, parent + d.node_off, P, q.x, q.y, q.z, 1.f,
-                    __builtin_inff(), best, tp, tn);
-    // d = neighbours with finite distance in heap order; mean; NN = d - mean; C = NN NN^T / k
-    float sx = 0.f, sy = 0.f, sz = 0.f;
-    int kk = 0;
+                                                 int32_t* __restrict__ ids, uint32_t* ctr) {
+  int cur = -1;
+  uint32_t cur_end = 0, cur_off = 0;
+  persistent_xcd<Trav<K>>(
+      total, ctr, 1.f, __builtin_inff(), nodes, bpts,
+      [&](uint32_t s, Trav<K>& t) {
+        if (cur < 0 || s < cur_off || s >= cur_end) {
+          cur = pair_of_ref(pd, n_pairs, s);
+          cur_off = pd[cur].ref_off;
+          cur_end = cur_off + pd[cur].n_ref;
+        }
+        const PairDesc& d = pd[cur];
+        t.nodes = nodes + d.node_off;
+        t.pts = bpts + d.ref_off;
+        const float4 q = bpts[s];
+        t.reset(q.x, q.y, q.z);
+      },
+      [&](uint32_t s, Trav<K>& t) {
 #pragma unroll
-    for (int i = 0; i < K; ++i)
-      if (best.v[i] != __builtin_inff()) {
-        const float4 p = P[best.id[i]];
-        sx += p.x;
-        sy += p.y;
-        sz += p.z;
-        ++kk;
-      }
-    const float fk = (float)kk;
-    const float mx = sx / fk, my = sy / fk, mz = sz / fk;
-    double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+        for (int i = 0; i < K; ++i) ids[(size_t)s * K + i] = (t.best.v[i] != __builtin_inff()) ? t.best.id[i] : -1;
+      });
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_normals_from_ids(int n_pairs, uint32_t total,
+                                                          const PairDesc* __restrict__ pd, PairState* st,
+                                                          const float4* __restrict__ bpts,
+                                                          const int32_t* __restrict__ ids,
+                                                          float4* __restrict__ bnrm) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= total) return;
+  const int pair = pair_of_ref(pd, n_pairs, s);
+  const float4* P = bpts + pd[pair].ref_off;
+  int32_t nb[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i)
-      if (best.v[i] != __builtin_inff()) {
-        const float4 p = P[best.id[i]];
-        const double a = (double)(p.x - mx), b = (double)(p.y - my), c = (double)(p.z - mz);
-        c00 += a * a;
-        c01 += a * b;
-        c02 += a * c;
-        c11 += b * b;
-        c12 += b * c;
-        c22 += c * c;
-      }
-    const double C[9] = {c00 / kk, c01 / kk, c02 / kk, c01 / kk, c11 / kk,
-                         c12 / kk, c02 / kk, c12 / kk, c22 / kk};
-    float nrm[3];
-    const bool dg = normal_from_cov(C, nrm);
-    bnrm[d.ref_off + j] = make_float4(nrm[0], nrm[1], nrm[2], 0.f);
-    if (dg) atomicAdd(&deg, 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && deg) atomicAdd(&st[pair].degenerate, (int)deg);
+  for (int i = 0; i < K; ++i) nb[i] = ids[(size_t)s * K + i];
+  // d = neighbours with finite distance in heap order; mean; NN = d - mean; C = NN NN^T / k
+  float sx = 0.f, sy = 0.f, sz = 0.f;
+  int kk = 0;
+#pragma unroll
+  for (int i = 0; i < K; ++i)
+    if (nb[i] >= 0) {
+      const float4 p = P[nb[i]];
+      sx += p.x;
+      sy += p.y;
+      sz += p.z;
+      ++kk;
+    }
+  const float fk = (float)kk;
+  const float mx = sx / fk, my = sy / fk, mz = sz / fk;
+  double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+#pragma unroll
+  for (int i = 0; i < K; ++i)
+    if (nb[i] >= 0) {
+      const float4 p = P[nb[i]];
+      const double a = (double)(p.x - mx), b = (double)(p.y - my), c = (double)(p.z - mz);
+      c00 += a * a;
+      c01 += a * b;
+      c02 += a * c;
+      c11 += b * b;
+      c12 += b * c;
+      c22 += c * c;
+    }
+  const double C[9] = {c00 / kk, c01 / kk, c02 / kk, c01 / kk, c11 / kk,
+                       c12 / kk, c02 / kk, c12 / kk, c22 / kk};
+  float nrm[3];
+  const bool dg = normal_from_cov(C, nrm);
+  bnrm[s] = make_float4(nrm[0], nrm[1], nrm[2], 0.f);
+  if (dg) atomicAdd(&st[pair].degenerate, 1);
 }
 
 // ------------------------------------------------------------------------------------------
 // ICP iteration
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kNNBlock) void k_icp_nn(
-    BlockMap m, const PairDesc* __restrict__ pd, PairState* st, const float4* __restrict__ read_c,
-    const uint2* __restrict__ nodes, const int32_t* __restrict__ parent,
-    const float4* __restrict__ bpts, int32_t* __restrict__ match, float* __restrict__ d2out,
-    uint32_t* __restrict__ hist1, IcpParams prm) {
-  int pair;
-  uint32_t j;
-  block_map(m, pair, j);
-  PairState& s = st[pair];
-  if (!s.active) return;
-  __shared__ uint32_t lh[kHistBins];
-  __shared__ uint32_t ltp, ltn;
-  for (int i = threadIdx.x; i < kHistBins; i += kNNBlock) lh[i] = 0;
-  if (threadIdx.x == 0) ltp = ltn = 0;
-  __syncthreads();
-  const PairDesc& d = pd[pair];
-  if (j < d.n_read) {
-    float T[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) T[i] = s.T[i];
-    const float4 r = read_c[d.read_off + j];
-    float q[3];
-    apply4(T, r.x, r.y, r.z, q);
-    Best<1> best;
-    best_init<1>(best);
-    uint32_t tp = 0, tn = 0;
-    knn_traverse<1>(nodes + d.node_off, parent + d.node_off, bpts + d.ref_off, q[0], q[1], q[2],
-                    prm.maxE2, prm.maxR2, best, tp, tn);
-    match[d.read_off + j] = best.id[0];
-    d2out[d.read_off + j] = best.v[0];
-    if (best.v[0] != __builtin_inff()) atomicAdd(&lh[__float_as_uint(best.v[0]) >> 21], 1u);
-    atomicAdd(&ltp, tp);
-    atomicAdd(&ltn, tn);
-  }
-  __syncthreads();
-  uint32_t* gh = hist1 + (size_t)pair * kHistBins;
-  for (int i = threadIdx.x; i < kHistBins; i += kNNBlock) {
-    const uint32_t v = lh[i];
-    if (v) atomicAdd(&gh[i], v);
-  }
-  if (threadIdx.x == 0) {
-    atomicAdd((unsigned long long*)&s.touched_pts, (unsigned long long)ltp);
-    atomicAdd((unsigned long long*)&s.touched_nodes, (unsigned long long)ltn);
-  }
+__device__ __forceinline__ void apply_cols(const float4& c0, const float4& c1, const float4& c2, const float4& c3,
+                                           float x, float y, float z, float& o0, float& o1, float& o2) {
+  // same operation order as apply4: ((T(r,0) x + T(r,1) y) + T(r,2) z) + T(r,3)
+  o0 = c0.x * x;
+  o0 += c1.x * y;
+  o0 += c2.x * z;
+  o0 += c3.x;
+  o1 = c0.y * x;
+  o1 += c1.y * y;
+  o1 += c2.y * z;
+  o1 += c3.y;
+  o2 = c0.z * x;
+  o2 += c1.z * y;
+  o2 += c2.z * z;
+  o2 += c3.z;
 }
 
-// rank k -> (bin, k - count before bin) over h[nb] with 1024 threads; result in res[0..2]
-__device__ void block_find_rank(const uint32_t* h, int nb, uint32_t k, uint32_t* res,
-                                uint32_t* wsum) {
+// NN kernel: also stores the query's touch counts (inner nodes << 16 | bucket points, each
+// saturated at 65535) for the reduce kernel to sum per pair without atomics.
+template <class Eng>
+__global__ __launch_bounds__(256) void k_icp_nn(const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
+                                                const ActiveList* __restrict__ al,
+                                                const float4* __restrict__ read_c,
+                                                const uint4* __restrict__ nodes,
+                                                const int32_t* __restrict__ parent,
+                                                const float4* __restrict__ bpts, int32_t* __restrict__ match,
+                                                float* __restrict__ d2out, uint32_t* __restrict__ touched,
+                                                uint32_t* ctr, IcpParams prm) {
+  const uint32_t total = al->total;
+  if (total == 0) return;
+  int e = -1;
+  uint32_t e_lo = 0, e_hi = 0, rbase = 0;
+  int cur_pair = -1;
+  uint32_t node_off = 0, ref_off = 0;
+  uint32_t qidx = 0;
+  persistent_xcd<Eng>(
+      total, ctr, prm.maxE2, prm.maxR2, nodes, bpts,
+      [&](uint32_t s, Eng& t) {
+        if (e < 0 || s < e_lo || s >= e_hi) {
+          int lo = 0, hi = (int)al->n - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (al->off[mid] <= s) lo = mid;
+            else hi = mid - 1;
+          }
+          e = lo;
+          e_lo = al->off[e];
+          e_hi = al->off[e + 1];
+          const int p = al->pair[e];
+          if (p != cur_pair) {
+            cur_pair = p;
+            rbase = pd[p].read_off;
+            node_off = pd[p].node_off;
+            ref_off = pd[p].ref_off;
+          }
+        }
+        t.bind(nodes, bpts, node_off, ref_off);
+        qidx = rbase + (s - e_lo);
+        const float4 r = read_c[qidx];
+        const float4* Tp = reinterpret_cast<const float4*>(st[cur_pair].T);
+        float q0, q1, q2;
+        apply_cols(Tp[0], Tp[1], Tp[2], Tp[3], r.x, r.y, r.z, q0, q1, q2);
+        t.reset(q0, q1, q2);
+      },
+      [&](uint32_t, Eng& t) {
+        match[qidx] = t.res_id();
+        d2out[qidx] = t.res_d2();
+        touched[qidx] = (min(t.tn, 65535u) << 16) | min(t.tp, 65535u);
+      });
+}
+
+// rank k -> (bin, k - count before bin) over h[nb] with 1024 threads; result in res[0..1]
+__device__ void block_find_rank(const uint32_t* h, int nb, uint32_t k, uint32_t* res, uint32_t* wsum) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int per = nb / 1024;
   uint32_t local = 0;
@@ -370,39 +688,58 @@ __device__ void block_find_rank(const uint32_t* h, int nb, uint32_t k, uint32_t*
   __syncthreads();
 }
 
-constexpr int kCand = 8192;
+constexpr int kCand = 6144;
+constexpr int kSubHist = 8;  // digit-1 sub-histograms (2 waves each) against LDS atomic conflicts
+constexpr uint32_t kInfBits = 0x7f800000u;
 
 __global__ __launch_bounds__(1024) void k_icp_select(const PairDesc* __restrict__ pd, PairState* st,
-                                                     const float* __restrict__ d2,
-                                                     const uint32_t* __restrict__ hist1) {
+                                                     const float* __restrict__ d2) {
   const int pair = blockIdx.x;
   PairState& s = st[pair];
   if (!s.active) return;
   const PairDesc& d = pd[pair];
-  __shared__ uint32_t h[kHistBins];
+  __shared__ uint32_t sub[kSubHist][kHistBins];
   __shared__ uint32_t cand[kCand];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t res[2];
-  __shared__ uint32_t total, ncand;
-  const int t = threadIdx.x;
-  for (int i = t; i < kHistBins; i += 1024) h[i] = hist1[(size_t)pair * kHistBins + i];
+  __shared__ uint32_t ncand;
+  uint32_t* h = sub[0];
+  const int t = threadIdx.x, lane = t & 63;
+  for (int i = t; i < kSubHist * kHistBins; i += 1024) (&sub[0][0])[i] = 0;
   if (t == 0) ncand = 0;
   __syncthreads();
-  // total finite = sum of digit-1 histogram
+  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
+  const uint32_t n_all = d.n_read;
+  // digit 1 (bits 31..21) of the finite values
+  uint32_t* mysub = sub[(t >> 6) % kSubHist];
+  for (uint32_t i = t; i < n_all; i += 1024) {
+    const uint32_t v = bits[i];
+    if (v != kInfBits) atomicAdd(&mysub[v >> 21], 1u);
+  }
+  __syncthreads();
+  for (int i = t; i < kHistBins; i += 1024) {
+    uint32_t a = 0;
+#pragma unroll
+    for (int k = 0; k < kSubHist; ++k) a += sub[k][i];
+    h[i] = a;
+  }
+  __syncthreads();
+  // total finite
   {
     uint32_t v = h[2 * t] + h[2 * t + 1];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if ((t & 63) == 0) wsum[t >> 6] = v;
+    if (lane == 0) wsum[t >> 6] = v;
     __syncthreads();
     if (t == 0) {
       uint32_t a = 0;
       for (int w = 0; w < 16; ++w) a += wsum[w];
-      total = a;
+      res[0] = a;
     }
     __syncthreads();
   }
-  const uint32_t n = total;
+  const uint32_t n = res[0];
+  __syncthreads();
   if (n == 0) {  // ConvergenceError("no outlier to filter")
     if (t == 0) {
       s.status = 1;
@@ -421,20 +758,29 @@ __global__ __launch_bounds__(1024) void k_icp_select(const PairDesc* __restrict_
   }
   block_find_rank(h, kHistBins, k, res, wsum);
   const uint32_t b1 = res[0], r1 = res[1];
+  __syncthreads();
   for (int i = t; i < kHistBins; i += 1024) h[i] = 0;
   __syncthreads();
-  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
-  for (uint32_t i = t; i < d.n_read; i += 1024) {
+  for (uint32_t i = t; i < n_all; i += 1024) {
     const uint32_t v = bits[i];
-    if ((v >> 21) == b1 && v != 0x7f800000u) {
-      atomicAdd(&h[(v >> 10) & 2047u], 1u);
-      const uint32_t slot = atomicAdd(&ncand, 1u);
-      if (slot < (uint32_t)kCand) cand[slot] = v;
+    const bool hit = (v >> 21) == b1 && v != kInfBits;
+    if (hit) atomicAdd(&h[(v >> 10) & 2047u], 1u);
+    const uint64_t m = __ballot(hit);
+    if (m) {
+      uint32_t base = 0;
+      const int leader = __builtin_ctzll(m);
+      if (lane == leader) base = atomicAdd(&ncand, (uint32_t)__popcll(m));
+      base = __shfl(base, leader, 64);
+      if (hit) {
+        const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (slot < (uint32_t)kCand) cand[slot] = v;
+      }
     }
   }
   __syncthreads();
   block_find_rank(h, kHistBins, r1, res, wsum);
   const uint32_t b2 = res[0], r2 = res[1];
+  __syncthreads();
   for (int i = t; i < kHistBins; i += 1024) h[i] = 0;
   __syncthreads();
   const uint32_t hi21 = (b1 << 11) | b2;
@@ -444,9 +790,9 @@ __global__ __launch_bounds__(1024) void k_icp_select(const PairDesc* __restrict_
       if ((v >> 10) == hi21) atomicAdd(&h[v & 1023u], 1u);
     }
   } else {
-    for (uint32_t i = t; i < d.n_read; i += 1024) {
+    for (uint32_t i = t; i < n_all; i += 1024) {
       const uint32_t v = bits[i];
-      if ((v >> 10) == hi21 && v != 0x7f800000u) atomicAdd(&h[v & 1023u], 1u);
+      if ((v >> 10) == hi21 && v != kInfBits) atomicAdd(&h[v & 1023u], 1u);
     }
   }
   __syncthreads();
@@ -466,7 +812,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
     BlockMap m, const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
     const float4* __restrict__ read_c, const int32_t* __restrict__ match,
-    const float* __restrict__ d2, const float4* __restrict__ bpts,
+    const float* __restrict__ d2, const uint32_t* __restrict__ touched, const float4* __restrict__ bpts,
     const float4* __restrict__ bnrm, double* __restrict__ slab) {
   const int pair = m.pair[blockIdx.x];
   const PairState& s = st[pair];
@@ -480,10 +826,14 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
 #pragma unroll
   for (int i = 0; i < kRedCols; ++i) acc[i] = 0.0;
   const uint32_t base = m.start[blockIdx.x];
+  uint32_t tpts = 0, tnod = 0;
 #pragma unroll
   for (int it = 0; it < kReducePerThread; ++it) {
     const uint32_t j = base + it * kNNBlock + threadIdx.x;
     if (j >= d.n_read) break;
+    const uint32_t tc = touched[d.read_off + j];
+    tpts += tc & 0xFFFFu;
+    tnod += tc >> 16;
     const float dd = d2[d.read_off + j];
     if (!(dd <= limit)) continue;
     const int32_t pos = match[d.read_off + j];
@@ -512,6 +862,8 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
     for (int a = 0; a < 6; ++a) acc[21 + a] += (double)F[a] * (double)dot;
     acc[27] += 1.0;
   }
+  acc[28] = (double)tpts;
+  acc[29] = (double)tnod;
   __shared__ double part[kNNBlock / 64][kRedCols];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -528,8 +880,7 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
 }
 
 __global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__ pd, PairState* st,
-                                                    const double* __restrict__ slab,
-                                                    uint32_t* __restrict__ hist1, IcpParams prm) {
+                                                    const double* __restrict__ slab, IcpParams prm) {
   const int pair = blockIdx.x;
   PairState& s = st[pair];
   if (!s.active) return;
@@ -545,10 +896,10 @@ __global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__
   }
   __syncthreads();
   if (t < kRedCols) tot[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
-  // clear the digit-1 histogram for the next iteration
-  for (int i = t; i < kHistBins; i += 256) hist1[(size_t)pair * kHistBins + i] = 0;
   __syncthreads();
   if (t != 0) return;
+  s.touched_pts += (uint64_t)tot[28];
+  s.touched_nodes += (uint64_t)tot[29];
   const int32_t kept = (int32_t)tot[27];
   s.kept = kept;
   if (kept == 0) {  // ConvergenceError("no point to minimize")
@@ -621,39 +972,75 @@ __global__ void k_finalize(int n_pairs, const PairDesc* __restrict__ pd,
 // kernel-level entry points
 // ------------------------------------------------------------------------------------------
 template <int K>
-__global__ __launch_bounds__(256) void k_knn_generic(int nq, const float4* __restrict__ q,
-                                                     const uint2* __restrict__ nodes,
+__global__ __launch_bounds__(256) void k_knn_generic(uint32_t nq, const float4* __restrict__ q,
+                                                     const uint4* __restrict__ nodes,
                                                      const int32_t* __restrict__ parent,
                                                      const float4* __restrict__ bpts, float maxE2,
                                                      float maxR2, int32_t* __restrict__ ids,
-                                                     float* __restrict__ d2,
-                                                     unsigned long long* touched) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq) return;
-  const float4 x = q[i];
-  Best<K> best;
-  best_init<K>(best);
+                                                     float* __restrict__ d2, unsigned long long* touched,
+                                                     uint32_t* ctr) {
   uint32_t tp = 0, tn = 0;
-  knn_traverse<K>(nodes, parent, bpts, x.x, x.y, x.z, maxE2, maxR2, best, tp, tn);
+  persistent_xcd<Trav<K>>(
+      nq, ctr, maxE2, maxR2, nodes, bpts,
+      [&](uint32_t s, Trav<K>& t) {
+        t.nodes = nodes;
+        t.pts = bpts;
+        const float4 x = q[s];
+        t.reset(x.x, x.y, x.z);
+      },
+      [&](uint32_t s, Trav<K>& t) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    ids[(size_t)i * K + j] = best.id[j] < 0 ? -1 : __float_as_int(bpts[best.id[j]].w);
-    d2[(size_t)i * K + j] = best.v[j];
+        for (int j = 0; j < K; ++j) {
+          ids[(size_t)s * K + j] = t.best.id[j] < 0 ? -1 : __float_as_int(bpts[t.best.id[j]].w);
+          d2[(size_t)s * K + j] = t.best.v[j];
+        }
+        tp += t.tp;
+        tn += t.tn;
+      });
+  unsigned long long a = tp, b = tn;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
   }
-  atomicAdd(&touched[0], (unsigned long long)tp);
-  atomicAdd(&touched[1], (unsigned long long)tn);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&touched[0], a);
+    atomicAdd(&touched[1], b);
+  }
 }
 
-__global__ __launch_bounds__(256) void k_hist_d2(BlockMap m, const PairDesc* __restrict__ pd,
-                                                 const float* __restrict__ d2,
-                                                 uint32_t* __restrict__ hist1) {
-  int pair;
-  uint32_t j;
-  block_map(m, pair, j);
-  const PairDesc& d = pd[pair];
-  if (j >= d.n_read) return;
-  const float v = d2[d.read_off + j];
-  if (v != __builtin_inff()) atomicAdd(&hist1[(size_t)pair * kHistBins + (__float_as_uint(v) >> 21)], 1u);
+// 1-NN through either engine (SM0: the ICP matcher's one-load-per-step traversal)
+template <class Eng>
+__global__ __launch_bounds__(256) void k_knn1_generic(uint32_t nq, const float4* __restrict__ q,
+                                                      const uint4* __restrict__ nodes,
+                                                      const float4* __restrict__ bpts, float maxE2, float maxR2,
+                                                      int32_t* __restrict__ ids, float* __restrict__ d2,
+                                                      unsigned long long* touched, uint32_t* ctr) {
+  uint32_t tp = 0, tn = 0;
+  persistent_xcd<Eng>(
+      nq, ctr, maxE2, maxR2, nodes, bpts,
+      [&](uint32_t s, Eng& t) {
+        t.bind(nodes, bpts, 0, 0);
+        const float4 x = q[s];
+        t.reset(x.x, x.y, x.z);
+      },
+      [&](uint32_t s, Eng& t) {
+        const int32_t id = t.res_id();
+        ids[s] = id < 0 ? -1 : __float_as_int(bpts[id].w);
+        d2[s] = t.res_d2();
+        tp += t.tp;
+        tn += t.tn;
+      });
+  unsigned long long a = tp, b = tn;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&touched[0], a);
+    atomicAdd(&touched[1], b);
+  }
 }
 
 __global__ void k_transform(int n, const float* __restrict__ T, const float4* __restrict__ in,
@@ -675,75 +1062,113 @@ __global__ void k_solve6(const double* A, const double* b, double* x, int32_t* p
 // ------------------------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------------------------
-void launch_prepare_read(hipStream_t s, BlockMap m, const PairDesc* pd, const float4* raw,
-                         float4* out) {
+static int persistent_grid(int n_items) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  // every work group (blockIdx % kXcdGroups) needs at least one block: a multiple of 8
+  int want = (n_items + 255) / 256;
+  if (want > cus * 8) want = cus * 8;
+  return (want + kXcdGroups - 1) / kXcdGroups * kXcdGroups;
+}
+
+void launch_prepare_read(hipStream_t s, BlockMap m, const PairDesc* pd, const float4* raw, float4* out) {
   if (m.n_blocks) k_prepare_read<<<m.n_blocks, 256, 0, s>>>(m, pd, raw, out);
 }
-void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const float4* raw,
-                       const int32_t* perm, float4* bpts) {
+void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const float4* raw, const int32_t* perm,
+                       float4* bpts) {
   if (m.n_blocks) k_gather_ref<<<m.n_blocks, 256, 0, s>>>(m, pd, raw, perm, bpts);
 }
-void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
-                       uint32_t* hist1) {
+void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st) {
   k_init_state<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st);
-  k_zero_hist<<<(n_pairs * kHistBins + 255) / 256, 256, 0, s>>>(n_pairs, hist1);
 }
-bool launch_normals(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
-                    const uint2* nodes, const int32_t* parent, const float4* bpts, float4* bnrm,
-                    int knn) {
-  if (!m.n_blocks) return true;
+bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
+                    const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
+                    int32_t* ids, uint32_t* ctr) {
+  if (!total_ref) return true;
+  const int g = persistent_grid((int)total_ref), gu = (int)((total_ref + 255) / 256);
   switch (knn) {
-    case 10: k_normals<10><<<m.n_blocks, 256, 0, s>>>(m, pd, st, nodes, parent, bpts, bnrm); break;
-    case 20: k_normals<20><<<m.n_blocks, 256, 0, s>>>(m, pd, st, nodes, parent, bpts, bnrm); break;
-    case 30: k_normals<30><<<m.n_blocks, 256, 0, s>>>(m, pd, st, nodes, parent, bpts, bnrm); break;
-    default: return false;
+    case 10:
+      k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr);
+      k_normals_from_ids<10><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
+      break;
+    case 20:
+      k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr);
+      k_normals_from_ids<20><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
+      break;
+    case 30:
+      k_knn_ids<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr);
+      k_normals_from_ids<30><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
+      break;
+    default:
+      return false;
   }
   return true;
 }
-void launch_icp_nn(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
-                   const float4* read_c, const uint2* nodes, const int32_t* parent,
-                   const float4* bpts, int32_t* match, float* d2, uint32_t* hist1,
-                   const IcpParams& prm) {
+void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st, ActiveList* al,
+                        uint32_t* ctr) {
+  k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr);
+}
+// NN engine for the 1-NN kernels: 1 = Trav<1> (default), 0 = SM0; AICP_NN_ENGINE overrides
+// (design experiments, tools/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:
+// Trav<1> 230 us per NN launch, SM0 436 us (profiles/README.md).
+static int nn_engine() {
+  static int e = -1;
+  if (e < 0) {
+    const char* v = getenv("AICP_NN_ENGINE");
+    e = (v && v[0] == '0') ? 0 : 1;
+  }
+  return e;
+}
+
+void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st, const ActiveList* al,
+                   const float4* read_c, const uint4* nodes, const int32_t* parent, const float4* bpts,
+                   int32_t* match, float* d2, uint32_t* touched, uint32_t* ctr, const IcpParams& prm) {
+  const int g = persistent_grid(grid_items);
+  if (nn_engine() == 1)
+    k_icp_nn<Trav<1>><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, match, d2, touched, ctr, prm);
+  else
+    k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, match, d2, touched, ctr, prm);
+}
+void launch_icp_select(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const float* d2) {
+  k_icp_select<<<n_pairs, 1024, 0, s>>>(pd, st, d2);
+}
+void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const PairState* st, const float4* read_c,
+                       const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
+                       const float4* bnrm, double* slab) {
   if (m.n_blocks)
-    k_icp_nn<<<m.n_blocks, kNNBlock, 0, s>>>(m, pd, st, read_c, nodes, parent, bpts, match, d2,
-                                             hist1, prm);
+    k_icp_reduce<<<m.n_blocks, kNNBlock, 0, s>>>(m, pd, st, read_c, match, d2, touched, bpts, bnrm, slab);
 }
-void launch_icp_select(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
-                       const float* d2, const uint32_t* hist1) {
-  k_icp_select<<<n_pairs, 1024, 0, s>>>(pd, st, d2, hist1);
+void launch_icp_update(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const double* slab,
+                       const IcpParams& prm) {
+  k_icp_update<<<n_pairs, 256, 0, s>>>(pd, st, slab, prm);
 }
-void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const PairState* st,
-                       const float4* read_c, const int32_t* match, const float* d2,
-                       const float4* bpts, const float4* bnrm, double* slab) {
-  if (m.n_blocks)
-    k_icp_reduce<<<m.n_blocks, kNNBlock, 0, s>>>(m, pd, st, read_c, match, d2, bpts, bnrm, slab);
-}
-void launch_icp_update(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
-                       const double* slab, uint32_t* hist1, const IcpParams& prm) {
-  k_icp_update<<<n_pairs, 256, 0, s>>>(pd, st, slab, hist1, prm);
-}
-void launch_finalize(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
-                     float* outT) {
+void launch_finalize(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st, float* outT) {
   k_finalize<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, outT);
 }
-bool launch_knn_generic(hipStream_t s, int nq, const float4* q, const uint2* nodes,
-                        const int32_t* parent, const float4* bpts, int k, float maxE2,
-                        float maxR2, int32_t* ids, float* d2, unsigned long long* touched) {
-  const int g = (nq + 255) / 256;
-  if (!g) return true;
+bool launch_knn_generic(hipStream_t s, uint32_t nq, const float4* q, const uint4* nodes, const int32_t* parent,
+                        const float4* bpts, int k, float maxE2, float maxR2, int32_t* ids, float* d2,
+                        unsigned long long* touched, uint32_t* ctr) {
+  if (!nq) return true;
+  const int g = persistent_grid((int)nq);
   switch (k) {
-    case 1: k_knn_generic<1><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched); break;
-    case 4: k_knn_generic<4><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched); break;
-    case 10: k_knn_generic<10><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched); break;
-    case 20: k_knn_generic<20><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched); break;
-    case 30: k_knn_generic<30><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched); break;
+    case 1:
+      if (nn_engine() == 1)
+        k_knn1_generic<Trav<1>><<<g, 256, 0, s>>>(nq, q, nodes, bpts, maxE2, maxR2, ids, d2, touched, ctr);
+      else
+        k_knn1_generic<SM0><<<g, 256, 0, s>>>(nq, q, nodes, bpts, maxE2, maxR2, ids, d2, touched, ctr);
+      break;
+    case 4: k_knn_generic<4><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched, ctr); break;
+    case 10: k_knn_generic<10><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched, ctr); break;
+    case 20: k_knn_generic<20><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched, ctr); break;
+    case 30: k_knn_generic<30><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched, ctr); break;
     default: return false;
   }
   return true;
-}
-void launch_hist_d2(hipStream_t s, BlockMap m, const PairDesc* pd, const float* d2,
-                    uint32_t* hist1) {
-  if (m.n_blocks) k_hist_d2<<<m.n_blocks, 256, 0, s>>>(m, pd, d2, hist1);
 }
 void launch_transform(hipStream_t s, int n, const float* T, const float4* in, float4* out) {
   if (n > 0) k_transform<<<(n + 255) / 256, 256, 0, s>>>(n, T, in, out);

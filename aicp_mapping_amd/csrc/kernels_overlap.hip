@@ -5,10 +5,11 @@
 // float direction, double tMax) plus every endpoint key; overlap% = min(|A∩B|/|A|,
 // |A∩B|/|B|) * 100. octomap stores S in an octree, prunes and expands it; only the set matters.
 //
-// Device form: one bit per voxel of the pair's padded key box (one bitmap per cloud),
-// each ray marks its keys with check-then-atomicOr, then popcounts give |A|, |B| and |A∩B|.
-// A 60 x 60 x 6 m scene at 0.2 m is ~2.7 M voxels = 340 KB per bitmap, so the sets stay
-// L2-resident while the rays are cast.
+// Device form: one byte per voxel of the pair's padded key box (one map per cloud). Every
+// ray key is a plain byte store of 1 -- concurrent writers store the same value, so no
+// atomics and no read-before-write are needed -- then byte sums give |A|, |B| and |A∩B|.
+// A 60 x 60 x 6 m scene at 0.2 m is ~2.7 M voxels = 2.7 MB per map (L2/MALL resident).
+// (tools/microbench.hip: with 16 distinct pairs, check+atomicOr bitmaps ran 11x slower.)
 #include <hip/hip_runtime.h>
 
 #include "aicp_common.hpp"
@@ -85,14 +86,14 @@ __global__ __launch_bounds__(256) void k_ovl_bbox(BlockMap m, const PairDesc* __
 // computeRayKeys(origin, end) + endpoint key, marking bits of one bitmap.
 __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __restrict__ pd,
                                                   PairState* st, const float4* __restrict__ pts,
-                                                  int side, double res, uint32_t* bitmap) {
+                                                  int side, double res, uint8_t* maps) {
   const int pair = m.pair[blockIdx.x];
   const uint32_t j = m.start[blockIdx.x] + threadIdx.x;
   const PairDesc& d = pd[pair];
   const uint32_t n = side ? d.n_read : d.n_ref;
   if (j >= n) return;
   const uint32_t off = side ? d.read_off : d.ref_off;
-  uint32_t* bm = bitmap + d.ovl_word_off + (side ? d.ovl_words : 0);
+  uint8_t* bm = maps + d.ovl_word_off + (side ? d.ovl_words : 0);
   const int mn0 = d.ovl_min[0], mn1 = d.ovl_min[1], mn2 = d.ovl_min[2];
   const int dm0 = d.ovl_dim[0], dm1 = d.ovl_dim[1], dm2 = d.ovl_dim[2];
   bool err = false;
@@ -103,9 +104,7 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
       return;
     }
     const uint64_t idx = ((uint64_t)a * (uint64_t)dm1 + (uint64_t)b) * (uint64_t)dm2 + (uint64_t)c;
-    const uint32_t bit = 1u << (idx & 31);
-    uint32_t* w = bm + (idx >> 5);
-    if (!(*(volatile uint32_t*)w & bit)) atomicOr(w, bit);  // stale read -> one extra OR
+    bm[idx] = 1;
   };
   const double* od = side ? d.read_origin : d.ref_origin;
   const float o[3] = {(float)od[0], (float)od[1], (float)od[2]};
@@ -160,19 +159,20 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
 // popcounts: |A|, |B|, |A & B| (64 workgroups per pair, integer atomics -> deterministic)
 constexpr int kCountBlocksPerPair = 64;
 __global__ __launch_bounds__(256) void k_ovl_count(const PairDesc* __restrict__ pd, PairState* st,
-                                                   const uint32_t* __restrict__ bitmap) {
+                                                   const uint8_t* __restrict__ maps) {
   const int pair = blockIdx.x / kCountBlocksPerPair;
   const int sub = blockIdx.x % kCountBlocksPerPair;
   const PairDesc& d = pd[pair];
-  const uint32_t* A = bitmap + d.ovl_word_off;
-  const uint32_t* B = A + d.ovl_words;
+  // maps are 16-byte aligned and padded to 16-byte multiples (host); bytes are 0 or 1
+  const uint4* A = (const uint4*)(maps + d.ovl_word_off);
+  const uint4* B = (const uint4*)(maps + d.ovl_word_off + d.ovl_words);
+  const uint64_t n16 = d.ovl_words / 16;
   unsigned long long ca = 0, cb = 0, cab = 0;
-  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < d.ovl_words;
-       w += (uint64_t)kCountBlocksPerPair * 256) {
-    const uint32_t a = A[w], b = B[w];
-    ca += __popc(a);
-    cb += __popc(b);
-    cab += __popc(a & b);
+  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)kCountBlocksPerPair * 256) {
+    const uint4 a = A[w], b = B[w];
+    ca += __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w);
+    cb += __popc(b.x) + __popc(b.y) + __popc(b.z) + __popc(b.w);
+    cab += __popc(a.x & b.x) + __popc(a.y & b.y) + __popc(a.z & b.z) + __popc(a.w & b.w);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -207,12 +207,12 @@ void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* s
   if (m.n_blocks) k_ovl_bbox<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res);
 }
 void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
-                     const float4* pts, int side, double res, uint32_t* bitmap) {
-  if (m.n_blocks) k_ovl_mark<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res, bitmap);
+                     const float4* pts, int side, double res, uint8_t* maps) {
+  if (m.n_blocks) k_ovl_mark<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res, maps);
 }
 void launch_ovl_count(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
-                      const uint32_t* bitmap) {
-  k_ovl_count<<<n_pairs * kCountBlocksPerPair, 256, 0, s>>>(pd, st, bitmap);
+                      const uint8_t* maps) {
+  k_ovl_count<<<n_pairs * kCountBlocksPerPair, 256, 0, s>>>(pd, st, maps);
 }
 void launch_ovl_finish(hipStream_t s, int n_pairs, PairState* st, int set_ratio) {
   k_ovl_finish<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, st, set_ratio);
