@@ -37,11 +37,11 @@ def cpu_model():
     return platform.processor()
 
 
-def make_pairs(n_pairs, n_points, seed0):
+def make_pairs(indices, n_points, seed0=1000):
     from aicp_mapping_amd import synthetic as sy
 
     out = []
-    for i in range(n_pairs):
+    for i in indices:
         pr = sy.make_pair(n_points, n_points, seed=seed0 + i)
         out.append(dict(ref=pr.ref, read=pr.read, ref_origin=pr.ref_origin, read_origin=pr.read_origin,
                         T_gt=pr.T_gt))
@@ -108,9 +108,11 @@ def main():
         dist.init_process_group(backend="nccl")
 
     import aicp_mapping_amd._lib as L
+    from aicp_mapping_amd import sharding as sh
 
     res = float(np.float32(0.2))  # octomapResolution read as<float> (yaml_configurator.cpp:81)
-    pairs = make_pairs(args.pairs, args.points, seed0=1000 + rank * args.pairs)
+    # global pair i (seed 1000 + i) belongs to rank i mod world; P pairs per rank (weak scaling)
+    pairs = make_pairs(sh.shard_pairs(args.pairs * world, world, rank), args.points)
     ctx = L.Context(local_rank)
     batch = ctx.upload(pairs)
     cfg = L.default_config()
@@ -119,18 +121,9 @@ def main():
     def gather():
         if dist is None:
             return None
-        import torch
-
-        T = batch.outT
         st = batch.stats
-        rec = np.zeros((args.pairs, 18), np.float32)
-        rec[:, :16] = T
-        rec[:, 16] = [s.iterations for s in st]
-        rec[:, 17] = [s.inlier_ratio for s in st]
-        t = torch.from_numpy(rec).cuda()
-        out = torch.empty((world * args.pairs, 18), dtype=torch.float32, device="cuda")
-        dist.all_gather_into_tensor(out, t)
-        return out
+        rec = sh.pack_records(batch.outT, [s.iterations for s in st], [s.inlier_ratio for s in st])
+        return sh.gather_records(rec, dist, device="cuda")
 
     def sync():
         if dist is not None:
@@ -161,15 +154,8 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        import torch
-
-        e = torch.tensor([elapsed, float(iters_total)], dtype=torch.float64, device="cuda")
-        emax = e.clone()
-        dist.all_reduce(emax, op=dist.ReduceOp.MAX)
-        esum = e.clone()
-        dist.all_reduce(esum, op=dist.ReduceOp.SUM)
-        elapsed = float(emax[0])
-        iters_total = int(esum[1])
+        elapsed = sh.max_over_ranks(elapsed, dist, device="cuda")
+        iters_total = int(sh.sum_over_ranks(float(iters_total), dist, device="cuda"))
 
     # accuracy of the last step (synthetic ground truth)
     from aicp_mapping_amd import synthetic as sy
