@@ -46,6 +46,7 @@ struct PairDesc {
   uint32_t read_off, n_read;    // into reading arrays
   uint32_t node_off, n_nodes;   // into nodes/parent
   uint32_t red_blk_off, n_red_blk;  // reduce blocks of this pair (slab rows)
+  float Tin[16];                // initial transform T0 (column-major)
   float Tinit[16];              // T_refMean_dataIn (column-major)
   float Tmean[16];              // T_refIn_refMean
   float mean[3];                // reference centroid (float)
@@ -80,6 +81,38 @@ struct PairState {
   int32_t pad_;
   double qh[kHistRing][4];
   double th[kHistRing][3];
+};
+
+// ---- device kd-tree construction (kernels_tree.hip) ----------------------------------------
+// A segment = a node still to split at the current level (count > bucket).
+struct TreeSeg {
+  uint32_t first, count;   // global point positions
+  int32_t pair, depth;
+  float mn[3], mx[3];      // node box (libnabo implicit bounds)
+  int32_t cd;
+  float ideal;             // (mx[cd] + mn[cd]) / 2
+  uint32_t lo, hi;         // ordered-int min / max of the points' cd coordinate
+  uint32_t br1, br2, left;
+  int32_t child[2];        // next-level segment index, -1 for a leaf child
+  int32_t parent_f, parent_depth;  // the parent node's first position and depth (-1: root)
+  uint32_t bmn[3], bmx[3]; // root only: ordered-int box of the centred points
+};
+
+// One record per node, emitted in any order; the preorder index is computed afterwards.
+struct NodeEvent {
+  uint32_t f, c;           // point range [f, f + c), global positions
+  int32_t depth, pair;
+  uint32_t cut_bits;
+  int32_t cd;              // kLeaf for a leaf
+  uint32_t left;           // left child point count
+  uint32_t parent_f;
+  int32_t parent_depth;    // -1 at the root
+};
+
+struct TreeCtl {
+  uint32_t nseg[kFarStack + 2];  // segments per level
+  uint32_t n_events;
+  int32_t error;
 };
 
 struct IcpParams {

@@ -1,13 +1,14 @@
 // aicp_hip.cpp — C-ABI of libaicp_hip.so: context, device arena, batch pipeline.
 //
 // One batch run (aicp_hip_batch_run) for P pairs, one HIP stream, no per-iteration host sync:
-//   1. [device] overlap: origin/endpoint key boxes (k_ovl_init, k_ovl_bbox) -> async D2H
-//   2. [host, overlapped with 1] per pair: centroid, centred reference, libnabo-order kd-tree
-//      (ICP::compute "matcher->init(reference)"), one std::thread per pair up to 16
-//   3. [device] voxel maps sized from the boxes; DDA ray marking, sums, overlap% and the
-//      auto-tuned ratio per pair (App::computeRegistration, app.cpp:197-205)
-//   4. [device] gather centred reference into bucket order, reading into the ref-mean
-//      frame, SurfaceNormal on the reference (k_normals)
+//   1. [device] overlap: origin/endpoint key boxes (k_ovl_init, k_ovl_bbox) -> D2H (the only
+//      host sync before the loop: it sizes the voxel maps)
+//   2. [device] voxel maps; DDA ray marking, sums, overlap% and the auto-tuned ratio per pair
+//      (App::computeRegistration, app.cpp:197-205)
+//   3. [device] centroid, centred reference and the libnabo-order kd-tree of every pair
+//      (ICP::compute "matcher->init(reference)", kernels_tree.hip), level by level; the host
+//      polls the segment count every few levels
+//   4. [device] reading into the ref-mean frame, SurfaceNormal on the reference
 //   5. [device] max_iter x {NN, select, reduce, update}; converged pairs exit early
 //   6. [device] T = T_refIn_refMean * T_iter * T_refMean_dataIn; D2H of T and pair states
 #include <hip/hip_runtime.h>
@@ -19,13 +20,11 @@
 #include <cstring>
 #include <limits>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/aicp_hip.h"
 #include "aicp_common.hpp"
 #include "icp_math.hpp"
-#include "kdtree_host.hpp"
 #include "kernels.hpp"
 
 using namespace aicp;
@@ -97,8 +96,6 @@ struct Maps {  // block maps of one flat grid
 struct aicp_hip_batch {
   size_t P = 0;
   std::vector<PairDesc> desc;
-  std::vector<std::vector<float>> ref_host;  // packed xyz (tree build input)
-  std::vector<float> initT;                  // 16 per pair
   uint64_t total_ref = 0, total_read = 0;
   uint32_t n_red_total = 0;
   DevBuf ref_raw, read_raw, maps;
@@ -109,10 +106,12 @@ struct aicp_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf read_c, bpts, bnrm, nodes, parent, perm, match, d2, desc, state, touch, slab, bitmap,
-      outT, scratch, active, ctrs, nbids;
-  PinBuf pin_desc, pin_tree, pin_state, pin_out, pin_io;
-  std::vector<HostTree> trees;
+  DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
+      ctrs, nbids, ref1;
+  // kd-tree construction work space (kernels_tree.hip)
+  DevBuf tw_W0, tw_W1, tw_segof0, tw_segof1, tw_seg0, tw_seg1, tw_flag, tw_X1, tw_X2, tw_posL, tw_posR, tw_ev,
+      tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
+  PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev[8] = {};
   int last_nn_launches = 0;
@@ -185,8 +184,6 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   if (!pairs || n == 0) FAIL(AICP_ERR_INVALID, "no pairs");
   B->P = n;
   B->desc.assign(n, PairDesc{});
-  B->ref_host.resize(n);
-  B->initT.assign(16 * n, 0.f);
   uint64_t ro = 0, wo = 0;
   uint32_t red = 0;
   Maps mr, mf, md;
@@ -209,11 +206,9 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     wo += p.n_read;
     if (ro >= (1ull << 31) || wo >= (1ull << 31)) FAIL(AICP_ERR_UNSUPPORTED, "batch too large");
     if (p.init_T)
-      std::memcpy(&B->initT[16 * i], p.init_T, 64);
+      std::memcpy(d.Tin, p.init_T, 64);
     else
-      ident4(&B->initT[16 * i]);
-    B->ref_host[i].resize(3 * p.n_ref);
-    pack_xyz(p.ref, p.n_ref, p.ref_stride, B->ref_host[i].data());
+      ident4(d.Tin);
     mr.add((int)i, d.n_read, kNNBlock);
     mf.add((int)i, d.n_ref, kNNBlock);
     md.add((int)i, d.n_read, kNNBlock * kReducePerThread);
@@ -263,35 +258,75 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   return AICP_OK;
 }
 
-void build_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, std::vector<float>& means) {
-  const size_t P = B->P;
-  ctx->trees.resize(P);
-  means.assign(3 * P, 0.f);
-  auto work = [&](size_t i) {
-    const std::vector<float>& ref = B->ref_host[i];
-    const size_t m = ref.size() / 3;
-    double acc[3] = {0, 0, 0};
-    for (size_t k = 0; k < m; ++k)
-      for (int d = 0; d < 3; ++d) acc[d] += (double)ref[3 * k + d];
-    float mu[3];
-    for (int d = 0; d < 3; ++d) mu[d] = (float)(acc[d] / (double)m);
-    std::vector<float> c(3 * m);
-    for (size_t k = 0; k < m; ++k)
-      for (int d = 0; d < 3; ++d) c[3 * k + d] = ref[3 * k + d] - mu[d];
-    build_kdtree_host(c.data(), (int64_t)m, bucket, ctx->trees[i]);
-    for (int d = 0; d < 3; ++d) means[3 * i + d] = mu[d];
-  };
-  const size_t nt = std::min<size_t>(P, std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())));
-  if (nt <= 1) {
-    for (size_t i = 0; i < P; ++i) work(i);
-    return;
+// Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device: raw[ΣM] float4,
+// dDesc with ref_off / n_ref / Tin. Writes ctx->bpts (bucket order, w = local id), ctx->nodes
+// and the desc fields mean, Tmean, Tinit, node_off, n_nodes, tree_depth.
+int device_trees(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc, const float4* raw,
+                 int center, int bucket) {
+  const size_t n = (size_t)total;
+  const size_t max_seg = n / 2 + P + 1;
+  HIPC(ensure(ctx->bpts, n * 16));
+  HIPC(ensure(ctx->nodes, (2 * n + 2) * 16));
+  HIPC(ensure(ctx->tw_W0, n * 16));
+  HIPC(ensure(ctx->tw_W1, n * 16));
+  HIPC(ensure(ctx->tw_segof0, n * 4));
+  HIPC(ensure(ctx->tw_segof1, n * 4));
+  HIPC(ensure(ctx->tw_seg0, max_seg * sizeof(TreeSeg)));
+  HIPC(ensure(ctx->tw_seg1, max_seg * sizeof(TreeSeg)));
+  HIPC(ensure(ctx->tw_flag, (n + 2) * 4));
+  HIPC(ensure(ctx->tw_X1, (n + 2) * 4));
+  HIPC(ensure(ctx->tw_X2, (n + 2) * 4));
+  HIPC(ensure(ctx->tw_posL, n * 4));
+  HIPC(ensure(ctx->tw_posR, n * 4));
+  HIPC(ensure(ctx->tw_ev, (2 * n + 2) * sizeof(NodeEvent)));
+  HIPC(ensure(ctx->tw_ecnt, (n + 2) * 4));
+  HIPC(ensure(ctx->tw_sums, P * 6 * 8));
+  HIPC(ensure(ctx->tw_pdepth, P * 4));
+  HIPC(ensure(ctx->tw_ctl, sizeof(TreeCtl)));
+  const size_t tb = tree_scan_temp_bytes(n + 2);
+  HIPC(ensure(ctx->tw_scan, tb));
+  HIPC(ensure(ctx->pin_ctl, sizeof(TreeCtl)));
+  TreeWork w{};
+  w.W[0] = ctx->tw_W0.as<float4>();
+  w.W[1] = ctx->tw_W1.as<float4>();
+  w.segof[0] = ctx->tw_segof0.as<int32_t>();
+  w.segof[1] = ctx->tw_segof1.as<int32_t>();
+  w.seg[0] = ctx->tw_seg0.as<TreeSeg>();
+  w.seg[1] = ctx->tw_seg1.as<TreeSeg>();
+  w.flag = ctx->tw_flag.as<uint32_t>();
+  w.X1 = ctx->tw_X1.as<uint32_t>();
+  w.X2 = ctx->tw_X2.as<uint32_t>();
+  w.posL = ctx->tw_posL.as<uint32_t>();
+  w.posR = ctx->tw_posR.as<uint32_t>();
+  w.ev = ctx->tw_ev.as<NodeEvent>();
+  w.ecnt = ctx->tw_ecnt.as<uint32_t>();
+  w.sums = ctx->tw_sums.as<uint64_t>();
+  w.pair_depth = ctx->tw_pdepth.as<int32_t>();
+  w.ctl = ctx->tw_ctl.as<TreeCtl>();
+  w.scan_temp = ctx->tw_scan.p;
+  w.scan_temp_bytes = ctx->tw_scan.cap;
+  w.max_seg = max_seg;
+  float4* bpts = ctx->bpts.as<float4>();
+  HIPC(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts, bucket));
+  TreeCtl* hctl = ctx->pin_ctl.as<TreeCtl>();
+  bool done = false;
+  for (int level = 0; level < kFarStack - 1 && !done; ++level) {
+    HIPC(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket));
+    // poll the next level's segment count every few levels (and at the depth limit)
+    const bool poll = (level >= 9 && (level % 3) == 0) || level == kFarStack - 2;
+    if (poll) {
+      HIPC(hipMemcpyAsync(&hctl->nseg[level + 1], &w.ctl->nseg[level + 1], 4, hipMemcpyDeviceToHost, s));
+      HIPC(hipStreamSynchronize(s));
+      if (hctl->nseg[level + 1] == 0) done = true;
+    }
   }
-  std::vector<std::thread> th;
-  for (size_t t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
-      for (size_t i = t; i < P; i += nt) work(i);
-    });
-  for (auto& x : th) x.join();
+  if (!done) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
+  HIPC(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, ctx->nodes.as<uint4>()));
+  HIPC(hipMemcpyAsync(&hctl->error, &w.ctl->error, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  if (hctl->error & 1) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
+  if (hctl->error) FAIL(AICP_ERR_HIP, "kd-tree construction overflow " + std::to_string(hctl->error));
+  return AICP_OK;
 }
 
 double ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -331,7 +366,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   HIPC(ensure(ctx->pin_out, P * 64));
   PairDesc* pdA = ctx->pin_desc.as<PairDesc>();
   PairDesc* pdB = pdA + P;
-  PairDesc* pdC = pdB + P;
+  PairDesc* pdC = pdB + P;  // device descriptors read back at the end
   PairDesc* dDesc = ctx->desc.as<PairDesc>();
   PairState* dState = ctx->state.as<PairState>();
   uint32_t* dCtr = ctx->ctrs.as<uint32_t>();
@@ -346,8 +381,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
   }
   HIPC(hipEventRecord(ctx->ev[1], s));
-  // overlap: size the voxel maps from the key boxes, then mark (device) while the host builds
-  // the kd-trees
+  // overlap: size the voxel maps from the key boxes, then mark
   uint64_t bm_bytes = 0;
   if (doOvl) {
     HIPC(hipEventSynchronize(ctx->ev[1]));
@@ -379,53 +413,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     launch_ovl_finish(s, (int)P, dState, doIcp ? 1 : 0);
   }
   HIPC(hipEventRecord(ctx->ev[2], s));
-  // host: kd-trees (overlaps the device work above)
-  std::vector<float> means;
-  double tree_ms = 0;
-  uint64_t total_nodes = 0;
+  // device: centroid + kd-trees
   if (doIcp) {
-    const auto t0 = std::chrono::steady_clock::now();
-    build_trees(ctx, B, cfg->bucket_size, means);
-    tree_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    for (size_t i = 0; i < P; ++i) {
-      const HostTree& t = ctx->trees[i];
-      if (t.depth >= kFarStack) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack");
-      PairDesc& d = desc[i];
-      d.node_off = (uint32_t)total_nodes;
-      d.n_nodes = (uint32_t)t.parent.size();
-      d.tree_depth = t.depth;
-      total_nodes += d.n_nodes;
-      for (int k = 0; k < 3; ++k) d.mean[k] = means[3 * i + k];
-      float Tm[16], Tmi[16];
-      ident4(Tm);
-      ident4(Tmi);
-      for (int k = 0; k < 3; ++k) {
-        Tm[12 + k] = d.mean[k];
-        Tmi[12 + k] = -d.mean[k];
-      }
-      std::memcpy(d.Tmean, Tm, 64);
-      mul4(Tmi, &B->initT[16 * i], d.Tinit);
-    }
-    if (total_nodes >= (1ull << 30)) FAIL(AICP_ERR_UNSUPPORTED, "too many kd-tree nodes");
-    // full descriptor + kd-trees
-    std::memcpy(pdC, desc.data(), P * sizeof(PairDesc));
-    HIPC(hipMemcpyAsync(dDesc, pdC, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
-    const size_t permB = B->total_ref * 4, nodeB = total_nodes * 16, parB = total_nodes * 4;
-    HIPC(ensure(ctx->pin_tree, permB + nodeB + parB));
-    HIPC(ensure(ctx->perm, permB));
-    HIPC(ensure(ctx->nodes, nodeB));
-    HIPC(ensure(ctx->parent, parB));
-    char* base = ctx->pin_tree.as<char>();
-    for (size_t i = 0; i < P; ++i) {
-      const HostTree& t = ctx->trees[i];
-      const PairDesc& d = desc[i];
-      std::memcpy(base + 4ull * d.ref_off, t.perm.data(), 4ull * d.n_ref);
-      std::memcpy(base + permB + 16ull * d.node_off, t.nodes.data(), 16ull * d.n_nodes);
-      std::memcpy(base + permB + nodeB + 4ull * d.node_off, t.parent.data(), 4ull * d.n_nodes);
-    }
-    HIPC(hipMemcpyAsync(ctx->perm.p, base, permB, hipMemcpyHostToDevice, s));
-    HIPC(hipMemcpyAsync(ctx->nodes.p, base + permB, nodeB, hipMemcpyHostToDevice, s));
-    HIPC(hipMemcpyAsync(ctx->parent.p, base + permB + nodeB, parB, hipMemcpyHostToDevice, s));
+    rc = device_trees(ctx, s, P, B->total_ref, dDesc, B->ref_raw.as<float4>(), 1, cfg->bucket_size);
+    if (rc) return rc;
   }
   HIPC(hipEventRecord(ctx->ev[3], s));
   IcpParams prm{};
@@ -442,8 +433,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     float4* bnrm = ctx->bnrm.as<float4>();
     float4* readc = ctx->read_c.as<float4>();
     const uint4* nodes = ctx->nodes.as<uint4>();
-    const int32_t* parent = ctx->parent.as<int32_t>();
-    launch_gather_ref(s, B->m_ref, dDesc, B->ref_raw.as<float4>(), ctx->perm.as<int32_t>(), bpts);
+    const int32_t* parent = nullptr;
     launch_prepare_read(s, B->m_read, dDesc, B->read_raw.as<float4>(), readc);
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
     uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
@@ -480,6 +470,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   HIPC(hipEventRecord(ctx->ev[5], s));
   HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
   if (doIcp) HIPC(hipMemcpyAsync(ctx->pin_out.p, ctx->outT.p, P * 64, hipMemcpyDeviceToHost, s));
+  HIPC(hipMemcpyAsync(pdC, dDesc, P * sizeof(PairDesc), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   // results
   const PairState* hs = ctx->pin_state.as<PairState>();
@@ -506,7 +497,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       o.inlier_ratio = st.inlier_ratio;
       o.trimmed_ratio = st.ratio;
       o.overlap_percent = st.overlap;
-      o.tree_depth = desc[i].tree_depth;
+      o.tree_depth = pdC[i].tree_depth;
       o.nn_points_touched = ptp;
       o.nn_nodes_touched = ptn;
       for (int k = 0; k < 3; ++k) o.overlap_keys[k] = st.ovl_counts[k];
@@ -520,7 +511,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   ctx->last_nn_bytes = (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0;
   ctx->last_queries = queries;
   ctx->last_phase[0] = doOvl ? ev_ms(ctx->ev[0], ctx->ev[1]) + ev_ms(ctx->ev[6], ctx->ev[2]) : 0;
-  ctx->last_phase[1] = tree_ms;
+  ctx->last_phase[1] = doIcp ? ev_ms(ctx->ev[2], ctx->ev[3]) : 0;
   ctx->last_phase[2] = doIcp ? ev_ms(ctx->ev[3], ctx->ev[4]) : 0;
   ctx->last_phase[3] = doIcp ? ev_ms(ctx->ev[4], ctx->ev[5]) : 0;
   ctx->last_phase[4] =
@@ -537,28 +528,23 @@ void free_batch(aicp_hip_batch* B) {
   delete B;
 }
 
-// single-pair tree on arbitrary points for the kernel-level entry points
-int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, HostTree& t) {
-  std::vector<float> xyz(3 * n);
-  pack_xyz(pts, n, stride, xyz.data());
-  build_kdtree_host(xyz.data(), (int64_t)n, 8, t);
-  if (t.depth >= kFarStack) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack");
-  HIPC(ensure(ctx->bpts, n * 16));
-  HIPC(ensure(ctx->nodes, t.parent.size() * 16));
-  HIPC(ensure(ctx->parent, t.parent.size() * 4));
-  HIPC(ensure(ctx->pin_io, std::max(n * 16, t.parent.size() * 16)));
-  float* b = ctx->pin_io.as<float>();
-  for (size_t j = 0; j < n; ++j) {
-    const int32_t id = t.perm[j];
-    b[4 * j] = xyz[3 * id];
-    b[4 * j + 1] = xyz[3 * id + 1];
-    b[4 * j + 2] = xyz[3 * id + 2];
-    std::memcpy(&b[4 * j + 3], &id, 4);
-  }
-  HIPC(hipMemcpyAsync(ctx->bpts.p, b, n * 16, hipMemcpyHostToDevice, ctx->stream));
-  HIPC(hipMemcpyAsync(ctx->nodes.p, t.nodes.data(), t.parent.size() * 16, hipMemcpyHostToDevice, ctx->stream));
-  HIPC(hipMemcpyAsync(ctx->parent.p, t.parent.data(), t.parent.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  HIPC(hipStreamSynchronize(ctx->stream));
+// single-cloud kd-tree on the points as given (no centring) for the kernel-level entry points
+int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, PairDesc& d) {
+  hipStream_t s = ctx->stream;
+  HIPC(ensure(ctx->ref1, n * 16));
+  HIPC(ensure(ctx->pin_io, n * 16));
+  pack_xyz4(pts, n, stride, ctx->pin_io.as<float>());
+  HIPC(hipMemcpyAsync(ctx->ref1.p, ctx->pin_io.p, n * 16, hipMemcpyHostToDevice, s));
+  d = PairDesc{};
+  d.n_ref = (uint32_t)n;
+  d.ratio = 0.5f;
+  ident4(d.Tin);
+  HIPC(ensure(ctx->desc, sizeof(PairDesc)));
+  HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
+  const int rc = device_trees(ctx, s, 1, n, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8);
+  if (rc) return rc;
+  HIPC(hipMemcpyAsync(&d, ctx->desc.p, sizeof(d), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
   return AICP_OK;
 }
 
@@ -589,11 +575,14 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->parent, &ctx->perm, &ctx->match,
-                    &ctx->d2, &ctx->desc, &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT,
-                    &ctx->scratch, &ctx->active, &ctx->ctrs, &ctx->nbids})
+  for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->match, &ctx->d2, &ctx->desc,
+                    &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
+                    &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
+                    &ctx->tw_segof1, &ctx->tw_seg0, &ctx->tw_seg1, &ctx->tw_flag, &ctx->tw_X1, &ctx->tw_X2,
+                    &ctx->tw_posL, &ctx->tw_posR, &ctx->tw_ev, &ctx->tw_ecnt, &ctx->tw_sums, &ctx->tw_pdepth,
+                    &ctx->tw_ctl, &ctx->tw_scan})
     release(*b);
-  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_tree, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io}) release(*b);
+  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_ctl, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io}) release(*b);
   for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
   for (auto e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -709,8 +698,8 @@ int aicp_hip_knn(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, c
                  uint64_t* out_touched) {
   if (!ctx || !pts || !queries || !out_ids || !out_d2 || n == 0 || stride < 12 || qstride < 12) return AICP_ERR_INVALID;
   HIPC(hipSetDevice(ctx->device));
-  HostTree t;
-  int rc = upload_tree(ctx, pts, n, stride, t);
+  PairDesc td;
+  int rc = upload_tree(ctx, pts, n, stride, td);
   if (rc) return rc;
   hipStream_t st_ = ctx->stream;
   HIPC(ensure(ctx->read_c, nq * 16 + 16));
@@ -725,7 +714,7 @@ int aicp_hip_knn(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, c
   const float maxE2 = (1 + epsilon) * (1 + epsilon);
   const float maxR2 = max_dist * max_dist;
   if (!launch_knn_generic(st_, (uint32_t)nq, ctx->read_c.as<float4>(), ctx->nodes.as<uint4>(),
-                          ctx->parent.as<int32_t>(), ctx->bpts.as<float4>(), k, maxE2, maxR2,
+                          nullptr, ctx->bpts.as<float4>(), k, maxE2, maxR2,
                           ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->scratch.as<unsigned long long>(),
                           (uint32_t*)(ctx->scratch.as<char>() + 16)))
     FAIL(AICP_ERR_UNSUPPORTED, "k must be 1, 4, 10, 20 or 30");
@@ -741,34 +730,32 @@ int aicp_hip_normals(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t strid
                      int32_t* out_degenerate) {
   if (!ctx || !pts || !out_normals || n == 0 || stride < 12) return AICP_ERR_INVALID;
   HIPC(hipSetDevice(ctx->device));
-  HostTree t;
-  int rc = upload_tree(ctx, pts, n, stride, t);
+  PairDesc d;
+  int rc = upload_tree(ctx, pts, n, stride, d);
   if (rc) return rc;
   hipStream_t st_ = ctx->stream;
-  PairDesc d{};
-  d.n_ref = (uint32_t)n;
-  d.n_nodes = (uint32_t)t.parent.size();
-  d.ratio = 0.5f;
-  HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(ensure(ctx->state, sizeof(PairState)));
   HIPC(ensure(ctx->bnrm, n * 16));
   HIPC(ensure(ctx->nbids, n * 4 * (size_t)std::max(knn, 1)));
   HIPC(ensure(ctx->ctrs, kCtrWords * 4));
-  HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, st_));
   HIPC(hipMemsetAsync(ctx->ctrs.p, 0, kCtrWords * 4, st_));
   launch_init_state(st_, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>());
   if (!launch_normals(st_, 1, (uint32_t)n, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(),
-                      ctx->nodes.as<uint4>(), ctx->parent.as<int32_t>(), ctx->bpts.as<float4>(),
+                      ctx->nodes.as<uint4>(), nullptr, ctx->bpts.as<float4>(),
                       ctx->bnrm.as<float4>(), knn, ctx->nbids.as<int32_t>(), ctx->ctrs.as<uint32_t>()))
     FAIL(AICP_ERR_UNSUPPORTED, "knn must be 10, 20 or 30");
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(st_));
-  std::vector<float> nb(4 * n);
+  std::vector<float> nb(4 * n), bp(4 * n);
   HIPC(hipMemcpy(nb.data(), ctx->bnrm.p, n * 16, hipMemcpyDeviceToHost));
+  HIPC(hipMemcpy(bp.data(), ctx->bpts.p, n * 16, hipMemcpyDeviceToHost));
   PairState st;
   HIPC(hipMemcpy(&st, ctx->state.p, sizeof(st), hipMemcpyDeviceToHost));
-  for (size_t j = 0; j < n; ++j)
-    for (int k = 0; k < 3; ++k) out_normals[3 * (size_t)t.perm[j] + k] = nb[4 * j + k];
+  for (size_t j = 0; j < n; ++j) {
+    int32_t id;
+    std::memcpy(&id, &bp[4 * j + 3], 4);  // bucket position -> input index
+    for (int k = 0; k < 3; ++k) out_normals[3 * (size_t)id + k] = nb[4 * j + k];
+  }
   if (out_degenerate) *out_degenerate = st.degenerate;
   return AICP_OK;
 }

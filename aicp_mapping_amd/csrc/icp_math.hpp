@@ -430,3 +430,30 @@ AICP_HD float autotune_ratio_fast(float overlap_percent) {
 }
 
 }  // namespace aicp
+
+namespace aicp {
+
+// ---- reference centroid (ICP::compute step 2) ----------------------------------
+// Order-independent definition shared with the oracle: every coordinate is rounded to a
+// multiple of 2^-40 (exact for |x| >= 2^-16; |x| < 2^23 m), summed exactly in 128-bit
+// two's complement, and mean = float((|S| as double) * 2^-40 / n) with the sign applied.
+AICP_HD int64_t fixed40(float x) {
+  const double v = rint((double)x * 1099511627776.0);
+  const double lim = 9.2233720368547748e18;  // 2^63
+  if (!(v < lim)) return INT64_MAX;
+  if (!(v > -lim)) return INT64_MIN;
+  return (int64_t)v;
+}
+
+AICP_HD float mean_from_fixed40(uint64_t lo, uint64_t hi, uint32_t n) {
+  const bool neg = (int64_t)hi < 0;
+  if (neg) {
+    lo = ~lo + 1;
+    hi = ~hi + (lo == 0 ? 1 : 0);
+  }
+  const double mag = (double)hi * 18446744073709551616.0 + (double)lo;
+  const double m = mag * (1.0 / 1099511627776.0) / (double)n;
+  return (float)(neg ? -m : m);
+}
+
+}  // namespace aicp

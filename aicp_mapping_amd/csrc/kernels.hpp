@@ -49,6 +49,36 @@ bool launch_knn_generic(hipStream_t s, uint32_t nq, const float4* q, const uint4
 void launch_transform(hipStream_t s, int n, const float* T, const float4* in, float4* out);
 void launch_solve6(hipStream_t s, const double* A, const double* b, double* x, int32_t* path);
 
+// ---- kd-tree construction (kernels_tree.hip) ---------------------------------------------
+struct TreeWork {
+  float4* W[2];          // points being partitioned (ping-pong), total
+  int32_t* segof[2];     // segment of each position at the current / next level, total
+  TreeSeg* seg[2];       // segments of the current / next level, max_seg
+  uint32_t* flag;        // total + 2
+  uint32_t* X1;          // scans, total + 2
+  uint32_t* X2;
+  uint32_t* posL;        // partner positions, total
+  uint32_t* posR;
+  NodeEvent* ev;         // 2 * total
+  uint32_t* ecnt;        // nodes ending at each position, total + 2
+  uint64_t* sums;        // 6 per pair (128-bit fixed-point coordinate sums)
+  int32_t* pair_depth;   // per pair
+  TreeCtl* ctl;
+  void* scan_temp;
+  size_t scan_temp_bytes;
+  size_t max_seg;
+};
+size_t tree_scan_temp_bytes(size_t n);
+// centroid (center = 1) + frames in pd, centred points, root segments
+hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
+                               int center, const TreeWork& w, float4* bpts, int bucket);
+// one level: nodes at depth `level` are split (their children get depth level + 1)
+hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const TreeWork& w, float4* bpts,
+                             int bucket);
+// node records (preorder) and PairDesc node_off / n_nodes / tree_depth
+hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const TreeWork& w,
+                              uint4* nodes);
+
 // ---- overlap -------------------------------------------------------------------------------
 void launch_ovl_init(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
                      double res);

@@ -30,6 +30,24 @@
 
 namespace {
 
+// round(x * 2^40) as int64 (|x| < 2^23), saturating
+int64_t fixed40(float x) {
+  const double v = std::rint((double)x * 1099511627776.0);
+  if (!(v < 9.2233720368547748e18)) return INT64_MAX;
+  if (!(v > -9.2233720368547748e18)) return INT64_MIN;
+  return (int64_t)v;
+}
+
+float mean_fixed40(__int128 acc, uint64_t n) {
+  const bool neg = acc < 0;
+  const unsigned __int128 mag = neg ? (unsigned __int128)(-acc) : (unsigned __int128)acc;
+  const uint64_t hi = (uint64_t)(mag >> 64), lo = (uint64_t)mag;
+  const double dm = (double)hi * 18446744073709551616.0 + (double)lo;
+  const double mm = dm * (1.0 / 1099511627776.0) / (double)n;
+  return (float)(neg ? -mm : mm);
+}
+
+
 constexpr float kInf = std::numeric_limits<float>::infinity();
 
 // ------------------------------------------------------------------------------------------
@@ -1013,12 +1031,16 @@ int ao_icp(const float* ref, int64_t m, int64_t rs, const float* read, int64_t n
   int32_t deg = 0;
   if (!cfg->normals_on_centered) normals_impl(ref, m, rs, cfg->knn_normals, refn.data(), nullptr, &deg);
 
-  // 2. centre of mass (double accumulation, rounded to float) and centred reference
-  double acc[3] = {0, 0, 0};
-  for (int64_t i = 0; i < m; ++i)
-    for (int d = 0; d < 3; ++d) acc[d] += (double)ref[i * rs + d];
+  // 2. centre of mass and centred reference. The reference's Eigen float row sum depends on
+  // the summation order; this restatement fixes an order-independent definition that the
+  // device shares: coordinates rounded to multiples of 2^-40, summed exactly
+  // (128-bit), then |S| as double * 2^-40 / m rounded to float.
   float mean[3];
-  for (int d = 0; d < 3; ++d) mean[d] = (float)(acc[d] / (double)m);
+  for (int d = 0; d < 3; ++d) {
+    __int128 acc = 0;
+    for (int64_t i = 0; i < m; ++i) acc += (__int128)fixed40(ref[i * rs + d]);
+    mean[d] = mean_fixed40(acc, (uint64_t)m);
+  }
   std::vector<float> refc((size_t)m * 3);
   for (int64_t i = 0; i < m; ++i)
     for (int d = 0; d < 3; ++d) refc[3 * i + d] = ref[i * rs + d] - mean[d];

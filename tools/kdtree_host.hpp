@@ -1,4 +1,5 @@
-// kdtree_host.hpp — libnabo-order kd-tree construction emitting the device node layout.
+// kdtree_host.hpp — host libnabo-order kd-tree (tools only: the library builds trees on the device,
+// kernels_tree.hip) emitting the device node layout.
 //
 // Same splitting rule as libnabo's KDTreeUnbalancedPtInLeavesImplicitBoundsStackOpt::
 // buildNodes (configured by KDTreeMatcher at icp_autotuned_default.yaml:27-30):

@@ -8,7 +8,7 @@
 #include <cstring>
 #include <string>
 #include <algorithm>
-#include "../aicp_mapping_amd/csrc/kdtree_host.hpp"
+#include "kdtree_host.hpp"
 #include "../aicp_mapping_amd/csrc/kernels.hpp"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
