@@ -78,6 +78,7 @@ struct PairState {
   uint64_t ovl_counts[3];
   int32_t ovl_bbox[6];  // kmin[3], kmax[3] (union of both clouds)
   int32_t ovl_err;
+  uint32_t sel_b1, sel_r1;  // trimmed select: digit-1 bin of the k-th value and its rank in it
   int32_t pad_;
   double qh[kHistRing][4];
   double th[kHistRing][3];
@@ -93,12 +94,14 @@ struct TreeSeg {
   float ideal;             // (mx[cd] + mn[cd]) / 2
   uint32_t lo, hi;         // ordered-int min / max of the points' cd coordinate
   uint32_t br1, br2, left;
-  int32_t child[2];        // next-level segment index, -1 for a leaf child
+  int32_t child[2];        // next-level segment index; -1 leaf child; -2 subtree (SubSeg) child
   int32_t parent_f, parent_depth;  // the parent node's first position and depth (-1: root)
   uint32_t bmn[3], bmx[3]; // root only: ordered-int box of the centred points
 };
 
-// One record per node, emitted in any order; the preorder index is computed afterwards.
+// One record per node, in a slot of its own: a leaf at its first position, an inner node at
+// total + its split position (first + left), which no other node shares; the preorder index
+// is computed afterwards.
 struct NodeEvent {
   uint32_t f, c;           // point range [f, f + c), global positions
   int32_t depth, pair;
@@ -109,9 +112,19 @@ struct NodeEvent {
   int32_t parent_depth;    // -1 at the root
 };
 
+// A segment small enough for one wave to finish its whole subtree in LDS (k_tr_subtree).
+constexpr int kSubMax = 1024;
+struct SubSeg {
+  uint32_t f, c;
+  int32_t pair, depth;
+  float mn[3], mx[3];
+  uint32_t parent_f;
+  int32_t parent_depth;
+};
+
 struct TreeCtl {
-  uint32_t nseg[kFarStack + 2];  // segments per level
-  uint32_t n_events;
+  uint32_t nseg[kFarStack + 2];  // segments per global level
+  uint32_t n_small;              // SubSeg entries
   int32_t error;
 };
 

@@ -107,10 +107,10 @@ struct aicp_hip_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
-      ctrs, nbids, ref1;
+      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap;
   // kd-tree construction work space (kernels_tree.hip)
   DevBuf tw_W0, tw_W1, tw_segof0, tw_segof1, tw_seg0, tw_seg1, tw_flag, tw_X1, tw_X2, tw_posL, tw_posR, tw_ev,
-      tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
+      tw_valid, tw_subs, tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
   PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev[8] = {};
@@ -279,6 +279,8 @@ int device_trees(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, Pai
   HIPC(ensure(ctx->tw_posL, n * 4));
   HIPC(ensure(ctx->tw_posR, n * 4));
   HIPC(ensure(ctx->tw_ev, (2 * n + 2) * sizeof(NodeEvent)));
+  HIPC(ensure(ctx->tw_valid, 2 * n + 2));
+  HIPC(ensure(ctx->tw_subs, max_seg * sizeof(SubSeg)));
   HIPC(ensure(ctx->tw_ecnt, (n + 2) * 4));
   HIPC(ensure(ctx->tw_sums, P * 6 * 8));
   HIPC(ensure(ctx->tw_pdepth, P * 4));
@@ -299,6 +301,9 @@ int device_trees(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, Pai
   w.posL = ctx->tw_posL.as<uint32_t>();
   w.posR = ctx->tw_posR.as<uint32_t>();
   w.ev = ctx->tw_ev.as<NodeEvent>();
+  w.valid = ctx->tw_valid.as<uint8_t>();
+  w.subs = ctx->tw_subs.as<SubSeg>();
+  w.n_pairs = (int)P;
   w.ecnt = ctx->tw_ecnt.as<uint32_t>();
   w.sums = ctx->tw_sums.as<uint64_t>();
   w.pair_depth = ctx->tw_pdepth.as<int32_t>();
@@ -309,18 +314,19 @@ int device_trees(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, Pai
   float4* bpts = ctx->bpts.as<float4>();
   HIPC(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts, bucket));
   TreeCtl* hctl = ctx->pin_ctl.as<TreeCtl>();
+  // global levels until every remaining segment fits one wave's LDS (kSubMax points); the
+  // host polls the next level's segment count from level 4 on
   bool done = false;
   for (int level = 0; level < kFarStack - 1 && !done; ++level) {
     HIPC(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket));
-    // poll the next level's segment count every few levels (and at the depth limit)
-    const bool poll = (level >= 9 && (level % 3) == 0) || level == kFarStack - 2;
-    if (poll) {
-      HIPC(hipMemcpyAsync(&hctl->nseg[level + 1], &w.ctl->nseg[level + 1], 4, hipMemcpyDeviceToHost, s));
+    if (level >= 4 || level == kFarStack - 2) {
+      HIPC(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
       HIPC(hipStreamSynchronize(s));
       if (hctl->nseg[level + 1] == 0) done = true;
     }
   }
   if (!done) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
+  HIPC(launch_tree_subtrees(s, (uint32_t)n, hctl->n_small, w, bpts, bucket));
   HIPC(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, ctx->nodes.as<uint4>()));
   HIPC(hipMemcpyAsync(&hctl->error, &w.ctl->error, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -429,6 +435,11 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(ensure(ctx->d2, B->total_read * 4));
     HIPC(ensure(ctx->touch, B->total_read * 4));
     HIPC(ensure(ctx->slab, (size_t)B->n_red_total * kRedCols * 8));
+    HIPC(ensure(ctx->sel_hist, P * kHistBins * 4));
+    HIPC(ensure(ctx->sel_cand, B->total_read * 4));
+    HIPC(ensure(ctx->sel_cnt, P * 4));
+    HIPC(hipMemsetAsync(ctx->sel_hist.p, 0, P * kHistBins * 4, s));
+    HIPC(hipMemsetAsync(ctx->sel_cnt.p, 0, P * 4, s));
     float4* bpts = ctx->bpts.as<float4>();
     float4* bnrm = ctx->bnrm.as<float4>();
     float4* readc = ctx->read_c.as<float4>();
@@ -457,7 +468,8 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
                     ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm);
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it + 1], s));
       ++nn_launches;
-      launch_icp_select(s, (int)P, dDesc, dState, ctx->d2.as<float>());
+      launch_icp_select(s, B->m_red, (int)P, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
+                        ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>());
       launch_icp_reduce(s, B->m_red, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
                         ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>());
       launch_icp_update(s, (int)P, dDesc, dState, ctx->slab.as<double>(), prm);
@@ -577,9 +589,11 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->match, &ctx->d2, &ctx->desc,
                     &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
-                    &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
+                    &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
+                    &ctx->qmap, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
                     &ctx->tw_segof1, &ctx->tw_seg0, &ctx->tw_seg1, &ctx->tw_flag, &ctx->tw_X1, &ctx->tw_X2,
-                    &ctx->tw_posL, &ctx->tw_posR, &ctx->tw_ev, &ctx->tw_ecnt, &ctx->tw_sums, &ctx->tw_pdepth,
+                    &ctx->tw_posL, &ctx->tw_posR, &ctx->tw_ev, &ctx->tw_valid, &ctx->tw_subs, &ctx->tw_ecnt,
+                    &ctx->tw_sums, &ctx->tw_pdepth,
                     &ctx->tw_ctl, &ctx->tw_scan})
     release(*b);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_ctl, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io}) release(*b);
@@ -775,8 +789,25 @@ int aicp_hip_dists_quantile(aicp_hip_ctx* ctx, const float* d2, size_t n, float 
   std::memcpy(ctx->pin_io.p, d2, n * 4);
   HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, st_));
   HIPC(hipMemcpyAsync(ctx->d2.p, ctx->pin_io.p, n * 4, hipMemcpyHostToDevice, st_));
+  // one pair: blocks of kNNBlock * kReducePerThread readings
+  const uint32_t per = kNNBlock * kReducePerThread, nb = (uint32_t)((n + per - 1) / per);
+  HIPC(ensure(ctx->qmap, (size_t)nb * 8));
+  HIPC(ensure(ctx->pin_desc, (size_t)nb * 8));
+  uint32_t* hm = ctx->pin_desc.as<uint32_t>();
+  for (uint32_t b = 0; b < nb; ++b) {
+    hm[b] = 0;
+    hm[nb + b] = b * per;
+  }
+  HIPC(hipMemcpyAsync(ctx->qmap.p, hm, (size_t)nb * 8, hipMemcpyHostToDevice, st_));
+  BlockMap qm{ctx->qmap.as<int32_t>(), ctx->qmap.as<uint32_t>() + nb, nb};
+  HIPC(ensure(ctx->sel_hist, kHistBins * 4));
+  HIPC(ensure(ctx->sel_cand, n * 4));
+  HIPC(ensure(ctx->sel_cnt, 4));
+  HIPC(hipMemsetAsync(ctx->sel_hist.p, 0, kHistBins * 4, st_));
+  HIPC(hipMemsetAsync(ctx->sel_cnt.p, 0, 4, st_));
   launch_init_state(st_, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>());
-  launch_icp_select(st_, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->d2.as<float>());
+  launch_icp_select(st_, qm, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(), ctx->d2.as<float>(),
+                    ctx->sel_hist.as<uint32_t>(), ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>());
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(st_));
   PairState st;

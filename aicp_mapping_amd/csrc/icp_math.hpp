@@ -133,28 +133,42 @@ AICP_HD double quat_angdist(const double* a, const double* b) {
   return 2.0 * atan2(sqrt(x * x + y * y + z * z), fabs(w));
 }
 
-// ---- full-pivoting Householder QR (Eigen FullPivHouseholderQR semantics), n <= 6 --------
+// ---- full-pivoting Householder QR (Eigen FullPivHouseholderQR semantics), N <= 6 --------
+// Register-resident forms: every loop has compile-time bounds and is unrolled, and the
+// data-dependent pivots / ranks act through selects and guards, never through a dynamic
+// array index (which would put the matrices in scratch memory). Operation order is that of
+// the plain loops (and of the oracle).
+#define AICP_UNROLL _Pragma("unroll")
+
+template <int N>
 struct PivQR {
-  int n, nonzero, rank;
-  double a[36];
-  double tau[6];
-  int rowT[6], colT[6];
+  int nonzero, rank;
+  double a[N * N];
+  double tau[N];
+  int rowT[N], colT[N];
   double maxpivot;
 };
 
-AICP_HD void pivqr(const double* A, int n, PivQR& q) {
-  q.n = n;
-  for (int i = 0; i < n * n; ++i) q.a[i] = A[i];
-  const double prec = (double)kFltEps * n;
-  q.nonzero = n;
+template <int N>
+AICP_HD void pivqr(const double* A, PivQR<N>& q) {
+  AICP_UNROLL for (int i = 0; i < N * N; ++i) q.a[i] = A[i];
+  const double prec = (double)kFltEps * N;
+  q.nonzero = N;
   q.maxpivot = 0;
   double biggest = 0;
-  for (int k = 0; k < n; ++k) {
+  bool stop = false;
+  AICP_UNROLL for (int k = 0; k < N; ++k) {
+    if (stop) {
+      q.rowT[k] = k;
+      q.colT[k] = k;
+      q.tau[k] = 0;
+      continue;
+    }
     int br = k, bc = k;
     double bv = -1;
-    for (int c = k; c < n; ++c)
-      for (int r = k; r < n; ++r) {
-        const double v = fabs(q.a[r * n + c]);
+    AICP_UNROLL for (int c = k; c < N; ++c)
+      AICP_UNROLL for (int r = k; r < N; ++r) {
+        const double v = fabs(q.a[r * N + c]);
         if (v > bv) {
           bv = v;
           br = r;
@@ -164,205 +178,239 @@ AICP_HD void pivqr(const double* A, int n, PivQR& q) {
     if (k == 0) biggest = bv;
     if (bv <= biggest * prec) {
       q.nonzero = k;
-      for (int i = k; i < n; ++i) {
-        q.rowT[i] = i;
-        q.colT[i] = i;
-        q.tau[i] = 0;
-      }
-      break;
+      q.rowT[k] = k;
+      q.colT[k] = k;
+      q.tau[k] = 0;
+      stop = true;
+      continue;
     }
     q.rowT[k] = br;
     q.colT[k] = bc;
-    if (br != k)
-      for (int c = k; c < n; ++c) {
-        const double t = q.a[k * n + c];
-        q.a[k * n + c] = q.a[br * n + c];
-        q.a[br * n + c] = t;
-      }
-    if (bc != k)
-      for (int r = 0; r < n; ++r) {
-        const double t = q.a[r * n + k];
-        q.a[r * n + k] = q.a[r * n + bc];
-        q.a[r * n + bc] = t;
-      }
+    AICP_UNROLL for (int r = k + 1; r < N; ++r)
+      if (r == br)
+        AICP_UNROLL for (int c = k; c < N; ++c) {
+          const double t = q.a[k * N + c];
+          q.a[k * N + c] = q.a[r * N + c];
+          q.a[r * N + c] = t;
+        }
+    AICP_UNROLL for (int c = k + 1; c < N; ++c)
+      if (c == bc)
+        AICP_UNROLL for (int r = 0; r < N; ++r) {
+          const double t = q.a[r * N + k];
+          q.a[r * N + k] = q.a[r * N + c];
+          q.a[r * N + c] = t;
+        }
     double tailSq = 0;
-    for (int r = k + 1; r < n; ++r) tailSq += q.a[r * n + k] * q.a[r * n + k];
-    const double c0 = q.a[k * n + k];
+    AICP_UNROLL for (int r = k + 1; r < N; ++r) tailSq += q.a[r * N + k] * q.a[r * N + k];
+    const double c0 = q.a[k * N + k];
     double beta, tau;
     if (tailSq <= kDblMin) {
       tau = 0;
       beta = c0;
-      for (int r = k + 1; r < n; ++r) q.a[r * n + k] = 0;
+      AICP_UNROLL for (int r = k + 1; r < N; ++r) q.a[r * N + k] = 0;
     } else {
       beta = sqrt(c0 * c0 + tailSq);
       if (c0 >= 0) beta = -beta;
       const double den = c0 - beta;
-      for (int r = k + 1; r < n; ++r) q.a[r * n + k] /= den;
+      AICP_UNROLL for (int r = k + 1; r < N; ++r) q.a[r * N + k] /= den;
       tau = (beta - c0) / beta;
     }
     q.tau[k] = tau;
-    q.a[k * n + k] = beta;
+    q.a[k * N + k] = beta;
     if (fabs(beta) > q.maxpivot) q.maxpivot = fabs(beta);
-    for (int c = k + 1; c < n; ++c) {
-      double s = q.a[k * n + c];
-      for (int r = k + 1; r < n; ++r) s += q.a[r * n + k] * q.a[r * n + c];
+    AICP_UNROLL for (int c = k + 1; c < N; ++c) {
+      double s = q.a[k * N + c];
+      AICP_UNROLL for (int r = k + 1; r < N; ++r) s += q.a[r * N + k] * q.a[r * N + c];
       s *= tau;
-      q.a[k * n + c] -= s;
-      for (int r = k + 1; r < n; ++r) q.a[r * n + c] -= s * q.a[r * n + k];
+      q.a[k * N + c] -= s;
+      AICP_UNROLL for (int r = k + 1; r < N; ++r) q.a[r * N + c] -= s * q.a[r * N + k];
     }
   }
-  const double thr = fabs(q.maxpivot) * ((double)kFltEps * n);
+  const double thr = fabs(q.maxpivot) * ((double)kFltEps * N);
   q.rank = 0;
-  for (int i = 0; i < q.nonzero; ++i) q.rank += (fabs(q.a[i * n + i]) > thr) ? 1 : 0;
+  AICP_UNROLL for (int i = 0; i < N; ++i)
+    if (i < q.nonzero) q.rank += (fabs(q.a[i * N + i]) > thr) ? 1 : 0;
 }
 
-// Q = P0 H0 P1 H1 ... (row-major n x n)
-AICP_HD void pivqr_Q(const PivQR& q, double* Q) {
-  const int n = q.n;
-  for (int i = 0; i < n * n; ++i) Q[i] = 0;
-  for (int i = 0; i < n; ++i) Q[i * n + i] = 1;
-  for (int k = n - 1; k >= 0; --k) {
+// Q = P0 H0 P1 H1 ... (row-major N x N)
+template <int N>
+AICP_HD void pivqr_Q(const PivQR<N>& q, double* Q) {
+  AICP_UNROLL for (int i = 0; i < N * N; ++i) Q[i] = 0;
+  AICP_UNROLL for (int i = 0; i < N; ++i) Q[i * N + i] = 1;
+  AICP_UNROLL for (int k = N - 1; k >= 0; --k) {
     const double tau = (k < q.nonzero) ? q.tau[k] : 0.0;
     if (tau != 0) {
-      for (int c = k; c < n; ++c) {
-        double s = Q[k * n + c];
-        for (int r = k + 1; r < n; ++r) s += q.a[r * n + k] * Q[r * n + c];
+      AICP_UNROLL for (int c = k; c < N; ++c) {
+        double s = Q[k * N + c];
+        AICP_UNROLL for (int r = k + 1; r < N; ++r) s += q.a[r * N + k] * Q[r * N + c];
         s *= tau;
-        Q[k * n + c] -= s;
-        for (int r = k + 1; r < n; ++r) Q[r * n + c] -= s * q.a[r * n + k];
+        Q[k * N + c] -= s;
+        AICP_UNROLL for (int r = k + 1; r < N; ++r) Q[r * N + c] -= s * q.a[r * N + k];
       }
     }
-    const int r = (k < q.nonzero) ? q.rowT[k] : k;
-    if (r != k)
-      for (int c = 0; c < n; ++c) {
-        const double t = Q[k * n + c];
-        Q[k * n + c] = Q[r * n + c];
-        Q[r * n + c] = t;
-      }
+    const int rr = (k < q.nonzero) ? q.rowT[k] : k;
+    AICP_UNROLL for (int r = k + 1; r < N; ++r)
+      if (r == rr)
+        AICP_UNROLL for (int c = 0; c < N; ++c) {
+          const double t = Q[k * N + c];
+          Q[k * N + c] = Q[r * N + c];
+          Q[r * N + c] = t;
+        }
   }
 }
 
+// Cholesky solve of the leading r x r block of M (row stride N)
+template <int N>
 AICP_HD bool llt_solve(const double* M, int r, const double* b, double* x) {
-  double L[36];
-  for (int i = 0; i < 36; ++i) L[i] = 0;
-  for (int j = 0; j < r; ++j) {
-    double d = M[j * r + j];
-    for (int k = 0; k < j; ++k) d -= L[j * r + k] * L[j * r + k];
-    if (!(d > 0)) return false;
-    const double ljj = sqrt(d);
-    L[j * r + j] = ljj;
-    for (int i = j + 1; i < r; ++i) {
-      double s = M[i * r + j];
-      for (int k = 0; k < j; ++k) s -= L[i * r + k] * L[j * r + k];
-      L[i * r + j] = s / ljj;
+  double L[N * N];
+  AICP_UNROLL for (int i = 0; i < N * N; ++i) L[i] = 0;
+  bool ok = true;
+  AICP_UNROLL for (int j = 0; j < N; ++j) {
+    if (j < r) {
+      double d = M[j * N + j];
+      AICP_UNROLL for (int k = 0; k < j; ++k) d -= L[j * N + k] * L[j * N + k];
+      if (!(d > 0)) ok = false;
+      const double ljj = sqrt(d);
+      L[j * N + j] = ljj;
+      AICP_UNROLL for (int i = j + 1; i < N; ++i)
+        if (i < r) {
+          double s = M[i * N + j];
+          AICP_UNROLL for (int k = 0; k < j; ++k) s -= L[i * N + k] * L[j * N + k];
+          L[i * N + j] = s / ljj;
+        }
     }
   }
-  double y[6];
-  for (int i = 0; i < r; ++i) {
-    double s = b[i];
-    for (int k = 0; k < i; ++k) s -= L[i * r + k] * y[k];
-    y[i] = s / L[i * r + i];
-  }
-  for (int i = r - 1; i >= 0; --i) {
-    double s = y[i];
-    for (int k = i + 1; k < r; ++k) s -= L[k * r + i] * x[k];
-    x[i] = s / L[i * r + i];
-  }
+  if (!ok) return false;
+  double y[N];
+  AICP_UNROLL for (int i = 0; i < N; ++i)
+    if (i < r) {
+      double s = b[i];
+      AICP_UNROLL for (int k = 0; k < i; ++k) s -= L[i * N + k] * y[k];
+      y[i] = s / L[i * N + i];
+    }
+  AICP_UNROLL for (int i = N - 1; i >= 0; --i)
+    if (i < r) {
+      double s = y[i];
+      AICP_UNROLL for (int k = i + 1; k < N; ++k)
+        if (k < r) s -= L[k * N + i] * x[k];
+      x[i] = s / L[i * N + i];
+    }
   return true;
 }
 
 // Cyclic Jacobi eigen-decomposition (symmetric, row-major), eigenvectors as columns of V.
-AICP_HD void jacobi_eig(const double* A, int n, double* w, double* V) {
-  double a[36];
-  for (int i = 0; i < n * n; ++i) a[i] = A[i];
-  for (int i = 0; i < n * n; ++i) V[i] = 0;
-  for (int i = 0; i < n; ++i) V[i * n + i] = 1;
+template <int N>
+AICP_HD void jacobi_eig(const double* A, double* w, double* V) {
+  double a[N * N];
+  AICP_UNROLL for (int i = 0; i < N * N; ++i) a[i] = A[i];
+  AICP_UNROLL for (int i = 0; i < N * N; ++i) V[i] = 0;
+  AICP_UNROLL for (int i = 0; i < N; ++i) V[i * N + i] = 1;
   for (int sweep = 0; sweep < 64; ++sweep) {
     double offn = 0, diag = 0;
-    for (int p = 0; p < n; ++p) {
-      diag += a[p * n + p] * a[p * n + p];
-      for (int q = p + 1; q < n; ++q) offn += a[p * n + q] * a[p * n + q];
+    AICP_UNROLL for (int p = 0; p < N; ++p) {
+      diag += a[p * N + p] * a[p * N + p];
+      AICP_UNROLL for (int q = p + 1; q < N; ++q) offn += a[p * N + q] * a[p * N + q];
     }
     if (offn <= 1e-30 * diag || offn == 0) break;
-    for (int p = 0; p < n; ++p)
-      for (int q = p + 1; q < n; ++q) {
-        const double apq = a[p * n + q];
-        if (apq == 0) continue;
-        const double app = a[p * n + p], aqq = a[q * n + q];
-        const double theta = (aqq - app) / (2 * apq);
-        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
-        const double c = 1 / sqrt(t * t + 1), s = t * c;
-        for (int k = 0; k < n; ++k) {
-          const double akp = a[k * n + p], akq = a[k * n + q];
-          a[k * n + p] = c * akp - s * akq;
-          a[k * n + q] = s * akp + c * akq;
-        }
-        for (int k = 0; k < n; ++k) {
-          const double apk = a[p * n + k], aqk = a[q * n + k];
-          a[p * n + k] = c * apk - s * aqk;
-          a[q * n + k] = s * apk + c * aqk;
-        }
-        for (int k = 0; k < n; ++k) {
-          const double vkp = V[k * n + p], vkq = V[k * n + q];
-          V[k * n + p] = c * vkp - s * vkq;
-          V[k * n + q] = s * vkp + c * vkq;
+    AICP_UNROLL for (int p = 0; p < N; ++p)
+      AICP_UNROLL for (int q = p + 1; q < N; ++q) {
+        const double apq = a[p * N + q];
+        if (apq != 0) {
+          const double app = a[p * N + p], aqq = a[q * N + q];
+          const double theta = (aqq - app) / (2 * apq);
+          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+          const double c = 1 / sqrt(t * t + 1), s = t * c;
+          AICP_UNROLL for (int k = 0; k < N; ++k) {
+            const double akp = a[k * N + p], akq = a[k * N + q];
+            a[k * N + p] = c * akp - s * akq;
+            a[k * N + q] = s * akp + c * akq;
+          }
+          AICP_UNROLL for (int k = 0; k < N; ++k) {
+            const double apk = a[p * N + k], aqk = a[q * N + k];
+            a[p * N + k] = c * apk - s * aqk;
+            a[q * N + k] = s * apk + c * aqk;
+          }
+          AICP_UNROLL for (int k = 0; k < N; ++k) {
+            const double vkp = V[k * N + p], vkq = V[k * N + q];
+            V[k * N + p] = c * vkp - s * vkq;
+            V[k * N + q] = s * vkp + c * vkq;
+          }
         }
       }
   }
-  for (int i = 0; i < n; ++i) w[i] = a[i * n + i];
+  AICP_UNROLL for (int i = 0; i < N; ++i) w[i] = a[i * N + i];
 }
 
 // solvePossiblyUnderdeterminedLinearSystem (A row-major 6x6). Returns the path taken:
 // 0 LLT (full rank), 1 rank-r minimal-norm QR, 2 pseudo-inverse (JacobiSVD fallback).
 AICP_HD int solve6(const double* A, const double* b, double* x) {
-  const int n = 6;
-  PivQR qr;
-  pivqr(A, n, qr);
+  constexpr int n = 6;
+  PivQR<6> qr;
+  pivqr<6>(A, qr);
   if (qr.rank == n) {
-    if (llt_solve(A, n, b, x)) return 0;
+    if (llt_solve<6>(A, n, b, x)) return 0;
   } else if (qr.rank > 0) {
     const int r = qr.rank;
     double Q[36];
-    pivqr_Q(qr, Q);
+    pivqr_Q<6>(qr, Q);
     int perm[6];
-    for (int i = 0; i < n; ++i) perm[i] = i;
-    for (int k = 0; k < n; ++k) {
+    AICP_UNROLL for (int i = 0; i < n; ++i) perm[i] = i;
+    AICP_UNROLL for (int k = 0; k < n; ++k) {
       const int c = (k < qr.nonzero) ? qr.colT[k] : k;
-      const int t = perm[k];
-      perm[k] = perm[c];
-      perm[c] = t;
+      AICP_UNROLL for (int j = k + 1; j < n; ++j)
+        if (j == c) {
+          const int t = perm[k];
+          perm[k] = perm[j];
+          perm[j] = t;
+        }
     }
+    // AP[k][j] = A[k][perm[j]] (column gather by selects)
+    double AP[36];
+    AICP_UNROLL for (int j = 0; j < n; ++j)
+      AICP_UNROLL for (int k = 0; k < n; ++k) {
+        double v = A[k * n + 0];
+        AICP_UNROLL for (int c = 1; c < n; ++c) v = (perm[j] == c) ? A[k * n + c] : v;
+        AP[k * n + j] = v;
+      }
     double R1[36], RRt[36], qb[6], y[6];
-    for (int i = 0; i < r; ++i)
-      for (int j = 0; j < n; ++j) {
+    AICP_UNROLL for (int i = 0; i < n; ++i)
+      if (i < r)
+        AICP_UNROLL for (int j = 0; j < n; ++j) {
+          double s = 0;
+          AICP_UNROLL for (int k = 0; k < n; ++k) s += Q[k * n + i] * AP[k * n + j];
+          R1[i * n + j] = s;
+        }
+    AICP_UNROLL for (int i = 0; i < n; ++i)
+      AICP_UNROLL for (int j = 0; j < n; ++j)
+        if (i < r && j < r) {
+          double s = 0;
+          AICP_UNROLL for (int k = 0; k < n; ++k) s += R1[i * n + k] * R1[j * n + k];
+          RRt[i * n + j] = s;
+        }
+    AICP_UNROLL for (int i = 0; i < n; ++i)
+      if (i < r) {
         double s = 0;
-        for (int k = 0; k < n; ++k) s += Q[k * n + i] * A[k * n + perm[j]];
-        R1[i * n + j] = s;
+        AICP_UNROLL for (int k = 0; k < n; ++k) s += Q[k * n + i] * b[k];
+        qb[i] = s;
       }
-    for (int i = 0; i < r; ++i)
-      for (int j = 0; j < r; ++j) {
-        double s = 0;
-        for (int k = 0; k < n; ++k) s += R1[i * n + k] * R1[j * n + k];
-        RRt[i * r + j] = s;
-      }
-    for (int i = 0; i < r; ++i) {
-      double s = 0;
-      for (int k = 0; k < n; ++k) s += Q[k * n + i] * b[k];
-      qb[i] = s;
-    }
-    if (llt_solve(RRt, r, qb, y)) {
+    if (llt_solve<6>(RRt, r, qb, y)) {
       double z[6];
-      for (int j = 0; j < n; ++j) {
+      AICP_UNROLL for (int j = 0; j < n; ++j) {
         double s = 0;
-        for (int i = 0; i < r; ++i)
-          if (j >= i) s += R1[i * n + j] * y[i];
+        AICP_UNROLL for (int i = 0; i < n; ++i)
+          if (i < r && j >= i) s += R1[i * n + j] * y[i];
         z[j] = s;
       }
-      for (int i = 0; i < n; ++i) x[perm[i]] = z[i];
+      // x[perm[i]] = z[i] (scatter by selects)
+      AICP_UNROLL for (int c = 0; c < n; ++c) {
+        double v = 0;
+        AICP_UNROLL for (int i = 0; i < n; ++i) v = (perm[i] == c) ? z[i] : v;
+        x[c] = v;
+      }
       double nb = 0, nax = 0, nd = 0;
-      for (int i = 0; i < n; ++i) {
+      AICP_UNROLL for (int i = 0; i < n; ++i) {
         double s = 0;
-        for (int k = 0; k < n; ++k) s += A[i * n + k] * x[k];
+        AICP_UNROLL for (int k = 0; k < n; ++k) s += A[i * n + k] * x[k];
         nb += b[i] * b[i];
         nax += s * s;
         nd += (b[i] - s) * (b[i] - s);
@@ -371,37 +419,37 @@ AICP_HD int solve6(const double* A, const double* b, double* x) {
     }
   }
   double w[6], V[36];
-  jacobi_eig(A, n, w, V);
+  jacobi_eig<6>(A, w, V);
   double wmax = 0;
-  for (int i = 0; i < n; ++i) wmax = fmax(wmax, fabs(w[i]));
+  AICP_UNROLL for (int i = 0; i < n; ++i) wmax = fmax(wmax, fabs(w[i]));
   double thr = wmax * (n * kDblEps);
   if (thr < kDblMin) thr = kDblMin;
-  for (int i = 0; i < n; ++i) x[i] = 0;
-  for (int e = 0; e < n; ++e) {
+  AICP_UNROLL for (int i = 0; i < n; ++i) x[i] = 0;
+  AICP_UNROLL for (int e = 0; e < n; ++e) {
     if (fabs(w[e]) <= thr) continue;
     double s = 0;
-    for (int k = 0; k < n; ++k) s += V[k * n + e] * b[k];
+    AICP_UNROLL for (int k = 0; k < n; ++k) s += V[k * n + e] * b[k];
     s /= w[e];
-    for (int k = 0; k < n; ++k) x[k] += V[k * n + e] * s;
+    AICP_UNROLL for (int k = 0; k < n; ++k) x[k] += V[k * n + e] * s;
   }
   return 2;
 }
 
 // SurfaceNormal: rank(fullPivQR(C)) + 1 >= 3 -> smallest eigenvector, else e_y.
 AICP_HD bool normal_from_cov(const double* C, float* nrm) {
-  PivQR qr;
-  pivqr(C, 3, qr);
+  PivQR<3> qr;
+  pivqr<3>(C, qr);
   if (qr.rank + 1 >= 3) {
     double w[3], V[9];
-    jacobi_eig(C, 3, w, V);
+    jacobi_eig<3>(C, w, V);
     int s = 0;
     double sv = 1.79769313486231570e308;
-    for (int j = 0; j < 3; ++j)
+    AICP_UNROLL for (int j = 0; j < 3; ++j)
       if (w[j] < sv) {
         sv = w[j];
         s = j;
       }
-    for (int r = 0; r < 3; ++r) nrm[r] = (float)V[r * 3 + s];
+    AICP_UNROLL for (int r = 0; r < 3; ++r) nrm[r] = (float)(s == 0 ? V[r * 3] : (s == 1 ? V[r * 3 + 1] : V[r * 3 + 2]));
     return false;
   }
   nrm[0] = 0.f;

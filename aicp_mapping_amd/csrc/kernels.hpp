@@ -31,8 +31,11 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
                    const ActiveList* al, const float4* read_c, const uint4* nodes,
                    const int32_t* parent, const float4* bpts, int32_t* match, float* d2,
                    uint32_t* touched, uint32_t* ctr, const IcpParams& prm);
-void launch_icp_select(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
-                       const float* d2);
+// TrimmedDist limit per active pair. m: blocks of kNNBlock * kReducePerThread readings;
+// hist1: n_pairs * kHistBins zeroed words, cand: total_read words, cand_cnt: n_pairs zeroed
+// words (both left zeroed for the next call).
+void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* pd, PairState* st,
+                       const float* d2, uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt);
 void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const PairState* st,
                        const float4* read_c, const int32_t* match, const float* d2,
                        const uint32_t* touched, const float4* bpts, const float4* bnrm, double* slab);
@@ -59,7 +62,9 @@ struct TreeWork {
   uint32_t* X2;
   uint32_t* posL;        // partner positions, total
   uint32_t* posR;
-  NodeEvent* ev;         // 2 * total
+  NodeEvent* ev;         // 2 * total slots (leaf: first position; inner: total + split position)
+  uint8_t* valid;        // 2 * total
+  SubSeg* subs;          // wave-subtree segments, max_seg
   uint32_t* ecnt;        // nodes ending at each position, total + 2
   uint64_t* sums;        // 6 per pair (128-bit fixed-point coordinate sums)
   int32_t* pair_depth;   // per pair
@@ -67,6 +72,7 @@ struct TreeWork {
   void* scan_temp;
   size_t scan_temp_bytes;
   size_t max_seg;
+  int n_pairs;
 };
 size_t tree_scan_temp_bytes(size_t n);
 // centroid (center = 1) + frames in pd, centred points, root segments
@@ -75,6 +81,9 @@ hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairD
 // one level: nodes at depth `level` are split (their children get depth level + 1)
 hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const TreeWork& w, float4* bpts,
                              int bucket);
+// subtrees of the segments with <= kSubMax points, one wave each (n_small read back by the host)
+hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, uint32_t n_small, const TreeWork& w, float4* bpts,
+                                int bucket);
 // node records (preorder) and PairDesc node_off / n_nodes / tree_depth
 hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const TreeWork& w,
                               uint4* nodes);

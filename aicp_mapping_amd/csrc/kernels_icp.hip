@@ -6,9 +6,9 @@
 //   k_icp_nn       persistent waves: transform by T_iter (fused) + libnabo-order approximate
 //                  1-NN; a lane that finishes its query refills from a 64-query chunk of the
 //                  work space, so far-descent tails do not hold whole waves
-//   k_icp_select   exact k-th smallest d^2 (Matches::getDistsQuantile) by 3-digit radix select,
-//                  one 1024-thread workgroup per pair (per-wave LDS sub-histograms, digit-1
-//                  candidates kept in LDS)
+//   k_sel_*        exact k-th smallest d^2 (Matches::getDistsQuantile) by 3-digit radix select
+//                  over the whole chip: digit-1 histograms per 1024 readings, then the bin's
+//                  values compacted per pair and finished by one workgroup per pair
 //   k_icp_reduce   TrimmedDist weights + getMatchedPoints gather + point-to-plane F, dot and the
 //                  27-entry normal-equation sums in double from exact float products; wave
 //                  butterfly + LDS, one deterministic partial row per workgroup (no atomics)
@@ -688,56 +688,69 @@ __device__ void block_find_rank(const uint32_t* h, int nb, uint32_t k, uint32_t*
   __syncthreads();
 }
 
-constexpr int kCand = 6144;
-constexpr int kSubHist = 8;  // digit-1 sub-histograms (2 waves each) against LDS atomic conflicts
 constexpr uint32_t kInfBits = 0x7f800000u;
 
-__global__ __launch_bounds__(1024) void k_icp_select(const PairDesc* __restrict__ pd, PairState* st,
-                                                     const float* __restrict__ d2) {
+// ---- TrimmedDist limit = exact k-th smallest finite d2, k = (size_t)(float(n) * ratio)
+// (getDistsQuantile), as a radix select on the float bits (non-negative floats
+// order like their bit patterns) spread over the whole chip:
+//   k_sel_hist    per 1024 readings: LDS histogram of digit 1 (bits 31..21) -> global
+//   k_sel_find1   per pair: n = #finite, k, bin b1 holding rank k, rank r1 inside it
+//   k_sel_compact per 1024 readings: the values of bin b1 -> per-pair candidate list
+//   k_sel_final   per pair: digits 2 (bits 20..10) and 3 (bits 9..0) over the candidates
+__global__ __launch_bounds__(256) void k_sel_hist(BlockMap m, const PairDesc* __restrict__ pd,
+                                                  const PairState* __restrict__ st, const float* __restrict__ d2,
+                                                  uint32_t* __restrict__ hist1) {
+  const int pair = m.pair[blockIdx.x];
+  if (!st[pair].active) return;
+  __shared__ uint32_t h[4][kHistBins];  // one sub-histogram per wave (LDS atomic conflicts)
+  const int t = threadIdx.x;
+  for (int i = t; i < 4 * kHistBins; i += 256) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const PairDesc& d = pd[pair];
+  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
+  uint32_t* mine = h[t >> 6];
+  const uint32_t j0 = m.start[blockIdx.x];
+#pragma unroll
+  for (int u = 0; u < kReducePerThread; ++u) {
+    const uint32_t j = j0 + t + 256u * u;
+    if (j < d.n_read) {
+      const uint32_t v = bits[j];
+      if (v != kInfBits) atomicAdd(&mine[v >> 21], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* g = hist1 + (size_t)pair * kHistBins;
+  for (int i = t; i < kHistBins; i += 256) {
+    const uint32_t c = h[0][i] + h[1][i] + h[2][i] + h[3][i];
+    if (c) atomicAdd(&g[i], c);
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_sel_find1(PairState* st, uint32_t* __restrict__ hist1) {
   const int pair = blockIdx.x;
   PairState& s = st[pair];
   if (!s.active) return;
-  const PairDesc& d = pd[pair];
-  __shared__ uint32_t sub[kSubHist][kHistBins];
-  __shared__ uint32_t cand[kCand];
+  __shared__ uint32_t h[kHistBins];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t res[2];
-  __shared__ uint32_t ncand;
-  uint32_t* h = sub[0];
   const int t = threadIdx.x, lane = t & 63;
-  for (int i = t; i < kSubHist * kHistBins; i += 1024) (&sub[0][0])[i] = 0;
-  if (t == 0) ncand = 0;
-  __syncthreads();
-  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
-  const uint32_t n_all = d.n_read;
-  // digit 1 (bits 31..21) of the finite values
-  uint32_t* mysub = sub[(t >> 6) % kSubHist];
-  for (uint32_t i = t; i < n_all; i += 1024) {
-    const uint32_t v = bits[i];
-    if (v != kInfBits) atomicAdd(&mysub[v >> 21], 1u);
-  }
-  __syncthreads();
-  for (int i = t; i < kHistBins; i += 1024) {
-    uint32_t a = 0;
+  uint32_t* g = hist1 + (size_t)pair * kHistBins;
+  const uint32_t a = g[2 * t], b = g[2 * t + 1];
+  h[2 * t] = a;
+  h[2 * t + 1] = b;
+  g[2 * t] = 0;  // ready for the next iteration
+  g[2 * t + 1] = 0;
+  uint32_t v = a + b;
 #pragma unroll
-    for (int k = 0; k < kSubHist; ++k) a += sub[k][i];
-    h[i] = a;
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane == 0) wsum[t >> 6] = v;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t n = 0;
+    for (int w = 0; w < 16; ++w) n += wsum[w];
+    res[0] = n;
   }
   __syncthreads();
-  // total finite
-  {
-    uint32_t v = h[2 * t] + h[2 * t + 1];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (lane == 0) wsum[t >> 6] = v;
-    __syncthreads();
-    if (t == 0) {
-      uint32_t a = 0;
-      for (int w = 0; w < 16; ++w) a += wsum[w];
-      res[0] = a;
-    }
-    __syncthreads();
-  }
   const uint32_t n = res[0];
   __syncthreads();
   if (n == 0) {  // ConvergenceError("no outlier to filter")
@@ -757,49 +770,83 @@ __global__ __launch_bounds__(1024) void k_icp_select(const PairDesc* __restrict_
     if (k >= n) k = n - 1;
   }
   block_find_rank(h, kHistBins, k, res, wsum);
-  const uint32_t b1 = res[0], r1 = res[1];
+  if (t == 0) {
+    s.sel_b1 = res[0];
+    s.sel_r1 = res[1];
+    s.n_finite = (int32_t)n;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc* __restrict__ pd,
+                                                     const PairState* __restrict__ st, const float* __restrict__ d2,
+                                                     uint32_t* __restrict__ cand, uint32_t* __restrict__ cand_cnt) {
+  const int pair = m.pair[blockIdx.x];
+  const PairState& s = st[pair];
+  if (!s.active) return;
+  __shared__ uint32_t wcount[4];
+  __shared__ uint32_t base;
+  const PairDesc& d = pd[pair];
+  const uint32_t b1 = s.sel_b1;
+  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t j0 = m.start[blockIdx.x];
+  uint32_t v[kReducePerThread];
+  uint64_t mk[kReducePerThread];
+  uint32_t mine = 0;  // this wave's hits
+#pragma unroll
+  for (int u = 0; u < kReducePerThread; ++u) {
+    const uint32_t j = j0 + t + 256u * u;
+    v[u] = j < d.n_read ? bits[j] : kInfBits;
+    mk[u] = __ballot(v[u] != kInfBits && (v[u] >> 21) == b1);
+    mine += (uint32_t)__popcll(mk[u]);
+  }
+  // one atomic per block (the per-pair counter is shared by ~120 blocks)
+  if (lane == 0) wcount[w] = mine;
   __syncthreads();
-  for (int i = t; i < kHistBins; i += 1024) h[i] = 0;
-  __syncthreads();
-  for (uint32_t i = t; i < n_all; i += 1024) {
-    const uint32_t v = bits[i];
-    const bool hit = (v >> 21) == b1 && v != kInfBits;
-    if (hit) atomicAdd(&h[(v >> 10) & 2047u], 1u);
-    const uint64_t m = __ballot(hit);
-    if (m) {
-      uint32_t base = 0;
-      const int leader = __builtin_ctzll(m);
-      if (lane == leader) base = atomicAdd(&ncand, (uint32_t)__popcll(m));
-      base = __shfl(base, leader, 64);
-      if (hit) {
-        const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (slot < (uint32_t)kCand) cand[slot] = v;
-      }
-    }
+  if (t == 0) {
+    const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    base = tot ? atomicAdd(&cand_cnt[pair], tot) : 0u;
   }
   __syncthreads();
-  block_find_rank(h, kHistBins, r1, res, wsum);
+  uint32_t o = base;
+  for (int k = 0; k < w; ++k) o += wcount[k];
+#pragma unroll
+  for (int u = 0; u < kReducePerThread; ++u) {
+    if ((mk[u] >> lane) & 1ull) cand[d.read_off + o + (uint32_t)__popcll(mk[u] & ((1ull << lane) - 1ull))] = v[u];
+    o += (uint32_t)__popcll(mk[u]);
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__ pd, PairState* st,
+                                                    const uint32_t* __restrict__ cand, uint32_t* __restrict__ cand_cnt) {
+  const int pair = blockIdx.x;
+  PairState& s = st[pair];
+  if (!s.active) return;
+  __shared__ uint32_t h[kHistBins];
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t res[2];
+  const int t = threadIdx.x;
+  const uint32_t c = cand_cnt[pair];
+  const uint32_t* cv = cand + pd[pair].read_off;
+  for (int i = t; i < kHistBins; i += 1024) h[i] = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < c; i += 1024) atomicAdd(&h[(cv[i] >> 10) & 2047u], 1u);
+  __syncthreads();
+  block_find_rank(h, kHistBins, s.sel_r1, res, wsum);
   const uint32_t b2 = res[0], r2 = res[1];
   __syncthreads();
   for (int i = t; i < kHistBins; i += 1024) h[i] = 0;
   __syncthreads();
-  const uint32_t hi21 = (b1 << 11) | b2;
-  if (ncand <= (uint32_t)kCand) {
-    for (uint32_t i = t; i < ncand; i += 1024) {
-      const uint32_t v = cand[i];
-      if ((v >> 10) == hi21) atomicAdd(&h[v & 1023u], 1u);
-    }
-  } else {
-    for (uint32_t i = t; i < n_all; i += 1024) {
-      const uint32_t v = bits[i];
-      if ((v >> 10) == hi21 && v != kInfBits) atomicAdd(&h[v & 1023u], 1u);
-    }
+  const uint32_t hi21 = (s.sel_b1 << 11) | b2;
+  for (uint32_t i = t; i < c; i += 1024) {
+    const uint32_t v = cv[i];
+    if ((v >> 10) == hi21) atomicAdd(&h[v & 1023u], 1u);
   }
   __syncthreads();
   block_find_rank(h, kHist3Bins, r2, res, wsum);
   if (t == 0) {
     s.limit = __uint_as_float((hi21 << 10) | res[0]);
-    s.n_finite = (int32_t)n;
+    cand_cnt[pair] = 0;  // ready for the next iteration
   }
 }
 
@@ -1055,7 +1102,7 @@ __global__ void k_transform(int n, const float* __restrict__ T, const float4* __
   out[i] = make_float4(o[0], o[1], o[2], 1.f);
 }
 
-__global__ void k_solve6(const double* A, const double* b, double* x, int32_t* path) {
+__global__ __launch_bounds__(64) void k_solve6(const double* A, const double* b, double* x, int32_t* path) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *path = solve6(A, b, x);
 }
 
@@ -1134,8 +1181,13 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
   else
     k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, match, d2, touched, ctr, prm);
 }
-void launch_icp_select(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const float* d2) {
-  k_icp_select<<<n_pairs, 1024, 0, s>>>(pd, st, d2);
+void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* pd, PairState* st, const float* d2,
+                       uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt) {
+  if (!m.n_blocks) return;
+  k_sel_hist<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, hist1);
+  k_sel_find1<<<n_pairs, 1024, 0, s>>>(st, hist1);
+  k_sel_compact<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, cand, cand_cnt);
+  k_sel_final<<<n_pairs, 1024, 0, s>>>(pd, st, cand, cand_cnt);
 }
 void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const PairState* st, const float4* read_c,
                        const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,

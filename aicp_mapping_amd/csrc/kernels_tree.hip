@@ -29,6 +29,8 @@
 
 #include <rocprim/device/device_scan.hpp>
 
+#include <algorithm>
+
 #include "aicp_common.hpp"
 #include "icp_math.hpp"
 #include "kernels.hpp"
@@ -68,6 +70,36 @@ __device__ __forceinline__ bool wave_seg_minmax(int key, float& mn, float& mx) {
   return lane == 63 || kn != key;
 }
 
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide min/max of (mn, mx) for a block whose valid threads share one key; the result
+// is valid on thread 0. 256-thread blocks.
+__device__ __forceinline__ void block_minmax(float& mn, float& mx) {
+  __shared__ float smn[4], smx[4];
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    smn[w] = mn;
+    smx[w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mn = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+    mx = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ int pair_of_pos(const PairDesc* pd, int n_pairs, uint32_t s) {
   int lo = 0, hi = n_pairs - 1;
   while (lo < hi) {
@@ -78,10 +110,25 @@ __device__ __forceinline__ int pair_of_pos(const PairDesc* pd, int n_pairs, uint
   return lo;
 }
 
-__device__ __forceinline__ void emit_event(TreeCtl* ctl, NodeEvent* ev, uint32_t* ecnt, const NodeEvent& e) {
-  const uint32_t i = atomicAdd(&ctl->n_events, 1u);
-  ev[i] = e;
+// slot of a node: a leaf at its first position, an inner node at total + its split position
+__device__ __forceinline__ void emit_event(NodeEvent* ev, uint8_t* valid, uint32_t* ecnt, uint32_t total,
+                                           const NodeEvent& e) {
+  const uint32_t slot = (e.cd == (int32_t)kLeaf) ? e.f : total + e.f + e.left;
+  ev[slot] = e;
+  valid[slot] = 1;
   atomicAdd(&ecnt[e.f + e.c], 1u);
+}
+
+__device__ __forceinline__ NodeEvent leaf_event(uint32_t f, uint32_t c, int depth, int pair, uint32_t pf, int pdepth) {
+  NodeEvent e{};
+  e.f = f;
+  e.c = c;
+  e.depth = depth;
+  e.pair = pair;
+  e.cd = (int32_t)kLeaf;
+  e.parent_f = pf;
+  e.parent_depth = pdepth;
+  return e;
 }
 
 // cd and ideal of a box (kdtree_host.cpp / oracle: first strict maximum of the extents)
@@ -96,7 +143,9 @@ __device__ __forceinline__ void split_dim(const float* mn, const float* mx, int&
       cd = d;
     }
   }
-  ideal = (mx[cd] + mn[cd]) / 2;
+  const float a = cd == 0 ? mx[0] : (cd == 1 ? mx[1] : mx[2]);
+  const float b = cd == 0 ? mn[0] : (cd == 1 ? mn[1] : mn[2]);
+  ideal = (a + b) / 2;
 }
 
 __device__ __forceinline__ float seg_cut(const TreeSeg& s) {
@@ -106,39 +155,70 @@ __device__ __forceinline__ float seg_cut(const TreeSeg& s) {
 
 // ---- centroid --------------------------------------------------------------------------------
 // Exact order-independent sum: every coordinate as round(x * 2^40) in 128-bit two's complement
-// (two 64-bit atomics with carry), so the result does not depend on the reduction order.
+// (64-bit atomics with carry), so the result does not depend on the reduction order.
+__device__ __forceinline__ void add128(uint64_t& lo, int64_t& hi, uint64_t lo2, int64_t hi2) {
+  const uint64_t s = lo + lo2;
+  hi = hi + hi2 + (s < lo ? 1 : 0);
+  lo = s;
+}
+
+__device__ __forceinline__ void atomic_add128(uint64_t* w, uint64_t lo, int64_t hi) {
+  const uint64_t old = atomicAdd((unsigned long long*)w, (unsigned long long)lo);
+  const uint64_t carry = (old + lo < old) ? 1u : 0u;
+  atomicAdd((unsigned long long*)(w + 1), (unsigned long long)((uint64_t)hi + carry));
+}
+
 __global__ __launch_bounds__(256) void k_tr_sum(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
                                                 const float4* __restrict__ raw, uint64_t* sums) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ uint64_t slo[3][4];
+  __shared__ int64_t shi[3][4];
+  const uint32_t base = blockIdx.x * blockDim.x;
+  const uint32_t i = base + threadIdx.x;
   const bool ok = i < total;
-  const int pair = ok ? pair_of_pos(pd, n_pairs, i) : -1;
+  const uint32_t last = min(base + 255u, total - 1);
+  // a block inside one pair (the common case) reduces in LDS and issues 2 atomics per axis
+  const int p_first = pair_of_pos(pd, n_pairs, base), p_last = pair_of_pos(pd, n_pairs, last);
+  const bool uniform = p_first == p_last;
+  const int pair = ok ? (uniform ? p_first : pair_of_pos(pd, n_pairs, i)) : -1;
   const float4 p = ok ? raw[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   const float c[3] = {p.x, p.y, p.z};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     const int64_t q = ok ? fixed40(c[d]) : 0;
-    // segmented 128-bit sum over the wave: (lo, hi) with carry
     uint64_t lo = (uint64_t)q;
     int64_t hi = q < 0 ? -1 : 0;
-    const int lane = threadIdx.x & 63;
+    if (uniform) {
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int ko = __shfl_up(pair, off, 64);
-      const uint64_t lo_o = __shfl_up(lo, off, 64);
-      const int64_t hi_o = __shfl_up(hi, off, 64);
-      if (lane >= off && ko == pair) {
-        const uint64_t s = lo + lo_o;
-        hi = hi + hi_o + (s < lo ? 1 : 0);
-        lo = s;
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t lo_o = __shfl_xor(lo, off, 64);
+        const int64_t hi_o = __shfl_xor(hi, off, 64);
+        add128(lo, hi, lo_o, hi_o);
       }
+      if (lane == 0) {
+        slo[d][w] = lo;
+        shi[d][w] = hi;
+      }
+    } else {  // pair boundary inside the block: segmented wave scan, one atomic pair per run
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int ko = __shfl_up(pair, off, 64);
+        const uint64_t lo_o = __shfl_up(lo, off, 64);
+        const int64_t hi_o = __shfl_up(hi, off, 64);
+        if (lane >= off && ko == pair) add128(lo, hi, lo_o, hi_o);
+      }
+      const int kn = __shfl_down(pair, 1, 64);
+      if (ok && (lane == 63 || kn != pair)) atomic_add128(sums + (size_t)pair * 6 + 2 * d, lo, hi);
     }
-    const int kn = __shfl_down(pair, 1, 64);
-    if (ok && (lane == 63 || kn != pair)) {
-      uint64_t* w = sums + (size_t)pair * 6 + 2 * d;
-      const uint64_t old = atomicAdd((unsigned long long*)w, (unsigned long long)lo);
-      const uint64_t carry = (old + lo < old) ? 1u : 0u;
-      atomicAdd((unsigned long long*)(w + 1), (unsigned long long)((uint64_t)hi + carry));
-    }
+  }
+  if (!uniform) return;
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int d = threadIdx.x;
+    uint64_t lo = slo[d][0];
+    int64_t hi = shi[d][0];
+    for (int k = 1; k < 4; ++k) add128(lo, hi, slo[d][k], shi[d][k]);
+    atomic_add128(sums + (size_t)p_first * 6 + 2 * d, lo, hi);
   }
 }
 
@@ -160,40 +240,64 @@ __global__ void k_tr_frames(int n_pairs, PairDesc* pd, const uint64_t* sums, int
   mul4(Tmi, d.Tin, d.Tinit);
 }
 
-// centred reference (w = local input id) into W0; the root segment of every pair; whole-cloud
-// bounding box of the centred points; a pair with n_ref <= bucket is one leaf.
+// root segment boxes start empty: min at the largest encoding, max at the smallest
+__global__ void k_tr_init_boxes(int n_pairs, TreeSeg* seg) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  for (int k = 0; k < 3; ++k) {
+    seg[p].bmn[k] = 0xffffffffu;
+    seg[p].bmx[k] = 0u;
+  }
+}
+
+// centred reference (w = local input id) into W0 and the bounding box of each pair's
+// centred points. Level-0 segment of every pair = its index; pairs small enough for the wave
+// subtree builder (or a single leaf, whose points are then final) leave the global levels.
 __global__ __launch_bounds__(256) void k_tr_center(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
                                                    const float4* __restrict__ raw, float4* __restrict__ W,
-                                                   float4* __restrict__ bpts, int32_t* __restrict__ segof,
-                                                   TreeSeg* seg, int bucket) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                   int32_t* __restrict__ segof, TreeSeg* seg,
+                                                   float4* __restrict__ bpts, int bucket) {
+  const uint32_t base = blockIdx.x * blockDim.x;
+  const uint32_t i = base + threadIdx.x;
   const bool ok = i < total;
-  const int pair = ok ? pair_of_pos(pd, n_pairs, i) : -1;
+  const uint32_t last = min(base + 255u, total - 1);
+  const int p_first = pair_of_pos(pd, n_pairs, base), p_last = pair_of_pos(pd, n_pairs, last);
+  const bool uniform = p_first == p_last;
+  const int pair = ok ? (uniform ? p_first : pair_of_pos(pd, n_pairs, i)) : -1;
   float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ok) {
     const PairDesc& d = pd[pair];
     const float4 p = raw[i];
     c = make_float4(p.x - d.mean[0], p.y - d.mean[1], p.z - d.mean[2], __int_as_float((int32_t)(i - d.ref_off)));
     W[i] = c;
-    const bool leaf = d.n_ref <= (uint32_t)bucket;
-    if (leaf) bpts[i] = c;
-    segof[i] = leaf ? -1 : pair;
+    segof[i] = d.n_ref <= (uint32_t)kSubMax ? -1 : pair;
+    if (d.n_ref <= (uint32_t)bucket) bpts[i] = c;
   }
   const float v[3] = {c.x, c.y, c.z};
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    float mn = v[k], mx = v[k];
-    const bool last = wave_seg_minmax(pair, mn, mx);
-    if (ok && last) {
-      atomicMin(&seg[pair].bmn[k], ord_enc(mn));
-      atomicMax(&seg[pair].bmx[k], ord_enc(mx));
+    float mn = ok ? v[k] : __builtin_inff(), mx = ok ? v[k] : -__builtin_inff();
+    if (uniform) {
+      block_minmax(mn, mx);
+      if (threadIdx.x == 0) {
+        atomicMin(&seg[p_first].bmn[k], ord_enc(mn));
+        atomicMax(&seg[p_first].bmx[k], ord_enc(mx));
+      }
+    } else {
+      const bool lastl = wave_seg_minmax(pair, mn, mx);
+      if (ok && lastl) {
+        atomicMin(&seg[pair].bmn[k], ord_enc(mn));
+        atomicMax(&seg[pair].bmx[k], ord_enc(mx));
+      }
     }
   }
 }
 
-// root segments (level 0, index = pair) from the boxes; single-leaf roots emit their event
-__global__ void k_tr_roots(int n_pairs, const PairDesc* __restrict__ pd, TreeSeg* seg, TreeCtl* ctl,
-                           NodeEvent* ev, uint32_t* ecnt, int bucket) {
+// Level-0 segments from the boxes. A pair with n_ref <= bucket is one leaf (its points are
+// final); one with n_ref <= kSubMax goes straight to the wave subtree builder.
+__global__ void k_tr_roots(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd, TreeSeg* seg,
+                           SubSeg* subs, TreeCtl* ctl, NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
+                           int bucket) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
   TreeSeg& s = seg[p];
@@ -211,28 +315,48 @@ __global__ void k_tr_roots(int n_pairs, const PairDesc* __restrict__ pd, TreeSeg
   split_dim(s.mn, s.mx, s.cd, s.ideal);
   s.lo = 0xffffffffu;
   s.hi = 0u;
-  if (d.n_ref <= (uint32_t)bucket) {
-    NodeEvent e{};
-    e.f = d.ref_off;
-    e.c = d.n_ref;
-    e.depth = 0;
-    e.pair = p;
-    e.cd = (int32_t)kLeaf;
-    e.parent_depth = -1;
-    emit_event(ctl, ev, ecnt, e);
-    s.count = 0;  // not split
+  if (d.n_ref <= (uint32_t)kSubMax) {
+    if (d.n_ref <= (uint32_t)bucket) {
+      emit_event(ev, valid, ecnt, total, leaf_event(d.ref_off, d.n_ref, 0, p, 0, -1));
+    } else {
+      const uint32_t si = atomicAdd(&ctl->n_small, 1u);
+      SubSeg& g = subs[si];
+      g.f = d.ref_off;
+      g.c = d.n_ref;
+      g.pair = p;
+      g.depth = 0;
+      for (int k = 0; k < 3; ++k) {
+        g.mn[k] = s.mn[k];
+        g.mx[k] = s.mx[k];
+      }
+      g.parent_f = 0;
+      g.parent_depth = -1;
+    }
+    s.count = 0;  // not split by the global levels
   }
   if (p == 0) ctl->nseg[0] = (uint32_t)n_pairs;
 }
 
-// ---- one level ---------------------------------------------------------------------------------
+// ---- one global level ------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_tr_minmax(uint32_t total, const int32_t* __restrict__ segof,
                                                    const float4* __restrict__ W, TreeSeg* seg) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t base = blockIdx.x * blockDim.x;
+  const uint32_t i = base + threadIdx.x;
   const int s = i < total ? segof[i] : -1;
+  // block inside one segment (contiguous ranges: first and last position suffice)
+  const int s_first = segof[base], s_last = segof[min(base + 255u, total - 1)];
+  const bool uniform = s_first >= 0 && s_first == s_last;
   float v = 0.f;
   if (s >= 0) v = coord(W[i], seg[s].cd);
-  float mn = v, mx = v;
+  float mn = s >= 0 ? v : __builtin_inff(), mx = s >= 0 ? v : -__builtin_inff();
+  if (uniform) {
+    block_minmax(mn, mx);
+    if (threadIdx.x == 0) {
+      atomicMin(&seg[s_first].lo, ord_enc(mn));
+      atomicMax(&seg[s_first].hi, ord_enc(mx));
+    }
+    return;
+  }
   const bool last = wave_seg_minmax(s, mn, mx);
   if (s >= 0 && last) {
     atomicMin(&seg[s].lo, ord_enc(mn));
@@ -335,15 +459,16 @@ __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t*
   if (li == 0) seg[s].br1 = br1;
 }
 
-// split: left-count rule, node event of this segment, children (leaf events or next-level
-// segments)
-__global__ __launch_bounds__(256) void k_tr_split(int level, TreeSeg* seg, TreeSeg* next, TreeCtl* ctl,
-                                                  const uint32_t* __restrict__ X2, NodeEvent* ev, uint32_t* ecnt,
+// split: left-count rule, node event of this segment, children: leaf events, wave-subtree
+// segments (count <= kSubMax) or next-level segments
+__global__ __launch_bounds__(256) void k_tr_split(int level, uint32_t total, TreeSeg* seg, TreeSeg* next,
+                                                  SubSeg* subs, TreeCtl* ctl, const uint32_t* __restrict__ X2,
+                                                  NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
                                                   int32_t* pair_depth, int bucket, uint32_t max_seg) {
   const uint32_t si = blockIdx.x * blockDim.x + threadIdx.x;
   if (si >= ctl->nseg[level]) return;
   TreeSeg& g = seg[si];
-  if (g.count == 0) return;  // single-leaf root
+  if (g.count == 0) return;  // root handled elsewhere
   const uint32_t f = g.first, count = g.count;
   const float lo = ord_dec(g.lo), hi = ord_dec(g.hi);
   const float cut = seg_cut(g);
@@ -366,22 +491,42 @@ __global__ __launch_bounds__(256) void k_tr_split(int level, TreeSeg* seg, TreeS
   e.left = left;
   e.parent_f = g.parent_f;
   e.parent_depth = g.parent_depth;
-  emit_event(ctl, ev, ecnt, e);
+  emit_event(ev, valid, ecnt, total, e);
   const int cdepth = g.depth + 1;
-  atomicMax(&pair_depth[g.pair], cdepth);
+  if (pair_depth[g.pair] < cdepth) atomicMax(&pair_depth[g.pair], cdepth);
   for (int side = 0; side < 2; ++side) {
     const uint32_t cf = side ? f + left : f, cc = side ? count - left : left;
+    float mn[3], mx[3];
+    for (int k = 0; k < 3; ++k) {
+      mn[k] = g.mn[k];
+      mx[k] = g.mx[k];
+    }
+    if (side) mn[g.cd] = cut;
+    else mx[g.cd] = cut;
     if (cc <= (uint32_t)bucket) {
-      NodeEvent l{};
-      l.f = cf;
-      l.c = cc;
-      l.depth = cdepth;
-      l.pair = g.pair;
-      l.cd = (int32_t)kLeaf;
-      l.parent_f = f;
-      l.parent_depth = g.depth;
-      emit_event(ctl, ev, ecnt, l);
+      emit_event(ev, valid, ecnt, total, leaf_event(cf, cc, cdepth, g.pair, f, g.depth));
       g.child[side] = -1;
+      continue;
+    }
+    if (cc <= (uint32_t)kSubMax) {
+      const uint32_t ni = atomicAdd(&ctl->n_small, 1u);
+      if (ni >= max_seg) {
+        atomicOr(&ctl->error, 4);
+        g.child[side] = -1;
+        continue;
+      }
+      SubSeg& c = subs[ni];
+      c.f = cf;
+      c.c = cc;
+      c.pair = g.pair;
+      c.depth = cdepth;
+      for (int k = 0; k < 3; ++k) {
+        c.mn[k] = mn[k];
+        c.mx[k] = mx[k];
+      }
+      c.parent_f = f;
+      c.parent_depth = g.depth;
+      g.child[side] = -2;
       continue;
     }
     const uint32_t ni = atomicAdd(&ctl->nseg[level + 1], 1u);
@@ -398,11 +543,9 @@ __global__ __launch_bounds__(256) void k_tr_split(int level, TreeSeg* seg, TreeS
     c.parent_f = f;
     c.parent_depth = g.depth;
     for (int k = 0; k < 3; ++k) {
-      c.mn[k] = g.mn[k];
-      c.mx[k] = g.mx[k];
+      c.mn[k] = mn[k];
+      c.mx[k] = mx[k];
     }
-    if (side) c.mn[g.cd] = cut;
-    else c.mx[g.cd] = cut;
     split_dim(c.mn, c.mx, c.cd, c.ideal);
     c.lo = 0xffffffffu;
     c.hi = 0u;
@@ -437,16 +580,169 @@ __global__ __launch_bounds__(256) void k_tr_move2(uint32_t total, const int32_t*
   const uint32_t q = f + p2;
   W2[q] = p;
   const int32_t child = g.child[p2 < g.left ? 0 : 1];
-  segof_next[q] = child;
-  if (child < 0) bpts[q] = p;
+  segof_next[q] = child >= 0 ? child : -1;
+  if (child == -1) bpts[q] = p;  // leaf: final; -2: the wave subtree builder takes it from W
+}
+
+// ---- wave subtree builder ----------------------------------------------------------------------
+// One wave finishes the whole subtree of a segment of <= kSubMax points in LDS, depth first,
+// with the same node rule; the Hoare passes use ballot/popcount ranks and swap each
+// misplaced pair in place (the pairs are disjoint). All control flow is wave-uniform.
+struct SubNode {
+  uint32_t lf, lc;  // local first / count
+  int32_t depth;
+  float mn[3], mx[3];
+  uint32_t pf;      // parent first (global)
+  int32_t pdepth;
+};
+
+__device__ __forceinline__ uint32_t popc_lt(uint64_t m) {
+  const int lane = threadIdx.x & 63;
+  return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// one Hoare pass over local [lo_b, end) with boundary br: elements with pred in [lo_b, br)
+template <class Pred>
+__device__ __forceinline__ void wave_hoare(float4* pts, uint16_t* posA, uint16_t* posB, uint32_t lo_b, uint32_t br,
+                                           uint32_t end, Pred pred) {
+  const int lane = threadIdx.x & 63;
+  uint32_t ra = 0, rb = 0;
+  for (uint32_t jb = lo_b; jb < end; jb += 64) {
+    const uint32_t j = jb + lane;
+    const bool ok = j < end;
+    const bool pr = ok && pred(pts[j]);
+    const bool ml = ok && j < br && !pr, mr = ok && j >= br && pr;
+    const uint64_t ma = __ballot(ml), mb = __ballot(mr);
+    if (ml) posA[ra + popc_lt(ma)] = (uint16_t)j;
+    if (mr) posB[rb + popc_lt(mb)] = (uint16_t)j;
+    ra += (uint32_t)__popcll(ma);
+    rb += (uint32_t)__popcll(mb);
+  }
+  __syncthreads();
+  // the k-th misplaced element from the left swaps with the k-th misplaced from the right
+  for (uint32_t k = lane; k < ra; k += 64) {
+    const uint32_t a = posA[k], b = posB[rb - 1 - k];
+    const float4 t = pts[a];
+    pts[a] = pts[b];
+    pts[b] = t;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void k_tr_subtree(uint32_t total, const TreeCtl* __restrict__ ctl,
+                                                   const SubSeg* __restrict__ subs, const float4* __restrict__ W,
+                                                   float4* __restrict__ bpts, NodeEvent* ev, uint8_t* valid,
+                                                   uint32_t* ecnt, int32_t* pair_depth, int bucket) {
+  __shared__ float4 pts[kSubMax];
+  __shared__ uint16_t posA[kSubMax / 2], posB[kSubMax / 2];
+  __shared__ SubNode stk[kFarStack];
+  if (blockIdx.x >= ctl->n_small) return;
+  const SubSeg g = subs[blockIdx.x];
+  const int lane = threadIdx.x;
+  const uint32_t gf = g.f;
+  for (uint32_t j = lane; j < g.c; j += 64) pts[j] = W[gf + j];
+  __syncthreads();
+  SubNode nd;
+  nd.lf = 0;
+  nd.lc = g.c;
+  nd.depth = g.depth;
+  for (int k = 0; k < 3; ++k) {
+    nd.mn[k] = g.mn[k];
+    nd.mx[k] = g.mx[k];
+  }
+  nd.pf = g.parent_f;
+  nd.pdepth = g.parent_depth;
+  int sp = 0;
+  int maxd = g.depth;
+  for (;;) {
+    if (nd.lc <= (uint32_t)bucket) {
+      if (lane == 0) emit_event(ev, valid, ecnt, total, leaf_event(gf + nd.lf, nd.lc, nd.depth, g.pair, nd.pf, nd.pdepth));
+      if (sp == 0) break;
+      nd = stk[--sp];
+      continue;
+    }
+    int cd;
+    float ideal;
+    split_dim(nd.mn, nd.mx, cd, ideal);
+    const uint32_t a0 = nd.lf, end = nd.lf + nd.lc;
+    float mn = __builtin_inff(), mx = -__builtin_inff();
+    for (uint32_t j = a0 + lane; j < end; j += 64) {
+      const float v = coord(pts[j], cd);
+      mn = fminf(mn, v);
+      mx = fmaxf(mx, v);
+    }
+    const float lo = wave_min(mn), hi = wave_max(mx);
+    const float cut = ideal < lo ? lo : (ideal > hi ? hi : ideal);
+    uint32_t nl = 0, ne = 0;
+    for (uint32_t j = a0 + lane; j < end; j += 64) {
+      const float v = coord(pts[j], cd);
+      nl += v < cut ? 1u : 0u;
+      ne += v == cut ? 1u : 0u;
+    }
+    nl = wave_sum_u(nl);
+    ne = wave_sum_u(ne);
+    const uint32_t br1 = nl, br2 = nl + ne, count = nd.lc;
+    wave_hoare(pts, posA, posB, a0, a0 + br1, end, [&](const float4& p) { return coord(p, cd) < cut; });
+    if (ne) wave_hoare(pts, posA, posB, a0 + br1, a0 + br2, end, [&](const float4& p) { return coord(p, cd) == cut; });
+    uint32_t left;
+    if (ideal < lo) left = 1;
+    else if (ideal > hi) left = count - 1;
+    else if (br1 > count / 2) left = br1;
+    else if (br2 < count / 2) left = br2;
+    else left = count / 2;
+    if (lane == 0) {
+      NodeEvent e{};
+      e.f = gf + nd.lf;
+      e.c = count;
+      e.depth = nd.depth;
+      e.pair = g.pair;
+      e.cut_bits = __float_as_uint(cut);
+      e.cd = cd;
+      e.left = left;
+      e.parent_f = nd.pf;
+      e.parent_depth = nd.pdepth;
+      emit_event(ev, valid, ecnt, total, e);
+    }
+    SubNode L, R;
+    L.lf = nd.lf;
+    L.lc = left;
+    R.lf = nd.lf + left;
+    R.lc = count - left;
+    L.depth = R.depth = nd.depth + 1;
+    L.pf = R.pf = gf + nd.lf;
+    L.pdepth = R.pdepth = nd.depth;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {  // selects, not a dynamic store (keeps the node in registers)
+      L.mn[k] = nd.mn[k];
+      R.mx[k] = nd.mx[k];
+      L.mx[k] = k == cd ? cut : nd.mx[k];
+      R.mn[k] = k == cd ? cut : nd.mn[k];
+    }
+    if (L.depth > maxd) maxd = L.depth;
+    if (sp >= kFarStack) break;  // deeper than the device stack: k_tr_desc reports it
+    if (lane == 0) stk[sp] = R;
+    ++sp;
+    __syncthreads();
+    nd = L;
+  }
+  __syncthreads();
+  for (uint32_t j = lane; j < g.c; j += 64) bpts[gf + j] = pts[j];
+  if (lane == 0 && pair_depth[g.pair] < maxd) atomicMax(&pair_depth[g.pair], maxd);
 }
 
 // ---- node records --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_tr_emit(TreeCtl* ctl, const NodeEvent* __restrict__ ev,
-                                                 const uint32_t* __restrict__ S, const PairDesc* __restrict__ pd,
-                                                 uint4* __restrict__ nodes, uint32_t cap) {
+__global__ __launch_bounds__(256) void k_tr_emit(uint32_t total, const NodeEvent* __restrict__ ev,
+                                                 const uint8_t* __restrict__ valid, const uint32_t* __restrict__ S,
+                                                 const PairDesc* __restrict__ pd, uint4* __restrict__ nodes,
+                                                 TreeCtl* ctl) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ctl->n_events || i >= cap) return;
+  if (i >= 2 * total || !valid[i]) return;
   const NodeEvent e = ev[i];
   const uint32_t ro = pd[e.pair].ref_off;
   const uint32_t base = S[ro + 1];  // nodes of earlier pairs (all end at or before ref_off)
@@ -459,7 +755,7 @@ __global__ __launch_bounds__(256) void k_tr_emit(TreeCtl* ctl, const NodeEvent* 
     const uint32_t right = (uint32_t)e.depth + 1 + S[e.f + e.left + 1] - base;
     r = make_uint4(e.cut_bits, (uint32_t)e.cd | (right << 2), par, 0u);
   }
-  if (pre >= cap) {
+  if (pre >= 2 * total + 2) {
     atomicOr(&ctl->error, 2);
     return;
   }
@@ -475,16 +771,6 @@ __global__ void k_tr_desc(int n_pairs, PairDesc* pd, const uint32_t* __restrict_
   d.n_nodes = S[d.ref_off + d.n_ref + 1] - d.node_off;
   d.tree_depth = pair_depth[p];
   if (d.tree_depth >= kFarStack) atomicOr(&ctl->error, 1);
-}
-
-// root segment boxes start empty: min at the largest encoding, max at the smallest
-__global__ void k_tr_init_boxes(int n_pairs, TreeSeg* seg) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n_pairs) return;
-  for (int k = 0; k < 3; ++k) {
-    seg[p].bmn[k] = 0xffffffffu;
-    seg[p].bmx[k] = 0u;
-  }
 }
 
 inline unsigned grid_of(size_t n) { return (unsigned)((n + 255) / 256); }
@@ -508,12 +794,14 @@ hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairD
   (void)hipMemsetAsync(w.sums, 0, (size_t)n_pairs * 6 * sizeof(uint64_t), s);
   (void)hipMemsetAsync(w.ctl, 0, sizeof(TreeCtl), s);
   (void)hipMemsetAsync(w.ecnt, 0, ((size_t)total + 2) * 4, s);
+  (void)hipMemsetAsync(w.valid, 0, 2 * (size_t)total, s);
   (void)hipMemsetAsync(w.pair_depth, 0, (size_t)n_pairs * 4, s);
   if (center) k_tr_sum<<<grid_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.sums);
   k_tr_frames<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.sums, center);
   k_tr_init_boxes<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, w.seg[0]);
-  k_tr_center<<<grid_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.W[0], bpts, w.segof[0], w.seg[0], bucket);
-  k_tr_roots<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.seg[0], w.ctl, w.ev, w.ecnt, bucket);
+  k_tr_center<<<grid_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.W[0], w.segof[0], w.seg[0], bpts, bucket);
+  k_tr_roots<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, total, pd, w.seg[0], w.subs, w.ctl, w.ev, w.valid, w.ecnt,
+                                                  bucket);
   return hipGetLastError();
 }
 
@@ -522,7 +810,9 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   const int a = level & 1, b = a ^ 1;
   TreeSeg* seg = w.seg[a];
   TreeSeg* next = w.seg[b];
-  const unsigned gp = grid_of(total), gp1 = grid_of((size_t)total + 1), gs = grid_of(w.max_seg);
+  const unsigned gp = grid_of(total), gp1 = grid_of((size_t)total + 1);
+  // segments at this level: at most n_pairs << level and at most total / kSubMax
+  const unsigned gs = grid_of(std::min<size_t>(w.max_seg, (size_t)w.n_pairs << std::min(level, 20)));
   k_tr_minmax<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[0], seg);
   k_tr_flag1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.flag);
   hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X1, (size_t)total + 1);
@@ -531,10 +821,17 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR, w.W[1], w.flag);
   e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X2, (size_t)total + 1);
   if (e != hipSuccess) return e;
-  k_tr_split<<<gs, 256, 0, s>>>(level, seg, next, w.ctl, w.X2, w.ev, w.ecnt, w.pair_depth, bucket,
-                                (uint32_t)w.max_seg);
+  k_tr_split<<<gs, 256, 0, s>>>(level, total, seg, next, w.subs, w.ctl, w.X2, w.ev, w.valid, w.ecnt, w.pair_depth,
+                                bucket, (uint32_t)w.max_seg);
   k_tr_pos<<<gp, 256, 0, s>>>(total, 2, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR);
   k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR, w.W[0], w.segof[b], bpts);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, uint32_t n_small, const TreeWork& w, float4* bpts,
+                                int bucket) {
+  if (n_small) k_tr_subtree<<<n_small, 64, 0, s>>>(total, w.ctl, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt,
+                                                   w.pair_depth, bucket);
   return hipGetLastError();
 }
 
@@ -543,7 +840,7 @@ hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDe
   // S[p] = #nodes with end < p  (exclusive scan over end positions 0..total+1)
   hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.ecnt, w.X1, (size_t)total + 2);
   if (e != hipSuccess) return e;
-  k_tr_emit<<<grid_of(2 * (size_t)total + 2), 256, 0, s>>>(w.ctl, w.ev, w.X1, pd, nodes, 2 * total + 2);
+  k_tr_emit<<<grid_of(2 * (size_t)total), 256, 0, s>>>(total, w.ev, w.valid, w.X1, pd, nodes, w.ctl);
   k_tr_desc<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.X1, w.pair_depth, w.ctl);
   return hipGetLastError();
 }

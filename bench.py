@@ -150,7 +150,7 @@ def main():
         nn_launches += t["launches"]
         iters_total += sum(s.iterations for s in batch.stats)
         ph = ctx.last_phase_ms()
-        phases += np.array([ph["overlap"], ph["centroid_tree_gpu"], ph["normals"], ph["icp_loop"], ph["total"]])
+        phases += np.array([ph["overlap"], ph["tree"], ph["normals"], ph["icp_loop"], ph["total"]])
     sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
