@@ -86,6 +86,8 @@ struct FarStack {
   int32_t P[kFarStack], PP[kFarStack];  // node whose far child began the frame, and its parent
 };
 
+constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
+
 template <int K>
 struct Trav {
   const uint4* nodes;
@@ -129,8 +131,27 @@ struct Trav {
       nd = nodes[n];
     }
     {
+      // bucket: the first kLeafBatch points are loaded before any is used (one round trip
+      // instead of one per point), then scanned in order
       const uint32_t b0 = nd.y >> 2, cnt = nd.x;
-      for (uint32_t i = 0; i < cnt; ++i) {
+      float3 P[kLeafBatch];
+#pragma unroll
+      for (int i = 0; i < kLeafBatch; ++i)
+        if ((uint32_t)i < cnt) {
+          const float4 p = pts[b0 + i];
+          P[i] = make_float3(p.x, p.y, p.z);
+        }
+#pragma unroll
+      for (int i = 0; i < kLeafBatch; ++i)
+        if ((uint32_t)i < cnt) {
+          const float d0 = q0 - P[i].x, d1 = q1 - P[i].y, d2 = q2 - P[i].z;
+          float dist = 0.f;
+          dist += d0 * d0;
+          dist += d1 * d1;
+          dist += d2 * d2;
+          if (dist <= maxR2 && dist < best.v[K - 1]) best_replace<K>(best, (int32_t)(b0 + i), dist);
+        }
+      for (uint32_t i = kLeafBatch; i < cnt; ++i) {  // buckets larger than the default 8
         const float4 p = pts[b0 + i];
         const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
         float dist = 0.f;
@@ -195,15 +216,13 @@ struct Trav {
 // advances its own phase (descent / bucket / climb), so lanes in different phases of their
 // traversals share every load instruction instead of serialising whole loops. Visit order,
 // far tests and results are those of Trav<1> (libnabo recurseKnn).
-enum : int32_t { kDesc = 0, kLeafScan = 1, kClimb = 2 };
+enum : int32_t { kDesc = 0, kClimb = 2 };
 
 struct SM0 {
   uint32_t nb, pb;  // node / bucket offsets of the query's pair
   float q0, q1, q2;
   float off0, off1, off2, rd, minFar;
   int32_t n, start, sp, phase;
-  uint32_t b, cnt;
-  int32_t lp;  // parent of the leaf being scanned
   float bestd;
   int32_t bid;
   uint32_t tp, tn;
@@ -237,7 +256,7 @@ struct SM0 {
 
   __device__ __forceinline__ bool advance(FarStack& fs, float E, float R, const uint4* __restrict__ nodes,
                                           const float4* __restrict__ pts) {
-    const uint4 v = (phase == kLeafScan) ? *reinterpret_cast<const uint4*>(pts + pb + b) : nodes[nb + n];
+    const uint4 v = nodes[nb + n];
     int32_t c, pc;
     if (phase == kDesc) {
       if ((v.y & 3u) != kLeaf) {
@@ -247,29 +266,45 @@ struct SM0 {
         minFar = fminf(minFar, rd + (-oc * oc + no * no));
         n = (no > 0.f) ? (int32_t)(v.y >> 2) : n + 1;
         ++tn;
-      } else {
-        b = v.y >> 2;
-        cnt = v.x;
-        lp = (int32_t)v.z;
-        phase = kLeafScan;
+        return false;
       }
-      return false;
-    }
-    if (phase == kLeafScan) {
-      const float d0 = q0 - __uint_as_float(v.x), d1 = q1 - __uint_as_float(v.y), d2 = q2 - __uint_as_float(v.z);
-      float dist = 0.f;
-      dist += d0 * d0;
-      dist += d1 * d1;
-      dist += d2 * d2;
-      if (dist <= R && dist < bestd) {
-        bestd = dist;
-        bid = (int32_t)b;
+      // bucket: all points loaded first (one round trip), then scanned in order
+      const uint32_t b0 = v.y >> 2, cn = v.x;
+      float3 P[kLeafBatch];
+#pragma unroll
+      for (int i = 0; i < kLeafBatch; ++i)
+        if ((uint32_t)i < cn) {
+          const float4 p = pts[pb + b0 + i];
+          P[i] = make_float3(p.x, p.y, p.z);
+        }
+#pragma unroll
+      for (int i = 0; i < kLeafBatch; ++i)
+        if ((uint32_t)i < cn) {
+          const float d0 = q0 - P[i].x, d1 = q1 - P[i].y, d2 = q2 - P[i].z;
+          float dist = 0.f;
+          dist += d0 * d0;
+          dist += d1 * d1;
+          dist += d2 * d2;
+          if (dist <= R && dist < bestd) {
+            bestd = dist;
+            bid = (int32_t)(b0 + i);
+          }
+        }
+      for (uint32_t i = kLeafBatch; i < cn; ++i) {
+        const float4 p = pts[pb + b0 + i];
+        const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
+        float dist = 0.f;
+        dist += d0 * d0;
+        dist += d1 * d1;
+        dist += d2 * d2;
+        if (dist <= R && dist < bestd) {
+          bestd = dist;
+          bid = (int32_t)(b0 + i);
+        }
       }
-      ++tp;
-      ++b;
-      if (--cnt != 0) return false;
+      tp += cn;
       c = n;
-      pc = lp;
+      pc = (int32_t)v.z;
       if (!(minFar <= R && minFar * E < bestd)) c = start;
     } else {  // kClimb: v = record of node n, parent of the finished near child
       const uint32_t cd = v.y & 3u;
