@@ -885,10 +885,25 @@ __global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__
   }
 }
 
+// DPP lane moves of a double (both halves with the same control); lanes outside the
+// pattern read 0 (bound_ctrl), which the sums below never use
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+// Sum over the 64 lanes in a fixed order (quads, rows of 16 via rotations, then the row
+// broadcasts), valid in every lane: DPP moves instead of LDS-crossbar shuffles.
 __device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  v += dpp_d<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);  // quad_perm [2,3,0,1]
+  v += dpp_d<0x124>(v); // row_ror:4
+  v += dpp_d<0x128>(v); // row_ror:8  -> every lane holds its row's sum
+  const double r0 = __shfl(v, 0, 64), r1 = __shfl(v, 16, 64), r2 = __shfl(v, 32, 64), r3 = __shfl(v, 48, 64);
+  return (r0 + r1) + (r2 + r3);
 }
 
 __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
@@ -909,32 +924,49 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
   for (int i = 0; i < kRedCols; ++i) acc[i] = 0.0;
   const uint32_t base = m.start[blockIdx.x];
   uint32_t tpts = 0, tnod = 0;
+  // all loads of the thread's readings first (independent), then the gathers of the kept
+  // ones, then the arithmetic: two round trips instead of three per reading
+  bool keep[kReducePerThread];
+  int32_t pos[kReducePerThread];
+  float4 r[kReducePerThread];
 #pragma unroll
   for (int it = 0; it < kReducePerThread; ++it) {
     const uint32_t j = base + it * kNNBlock + threadIdx.x;
-    if (j >= d.n_read) break;
-    const uint32_t tc = touched[d.read_off + j];
-    tpts += tc & 0xFFFFu;
-    tnod += tc >> 16;
-    const float dd = d2[d.read_off + j];
-    if (!(dd <= limit)) continue;
-    const int32_t pos = match[d.read_off + j];
-    const float4 r = read_c[d.read_off + j];
+    keep[it] = false;
+    pos[it] = 0;
+    if (j < d.n_read) {
+      const uint32_t tc = touched[d.read_off + j];
+      tpts += tc & 0xFFFFu;
+      tnod += tc >> 16;
+      keep[it] = d2[d.read_off + j] <= limit;
+      pos[it] = match[d.read_off + j];
+      r[it] = read_c[d.read_off + j];
+    }
+  }
+  float4 q[kReducePerThread], nr[kReducePerThread];
+#pragma unroll
+  for (int it = 0; it < kReducePerThread; ++it)
+    if (keep[it]) {
+      q[it] = bpts[d.ref_off + pos[it]];
+      nr[it] = bnrm[d.ref_off + pos[it]];
+    }
+#pragma unroll
+  for (int it = 0; it < kReducePerThread; ++it) {
+    if (!keep[it]) continue;
     float p[3];
-    apply4(T, r.x, r.y, r.z, p);
-    const float4 q = bpts[d.ref_off + pos];
-    const float4 nr = bnrm[d.ref_off + pos];
+    apply4(T, r[it].x, r[it].y, r[it].z, p);
+    const float4 n4 = nr[it];
     float F[6];
-    F[0] = p[1] * nr.z - p[2] * nr.y;
-    F[1] = p[2] * nr.x - p[0] * nr.z;
-    F[2] = p[0] * nr.y - p[1] * nr.x;
-    F[3] = nr.x;
-    F[4] = nr.y;
-    F[5] = nr.z;
-    const float dl0 = p[0] - q.x, dl1 = p[1] - q.y, dl2 = p[2] - q.z;
-    float dot = dl0 * nr.x;
-    dot += dl1 * nr.y;
-    dot += dl2 * nr.z;
+    F[0] = p[1] * n4.z - p[2] * n4.y;
+    F[1] = p[2] * n4.x - p[0] * n4.z;
+    F[2] = p[0] * n4.y - p[1] * n4.x;
+    F[3] = n4.x;
+    F[4] = n4.y;
+    F[5] = n4.z;
+    const float dl0 = p[0] - q[it].x, dl1 = p[1] - q[it].y, dl2 = p[2] - q[it].z;
+    float dot = dl0 * n4.x;
+    dot += dl1 * n4.y;
+    dot += dl2 * n4.z;
     int c = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a)

@@ -151,18 +151,38 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
       }
     }
     const double len = (double)length;
+    // the linear map index follows the walk: one add per step, one bounds test on the axis
+    // that moved (the other two are unchanged)
+    const int64_t stride[3] = {(int64_t)dm1 * dm2, (int64_t)dm2, 1};
+    int rel[3] = {cur[0] - mn0, cur[1] - mn1, cur[2] - mn2};
+    const int dims[3] = {dm0, dm1, dm2}, mins[3] = {mn0, mn1, mn2};
+    int64_t idx = (int64_t)rel[0] * stride[0] + (int64_t)rel[1] * stride[1] + rel[2];
     for (;;) {
       int dim;
       if (tMax[0] < tMax[1])
         dim = (tMax[0] < tMax[2]) ? 0 : 2;
       else
         dim = (tMax[1] < tMax[2]) ? 1 : 2;
-      cur[dim] = (cur[dim] + step[dim]) & 0xFFFF;
-      tMax[dim] += tDelta[dim];
+      // cur[dim] = (cur[dim] + step[dim]) & 0xFFFF, on registers without dynamic indexing
+      bool bad = false;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (i == dim) {
+          cur[i] = (cur[i] + step[i]) & 0xFFFF;
+          tMax[i] += tDelta[i];
+          rel[i] += step[i];
+          idx += step[i] * stride[i];
+          // a key wrap (0xFFFF) or a walk leaving the padded box is reported, never stored
+          bad = (cur[i] - mins[i]) != rel[i] || (unsigned)rel[i] >= (unsigned)dims[i];
+        }
       if (cur[0] == ke[0] && cur[1] == ke[1] && cur[2] == ke[2]) break;
       const double dfo = fmin(fmin(tMax[0], tMax[1]), tMax[2]);
       if (dfo > len) break;
-      mark(cur[0], cur[1], cur[2]);
+      if (bad) {
+        err = true;
+        break;
+      }
+      bm[idx] = 1;
     }
   }
   if (okE) mark(ke[0], ke[1], ke[2]);
