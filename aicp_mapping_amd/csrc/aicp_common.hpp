@@ -52,12 +52,17 @@ struct PairDesc {
   float mean[3];                // reference centroid (float)
   float ratio;                  // configured trimmed ratio (overridden by overlap)
   int32_t tree_depth;
-  // overlap voxel maps (AICP_RUN_OVERLAP): one byte per voxel of the padded key box
-  int32_t ovl_min[3];           // key of voxel (0,0,0)
-  int32_t ovl_dim[3];           // box extent in voxels
-  uint64_t ovl_word_off;        // byte offset into the map arena (ref map, then read map)
-  uint64_t ovl_words;           // bytes per map (multiple of 16)
   double ref_origin[3], read_origin[3];
+};
+
+// Overlap voxel maps of a pair (AICP_RUN_OVERLAP): one byte per voxel of the padded key box.
+// Kept apart from PairDesc so the overlap (its own stream) never rewrites descriptors the
+// kd-tree stream is filling in.
+struct OvlDesc {
+  int32_t min[3];   // key of voxel (0,0,0)
+  int32_t dim[3];   // box extent in voxels
+  uint64_t off;     // byte offset into the map arena (ref map, then read map)
+  uint64_t bytes;   // bytes per map (multiple of 16)
 };
 
 struct PairState {

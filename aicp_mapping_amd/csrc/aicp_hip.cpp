@@ -105,15 +105,17 @@ struct aicp_hip_batch {
 struct aicp_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // kd-tree + normals, concurrent with the overlap on `stream`
   std::string err;
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
-      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap;
+      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl;
   // kd-tree construction work space (kernels_tree.hip)
   DevBuf tw_W0, tw_W1, tw_segof0, tw_segof1, tw_seg0, tw_seg1, tw_flag, tw_X1, tw_X2, tw_posL, tw_posR, tw_ev,
       tw_valid, tw_subs, tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
-  PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io;
+  PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io, pin_ovl;
   std::vector<hipEvent_t> nn_ev;
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[12] = {};
+  TreeWork tw{};  // device_trees_begin -> device_trees_end
   int last_nn_launches = 0;
   double last_nn_ms = 0, last_nn_bytes = 0;
   uint64_t last_queries = 0;
@@ -261,8 +263,8 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
 // Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device: raw[ΣM] float4,
 // dDesc with ref_off / n_ref / Tin. Writes ctx->bpts (bucket order, w = local id), ctx->nodes
 // and the desc fields mean, Tmean, Tinit, node_off, n_nodes, tree_depth.
-int device_trees(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc, const float4* raw,
-                 int center, int bucket) {
+int device_trees_begin(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
+                       const float4* raw, int center, int bucket) {
   const size_t n = (size_t)total;
   const size_t max_seg = n / 2 + P + 1;
   HIPC(ensure(ctx->bpts, n * 16));
@@ -313,6 +315,15 @@ int device_trees(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, Pai
   w.max_seg = max_seg;
   float4* bpts = ctx->bpts.as<float4>();
   HIPC(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts, bucket));
+  ctx->tw = w;
+  return AICP_OK;
+}
+
+// global levels (host polls), wave subtrees, node records; see device_trees_begin
+int device_trees_end(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc, int bucket) {
+  const size_t n = (size_t)total;
+  const TreeWork& w = ctx->tw;
+  float4* bpts = ctx->bpts.as<float4>();
   TreeCtl* hctl = ctx->pin_ctl.as<TreeCtl>();
   // global levels until every remaining segment fits one wave's LDS (kSubMax points); the
   // host polls the next level's segment count from level 4 on
@@ -376,10 +387,14 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   PairDesc* dDesc = ctx->desc.as<PairDesc>();
   PairState* dState = ctx->state.as<PairState>();
   uint32_t* dCtr = ctx->ctrs.as<uint32_t>();
+  // Two streams: s runs the overlap (bbox -> host sizes the voxel maps -> marking -> counts ->
+  // ratio), s2 the centroid, kd-trees, reading frame and normals; s joins s2 before the loop.
+  hipStream_t s2 = ctx->stream2;
   std::memcpy(pdA, desc.data(), P * sizeof(PairDesc));
   HIPC(hipEventRecord(ctx->ev[0], s));
   HIPC(hipMemcpyAsync(dDesc, pdA, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
   launch_init_state(s, (int)P, dDesc, dState);
+  HIPC(hipEventRecord(ctx->ev[7], s));
   if (doOvl) {
     launch_ovl_init(s, (int)P, dDesc, dState, res);
     launch_ovl_bbox(s, B->m_ref, dDesc, dState, B->ref_raw.as<float4>(), 0, res);
@@ -387,47 +402,55 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
   }
   HIPC(hipEventRecord(ctx->ev[1], s));
+  // s2: centroid, centred reference, root segments (the levels follow after the overlap is queued)
+  if (doIcp) {
+    HIPC(hipStreamWaitEvent(s2, ctx->ev[7], 0));
+    HIPC(hipEventRecord(ctx->ev[8], s2));
+    rc = device_trees_begin(ctx, s2, P, B->total_ref, dDesc, B->ref_raw.as<float4>(), 1, cfg->bucket_size);
+    if (rc) return rc;
+  }
   // overlap: size the voxel maps from the key boxes, then mark
   uint64_t bm_bytes = 0;
   if (doOvl) {
     HIPC(hipEventSynchronize(ctx->ev[1]));
     const PairState* hs = ctx->pin_state.as<PairState>();
+    HIPC(ensure(ctx->pin_ovl, P * sizeof(OvlDesc)));
+    HIPC(ensure(ctx->ovl, P * sizeof(OvlDesc)));
+    OvlDesc* ho = ctx->pin_ovl.as<OvlDesc>();
     for (size_t i = 0; i < P; ++i) {
-      PairDesc& d = desc[i];
+      OvlDesc& o = ho[i];
       uint64_t vox = 1;
       for (int k = 0; k < 3; ++k) {
         int lo = hs[i].ovl_bbox[k], hi = hs[i].ovl_bbox[3 + k];
         if (lo > hi) lo = hi = 0;  // nothing inside the key range
-        d.ovl_min[k] = lo - 2;
-        d.ovl_dim[k] = (hi - lo) + 5;
-        vox *= (uint64_t)d.ovl_dim[k];
+        o.min[k] = lo - 2;
+        o.dim[k] = (hi - lo) + 5;
+        vox *= (uint64_t)o.dim[k];
       }
       if (vox > (1ull << 34)) FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
-      d.ovl_words = (vox + 15) / 16 * 16;
-      d.ovl_word_off = bm_bytes;
-      bm_bytes += 2 * d.ovl_words;
+      o.bytes = (vox + 15) / 16 * 16;
+      o.off = bm_bytes;
+      bm_bytes += 2 * o.bytes;
     }
     HIPC(ensure(ctx->bitmap, bm_bytes));
-    std::memcpy(pdB, desc.data(), P * sizeof(PairDesc));
-    HIPC(hipMemcpyAsync(dDesc, pdB, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(ctx->ovl.p, ho, P * sizeof(OvlDesc), hipMemcpyHostToDevice, s));
     HIPC(hipEventRecord(ctx->ev[6], s));
     uint8_t* bm = ctx->bitmap.as<uint8_t>();
+    const OvlDesc* dOvl = ctx->ovl.as<OvlDesc>();
     HIPC(hipMemsetAsync(bm, 0, bm_bytes, s));
-    launch_ovl_mark(s, B->m_ref, dDesc, dState, B->ref_raw.as<float4>(), 0, res, bm);
-    launch_ovl_mark(s, B->m_read, dDesc, dState, B->read_raw.as<float4>(), 1, res, bm);
-    launch_ovl_count(s, (int)P, dDesc, dState, bm);
+    launch_ovl_mark(s, B->m_ref, dDesc, dOvl, dState, B->ref_raw.as<float4>(), 0, res, bm);
+    launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, B->read_raw.as<float4>(), 1, res, bm);
+    launch_ovl_count(s, (int)P, dOvl, dState, bm);
     launch_ovl_finish(s, (int)P, dState, doIcp ? 1 : 0);
   }
   HIPC(hipEventRecord(ctx->ev[2], s));
-  // device: centroid + kd-trees
-  if (doIcp) {
-    rc = device_trees(ctx, s, P, B->total_ref, dDesc, B->ref_raw.as<float4>(), 1, cfg->bucket_size);
-    if (rc) return rc;
-  }
-  HIPC(hipEventRecord(ctx->ev[3], s));
   IcpParams prm{};
   int nn_launches = 0;
   if (doIcp) {
+    // s2: kd-tree levels + subtrees, reading frame, SurfaceNormal
+    rc = device_trees_end(ctx, s2, P, B->total_ref, dDesc, cfg->bucket_size);
+    if (rc) return rc;
+    HIPC(hipEventRecord(ctx->ev[3], s2));
     HIPC(ensure(ctx->read_c, B->total_read * 16));
     HIPC(ensure(ctx->bpts, B->total_ref * 16));
     HIPC(ensure(ctx->bnrm, B->total_ref * 16));
@@ -445,14 +468,16 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     float4* readc = ctx->read_c.as<float4>();
     const uint4* nodes = ctx->nodes.as<uint4>();
     const int32_t* parent = nullptr;
-    launch_prepare_read(s, B->m_read, dDesc, B->read_raw.as<float4>(), readc);
+    launch_prepare_read(s2, B->m_read, dDesc, B->read_raw.as<float4>(), readc);
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
     uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
-    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s));
-    if (!launch_normals(s, (int)P, (uint32_t)B->total_ref, dDesc, dState, nodes, parent, bpts, bnrm,
+    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
+    if (!launch_normals(s2, (int)P, (uint32_t)B->total_ref, dDesc, dState, nodes, parent, bpts, bnrm,
                         cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
-    HIPC(hipEventRecord(ctx->ev[4], s));
+    HIPC(hipEventRecord(ctx->ev[4], s2));
+    HIPC(hipStreamWaitEvent(s, ctx->ev[4], 0));
+    HIPC(hipEventRecord(ctx->ev[9], s));
     prm.maxE2 = (1 + cfg->nn_epsilon) * (1 + cfg->nn_epsilon);
     prm.maxR2 = cfg->nn_max_dist * cfg->nn_max_dist;
     prm.max_iter = cfg->max_iter;
@@ -476,7 +501,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     }
     launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
   } else {
+    HIPC(hipEventRecord(ctx->ev[8], s));
+    HIPC(hipEventRecord(ctx->ev[3], s));
     HIPC(hipEventRecord(ctx->ev[4], s));
+    HIPC(hipEventRecord(ctx->ev[9], s));
   }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(ctx->ev[5], s));
@@ -523,9 +551,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   ctx->last_nn_bytes = (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0;
   ctx->last_queries = queries;
   ctx->last_phase[0] = doOvl ? ev_ms(ctx->ev[0], ctx->ev[1]) + ev_ms(ctx->ev[6], ctx->ev[2]) : 0;
-  ctx->last_phase[1] = doIcp ? ev_ms(ctx->ev[2], ctx->ev[3]) : 0;
+  // tree and normals run on the second stream, concurrently with the overlap
+  ctx->last_phase[1] = doIcp ? ev_ms(ctx->ev[8], ctx->ev[3]) : 0;
   ctx->last_phase[2] = doIcp ? ev_ms(ctx->ev[3], ctx->ev[4]) : 0;
-  ctx->last_phase[3] = doIcp ? ev_ms(ctx->ev[4], ctx->ev[5]) : 0;
+  ctx->last_phase[3] = doIcp ? ev_ms(ctx->ev[9], ctx->ev[5]) : 0;
   ctx->last_phase[4] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   if (first_err) ctx->err = "pair status " + std::to_string(first_err);
@@ -553,7 +582,9 @@ int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, Pa
   ident4(d.Tin);
   HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
-  const int rc = device_trees(ctx, s, 1, n, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8);
+  int rc = device_trees_begin(ctx, s, 1, n, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8);
+  if (rc) return rc;
+  rc = device_trees_end(ctx, s, 1, n, ctx->desc.as<PairDesc>(), 8);
   if (rc) return rc;
   HIPC(hipMemcpyAsync(&d, ctx->desc.p, sizeof(d), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -579,6 +610,11 @@ int aicp_hip_create(int device, aicp_hip_ctx** out) {
     delete c;
     return AICP_ERR_HIP;
   }
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return AICP_ERR_HIP;
+  }
   *out = c;
   return AICP_OK;
 }
@@ -590,17 +626,19 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->match, &ctx->d2, &ctx->desc,
                     &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
-                    &ctx->qmap, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
+                    &ctx->qmap, &ctx->ovl, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
                     &ctx->tw_segof1, &ctx->tw_seg0, &ctx->tw_seg1, &ctx->tw_flag, &ctx->tw_X1, &ctx->tw_X2,
                     &ctx->tw_posL, &ctx->tw_posR, &ctx->tw_ev, &ctx->tw_valid, &ctx->tw_subs, &ctx->tw_ecnt,
                     &ctx->tw_sums, &ctx->tw_pdepth,
                     &ctx->tw_ctl, &ctx->tw_scan})
     release(*b);
-  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_ctl, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io}) release(*b);
+  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_ctl, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl})
+    release(*b);
   for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
   for (auto e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   delete ctx;
 }
 

@@ -93,9 +93,9 @@ void launch_ovl_init(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* 
                      double res);
 void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
                      const float4* pts, int side, double res);
-void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
+void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDesc* od, PairState* st,
                      const float4* pts, int side, double res, uint8_t* maps);
-void launch_ovl_count(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
+void launch_ovl_count(hipStream_t s, int n_pairs, const OvlDesc* od, PairState* st,
                       const uint8_t* maps);
 void launch_ovl_finish(hipStream_t s, int n_pairs, PairState* st, int set_ratio);
 

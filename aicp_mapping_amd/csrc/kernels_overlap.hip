@@ -98,17 +98,19 @@ __global__ __launch_bounds__(256) void k_ovl_bbox(BlockMap m, const PairDesc* __
 
 // computeRayKeys(origin, end) + endpoint key, marking bits of one bitmap.
 __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __restrict__ pd,
-                                                  PairState* st, const float4* __restrict__ pts,
-                                                  int side, double res, uint8_t* maps) {
+                                                  const OvlDesc* __restrict__ od, PairState* st,
+                                                  const float4* __restrict__ pts, int side, double res,
+                                                  uint8_t* maps) {
   const int pair = m.pair[blockIdx.x];
   const uint32_t j = m.start[blockIdx.x] + threadIdx.x;
   const PairDesc& d = pd[pair];
   const uint32_t n = side ? d.n_read : d.n_ref;
   if (j >= n) return;
   const uint32_t off = side ? d.read_off : d.ref_off;
-  uint8_t* bm = maps + d.ovl_word_off + (side ? d.ovl_words : 0);
-  const int mn0 = d.ovl_min[0], mn1 = d.ovl_min[1], mn2 = d.ovl_min[2];
-  const int dm0 = d.ovl_dim[0], dm1 = d.ovl_dim[1], dm2 = d.ovl_dim[2];
+  const OvlDesc& ov = od[pair];
+  uint8_t* bm = maps + ov.off + (side ? ov.bytes : 0);
+  const int mn0 = ov.min[0], mn1 = ov.min[1], mn2 = ov.min[2];
+  const int dm0 = ov.dim[0], dm1 = ov.dim[1], dm2 = ov.dim[2];
   bool err = false;
   auto mark = [&](int k0, int k1, int k2) {
     const int a = k0 - mn0, b = k1 - mn1, c = k2 - mn2;
@@ -119,8 +121,8 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
     const uint64_t idx = ((uint64_t)a * (uint64_t)dm1 + (uint64_t)b) * (uint64_t)dm2 + (uint64_t)c;
     bm[idx] = 1;  // (a test-before-store measured slower: 867 vs 690 us per launch)
   };
-  const double* od = side ? d.read_origin : d.ref_origin;
-  const float o[3] = {(float)od[0], (float)od[1], (float)od[2]};
+  const double* org = side ? d.read_origin : d.ref_origin;
+  const float o[3] = {(float)org[0], (float)org[1], (float)org[2]};
   const float4 p4 = pts[off + j];
   const float e[3] = {p4.x, p4.y, p4.z};
   const double rf = 1.0 / res;
@@ -191,15 +193,15 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
 
 // popcounts: |A|, |B|, |A & B| (64 workgroups per pair, integer atomics -> deterministic)
 constexpr int kCountBlocksPerPair = 64;
-__global__ __launch_bounds__(256) void k_ovl_count(const PairDesc* __restrict__ pd, PairState* st,
+__global__ __launch_bounds__(256) void k_ovl_count(const OvlDesc* __restrict__ od, PairState* st,
                                                    const uint8_t* __restrict__ maps) {
   const int pair = blockIdx.x / kCountBlocksPerPair;
   const int sub = blockIdx.x % kCountBlocksPerPair;
-  const PairDesc& d = pd[pair];
   // maps are 16-byte aligned and padded to 16-byte multiples (host); bytes are 0 or 1
-  const uint4* A = (const uint4*)(maps + d.ovl_word_off);
-  const uint4* B = (const uint4*)(maps + d.ovl_word_off + d.ovl_words);
-  const uint64_t n16 = d.ovl_words / 16;
+  const OvlDesc& ov = od[pair];
+  const uint4* A = (const uint4*)(maps + ov.off);
+  const uint4* B = (const uint4*)(maps + ov.off + ov.bytes);
+  const uint64_t n16 = ov.bytes / 16;
   unsigned long long ca = 0, cb = 0, cab = 0;
   for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)kCountBlocksPerPair * 256) {
     const uint4 a = A[w], b = B[w];
@@ -239,13 +241,13 @@ void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* s
                      const float4* pts, int side, double res) {
   if (m.n_blocks) k_ovl_bbox<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res);
 }
-void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
+void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDesc* od, PairState* st,
                      const float4* pts, int side, double res, uint8_t* maps) {
-  if (m.n_blocks) k_ovl_mark<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res, maps);
+  if (m.n_blocks) k_ovl_mark<<<m.n_blocks, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
 }
-void launch_ovl_count(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
+void launch_ovl_count(hipStream_t s, int n_pairs, const OvlDesc* od, PairState* st,
                       const uint8_t* maps) {
-  k_ovl_count<<<n_pairs * kCountBlocksPerPair, 256, 0, s>>>(pd, st, maps);
+  k_ovl_count<<<n_pairs * kCountBlocksPerPair, 256, 0, s>>>(od, st, maps);
 }
 void launch_ovl_finish(hipStream_t s, int n_pairs, PairState* st, int set_ratio) {
   k_ovl_finish<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, st, set_ratio);
