@@ -52,6 +52,7 @@ struct PairDesc {
   float mean[3];                // reference centroid (float)
   float ratio;                  // configured trimmed ratio (overridden by overlap)
   int32_t tree_depth;
+  int32_t ref_id;               // index of the pair's (deduplicated) reference cloud
   double ref_origin[3], read_origin[3];
 };
 

@@ -96,6 +96,7 @@ struct Maps {  // block maps of one flat grid
 struct aicp_hip_batch {
   size_t P = 0;
   std::vector<PairDesc> desc;
+  std::vector<PairDesc> rdesc;  // one per distinct reference cloud (tree + normals built once)
   uint64_t total_ref = 0, total_read = 0;
   uint32_t n_red_total = 0;
   DevBuf ref_raw, read_raw, maps;
@@ -108,11 +109,11 @@ struct aicp_hip_ctx {
   hipStream_t stream2 = nullptr;  // kd-tree + normals, concurrent with the overlap on `stream`
   std::string err;
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
-      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl;
+      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate;
   // kd-tree construction work space (kernels_tree.hip)
   DevBuf tw_W0, tw_W1, tw_segof0, tw_segof1, tw_seg0, tw_seg1, tw_flag, tw_X1, tw_X2, tw_posL, tw_posR, tw_ev,
       tw_valid, tw_subs, tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
-  PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io, pin_ovl;
+  PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev[12] = {};
   TreeWork tw{};  // device_trees_begin -> device_trees_end
@@ -186,14 +187,39 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   if (!pairs || n == 0) FAIL(AICP_ERR_INVALID, "no pairs");
   B->P = n;
   B->desc.assign(n, PairDesc{});
+  B->rdesc.clear();
   uint64_t ro = 0, wo = 0;
   uint32_t red = 0;
   Maps mr, mf, md;
+  // pairs whose reference is the same caller array (pointer, count, stride) share one copy,
+  // one kd-tree and one set of normals (a reference window serves several readings)
+  std::vector<size_t> rep;  // representative pair of each distinct reference
   for (size_t i = 0; i < n; ++i) {
     const aicp_pair& p = pairs[i];
     if (!valid_pair(p)) FAIL(AICP_ERR_INVALID, "invalid pair " + std::to_string(i));
     PairDesc& d = B->desc[i];
-    d.ref_off = (uint32_t)ro;
+    int32_t rid = -1;
+    for (size_t r = 0; r < rep.size(); ++r) {
+      const aicp_pair& q = pairs[rep[r]];
+      if (q.ref == p.ref && q.n_ref == p.n_ref && q.ref_stride == p.ref_stride) {
+        rid = (int32_t)r;
+        break;
+      }
+    }
+    if (rid < 0) {
+      rid = (int32_t)rep.size();
+      rep.push_back(i);
+      PairDesc r{};
+      r.ref_off = (uint32_t)ro;
+      r.n_ref = (uint32_t)p.n_ref;
+      r.ref_id = rid;
+      r.ratio = 0.5f;
+      ident4(r.Tin);
+      B->rdesc.push_back(r);
+      ro += p.n_ref;
+    }
+    d.ref_id = rid;
+    d.ref_off = B->rdesc[rid].ref_off;
     d.n_ref = (uint32_t)p.n_ref;
     d.read_off = (uint32_t)wo;
     d.n_read = (uint32_t)p.n_read;
@@ -204,7 +230,6 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
       d.read_origin[k] = p.read_origin[k];
     }
     red += d.n_red_blk;
-    ro += p.n_ref;
     wo += p.n_read;
     if (ro >= (1ull << 31) || wo >= (1ull << 31)) FAIL(AICP_ERR_UNSUPPORTED, "batch too large");
     if (p.init_T)
@@ -223,9 +248,9 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   HIPC(ensure(B->read_raw, wo * 16));
   HIPC(ensure(ctx->pin_io, std::max(ro, wo) * 16));
   float* st = ctx->pin_io.as<float>();
-  for (size_t i = 0; i < n; ++i) {
-    const PairDesc& d = B->desc[i];
-    pack_xyz4(pairs[i].ref, d.n_ref, pairs[i].ref_stride, st + 4ull * d.ref_off);
+  for (size_t r = 0; r < rep.size(); ++r) {
+    const PairDesc& d = B->rdesc[r];
+    pack_xyz4(pairs[rep[r]].ref, d.n_ref, pairs[rep[r]].ref_stride, st + 4ull * d.ref_off);
   }
   HIPC(hipMemcpyAsync(B->ref_raw.p, st, ro * 16, hipMemcpyHostToDevice, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
@@ -402,11 +427,23 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
   }
   HIPC(hipEventRecord(ctx->ev[1], s));
-  // s2: centroid, centred reference, root segments (the levels follow after the overlap is queued)
+  // s2: per distinct reference: centroid, centred cloud, root segments (the levels follow
+  // once the overlap is queued)
+  const size_t R = B->rdesc.size();
+  PairDesc* dRdesc = nullptr;
+  PairState* dRstate = nullptr;
   if (doIcp) {
+    HIPC(ensure(ctx->rdesc, R * sizeof(PairDesc)));
+    HIPC(ensure(ctx->rstate, R * sizeof(PairState)));
+    HIPC(ensure(ctx->pin_rdesc, R * sizeof(PairDesc)));
+    dRdesc = ctx->rdesc.as<PairDesc>();
+    dRstate = ctx->rstate.as<PairState>();
+    std::memcpy(ctx->pin_rdesc.p, B->rdesc.data(), R * sizeof(PairDesc));
     HIPC(hipStreamWaitEvent(s2, ctx->ev[7], 0));
     HIPC(hipEventRecord(ctx->ev[8], s2));
-    rc = device_trees_begin(ctx, s2, P, B->total_ref, dDesc, B->ref_raw.as<float4>(), 1, cfg->bucket_size);
+    HIPC(hipMemcpyAsync(dRdesc, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s2));
+    launch_init_state(s2, (int)R, dRdesc, dRstate);
+    rc = device_trees_begin(ctx, s2, R, B->total_ref, dRdesc, B->ref_raw.as<float4>(), 1, cfg->bucket_size);
     if (rc) return rc;
   }
   // overlap: size the voxel maps from the key boxes, then mark
@@ -448,8 +485,9 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   int nn_launches = 0;
   if (doIcp) {
     // s2: kd-tree levels + subtrees, reading frame, SurfaceNormal
-    rc = device_trees_end(ctx, s2, P, B->total_ref, dDesc, cfg->bucket_size);
+    rc = device_trees_end(ctx, s2, R, B->total_ref, dRdesc, cfg->bucket_size);
     if (rc) return rc;
+    launch_pairs_from_refs(s2, (int)P, dDesc, dRdesc);
     HIPC(hipEventRecord(ctx->ev[3], s2));
     HIPC(ensure(ctx->read_c, B->total_read * 16));
     HIPC(ensure(ctx->bpts, B->total_ref * 16));
@@ -472,9 +510,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
     uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
     HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
-    if (!launch_normals(s2, (int)P, (uint32_t)B->total_ref, dDesc, dState, nodes, parent, bpts, bnrm,
+    if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, dRdesc, dRstate, nodes, parent, bpts, bnrm,
                         cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
+    launch_pairs_degenerate(s2, (int)P, dDesc, dState, dRstate);
     HIPC(hipEventRecord(ctx->ev[4], s2));
     HIPC(hipStreamWaitEvent(s, ctx->ev[4], 0));
     HIPC(hipEventRecord(ctx->ev[9], s));
@@ -626,13 +665,14 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->match, &ctx->d2, &ctx->desc,
                     &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
-                    &ctx->qmap, &ctx->ovl, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
+                    &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
                     &ctx->tw_segof1, &ctx->tw_seg0, &ctx->tw_seg1, &ctx->tw_flag, &ctx->tw_X1, &ctx->tw_X2,
                     &ctx->tw_posL, &ctx->tw_posR, &ctx->tw_ev, &ctx->tw_valid, &ctx->tw_subs, &ctx->tw_ecnt,
                     &ctx->tw_sums, &ctx->tw_pdepth,
                     &ctx->tw_ctl, &ctx->tw_scan})
     release(*b);
-  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_ctl, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl})
+  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_ctl, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
+                    &ctx->pin_rdesc})
     release(*b);
   for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
   for (auto e : ctx->ev)

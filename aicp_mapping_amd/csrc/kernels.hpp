@@ -88,6 +88,11 @@ hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, uint32_t n_small,
 hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const TreeWork& w,
                               uint4* nodes);
 
+// pairs -> their shared reference's centroid / tree fields (+ T_refMean_dataIn), and its
+// SurfaceNormal degenerate count
+void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd);
+void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst);
+
 // ---- overlap -------------------------------------------------------------------------------
 void launch_ovl_init(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
                      double res);

@@ -773,6 +773,34 @@ __global__ void k_tr_desc(int n_pairs, PairDesc* pd, const uint32_t* __restrict_
   if (d.tree_depth >= kFarStack) atomicOr(&ctl->error, 1);
 }
 
+// Pairs sharing a reference cloud share its centroid, kd-tree and normals (built once per
+// reference): copy the reference's fields into the pair descriptors;
+// T_refMean_dataIn depends on the pair's own initial transform.
+__global__ void k_pairs_from_refs(int n_pairs, PairDesc* pd, const PairDesc* __restrict__ rd) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  PairDesc& d = pd[p];
+  const PairDesc& r = rd[d.ref_id];
+  d.node_off = r.node_off;
+  d.n_nodes = r.n_nodes;
+  d.tree_depth = r.tree_depth;
+  float Tmi[16];
+  ident4(Tmi);
+  for (int k = 0; k < 3; ++k) {
+    d.mean[k] = r.mean[k];
+    Tmi[12 + k] = -r.mean[k];
+  }
+  for (int k = 0; k < 16; ++k) d.Tmean[k] = r.Tmean[k];
+  mul4(Tmi, d.Tin, d.Tinit);
+}
+
+__global__ void k_pairs_degenerate(int n_pairs, const PairDesc* __restrict__ pd, PairState* st,
+                                   const PairState* __restrict__ rst) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  st[p].degenerate = rst[pd[p].ref_id].degenerate;
+}
+
 inline unsigned grid_of(size_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
@@ -787,6 +815,13 @@ size_t tree_scan_temp_bytes(size_t n) {
 static hipError_t scan_u32(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, size_t n) {
   size_t bytes = temp_bytes;
   return rocprim::exclusive_scan(temp, bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), s);
+}
+
+void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd) {
+  k_pairs_from_refs<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, rd);
+}
+void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst) {
+  k_pairs_degenerate<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, rst);
 }
 
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,

@@ -133,6 +133,34 @@ def make_pair(n_ref: int, n_read: int, seed: int = 1, T_gt=None, move=1.5, senso
     return Pair(ref.astype(np.float32), read.astype(np.float32), o_ref, o_read, T_gt)
 
 
+def make_sequence(n_readings: int = 64, ref_every: int = 5, n_points: int = 120000, seed: int = 1,
+                  step: float = 0.3, sensor_z: float = 0.7, half: float = 30.0, T_gt=None) -> list:
+    """C2 of SURVEY.md §8(d): a streamed sequence of readings registered frame-to-reference,
+    the reference replaced every `ref_every` readings (aicp.launch reference_update_frequency
+    5). Reading i is taken `step` m further along x than reading i-1 and is perturbed by T_gt;
+    reading i is paired with reference i // ref_every, and pairs of one window share the SAME
+    reference array (the C-ABI then builds its kd-tree and normals once)."""
+    T_gt = T_GT if T_gt is None else np.asarray(T_gt, np.float64)
+    scene = make_scene(seed)
+    Ti = np.linalg.inv(T_gt)
+    refs, pairs = [], []
+    for i in range(n_readings):
+        j = i // ref_every
+        if j == len(refs):
+            o_ref = np.array([j * ref_every * step, 0.0, sensor_z])
+            rng_r = np.random.default_rng(seed * 7919 + 1000 + j)
+            ref = _subsample_raster(sample_scene(scene, rng_r, o_ref, half=half), n_points, rng_r)
+            refs.append((ref.astype(np.float32), o_ref))
+        ref, o_ref = refs[j]
+        o_read_w = np.array([(i + 1) * step, 0.0, sensor_z])
+        rng_d = np.random.default_rng(seed * 7919 + 5000 + i)
+        read_w = _subsample_raster(sample_scene(scene, rng_d, o_read_w, half=half), n_points, rng_d)
+        read = (read_w @ Ti[:3, :3].T + Ti[:3, 3]).astype(np.float32)
+        o_read = Ti[:3, :3] @ o_read_w + Ti[:3, 3]
+        pairs.append(Pair(ref, read, o_ref, o_read, T_gt))
+    return pairs
+
+
 def make_cube(min_corner=-2.0, max_corner=2.0, step=0.05):
     """The cube of aicp_core/src/tools/create_cube_cloud.cpp:13-90 (float loop counters)."""
     vals = []

@@ -234,6 +234,30 @@ def test_align_batch_ragged_matches_oracle(ctx, oracle, L):
         assert st[i]["iterations"] == st1.iterations
 
 
+def test_shared_reference_window(ctx, oracle, L):
+    """C2 reference windows: pairs that pass the SAME reference array share one centroid,
+    kd-tree and normals on the device; every pair must still match the oracle (which rebuilds
+    them per registration, as libpointmatcher does), and match a batch with copied refs."""
+    seq = sy.make_sequence(n_readings=6, ref_every=3, n_points=6000, seed=3, half=20.0)
+    assert seq[0].ref is seq[2].ref and seq[3].ref is not seq[2].ref
+    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+    shared = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in seq]
+    copied = [dict(ref=p.ref.copy(), read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in seq]
+    Ts, ss, _ = ctx.align_batch(shared, flags=flags, resolution=RES)
+    Tc, sc, _ = ctx.align_batch(copied, flags=flags, resolution=RES)
+    np.testing.assert_array_equal(Ts, Tc)
+    assert [x["iterations"] for x in ss] == [x["iterations"] for x in sc]
+    assert [x["degenerate_normals"] for x in ss] == [x["degenerate_normals"] for x in sc]
+    for i, pr in enumerate(seq):
+        ov, cnt = oracle.overlap(pr.ref, pr.ref_origin, pr.read, pr.read_origin, RES)
+        assert ss[i]["overlap_keys"] == [int(c) for c in cnt]
+        ratio = oracle.autotune_ratio(ov)
+        rc1, T1, st1 = oracle.icp(pr.ref, pr.read, oracle.default_config(trimmed_ratio=ratio, normals_on_centered=1))
+        r, t = sy.rot_err(T1, Ts[i])
+        assert rc1 == 0 and r < 1e-6 and t < 1e-5, (i, r, t)
+        assert ss[i]["iterations"] == st1.iterations
+
+
 def test_batch_deterministic_and_order_independent(ctx, L):
     prs = [sy.make_pair(8000, 8000, seed=50 + i) for i in range(3)]
     pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
