@@ -353,26 +353,28 @@ struct SM0 {
 };
 
 // Persistent waves with XCD-affine work: the slot space [0, total) is cut into kXcdGroups
-// contiguous ranges and group g is served only by blocks with blockIdx % 8 == g, which the
-// dispatcher places on one XCD (MI355X_MICROARCH.md, workgroup dispatch: speed only, never
-// correctness -- any placement still processes every slot exactly once). Consecutive slots
-// belong to the same pair, so each XCD's 4 MiB L2 holds the trees of ~P/8 pairs instead of
-// all P. Each group has its own counter (64-byte stride); slots are taken in 64-slot chunks
-// per wave and handed to the lanes that need work in lane order, so a lane starts a new query
-// as soon as its previous one completes. fetch(slot, eng) initialises a lane's query;
-// done(slot, eng) consumes the result.
-template <class Eng, class Fetch, class Done>
+// contiguous ranges (64-slot aligned) and group g is served only by blocks with
+// blockIdx % 8 == g, which the dispatcher places on one XCD (MI355X_MICROARCH.md, workgroup
+// dispatch: speed only, never correctness -- any placement still processes every slot exactly
+// once). Consecutive slots belong to the same pair, so each XCD's 4 MiB L2 holds the trees of
+// ~P/8 pairs instead of all P. Each group has its own counter (64-byte stride); a wave takes
+// 64-slot chunks (one atomic each) and hands their slots to the lanes that need work in lane
+// order, so a lane starts a new query as soon as its previous one completes.
+//   on_chunk(base)      wave-uniform, once per chunk, before its slots are handed out
+//   fetch(slot, eng)    initialises a lane's query; false: the slot has no work
+//   done(slot, eng)     consumes the result
+template <class Eng, class OnChunk, class Fetch, class Done>
 __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, float maxE2, float maxR2,
                                                const uint4* __restrict__ nodes, const float4* __restrict__ pts,
-                                               Fetch&& fetch, Done&& done) {
+                                               OnChunk&& on_chunk, Fetch&& fetch, Done&& done) {
   const int lane = threadIdx.x & 63;
   const uint32_t g = blockIdx.x % kXcdGroups;
-  const uint32_t lo = (uint32_t)(((uint64_t)total * g) / kXcdGroups);
-  const uint32_t hi = (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups);
+  const uint32_t lo = (uint32_t)(((uint64_t)total * g) / kXcdGroups) & ~63u;
+  const uint32_t hi = g + 1 == kXcdGroups ? total : (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups) & ~63u;
   uint32_t* gctr = ctr + g * kCtrStride;
   Eng t;
   FarStack fs;
-  bool has = false, fresh = false;
+  bool has = false;
   uint32_t pool = 0, pool_end = 0, my = 0;
   bool exhausted = false;
   for (;;) {
@@ -382,26 +384,22 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       if (pool >= pool_end) {
         uint32_t base = 0;
         if (lane == 0) base = lo + atomicAdd(gctr, 64u);
-        base = __shfl(base, 0, 64);
+        base = __builtin_amdgcn_readfirstlane(base);
         if (base >= hi) {
           exhausted = true;
           break;
         }
         pool = base;
         pool_end = min(base + 64u, hi);
+        on_chunk(base);
       }
       const uint32_t rank = (uint32_t)__popcll(needm & ((1ull << lane) - 1ull));
       const uint32_t avail = pool_end - pool;
       if (!has && rank < avail) {
         my = pool + rank;
-        has = true;
-        fresh = true;
+        has = fetch(my, t);
       }
       pool += min(avail, (uint32_t)__popcll(needm));
-    }
-    if (fresh) {
-      fetch(my, t);
-      fresh = false;
     }
     if (__ballot(has) == 0) break;
     if (has && t.advance(fs, maxE2, maxR2, nodes, pts)) {
@@ -487,7 +485,9 @@ __global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDes
   for (int base = 0; base < n_pairs; base += 1024) {
     const int p = base + t;
     const bool a = p < n_pairs && st[p].active;
-    const uint32_t v = a ? pd[p].n_read : 0u;
+    // each pair's slot range is padded to a multiple of 64: a 64-slot chunk of the NN work space
+    // then belongs to one pair, whose parameters the wave keeps in scalar registers
+    const uint32_t v = a ? (pd[p].n_read + 63u) & ~63u : 0u;
     uint32_t x = v, c = a ? 1u : 0u;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, co
   int cur = -1;
   uint32_t cur_end = 0, cur_off = 0;
   persistent_xcd<Trav<K>>(
-      total, ctr, 1.f, __builtin_inff(), nodes, bpts,
+      total, ctr, 1.f, __builtin_inff(), nodes, bpts, [](uint32_t) {},
       [&](uint32_t s, Trav<K>& t) {
         if (cur < 0 || s < cur_off || s >= cur_end) {
           cur = pair_of_ref(pd, n_pairs, s);
@@ -562,6 +562,7 @@ __global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, co
         t.pts = bpts + d.ref_off;
         const float4 q = bpts[s];
         t.reset(q.x, q.y, q.z);
+        return true;
       },
       [&](uint32_t s, Trav<K>& t) {
 #pragma unroll
@@ -650,39 +651,38 @@ __global__ __launch_bounds__(256) void k_icp_nn(const PairDesc* __restrict__ pd,
                                                 uint32_t* ctr, IcpParams prm) {
   const uint32_t total = al->total;
   if (total == 0) return;
-  int e = -1;
-  uint32_t e_lo = 0, e_hi = 0, rbase = 0;
-  int cur_pair = -1;
-  uint32_t node_off = 0, ref_off = 0;
+  // chunk context: wave-uniform (scalar registers)
+  uint32_t c_lo = 0, c_n = 0, c_read = 0, c_node = 0, c_ref = 0;
+  int c_pair = 0;
   uint32_t qidx = 0;
   persistent_xcd<Eng>(
       total, ctr, prm.maxE2, prm.maxR2, nodes, bpts,
-      [&](uint32_t s, Eng& t) {
-        if (e < 0 || s < e_lo || s >= e_hi) {
-          int lo = 0, hi = (int)al->n - 1;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (al->off[mid] <= s) lo = mid;
-            else hi = mid - 1;
-          }
-          e = lo;
-          e_lo = al->off[e];
-          e_hi = al->off[e + 1];
-          const int p = al->pair[e];
-          if (p != cur_pair) {
-            cur_pair = p;
-            rbase = pd[p].read_off;
-            node_off = pd[p].node_off;
-            ref_off = pd[p].ref_off;
-          }
+      [&](uint32_t base) {
+        int lo = 0, hi = (int)al->n - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (al->off[mid] <= base) lo = mid;
+          else hi = mid - 1;
         }
-        t.bind(nodes, bpts, node_off, ref_off);
-        qidx = rbase + (s - e_lo);
+        c_pair = __builtin_amdgcn_readfirstlane(al->pair[lo]);
+        c_lo = __builtin_amdgcn_readfirstlane(al->off[lo]);
+        const PairDesc& d = pd[c_pair];
+        c_n = __builtin_amdgcn_readfirstlane(d.n_read);
+        c_read = __builtin_amdgcn_readfirstlane(d.read_off);
+        c_node = __builtin_amdgcn_readfirstlane(d.node_off);
+        c_ref = __builtin_amdgcn_readfirstlane(d.ref_off);
+      },
+      [&](uint32_t s, Eng& t) {
+        const uint32_t j = s - c_lo;
+        if (j >= c_n) return false;  // padding slot
+        t.bind(nodes, bpts, c_node, c_ref);
+        qidx = c_read + j;
         const float4 r = read_c[qidx];
-        const float4* Tp = reinterpret_cast<const float4*>(st[cur_pair].T);
+        const float4* Tp = reinterpret_cast<const float4*>(st[c_pair].T);
         float q0, q1, q2;
         apply_cols(Tp[0], Tp[1], Tp[2], Tp[3], r.x, r.y, r.z, q0, q1, q2);
         t.reset(q0, q1, q2);
+        return true;
       },
       [&](uint32_t, Eng& t) {
         match[qidx] = t.res_id();
@@ -1095,12 +1095,13 @@ __global__ __launch_bounds__(256) void k_knn_generic(uint32_t nq, const float4* 
                                                      uint32_t* ctr) {
   uint32_t tp = 0, tn = 0;
   persistent_xcd<Trav<K>>(
-      nq, ctr, maxE2, maxR2, nodes, bpts,
+      nq, ctr, maxE2, maxR2, nodes, bpts, [](uint32_t) {},
       [&](uint32_t s, Trav<K>& t) {
         t.nodes = nodes;
         t.pts = bpts;
         const float4 x = q[s];
         t.reset(x.x, x.y, x.z);
+        return true;
       },
       [&](uint32_t s, Trav<K>& t) {
 #pragma unroll
@@ -1132,11 +1133,12 @@ __global__ __launch_bounds__(256) void k_knn1_generic(uint32_t nq, const float4*
                                                       unsigned long long* touched, uint32_t* ctr) {
   uint32_t tp = 0, tn = 0;
   persistent_xcd<Eng>(
-      nq, ctr, maxE2, maxR2, nodes, bpts,
+      nq, ctr, maxE2, maxR2, nodes, bpts, [](uint32_t) {},
       [&](uint32_t s, Eng& t) {
         t.bind(nodes, bpts, 0, 0);
         const float4 x = q[s];
         t.reset(x.x, x.y, x.z);
+        return true;
       },
       [&](uint32_t s, Eng& t) {
         const int32_t id = t.res_id();
