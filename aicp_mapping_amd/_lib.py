@@ -265,7 +265,7 @@ class Context:
     def last_phase_ms(self):
         a = (C.c_double * 5)()
         lib.aicp_hip_last_phase_ms(self.h, a)
-        return dict(overlap=a[0], tree=a[1], normals=a[2], icp_loop=a[3], total=a[4])
+        return dict(overlap=a[0], normals=a[1], matcher_tree=a[2], icp_loop=a[3], total=a[4])
 
     # -------------------------------------------------------------- kernel-level -----------
     def knn(self, pts, queries, k=1, eps=0.0, max_dist=float("inf")):

@@ -109,7 +109,8 @@ struct aicp_hip_ctx {
   hipStream_t stream2 = nullptr;  // kd-tree + normals, concurrent with the overlap on `stream`
   std::string err;
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
-      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate;
+      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
+      nrm_raw, inv;
   // kd-tree construction work space (kernels_tree.hip)
   DevBuf tw_W0, tw_W1, tw_segof0, tw_segof1, tw_seg0, tw_seg1, tw_flag, tw_X1, tw_X2, tw_posL, tw_posR, tw_ev,
       tw_valid, tw_subs, tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
@@ -289,11 +290,11 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
 // dDesc with ref_off / n_ref / Tin. Writes ctx->bpts (bucket order, w = local id), ctx->nodes
 // and the desc fields mean, Tmean, Tinit, node_off, n_nodes, tree_depth.
 int device_trees_begin(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                       const float4* raw, int center, int bucket) {
+                       const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out) {
   const size_t n = (size_t)total;
   const size_t max_seg = n / 2 + P + 1;
-  HIPC(ensure(ctx->bpts, n * 16));
-  HIPC(ensure(ctx->nodes, (2 * n + 2) * 16));
+  HIPC(ensure(bpts_out, n * 16));
+  HIPC(ensure(nodes_out, (2 * n + 2) * 16));
   HIPC(ensure(ctx->tw_W0, n * 16));
   HIPC(ensure(ctx->tw_W1, n * 16));
   HIPC(ensure(ctx->tw_segof0, n * 4));
@@ -338,17 +339,18 @@ int device_trees_begin(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t tota
   w.scan_temp = ctx->tw_scan.p;
   w.scan_temp_bytes = ctx->tw_scan.cap;
   w.max_seg = max_seg;
-  float4* bpts = ctx->bpts.as<float4>();
+  float4* bpts = bpts_out.as<float4>();
   HIPC(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts, bucket));
   ctx->tw = w;
   return AICP_OK;
 }
 
 // global levels (host polls), wave subtrees, node records; see device_trees_begin
-int device_trees_end(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc, int bucket) {
+int device_trees_end(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc, int bucket,
+                     DevBuf& bpts_out, DevBuf& nodes_out) {
   const size_t n = (size_t)total;
   const TreeWork& w = ctx->tw;
-  float4* bpts = ctx->bpts.as<float4>();
+  float4* bpts = bpts_out.as<float4>();
   TreeCtl* hctl = ctx->pin_ctl.as<TreeCtl>();
   // global levels until every remaining segment fits one wave's LDS (kSubMax points); the
   // host polls the next level's segment count from level 4 on
@@ -363,7 +365,7 @@ int device_trees_end(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total,
   }
   if (!done) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
   HIPC(launch_tree_subtrees(s, (uint32_t)n, hctl->n_small, w, bpts, bucket));
-  HIPC(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, ctx->nodes.as<uint4>()));
+  HIPC(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
   HIPC(hipMemcpyAsync(&hctl->error, &w.ctl->error, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   if (hctl->error & 1) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
@@ -439,11 +441,16 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     dRdesc = ctx->rdesc.as<PairDesc>();
     dRstate = ctx->rstate.as<PairState>();
     std::memcpy(ctx->pin_rdesc.p, B->rdesc.data(), R * sizeof(PairDesc));
+    HIPC(ensure(ctx->rdesc_raw, R * sizeof(PairDesc)));
     HIPC(hipStreamWaitEvent(s2, ctx->ev[7], 0));
     HIPC(hipEventRecord(ctx->ev[8], s2));
     HIPC(hipMemcpyAsync(dRdesc, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s2));
+    HIPC(hipMemcpyAsync(ctx->rdesc_raw.p, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s2));
     launch_init_state(s2, (int)R, dRdesc, dRstate);
-    rc = device_trees_begin(ctx, s2, R, B->total_ref, dRdesc, B->ref_raw.as<float4>(), 1, cfg->bucket_size);
+    // SurfaceNormal runs on the reference as given, before the centring (ICP::compute,
+    // SURVEY A.1 steps 1-2): its own libnabo tree over the raw coordinates first
+    rc = device_trees_begin(ctx, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), B->ref_raw.as<float4>(), 0,
+                            cfg->bucket_size, ctx->bpts_raw, ctx->nodes_raw);
     if (rc) return rc;
   }
   // overlap: size the voxel maps from the key boxes, then mark
@@ -485,7 +492,24 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   int nn_launches = 0;
   if (doIcp) {
     // s2: kd-tree levels + subtrees, reading frame, SurfaceNormal
-    rc = device_trees_end(ctx, s2, R, B->total_ref, dRdesc, cfg->bucket_size);
+    rc = device_trees_end(ctx, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), cfg->bucket_size, ctx->bpts_raw,
+                          ctx->nodes_raw);
+    if (rc) return rc;
+    // normals on the raw tree (bucket order of that tree)
+    HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
+    HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
+    uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
+    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
+    if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, ctx->rdesc_raw.as<PairDesc>(), dRstate,
+                        ctx->nodes_raw.as<uint4>(), nullptr, ctx->bpts_raw.as<float4>(), ctx->nrm_raw.as<float4>(),
+                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
+      FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
+    HIPC(hipEventRecord(ctx->ev[10], s2));
+    // centroid + the matcher's tree over the centred reference
+    rc = device_trees_begin(ctx, s2, R, B->total_ref, dRdesc, B->ref_raw.as<float4>(), 1, cfg->bucket_size,
+                            ctx->bpts, ctx->nodes);
+    if (rc) return rc;
+    rc = device_trees_end(ctx, s2, R, B->total_ref, dRdesc, cfg->bucket_size, ctx->bpts, ctx->nodes);
     if (rc) return rc;
     launch_pairs_from_refs(s2, (int)P, dDesc, dRdesc);
     HIPC(hipEventRecord(ctx->ev[3], s2));
@@ -507,12 +531,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     const uint4* nodes = ctx->nodes.as<uint4>();
     const int32_t* parent = nullptr;
     launch_prepare_read(s2, B->m_read, dDesc, B->read_raw.as<float4>(), readc);
-    HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
-    uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
-    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
-    if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, dRdesc, dRstate, nodes, parent, bpts, bnrm,
-                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
-      FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
+    // normals from the raw tree's bucket order into the matcher tree's bucket order
+    HIPC(ensure(ctx->inv, B->total_ref * 4));
+    launch_normals_to_matcher(s2, (int)R, (uint32_t)B->total_ref, dRdesc, bpts, ctx->bpts_raw.as<float4>(),
+                              ctx->nrm_raw.as<float4>(), ctx->inv.as<uint32_t>(), bnrm);
     launch_pairs_degenerate(s2, (int)P, dDesc, dState, dRstate);
     HIPC(hipEventRecord(ctx->ev[4], s2));
     HIPC(hipStreamWaitEvent(s, ctx->ev[4], 0));
@@ -541,6 +563,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
   } else {
     HIPC(hipEventRecord(ctx->ev[8], s));
+    HIPC(hipEventRecord(ctx->ev[10], s));
     HIPC(hipEventRecord(ctx->ev[3], s));
     HIPC(hipEventRecord(ctx->ev[4], s));
     HIPC(hipEventRecord(ctx->ev[9], s));
@@ -591,8 +614,9 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   ctx->last_queries = queries;
   ctx->last_phase[0] = doOvl ? ev_ms(ctx->ev[0], ctx->ev[1]) + ev_ms(ctx->ev[6], ctx->ev[2]) : 0;
   // tree and normals run on the second stream, concurrently with the overlap
-  ctx->last_phase[1] = doIcp ? ev_ms(ctx->ev[8], ctx->ev[3]) : 0;
-  ctx->last_phase[2] = doIcp ? ev_ms(ctx->ev[3], ctx->ev[4]) : 0;
+  // [1] raw-coordinate tree + SurfaceNormal, [2] centroid + matcher tree + normal scatter
+  ctx->last_phase[1] = doIcp ? ev_ms(ctx->ev[8], ctx->ev[10]) : 0;
+  ctx->last_phase[2] = doIcp ? ev_ms(ctx->ev[10], ctx->ev[4]) : 0;
   ctx->last_phase[3] = doIcp ? ev_ms(ctx->ev[9], ctx->ev[5]) : 0;
   ctx->last_phase[4] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
@@ -621,9 +645,10 @@ int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, Pa
   ident4(d.Tin);
   HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
-  int rc = device_trees_begin(ctx, s, 1, n, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8);
+  int rc = device_trees_begin(ctx, s, 1, n, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8, ctx->bpts,
+                              ctx->nodes);
   if (rc) return rc;
-  rc = device_trees_end(ctx, s, 1, n, ctx->desc.as<PairDesc>(), 8);
+  rc = device_trees_end(ctx, s, 1, n, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes);
   if (rc) return rc;
   HIPC(hipMemcpyAsync(&d, ctx->desc.p, sizeof(d), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -665,7 +690,8 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->match, &ctx->d2, &ctx->desc,
                     &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
-                    &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
+                    &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
+                    &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
                     &ctx->tw_segof1, &ctx->tw_seg0, &ctx->tw_seg1, &ctx->tw_flag, &ctx->tw_X1, &ctx->tw_X2,
                     &ctx->tw_posL, &ctx->tw_posR, &ctx->tw_ev, &ctx->tw_valid, &ctx->tw_subs, &ctx->tw_ecnt,
                     &ctx->tw_sums, &ctx->tw_pdepth,

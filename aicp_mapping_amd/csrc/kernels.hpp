@@ -91,6 +91,9 @@ hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDe
 // pairs -> their shared reference's centroid / tree fields (+ T_refMean_dataIn), and its
 // SurfaceNormal degenerate count
 void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd);
+// normals of the raw-coordinate tree's bucket order -> bnrm in the matcher tree's order
+void launch_normals_to_matcher(hipStream_t s, int n_refs, uint32_t total, const PairDesc* rd, const float4* bpts,
+                               const float4* bpts_raw, const float4* nrm_raw, uint32_t* inv, float4* bnrm);
 void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst);
 
 // ---- overlap -------------------------------------------------------------------------------

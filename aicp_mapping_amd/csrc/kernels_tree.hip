@@ -794,6 +794,26 @@ __global__ void k_pairs_from_refs(int n_pairs, PairDesc* pd, const PairDesc* __r
   mul4(Tmi, d.Tin, d.Tinit);
 }
 
+// normals computed in the raw tree's bucket order -> the matcher tree's bucket order, through
+// the input id each point carries in w
+__global__ __launch_bounds__(256) void k_inv_perm(int n_refs, uint32_t total, const PairDesc* __restrict__ rd,
+                                                  const float4* __restrict__ bpts, uint32_t* __restrict__ inv) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  const uint32_t ro = rd[pair_of_pos(rd, n_refs, j)].ref_off;
+  inv[ro + (uint32_t)__float_as_int(bpts[j].w)] = j;
+}
+
+__global__ __launch_bounds__(256) void k_scatter_normals(int n_refs, uint32_t total, const PairDesc* __restrict__ rd,
+                                                         const float4* __restrict__ bpts_raw,
+                                                         const float4* __restrict__ nrm_raw,
+                                                         const uint32_t* __restrict__ inv, float4* __restrict__ bnrm) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  const uint32_t ro = rd[pair_of_pos(rd, n_refs, j)].ref_off;
+  bnrm[inv[ro + (uint32_t)__float_as_int(bpts_raw[j].w)]] = nrm_raw[j];
+}
+
 __global__ void k_pairs_degenerate(int n_pairs, const PairDesc* __restrict__ pd, PairState* st,
                                    const PairState* __restrict__ rst) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -819,6 +839,12 @@ static hipError_t scan_u32(hipStream_t s, void* temp, size_t temp_bytes, const u
 
 void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd) {
   k_pairs_from_refs<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, rd);
+}
+void launch_normals_to_matcher(hipStream_t s, int n_refs, uint32_t total, const PairDesc* rd, const float4* bpts,
+                               const float4* bpts_raw, const float4* nrm_raw, uint32_t* inv, float4* bnrm) {
+  if (!total) return;
+  k_inv_perm<<<grid_of(total), 256, 0, s>>>(n_refs, total, rd, bpts, inv);
+  k_scatter_normals<<<grid_of(total), 256, 0, s>>>(n_refs, total, rd, bpts_raw, nrm_raw, inv, bnrm);
 }
 void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst) {
   k_pairs_degenerate<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, rst);

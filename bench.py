@@ -151,7 +151,7 @@ def main():
         nn_launches += t["launches"]
         iters_total += sum(s.iterations for s in batch.stats)
         ph = ctx.last_phase_ms()
-        phases += np.array([ph["overlap"], ph["tree"], ph["normals"], ph["icp_loop"], ph["total"]])
+        phases += np.array([ph["overlap"], ph["normals"], ph["matcher_tree"], ph["icp_loop"], ph["total"]])
     sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -195,8 +195,8 @@ def main():
             },
             "icp_iters_per_s": round(iters_total / elapsed, 1),
             "mean_iterations": float(np.mean([s["iterations"] for s in st])),
-            "phase_ms_per_step": dict(zip(["overlap_gpu", "centroid_tree_gpu (stream 2)", "normals_gpu (stream 2)",
-                                           "icp_loop_gpu", "total"],
+            "phase_ms_per_step": dict(zip(["overlap_gpu (stream 1)", "normal_tree_and_normals_gpu (stream 2)",
+                                           "centroid_matcher_tree_gpu (stream 2)", "icp_loop_gpu", "total"],
                                           [round(x / args.steps, 3) for x in phases])),
             "accuracy_vs_ground_truth": {
                 "median_rot_rad": float(np.median([e[0] for e in errs])),

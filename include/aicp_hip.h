@@ -141,8 +141,9 @@ void aicp_hip_batch_free(aicp_hip_ctx* ctx, aicp_hip_batch* batch);
  * (HIP events on the context stream), and the algorithmic bytes they moved. */
 int aicp_hip_last_nn_timing(const aicp_hip_ctx* ctx, int* n_launches, double* total_ms,
                             double* algorithmic_bytes, uint64_t* queries);
-/* Phase wall times (ms) of the last batch_run: [0] overlap, [1] centre+tree,
- * [2] normals, [3] icp loop, [4] total. */
+/* Phase times (ms, HIP events) of the last batch_run: [0] overlap (stream 1), [1] raw-
+ * coordinate kd-tree + SurfaceNormal (stream 2), [2] centroid + matcher kd-tree (stream 2),
+ * [3] icp loop, [4] total wall time. [0] runs concurrently with [1]-[2]. */
 int aicp_hip_last_phase_ms(const aicp_hip_ctx* ctx, double out_ms[5]);
 
 /* ---- kernel-level entry points (parity tests and diagnostics) --------------------------- */
