@@ -53,6 +53,7 @@ struct PairDesc {
   float ratio;                  // configured trimmed ratio (overridden by overlap)
   int32_t tree_depth;
   int32_t ref_id;               // index of the pair's (deduplicated) reference cloud
+  int32_t ogroup;               // overlap group: distinct (reference cloud, reference origin)
   double ref_origin[3], read_origin[3];
 };
 
@@ -62,8 +63,8 @@ struct PairDesc {
 struct OvlDesc {
   int32_t min[3];   // key of voxel (0,0,0)
   int32_t dim[3];   // box extent in voxels
-  uint64_t off;     // byte offset into the map arena (ref map, then read map)
-  uint64_t bytes;   // bytes per map (multiple of 16)
+  uint64_t off;     // byte offset of this cloud's map in the map arena
+  uint64_t bytes;   // map bytes (multiple of 16)
 };
 
 struct PairState {

@@ -97,10 +97,11 @@ struct aicp_hip_batch {
   size_t P = 0;
   std::vector<PairDesc> desc;
   std::vector<PairDesc> rdesc;  // one per distinct reference cloud (tree + normals built once)
+  std::vector<PairDesc> gdesc;  // one per overlap group: distinct (reference cloud, origin)
   uint64_t total_ref = 0, total_read = 0;
   uint32_t n_red_total = 0;
   DevBuf ref_raw, read_raw, maps;
-  BlockMap m_read{}, m_ref{}, m_red{};
+  BlockMap m_read{}, m_gref{}, m_red{};
 };
 
 struct aicp_hip_ctx {
@@ -110,11 +111,11 @@ struct aicp_hip_ctx {
   std::string err;
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
       ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
-      nrm_raw, inv;
+      nrm_raw, inv, gdesc, gstate;
   // kd-tree construction work space (kernels_tree.hip)
   DevBuf tw_W0, tw_W1, tw_segof0, tw_segof1, tw_seg0, tw_seg1, tw_flag, tw_X1, tw_X2, tw_posL, tw_posR, tw_ev,
       tw_valid, tw_subs, tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
-  PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc;
+  PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev[12] = {};
   TreeWork tw{};  // device_trees_begin -> device_trees_end
@@ -189,6 +190,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   B->P = n;
   B->desc.assign(n, PairDesc{});
   B->rdesc.clear();
+  B->gdesc.clear();
   uint64_t ro = 0, wo = 0;
   uint32_t red = 0;
   Maps mr, mf, md;
@@ -221,6 +223,26 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     }
     d.ref_id = rid;
     d.ref_off = B->rdesc[rid].ref_off;
+    int32_t gid = -1;
+    for (size_t g = 0; g < B->gdesc.size(); ++g) {
+      const PairDesc& gd = B->gdesc[g];
+      if (gd.ref_id == rid && gd.ref_origin[0] == p.ref_origin[0] && gd.ref_origin[1] == p.ref_origin[1] &&
+          gd.ref_origin[2] == p.ref_origin[2]) {
+        gid = (int32_t)g;
+        break;
+      }
+    }
+    if (gid < 0) {
+      gid = (int32_t)B->gdesc.size();
+      PairDesc g{};
+      g.ref_id = rid;
+      g.ref_off = d.ref_off;
+      g.n_ref = (uint32_t)p.n_ref;
+      for (int k = 0; k < 3; ++k) g.ref_origin[k] = p.ref_origin[k];
+      B->gdesc.push_back(g);
+      mf.add(gid, g.n_ref, kNNBlock);
+    }
+    d.ogroup = gid;
     d.n_ref = (uint32_t)p.n_ref;
     d.read_off = (uint32_t)wo;
     d.n_read = (uint32_t)p.n_read;
@@ -238,7 +260,6 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     else
       ident4(d.Tin);
     mr.add((int)i, d.n_read, kNNBlock);
-    mf.add((int)i, d.n_ref, kNNBlock);
     md.add((int)i, d.n_read, kNNBlock * kReducePerThread);
   }
   B->total_ref = ro;
@@ -279,7 +300,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   HIPC(ensure(ctx->pin_io, words * 4));
   mp = ctx->pin_io.as<uint32_t>();
   put(mr, B->m_read);
-  put(mf, B->m_ref);
+  put(mf, B->m_gref);
   put(md, B->m_red);
   HIPC(hipMemcpyAsync(B->maps.p, mp, words * 4, hipMemcpyHostToDevice, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
@@ -422,11 +443,24 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   HIPC(hipMemcpyAsync(dDesc, pdA, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
   launch_init_state(s, (int)P, dDesc, dState);
   HIPC(hipEventRecord(ctx->ev[7], s));
+  const size_t G = B->gdesc.size();
+  PairDesc* dG = nullptr;
+  PairState* dGst = nullptr;
   if (doOvl) {
-    launch_ovl_init(s, (int)P, dDesc, dState, res);
-    launch_ovl_bbox(s, B->m_ref, dDesc, dState, B->ref_raw.as<float4>(), 0, res);
+    HIPC(ensure(ctx->gdesc, G * sizeof(PairDesc)));
+    HIPC(ensure(ctx->gstate, G * sizeof(PairState)));
+    HIPC(ensure(ctx->pin_gdesc, G * sizeof(PairDesc)));
+    HIPC(ensure(ctx->pin_gstate, G * sizeof(PairState)));
+    dG = ctx->gdesc.as<PairDesc>();
+    dGst = ctx->gstate.as<PairState>();
+    std::memcpy(ctx->pin_gdesc.p, B->gdesc.data(), G * sizeof(PairDesc));
+    HIPC(hipMemcpyAsync(dG, ctx->pin_gdesc.p, G * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+    launch_ovl_init(s, (int)P, dDesc, dState, res, 2);
+    launch_ovl_init(s, (int)G, dG, dGst, res, 1);
+    launch_ovl_bbox(s, B->m_gref, dG, dGst, B->ref_raw.as<float4>(), 0, res);
     launch_ovl_bbox(s, B->m_read, dDesc, dState, B->read_raw.as<float4>(), 1, res);
     HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(ctx->pin_gstate.p, dGst, G * sizeof(PairState), hipMemcpyDeviceToHost, s));
   }
   HIPC(hipEventRecord(ctx->ev[1], s));
   // s2: per distinct reference: centroid, centred cloud, root segments (the levels follow
@@ -457,35 +491,41 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   uint64_t bm_bytes = 0;
   if (doOvl) {
     HIPC(hipEventSynchronize(ctx->ev[1]));
-    const PairState* hs = ctx->pin_state.as<PairState>();
-    HIPC(ensure(ctx->pin_ovl, P * sizeof(OvlDesc)));
-    HIPC(ensure(ctx->ovl, P * sizeof(OvlDesc)));
+    // one map per overlap group (reference side) and one per pair (reading side), each over
+    // the padded key box of that cloud's keys and origin
+    HIPC(ensure(ctx->pin_ovl, (P + G) * sizeof(OvlDesc)));
+    HIPC(ensure(ctx->ovl, (P + G) * sizeof(OvlDesc)));
     OvlDesc* ho = ctx->pin_ovl.as<OvlDesc>();
-    for (size_t i = 0; i < P; ++i) {
-      OvlDesc& o = ho[i];
+    auto size_map = [&](const PairState& hs, OvlDesc& o) -> bool {
       uint64_t vox = 1;
       for (int k = 0; k < 3; ++k) {
-        int lo = hs[i].ovl_bbox[k], hi = hs[i].ovl_bbox[3 + k];
+        int lo = hs.ovl_bbox[k], hi = hs.ovl_bbox[3 + k];
         if (lo > hi) lo = hi = 0;  // nothing inside the key range
         o.min[k] = lo - 2;
         o.dim[k] = (hi - lo) + 5;
         vox *= (uint64_t)o.dim[k];
       }
-      if (vox > (1ull << 34)) FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
       o.bytes = (vox + 15) / 16 * 16;
       o.off = bm_bytes;
-      bm_bytes += 2 * o.bytes;
-    }
+      bm_bytes += o.bytes;
+      return vox <= (1ull << 34);
+    };
+    for (size_t i = 0; i < P; ++i)
+      if (!size_map(ctx->pin_state.as<PairState>()[i], ho[i]))
+        FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
+    for (size_t g = 0; g < G; ++g)
+      if (!size_map(ctx->pin_gstate.as<PairState>()[g], ho[P + g]))
+        FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
     HIPC(ensure(ctx->bitmap, bm_bytes));
-    HIPC(hipMemcpyAsync(ctx->ovl.p, ho, P * sizeof(OvlDesc), hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(ctx->ovl.p, ho, (P + G) * sizeof(OvlDesc), hipMemcpyHostToDevice, s));
     HIPC(hipEventRecord(ctx->ev[6], s));
     uint8_t* bm = ctx->bitmap.as<uint8_t>();
     const OvlDesc* dOvl = ctx->ovl.as<OvlDesc>();
     HIPC(hipMemsetAsync(bm, 0, bm_bytes, s));
-    launch_ovl_mark(s, B->m_ref, dDesc, dOvl, dState, B->ref_raw.as<float4>(), 0, res, bm);
+    launch_ovl_mark(s, B->m_gref, dG, dOvl + P, dGst, B->ref_raw.as<float4>(), 0, res, bm);
     launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, B->read_raw.as<float4>(), 1, res, bm);
-    launch_ovl_count(s, (int)P, dOvl, dState, bm);
-    launch_ovl_finish(s, (int)P, dState, doIcp ? 1 : 0);
+    launch_ovl_count(s, (int)P, (int)G, dDesc, dOvl, dOvl + P, dState, dGst, bm);
+    launch_ovl_finish(s, (int)P, dDesc, dState, dGst, doIcp ? 1 : 0);
   }
   HIPC(hipEventRecord(ctx->ev[2], s));
   IcpParams prm{};
@@ -691,14 +731,14 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
                     &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
-                    &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
+                    &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->gdesc, &ctx->gstate, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
                     &ctx->tw_segof1, &ctx->tw_seg0, &ctx->tw_seg1, &ctx->tw_flag, &ctx->tw_X1, &ctx->tw_X2,
                     &ctx->tw_posL, &ctx->tw_posR, &ctx->tw_ev, &ctx->tw_valid, &ctx->tw_subs, &ctx->tw_ecnt,
                     &ctx->tw_sums, &ctx->tw_pdepth,
                     &ctx->tw_ctl, &ctx->tw_scan})
     release(*b);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_ctl, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
-                    &ctx->pin_rdesc})
+                    &ctx->pin_rdesc, &ctx->pin_gdesc, &ctx->pin_gstate})
     release(*b);
   for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
   for (auto e : ctx->ev)

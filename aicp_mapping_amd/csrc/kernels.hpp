@@ -96,15 +96,20 @@ void launch_normals_to_matcher(hipStream_t s, int n_refs, uint32_t total, const 
                                const float4* bpts_raw, const float4* nrm_raw, uint32_t* inv, float4* bnrm);
 void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst);
 
-// ---- overlap -------------------------------------------------------------------------------
-void launch_ovl_init(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
-                     double res);
+// ---- overlap ------------------------------------------------------------------------------
+// Clouds: the reference side runs over overlap groups (one per distinct reference cloud and
+// origin; pd = group descriptors, st = group states), the reading side over pairs.
+// sides: 1 = reference origin, 2 = reading origin
+void launch_ovl_init(hipStream_t s, int n, const PairDesc* pd, PairState* st, double res, int sides);
 void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
                      const float4* pts, int side, double res);
+// od[i]: the map of entry i (group or pair) of the side being marked
 void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDesc* od, PairState* st,
                      const float4* pts, int side, double res, uint8_t* maps);
-void launch_ovl_count(hipStream_t s, int n_pairs, const OvlDesc* od, PairState* st,
-                      const uint8_t* maps);
-void launch_ovl_finish(hipStream_t s, int n_pairs, PairState* st, int set_ratio);
+// |A| per group (gst.ovl_counts[0]), |B| and |A∩B| per pair (st.ovl_counts[1], [2])
+void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
+                      const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps);
+void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
+                       int set_ratio);
 
 }  // namespace aicp

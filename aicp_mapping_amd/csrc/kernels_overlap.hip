@@ -5,9 +5,12 @@
 // float direction, double tMax) plus every endpoint key; overlap% = min(|A∩B|/|A|,
 // |A∩B|/|B|) * 100. octomap stores S in an octree, prunes and expands it; only the set matters.
 //
-// Device form: one byte per voxel of the pair's padded key box (one map per cloud). Every
-// ray key is a plain byte store of 1 -- concurrent writers store the same value, so no
-// atomics and no read-before-write are needed -- then byte sums give |A|, |B| and |A∩B|.
+// Device form: one byte per voxel of a padded key box per cloud. Every ray key is a plain
+// byte store of 1 -- concurrent writers store the same value, so no atomics and no
+// read-before-write are needed. A reference cloud seen from one origin has one voxel set
+// whatever reading it is paired with, so its map is built once per (reference, origin)
+// group and shared by the pairs of a reference window; |A| is counted once per group, |B|
+// per reading, and |A∩B| by looking every voxel of a reading's map up in its group's map.
 // A 60 x 60 x 6 m scene at 0.2 m is ~2.7 M voxels = 2.7 MB per map (L2/MALL resident).
 // (tools/microbench.hip: with 16 distinct pairs, check+atomicOr bitmaps ran 11x slower.)
 #include <hip/hip_runtime.h>
@@ -29,12 +32,14 @@ __device__ __forceinline__ bool key_checked(double rf, float c, int& key) {
   return false;
 }
 
-__global__ void k_ovl_init(int n_pairs, const PairDesc* __restrict__ pd, PairState* st, double res) {
+// sides: 1 = the reference origin, 2 = the reading origin
+__global__ void k_ovl_init(int n_pairs, const PairDesc* __restrict__ pd, PairState* st, double res, int sides) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
   const double rf = 1.0 / res;
   int lo[3] = {1 << 30, 1 << 30, 1 << 30}, hi[3] = {-(1 << 30), -(1 << 30), -(1 << 30)};
   for (int side = 0; side < 2; ++side) {
+    if (!((sides >> side) & 1)) continue;
     const double* o = side ? pd[p].read_origin : pd[p].ref_origin;
     int k[3];
     bool ok = true;
@@ -108,7 +113,7 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
   if (j >= n) return;
   const uint32_t off = side ? d.read_off : d.ref_off;
   const OvlDesc& ov = od[pair];
-  uint8_t* bm = maps + ov.off + (side ? ov.bytes : 0);
+  uint8_t* bm = maps + ov.off;
   const int mn0 = ov.min[0], mn1 = ov.min[1], mn2 = ov.min[2];
   const int dm0 = ov.dim[0], dm1 = ov.dim[1], dm2 = ov.dim[2];
   bool err = false;
@@ -192,40 +197,83 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
 }
 
 // popcounts: |A|, |B|, |A & B| (64 workgroups per pair, integer atomics -> deterministic)
-constexpr int kCountBlocksPerPair = 64;
-__global__ __launch_bounds__(256) void k_ovl_count(const OvlDesc* __restrict__ od, PairState* st,
-                                                   const uint8_t* __restrict__ maps) {
-  const int pair = blockIdx.x / kCountBlocksPerPair;
-  const int sub = blockIdx.x % kCountBlocksPerPair;
-  // maps are 16-byte aligned and padded to 16-byte multiples (host); bytes are 0 or 1
-  const OvlDesc& ov = od[pair];
+constexpr int kCountBlocksPerMap = 64;
+
+// |S| of every map in od[]: byte sums (bytes are 0 or 1; maps 16-byte aligned and padded)
+__global__ __launch_bounds__(256) void k_ovl_popcount(const OvlDesc* __restrict__ od, PairState* st, int slot,
+                                                      const uint8_t* __restrict__ maps) {
+  const int m = blockIdx.x / kCountBlocksPerMap;
+  const int sub = blockIdx.x % kCountBlocksPerMap;
+  const OvlDesc& ov = od[m];
   const uint4* A = (const uint4*)(maps + ov.off);
-  const uint4* B = (const uint4*)(maps + ov.off + ov.bytes);
   const uint64_t n16 = ov.bytes / 16;
-  unsigned long long ca = 0, cb = 0, cab = 0;
-  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)kCountBlocksPerPair * 256) {
-    const uint4 a = A[w], b = B[w];
-    ca += __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w);
-    cb += __popc(b.x) + __popc(b.y) + __popc(b.z) + __popc(b.w);
-    cab += __popc(a.x & b.x) + __popc(a.y & b.y) + __popc(a.z & b.z) + __popc(a.w & b.w);
+  unsigned long long c = 0;
+  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)kCountBlocksPerMap * 256) {
+    const uint4 a = A[w];
+    c += __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w);
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    ca += __shfl_xor(ca, o, 64);
-    cb += __shfl_xor(cb, o, 64);
-    cab += __shfl_xor(cab, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd((unsigned long long*)&st[pair].ovl_counts[0], ca);
-    atomicAdd((unsigned long long*)&st[pair].ovl_counts[1], cb);
-    atomicAdd((unsigned long long*)&st[pair].ovl_counts[2], cab);
-  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd((unsigned long long*)&st[m].ovl_counts[slot], c);
 }
 
-__global__ void k_ovl_finish(int n_pairs, PairState* st, int set_ratio) {
+// |A ∩ B|: every set voxel of a reading's map looked up in its group's reference map
+__global__ __launch_bounds__(256) void k_ovl_intersect(const PairDesc* __restrict__ pd,
+                                                       const OvlDesc* __restrict__ od_read,
+                                                       const OvlDesc* __restrict__ od_ref, PairState* st,
+                                                       const uint8_t* __restrict__ maps) {
+  const int p = blockIdx.x / kCountBlocksPerMap;
+  const int sub = blockIdx.x % kCountBlocksPerMap;
+  const OvlDesc& rb = od_read[p];
+  const OvlDesc& ra = od_ref[pd[p].ogroup];
+  const uint4* B = (const uint4*)(maps + rb.off);
+  const uint8_t* A = maps + ra.off;
+  const uint64_t n16 = rb.bytes / 16;
+  const uint64_t vox = (uint64_t)rb.dim[0] * rb.dim[1] * rb.dim[2];
+  const uint32_t d1 = (uint32_t)rb.dim[1], d2 = (uint32_t)rb.dim[2];
+  const int o0 = rb.min[0] - ra.min[0], o1 = rb.min[1] - ra.min[1], o2 = rb.min[2] - ra.min[2];
+  unsigned long long c = 0;
+  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)kCountBlocksPerMap * 256) {
+    const uint4 b = B[w];
+    if ((b.x | b.y | b.z | b.w) == 0) continue;
+    const uint32_t words[4] = {b.x, b.y, b.z, b.w};
+    uint64_t i0 = w * 16;
+    // (a, bb, cc) of the word's first voxel, then step along the fastest axis
+    uint32_t a = (uint32_t)(i0 / ((uint64_t)d1 * d2));
+    const uint64_t rem = i0 - (uint64_t)a * d1 * d2;
+    uint32_t bb = (uint32_t)(rem / d2), cc = (uint32_t)(rem - (uint64_t)bb * d2);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const bool set = ((words[k >> 2] >> ((k & 3) * 8)) & 0xFFu) != 0u;
+      if (set && i0 + k < vox) {
+        const int x = (int)a + o0, y = (int)bb + o1, z = (int)cc + o2;
+        if ((unsigned)x < (unsigned)ra.dim[0] && (unsigned)y < (unsigned)ra.dim[1] && (unsigned)z < (unsigned)ra.dim[2]) {
+          const uint64_t j = ((uint64_t)x * (uint64_t)ra.dim[1] + (uint64_t)y) * (uint64_t)ra.dim[2] + (uint64_t)z;
+          c += A[j];
+        }
+      }
+      if (++cc == d2) {
+        cc = 0;
+        if (++bb == d1) {
+          bb = 0;
+          ++a;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd((unsigned long long*)&st[p].ovl_counts[2], c);
+}
+
+__global__ void k_ovl_finish(int n_pairs, const PairDesc* __restrict__ pd, PairState* st,
+                             const PairState* __restrict__ gst, int set_ratio) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
   PairState& s = st[p];
+  const PairState& g = gst[pd[p].ogroup];
+  s.ovl_counts[0] = g.ovl_counts[0];
+  if (g.ovl_err) s.ovl_err = 1;
   const float ov = (float)s.ovl_counts[2];
   const float a = ov / (float)s.ovl_counts[0];
   const float b = ov / (float)s.ovl_counts[1];
@@ -234,8 +282,8 @@ __global__ void k_ovl_finish(int n_pairs, PairState* st, int set_ratio) {
   if (set_ratio) s.ratio = autotune_ratio_fast(s.overlap);
 }
 
-void launch_ovl_init(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, double res) {
-  k_ovl_init<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, res);
+void launch_ovl_init(hipStream_t s, int n, const PairDesc* pd, PairState* st, double res, int sides) {
+  if (n) k_ovl_init<<<(n + 63) / 64, 64, 0, s>>>(n, pd, st, res, sides);
 }
 void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
                      const float4* pts, int side, double res) {
@@ -245,12 +293,15 @@ void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDes
                      const float4* pts, int side, double res, uint8_t* maps) {
   if (m.n_blocks) k_ovl_mark<<<m.n_blocks, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
 }
-void launch_ovl_count(hipStream_t s, int n_pairs, const OvlDesc* od, PairState* st,
-                      const uint8_t* maps) {
-  k_ovl_count<<<n_pairs * kCountBlocksPerPair, 256, 0, s>>>(od, st, maps);
+void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
+                      const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps) {
+  k_ovl_popcount<<<n_groups * kCountBlocksPerMap, 256, 0, s>>>(od_ref, gst, 0, maps);
+  k_ovl_popcount<<<n_pairs * kCountBlocksPerMap, 256, 0, s>>>(od_read, st, 1, maps);
+  k_ovl_intersect<<<n_pairs * kCountBlocksPerMap, 256, 0, s>>>(pd, od_read, od_ref, st, maps);
 }
-void launch_ovl_finish(hipStream_t s, int n_pairs, PairState* st, int set_ratio) {
-  k_ovl_finish<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, st, set_ratio);
+void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
+                       int set_ratio) {
+  k_ovl_finish<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, gst, set_ratio);
 }
 
 }  // namespace aicp
