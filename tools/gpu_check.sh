@@ -2,7 +2,7 @@
 # GPU round-trip: parity tests, smoke, short bench. Each step bounded; stop at first failure.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -m gpu -x -q > gpurun_out/parity.log 2>&1 || { tail -40 gpurun_out/parity.log; exit 1; }
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/parity.log 2>&1 || { tail -40 gpurun_out/parity.log; exit 1; }
 tail -3 gpurun_out/parity.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -30 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
