@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -111,7 +112,7 @@ struct aicp_hip_ctx {
   std::string err;
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
       ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
-      nrm_raw, inv, gdesc, gstate;
+      nrm_raw, inv, gdesc, gstate, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp;
   // kd-tree construction work space (kernels_tree.hip)
   DevBuf tw_W0, tw_W1, tw_segof0, tw_segof1, tw_seg0, tw_seg1, tw_flag, tw_X1, tw_X2, tw_posL, tw_posR, tw_ev,
       tw_valid, tw_subs, tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
@@ -394,6 +395,14 @@ int device_trees_end(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total,
   return AICP_OK;
 }
 
+bool read_order_enabled() {  // AICP_READ_ORDER=0 keeps the caller's order (A/B measurements)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_READ_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 double ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
@@ -443,6 +452,24 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   HIPC(hipMemcpyAsync(dDesc, pdA, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
   launch_init_state(s, (int)P, dDesc, dState);
   HIPC(hipEventRecord(ctx->ev[7], s));
+  // readings in Morton order inside each pair's range (kernels_order.hip): the overlap and
+  // the ICP loop both visit the sorted copy
+  const float4* readS = B->read_raw.as<float4>();
+  if (read_order_enabled()) {
+    const size_t n = B->total_read;
+    const size_t tb = read_order_temp_bytes(n, (int)P);
+    HIPC(ensure(ctx->read_s, n * 16));
+    HIPC(ensure(ctx->ord_k0, n * 8));
+    HIPC(ensure(ctx->ord_k1, n * 8));
+    HIPC(ensure(ctx->ord_v0, n * 4));
+    HIPC(ensure(ctx->ord_v1, n * 4));
+    HIPC(ensure(ctx->ord_tmp, tb));
+    HIPC(launch_read_order(s, B->m_read, (int)P, dDesc, B->read_raw.as<float4>(), (uint32_t)n,
+                           ctx->ord_k0.as<uint64_t>(), ctx->ord_k1.as<uint64_t>(), ctx->ord_v0.as<uint32_t>(),
+                           ctx->ord_v1.as<uint32_t>(), ctx->ord_tmp.p, tb, ctx->read_s.as<float4>()));
+    readS = ctx->read_s.as<float4>();
+  }
+  HIPC(hipEventRecord(ctx->ev[11], s));
   const size_t G = B->gdesc.size();
   PairDesc* dG = nullptr;
   PairState* dGst = nullptr;
@@ -458,7 +485,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     launch_ovl_init(s, (int)P, dDesc, dState, res, 2);
     launch_ovl_init(s, (int)G, dG, dGst, res, 1);
     launch_ovl_bbox(s, B->m_gref, dG, dGst, B->ref_raw.as<float4>(), 0, res);
-    launch_ovl_bbox(s, B->m_read, dDesc, dState, B->read_raw.as<float4>(), 1, res);
+    launch_ovl_bbox(s, B->m_read, dDesc, dState, readS, 1, res);
     HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(ctx->pin_gstate.p, dGst, G * sizeof(PairState), hipMemcpyDeviceToHost, s));
   }
@@ -523,7 +550,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     const OvlDesc* dOvl = ctx->ovl.as<OvlDesc>();
     HIPC(hipMemsetAsync(bm, 0, bm_bytes, s));
     launch_ovl_mark(s, B->m_gref, dG, dOvl + P, dGst, B->ref_raw.as<float4>(), 0, res, bm);
-    launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, B->read_raw.as<float4>(), 1, res, bm);
+    launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm);
     launch_ovl_count(s, (int)P, (int)G, dDesc, dOvl, dOvl + P, dState, dGst, bm);
     launch_ovl_finish(s, (int)P, dDesc, dState, dGst, doIcp ? 1 : 0);
   }
@@ -570,7 +597,8 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     float4* readc = ctx->read_c.as<float4>();
     const uint4* nodes = ctx->nodes.as<uint4>();
     const int32_t* parent = nullptr;
-    launch_prepare_read(s2, B->m_read, dDesc, B->read_raw.as<float4>(), readc);
+    HIPC(hipStreamWaitEvent(s2, ctx->ev[11], 0));
+    launch_prepare_read(s2, B->m_read, dDesc, readS, readc);
     // normals from the raw tree's bucket order into the matcher tree's bucket order
     HIPC(ensure(ctx->inv, B->total_ref * 4));
     launch_normals_to_matcher(s2, (int)R, (uint32_t)B->total_ref, dRdesc, bpts, ctx->bpts_raw.as<float4>(),
@@ -727,7 +755,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  for (DevBuf* b : {&ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->match, &ctx->d2, &ctx->desc,
+  for (DevBuf* b : {&ctx->read_s, &ctx->ord_k0, &ctx->ord_k1, &ctx->ord_v0, &ctx->ord_v1, &ctx->ord_tmp, &ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->match, &ctx->d2, &ctx->desc,
                     &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,

@@ -17,6 +17,12 @@ struct BlockMap {
 // ---- ICP ---------------------------------------------------------------------------------
 void launch_prepare_read(hipStream_t s, BlockMap m, const PairDesc* pd, const float4* read_raw,
                          float4* read_c);
+// Spatial (Morton) order of the reading points of every pair, inside each pair's own range
+// (kernels_order.hip). keys*/vals*: total entries each; temp: read_order_temp_bytes.
+size_t read_order_temp_bytes(size_t n, int n_pairs);
+hipError_t launch_read_order(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* pd, const float4* raw,
+                             uint32_t total, uint64_t* keys0, uint64_t* keys1, uint32_t* vals0, uint32_t* vals1,
+                             void* temp, size_t temp_bytes, float4* out);
 void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const float4* ref_raw,
                        const int32_t* perm, float4* bpts);
 void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st);

@@ -113,6 +113,21 @@ def main():
     res = float(np.float32(0.2))  # octomapResolution read as<float> (yaml_configurator.cpp:81)
     # each rank streams its own C2 sequence (seed 1 + rank): weak scaling over independent pairs
     pairs = make_pairs(args.pairs, args.ref_every, args.points, seed=1 + rank)
+    order = os.environ.get("AICP_BENCH_READ_ORDER")  # experiment: host-side reading order
+    if order:
+        rng = np.random.default_rng(0)
+        for p in pairs:
+            r = p["read"]
+            if order == "shuffle":
+                idx = rng.permutation(len(r))
+            else:  # morton on 0.25 m cells
+                q = (np.floor(r / 0.25).astype(np.int64) & 1023)
+                key = np.zeros(len(r), np.int64)
+                for b in range(10):
+                    for a in range(3):
+                        key |= ((q[:, a] >> b) & 1) << (3 * b + a)
+                idx = np.argsort(key, kind="stable")
+            p["read"] = np.ascontiguousarray(r[idx])
     n_refs = len({id(p["ref"]) for p in pairs})
     ctx = L.Context(local_rank)
     batch = ctx.upload(pairs)
