@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libaicp_hip.so")
+LIB_PATH = os.environ.get("AICP_HIP_LIB") or os.path.join(PKG_DIR, "libaicp_hip.so")  # override: A/B builds
 
 AICP_OK = 0
 AICP_ERR_CONVERGENCE = 1

@@ -23,6 +23,7 @@ constexpr int kHistBins = 2048;     // radix-select digit 1/2 (11 bits)
 constexpr int kHist3Bins = 1024;    // digit 3 (10 bits)
 constexpr int kNNBlock = 256;       // NN / reduce kernel block
 constexpr int kReducePerThread = 4; // reading points per thread in the reduce kernel
+constexpr int kSelPerThread = 16;   // reading points per thread in the select passes
 constexpr int kRedCols = 30;        // 21 unique A entries + 6 b + kept + NN touch counts (2)
 constexpr int kFarStack = 48;       // max nested far descents (= max tree depth supported)
 constexpr int kHistRing = 32;       // differential checker history ring
@@ -120,7 +121,10 @@ struct NodeEvent {
 };
 
 // A segment small enough for one wave to finish its whole subtree in LDS (k_tr_subtree).
-constexpr int kSubMax = 1024;
+#ifndef AICP_SUBMAX
+#define AICP_SUBMAX 1024
+#endif
+constexpr int kSubMax = AICP_SUBMAX;  // largest segment one wave finishes in LDS (k_tr_subtree)
 struct SubSeg {
   uint32_t f, c;
   int32_t pair, depth;

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/aicp_hip.h"
@@ -81,6 +82,21 @@ void release(PinBuf& b) {
   b.cap = 0;
 }
 
+// Work space of one kd-tree construction (kernels_tree.hip). Two sets: the raw-coordinate
+// tree (SurfaceNormal) and the centred matcher tree are built concurrently on two streams.
+struct TreeBufs {
+  DevBuf W0, W1, segof0, segof1, seg0, seg1, flag, X1, X2, posL, posR, ev, valid, subs, ecnt, sums, pdepth, ctl,
+      scan;
+  PinBuf pin_ctl;
+  TreeWork tw{};  // device_trees_begin -> device_trees_end
+  void release_all() {
+    for (DevBuf* b : {&W0, &W1, &segof0, &segof1, &seg0, &seg1, &flag, &X1, &X2, &posL, &posR, &ev, &valid, &subs,
+                      &ecnt, &sums, &pdepth, &ctl, &scan})
+      release(*b);
+    release(pin_ctl);
+  }
+};
+
 struct Maps {  // block maps of one flat grid
   std::vector<int32_t> pair;
   std::vector<uint32_t> start;
@@ -102,24 +118,22 @@ struct aicp_hip_batch {
   uint64_t total_ref = 0, total_read = 0;
   uint32_t n_red_total = 0;
   DevBuf ref_raw, read_raw, maps;
-  BlockMap m_read{}, m_gref{}, m_red{};
+  BlockMap m_read{}, m_gref{}, m_red{}, m_sel{};
 };
 
 struct aicp_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // kd-tree + normals, concurrent with the overlap on `stream`
+  hipStream_t stream2 = nullptr;  // raw kd-tree + normals, concurrent with the overlap on `stream`
+  hipStream_t stream3 = nullptr;  // centroid + matcher kd-tree, concurrent with both
   std::string err;
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
       ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
-      nrm_raw, inv, gdesc, gstate, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp;
-  // kd-tree construction work space (kernels_tree.hip)
-  DevBuf tw_W0, tw_W1, tw_segof0, tw_segof1, tw_seg0, tw_seg1, tw_flag, tw_X1, tw_X2, tw_posL, tw_posR, tw_ev,
-      tw_valid, tw_subs, tw_ecnt, tw_sums, tw_pdepth, tw_ctl, tw_scan;
-  PinBuf pin_desc, pin_ctl, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
+      nrm_raw, inv, gdesc, gstate, sup, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp;
+  TreeBufs tb[2];  // [0] raw-coordinate tree (stream2), [1] centred matcher tree (stream3)
+  PinBuf pin_desc, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
   std::vector<hipEvent_t> nn_ev;
-  hipEvent_t ev[12] = {};
-  TreeWork tw{};  // device_trees_begin -> device_trees_end
+  hipEvent_t ev[16] = {};
   int last_nn_launches = 0;
   double last_nn_ms = 0, last_nn_bytes = 0;
   uint64_t last_queries = 0;
@@ -194,7 +208,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   B->gdesc.clear();
   uint64_t ro = 0, wo = 0;
   uint32_t red = 0;
-  Maps mr, mf, md;
+  Maps mr, mf, md, ms;
   // pairs whose reference is the same caller array (pointer, count, stride) share one copy,
   // one kd-tree and one set of normals (a reference window serves several readings)
   std::vector<size_t> rep;  // representative pair of each distinct reference
@@ -262,6 +276,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
       ident4(d.Tin);
     mr.add((int)i, d.n_read, kNNBlock);
     md.add((int)i, d.n_read, kNNBlock * kReducePerThread);
+    ms.add((int)i, d.n_read, kNNBlock * kSelPerThread);
   }
   B->total_ref = ro;
   B->total_read = wo;
@@ -283,8 +298,8 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   }
   HIPC(hipMemcpyAsync(B->read_raw.p, st, wo * 16, hipMemcpyHostToDevice, ctx->stream));
   // block maps: [read pair][read start][ref pair][ref start][red pair][red start]
-  const size_t nr = mr.pair.size(), nf = mf.pair.size(), nd = md.pair.size();
-  const size_t words = 2 * (nr + nf + nd);
+  const size_t nr = mr.pair.size(), nf = mf.pair.size(), nd = md.pair.size(), ns = ms.pair.size();
+  const size_t words = 2 * (nr + nf + nd + ns);
   HIPC(ensure(B->maps, words * 4));
   HIPC(hipStreamSynchronize(ctx->stream));
   uint32_t* mp = ctx->pin_io.as<uint32_t>();
@@ -303,96 +318,140 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   put(mr, B->m_read);
   put(mf, B->m_gref);
   put(md, B->m_red);
+  put(ms, B->m_sel);
   HIPC(hipMemcpyAsync(B->maps.p, mp, words * 4, hipMemcpyHostToDevice, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
   return AICP_OK;
 }
 
+// Tree builders report errors into `err` (they also run on a worker thread, see run_batch).
+#define TCHK(x)                                                                   \
+  do {                                                                            \
+    const hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess) {                                                       \
+      err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
+      return AICP_ERR_HIP;                                                        \
+    }                                                                             \
+  } while (0)
+#define TFAIL(code, msg) \
+  do {                   \
+    err = (msg);         \
+    return (code);       \
+  } while (0)
+
 // Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device: raw[ΣM] float4,
-// dDesc with ref_off / n_ref / Tin. Writes ctx->bpts (bucket order, w = local id), ctx->nodes
+// dDesc with ref_off / n_ref / Tin. Writes bpts_out (bucket order, w = local id), nodes_out
 // and the desc fields mean, Tmean, Tinit, node_off, n_nodes, tree_depth.
-int device_trees_begin(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
+int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
                        const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out) {
   const size_t n = (size_t)total;
   const size_t max_seg = n / 2 + P + 1;
-  HIPC(ensure(bpts_out, n * 16));
-  HIPC(ensure(nodes_out, (2 * n + 2) * 16));
-  HIPC(ensure(ctx->tw_W0, n * 16));
-  HIPC(ensure(ctx->tw_W1, n * 16));
-  HIPC(ensure(ctx->tw_segof0, n * 4));
-  HIPC(ensure(ctx->tw_segof1, n * 4));
-  HIPC(ensure(ctx->tw_seg0, max_seg * sizeof(TreeSeg)));
-  HIPC(ensure(ctx->tw_seg1, max_seg * sizeof(TreeSeg)));
-  HIPC(ensure(ctx->tw_flag, (n + 2) * 4));
-  HIPC(ensure(ctx->tw_X1, (n + 2) * 4));
-  HIPC(ensure(ctx->tw_X2, (n + 2) * 4));
-  HIPC(ensure(ctx->tw_posL, n * 4));
-  HIPC(ensure(ctx->tw_posR, n * 4));
-  HIPC(ensure(ctx->tw_ev, (2 * n + 2) * sizeof(NodeEvent)));
-  HIPC(ensure(ctx->tw_valid, 2 * n + 2));
-  HIPC(ensure(ctx->tw_subs, max_seg * sizeof(SubSeg)));
-  HIPC(ensure(ctx->tw_ecnt, (n + 2) * 4));
-  HIPC(ensure(ctx->tw_sums, P * 6 * 8));
-  HIPC(ensure(ctx->tw_pdepth, P * 4));
-  HIPC(ensure(ctx->tw_ctl, sizeof(TreeCtl)));
+  TCHK(ensure(bpts_out, n * 16));
+  TCHK(ensure(nodes_out, (2 * n + 2) * 16));
+  TCHK(ensure(T.W0, n * 16));
+  TCHK(ensure(T.W1, n * 16));
+  TCHK(ensure(T.segof0, n * 4));
+  TCHK(ensure(T.segof1, n * 4));
+  TCHK(ensure(T.seg0, max_seg * sizeof(TreeSeg)));
+  TCHK(ensure(T.seg1, max_seg * sizeof(TreeSeg)));
+  TCHK(ensure(T.flag, (n + 2) * 4));
+  TCHK(ensure(T.X1, (n + 2) * 4));
+  TCHK(ensure(T.X2, (n + 2) * 4));
+  TCHK(ensure(T.posL, n * 4));
+  TCHK(ensure(T.posR, n * 4));
+  TCHK(ensure(T.ev, (2 * n + 2) * sizeof(NodeEvent)));
+  TCHK(ensure(T.valid, 2 * n + 2));
+  TCHK(ensure(T.subs, max_seg * sizeof(SubSeg)));
+  TCHK(ensure(T.ecnt, (n + 2) * 4));
+  TCHK(ensure(T.sums, P * 6 * 8));
+  TCHK(ensure(T.pdepth, P * 4));
+  TCHK(ensure(T.ctl, sizeof(TreeCtl)));
   const size_t tb = tree_scan_temp_bytes(n + 2);
-  HIPC(ensure(ctx->tw_scan, tb));
-  HIPC(ensure(ctx->pin_ctl, sizeof(TreeCtl)));
+  TCHK(ensure(T.scan, tb));
+  TCHK(ensure(T.pin_ctl, sizeof(TreeCtl)));
   TreeWork w{};
-  w.W[0] = ctx->tw_W0.as<float4>();
-  w.W[1] = ctx->tw_W1.as<float4>();
-  w.segof[0] = ctx->tw_segof0.as<int32_t>();
-  w.segof[1] = ctx->tw_segof1.as<int32_t>();
-  w.seg[0] = ctx->tw_seg0.as<TreeSeg>();
-  w.seg[1] = ctx->tw_seg1.as<TreeSeg>();
-  w.flag = ctx->tw_flag.as<uint32_t>();
-  w.X1 = ctx->tw_X1.as<uint32_t>();
-  w.X2 = ctx->tw_X2.as<uint32_t>();
-  w.posL = ctx->tw_posL.as<uint32_t>();
-  w.posR = ctx->tw_posR.as<uint32_t>();
-  w.ev = ctx->tw_ev.as<NodeEvent>();
-  w.valid = ctx->tw_valid.as<uint8_t>();
-  w.subs = ctx->tw_subs.as<SubSeg>();
+  w.W[0] = T.W0.as<float4>();
+  w.W[1] = T.W1.as<float4>();
+  w.segof[0] = T.segof0.as<int32_t>();
+  w.segof[1] = T.segof1.as<int32_t>();
+  w.seg[0] = T.seg0.as<TreeSeg>();
+  w.seg[1] = T.seg1.as<TreeSeg>();
+  w.flag = T.flag.as<uint32_t>();
+  w.X1 = T.X1.as<uint32_t>();
+  w.X2 = T.X2.as<uint32_t>();
+  w.posL = T.posL.as<uint32_t>();
+  w.posR = T.posR.as<uint32_t>();
+  w.ev = T.ev.as<NodeEvent>();
+  w.valid = T.valid.as<uint8_t>();
+  w.subs = T.subs.as<SubSeg>();
   w.n_pairs = (int)P;
-  w.ecnt = ctx->tw_ecnt.as<uint32_t>();
-  w.sums = ctx->tw_sums.as<uint64_t>();
-  w.pair_depth = ctx->tw_pdepth.as<int32_t>();
-  w.ctl = ctx->tw_ctl.as<TreeCtl>();
-  w.scan_temp = ctx->tw_scan.p;
-  w.scan_temp_bytes = ctx->tw_scan.cap;
+  w.ecnt = T.ecnt.as<uint32_t>();
+  w.sums = T.sums.as<uint64_t>();
+  w.pair_depth = T.pdepth.as<int32_t>();
+  w.ctl = T.ctl.as<TreeCtl>();
+  w.scan_temp = T.scan.p;
+  w.scan_temp_bytes = T.scan.cap;
   w.max_seg = max_seg;
   float4* bpts = bpts_out.as<float4>();
-  HIPC(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts, bucket));
-  ctx->tw = w;
+  TCHK(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts, bucket));
+  T.tw = w;
   return AICP_OK;
 }
 
 // global levels (host polls), wave subtrees, node records; see device_trees_begin
-int device_trees_end(aicp_hip_ctx* ctx, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc, int bucket,
-                     DevBuf& bpts_out, DevBuf& nodes_out) {
+int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
+                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out) {
   const size_t n = (size_t)total;
-  const TreeWork& w = ctx->tw;
+  const TreeWork& w = T.tw;
   float4* bpts = bpts_out.as<float4>();
-  TreeCtl* hctl = ctx->pin_ctl.as<TreeCtl>();
+  TreeCtl* hctl = T.pin_ctl.as<TreeCtl>();
   // global levels until every remaining segment fits one wave's LDS (kSubMax points); the
   // host polls the next level's segment count from level 4 on
   bool done = false;
   for (int level = 0; level < kFarStack - 1 && !done; ++level) {
-    HIPC(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket));
+    TCHK(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket));
     if (level >= 4 || level == kFarStack - 2) {
-      HIPC(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
-      HIPC(hipStreamSynchronize(s));
+      TCHK(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
+      TCHK(hipStreamSynchronize(s));
       if (hctl->nseg[level + 1] == 0) done = true;
     }
   }
-  if (!done) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
-  HIPC(launch_tree_subtrees(s, (uint32_t)n, hctl->n_small, w, bpts, bucket));
-  HIPC(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
-  HIPC(hipMemcpyAsync(&hctl->error, &w.ctl->error, 4, hipMemcpyDeviceToHost, s));
-  HIPC(hipStreamSynchronize(s));
-  if (hctl->error & 1) FAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
-  if (hctl->error) FAIL(AICP_ERR_HIP, "kd-tree construction overflow " + std::to_string(hctl->error));
+  if (!done) TFAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
+  TCHK(launch_tree_subtrees(s, (uint32_t)n, hctl->n_small, w, bpts, bucket));
+  TCHK(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
+  TCHK(hipMemcpyAsync(&hctl->error, &w.ctl->error, 4, hipMemcpyDeviceToHost, s));
+  TCHK(hipStreamSynchronize(s));
+  if (hctl->error & 1) TFAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
+  if (hctl->error) TFAIL(AICP_ERR_HIP, "kd-tree construction overflow " + std::to_string(hctl->error));
   return AICP_OK;
+}
+
+// the centred reference's matcher tree and the pairs' frames, on stream3 (worker thread)
+int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dDesc, PairDesc* dRdesc,
+                  std::string& err) {
+  hipStream_t s3 = ctx->stream3;
+  const size_t R = B->rdesc.size();
+  TCHK(hipSetDevice(ctx->device));  // the current device is per host thread
+  TCHK(hipStreamWaitEvent(s3, ctx->ev[7], 0));
+  TCHK(hipEventRecord(ctx->ev[12], s3));
+  TCHK(hipMemcpyAsync(dRdesc, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s3));
+  int rc = device_trees_begin(ctx->tb[1], err, s3, R, B->total_ref, dRdesc, B->ref_raw.as<float4>(), 1, bucket,
+                              ctx->bpts, ctx->nodes);
+  if (rc) return rc;
+  rc = device_trees_end(ctx->tb[1], err, s3, R, B->total_ref, dRdesc, bucket, ctx->bpts, ctx->nodes);
+  if (rc) return rc;
+  // two-level node records for the matcher (Trav2)
+  const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);
+  TCHK(ensure(ctx->sup, (size_t)cap * 32));
+  launch_super_nodes(s3, (int)R, cap, dRdesc, ctx->nodes.as<uint4>(), ctx->sup.as<uint4>());
+  launch_pairs_from_refs(s3, (int)B->P, dDesc, dRdesc);
+  TCHK(hipEventRecord(ctx->ev[3], s3));
+  return AICP_OK;
+}
+
+bool stream_prio_enabled() {  // AICP_STREAM_PRIO=0: all streams at the default priority
+  const char* e = std::getenv("AICP_STREAM_PRIO");
+  return !(e && e[0] == '0');
 }
 
 bool read_order_enabled() {  // AICP_READ_ORDER=0 keeps the caller's order (A/B measurements)
@@ -495,6 +554,23 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   const size_t R = B->rdesc.size();
   PairDesc* dRdesc = nullptr;
   PairState* dRstate = nullptr;
+  std::thread worker;
+  int wrc = AICP_OK;
+  std::string werr;
+  struct Joiner {  // every return after the worker started joins it (std::thread must not leak)
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } joiner{worker};
+  auto join_worker = [&](int r) {
+    if (worker.joinable()) worker.join();
+    if (!r && wrc) {
+      ctx->err = werr;
+      r = wrc;
+    }
+    return r;
+  };
   if (doIcp) {
     HIPC(ensure(ctx->rdesc, R * sizeof(PairDesc)));
     HIPC(ensure(ctx->rstate, R * sizeof(PairState)));
@@ -505,14 +581,16 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(ensure(ctx->rdesc_raw, R * sizeof(PairDesc)));
     HIPC(hipStreamWaitEvent(s2, ctx->ev[7], 0));
     HIPC(hipEventRecord(ctx->ev[8], s2));
-    HIPC(hipMemcpyAsync(dRdesc, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s2));
     HIPC(hipMemcpyAsync(ctx->rdesc_raw.p, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s2));
-    launch_init_state(s2, (int)R, dRdesc, dRstate);
+    launch_init_state(s2, (int)R, ctx->rdesc_raw.as<PairDesc>(), dRstate);
+    // s3 (worker thread, it polls its own tree levels): centroid, centred reference, matcher
+    // tree, pair frames
+    worker = std::thread([&] { wrc = matcher_trees(ctx, B, cfg->bucket_size, dDesc, dRdesc, werr); });
     // SurfaceNormal runs on the reference as given, before the centring (ICP::compute,
     // SURVEY A.1 steps 1-2): its own libnabo tree over the raw coordinates first
-    rc = device_trees_begin(ctx, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), B->ref_raw.as<float4>(), 0,
-                            cfg->bucket_size, ctx->bpts_raw, ctx->nodes_raw);
-    if (rc) return rc;
+    rc = device_trees_begin(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(),
+                            B->ref_raw.as<float4>(), 0, cfg->bucket_size, ctx->bpts_raw, ctx->nodes_raw);
+    if (rc) return join_worker(rc);
   }
   // overlap: size the voxel maps from the key boxes, then mark
   uint64_t bm_bytes = 0;
@@ -558,10 +636,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   IcpParams prm{};
   int nn_launches = 0;
   if (doIcp) {
-    // s2: kd-tree levels + subtrees, reading frame, SurfaceNormal
-    rc = device_trees_end(ctx, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), cfg->bucket_size, ctx->bpts_raw,
-                          ctx->nodes_raw);
-    if (rc) return rc;
+    // s2: raw tree levels + subtrees, SurfaceNormal
+    rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), cfg->bucket_size,
+                          ctx->bpts_raw, ctx->nodes_raw);
+    if (rc) return join_worker(rc);
     // normals on the raw tree (bucket order of that tree)
     HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
@@ -572,14 +650,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
                         cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
     HIPC(hipEventRecord(ctx->ev[10], s2));
-    // centroid + the matcher's tree over the centred reference
-    rc = device_trees_begin(ctx, s2, R, B->total_ref, dRdesc, B->ref_raw.as<float4>(), 1, cfg->bucket_size,
-                            ctx->bpts, ctx->nodes);
+    // the matcher tree (s3) must be complete, and the worker done with ctx->bpts / nodes
+    rc = join_worker(AICP_OK);
     if (rc) return rc;
-    rc = device_trees_end(ctx, s2, R, B->total_ref, dRdesc, cfg->bucket_size, ctx->bpts, ctx->nodes);
-    if (rc) return rc;
-    launch_pairs_from_refs(s2, (int)P, dDesc, dRdesc);
-    HIPC(hipEventRecord(ctx->ev[3], s2));
+    HIPC(hipStreamWaitEvent(s2, ctx->ev[3], 0));
     HIPC(ensure(ctx->read_c, B->total_read * 16));
     HIPC(ensure(ctx->bpts, B->total_ref * 16));
     HIPC(ensure(ctx->bnrm, B->total_ref * 16));
@@ -618,11 +692,11 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     for (int it = 0; it < cfg->max_iter; ++it) {
       launch_active_list(s, (int)P, dDesc, dState, dAl, dCtr);
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it], s));
-      launch_icp_nn(s, (int)B->total_read, dDesc, dState, dAl, readc, nodes, parent, bpts,
+      launch_icp_nn(s, (int)B->total_read, dDesc, dState, dAl, readc, nodes, ctx->sup.as<uint4>(), parent, bpts,
                     ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm);
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it + 1], s));
       ++nn_launches;
-      launch_icp_select(s, B->m_red, (int)P, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
+      launch_icp_select(s, B->m_sel, (int)P, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
                         ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>());
       launch_icp_reduce(s, B->m_red, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
                         ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>());
@@ -632,6 +706,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   } else {
     HIPC(hipEventRecord(ctx->ev[8], s));
     HIPC(hipEventRecord(ctx->ev[10], s));
+    HIPC(hipEventRecord(ctx->ev[12], s));
     HIPC(hipEventRecord(ctx->ev[3], s));
     HIPC(hipEventRecord(ctx->ev[4], s));
     HIPC(hipEventRecord(ctx->ev[9], s));
@@ -682,9 +757,9 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   ctx->last_queries = queries;
   ctx->last_phase[0] = doOvl ? ev_ms(ctx->ev[0], ctx->ev[1]) + ev_ms(ctx->ev[6], ctx->ev[2]) : 0;
   // tree and normals run on the second stream, concurrently with the overlap
-  // [1] raw-coordinate tree + SurfaceNormal, [2] centroid + matcher tree + normal scatter
+  // [1] raw-coordinate tree + SurfaceNormal (s2), [2] centroid + matcher tree (s3)
   ctx->last_phase[1] = doIcp ? ev_ms(ctx->ev[8], ctx->ev[10]) : 0;
-  ctx->last_phase[2] = doIcp ? ev_ms(ctx->ev[10], ctx->ev[4]) : 0;
+  ctx->last_phase[2] = doIcp ? ev_ms(ctx->ev[12], ctx->ev[3]) : 0;
   ctx->last_phase[3] = doIcp ? ev_ms(ctx->ev[9], ctx->ev[5]) : 0;
   ctx->last_phase[4] =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
@@ -713,10 +788,10 @@ int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, Pa
   ident4(d.Tin);
   HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
-  int rc = device_trees_begin(ctx, s, 1, n, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8, ctx->bpts,
-                              ctx->nodes);
+  int rc = device_trees_begin(ctx->tb[0], ctx->err, s, 1, n, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8,
+                              ctx->bpts, ctx->nodes);
   if (rc) return rc;
-  rc = device_trees_end(ctx, s, 1, n, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes);
+  rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, n, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes);
   if (rc) return rc;
   HIPC(hipMemcpyAsync(&d, ctx->desc.p, sizeof(d), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -738,12 +813,16 @@ int aicp_hip_create(int device, aicp_hip_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return AICP_ERR_HIP;
   aicp_hip_ctx* c = new aicp_hip_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
-    return AICP_ERR_HIP;
-  }
-  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipStreamDestroy(c->stream);
+  // the overlap (stream) yields the CUs to the kd-tree streams, whose chains of short
+  // level kernels are the critical path before the ICP loop
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+  if (!stream_prio_enabled()) prio_lo = prio_hi = 0;
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+    for (hipStream_t q : {c->stream, c->stream2, c->stream3})
+      if (q) (void)hipStreamDestroy(q);
     delete c;
     return AICP_ERR_HIP;
   }
@@ -754,18 +833,15 @@ int aicp_hip_create(int device, aicp_hip_ctx** out) {
 void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipDeviceSynchronize();
   for (DevBuf* b : {&ctx->read_s, &ctx->ord_k0, &ctx->ord_k1, &ctx->ord_v0, &ctx->ord_v1, &ctx->ord_tmp, &ctx->read_c, &ctx->bpts, &ctx->bnrm, &ctx->nodes, &ctx->match, &ctx->d2, &ctx->desc,
                     &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
-                    &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->gdesc, &ctx->gstate, &ctx->tw_W0, &ctx->tw_W1, &ctx->tw_segof0,
-                    &ctx->tw_segof1, &ctx->tw_seg0, &ctx->tw_seg1, &ctx->tw_flag, &ctx->tw_X1, &ctx->tw_X2,
-                    &ctx->tw_posL, &ctx->tw_posR, &ctx->tw_ev, &ctx->tw_valid, &ctx->tw_subs, &ctx->tw_ecnt,
-                    &ctx->tw_sums, &ctx->tw_pdepth,
-                    &ctx->tw_ctl, &ctx->tw_scan})
+                    &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->sup, &ctx->gdesc, &ctx->gstate})
     release(*b);
-  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_ctl, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
+  for (auto& t : ctx->tb) t.release_all();
+  for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
                     &ctx->pin_rdesc, &ctx->pin_gdesc, &ctx->pin_gstate})
     release(*b);
   for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
@@ -773,6 +849,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   delete ctx;
 }
 
@@ -961,8 +1038,8 @@ int aicp_hip_dists_quantile(aicp_hip_ctx* ctx, const float* d2, size_t n, float 
   std::memcpy(ctx->pin_io.p, d2, n * 4);
   HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, st_));
   HIPC(hipMemcpyAsync(ctx->d2.p, ctx->pin_io.p, n * 4, hipMemcpyHostToDevice, st_));
-  // one pair: blocks of kNNBlock * kReducePerThread readings
-  const uint32_t per = kNNBlock * kReducePerThread, nb = (uint32_t)((n + per - 1) / per);
+  // one pair: blocks of kNNBlock * kSelPerThread readings
+  const uint32_t per = kNNBlock * kSelPerThread, nb = (uint32_t)((n + per - 1) / per);
   HIPC(ensure(ctx->qmap, (size_t)nb * 8));
   HIPC(ensure(ctx->pin_desc, (size_t)nb * 8));
   uint32_t* hm = ctx->pin_desc.as<uint32_t>();

@@ -211,6 +211,147 @@ struct Trav {
   }
 };
 
+// 1-NN (the ICP matcher) over two-level node records: record n of the matcher tree carries,
+// besides its own {cut, cd | right, parent}, the {x, y} words of both children (k_super_nodes,
+// 32 bytes = two loads from one cache line issued together). A descent step therefore decides
+// two levels -- the node's and the chosen child's -- per round trip: the descent, ~70 % of the
+// dependent loads of a query (tools/travstats.cpp: 18.3 of 26), takes half as many. Visit
+// order, far tests, counts and results are Trav<1>'s (libnabo recurseKnn).
+struct Trav2 {
+  const uint4* nodes;  // super records: [2n] = {x, y, parent, left.x}, [2n + 1] = {left.y, right.x, right.y, 0}
+  const float4* pts;
+  float q0, q1, q2;
+  float off0, off1, off2, rd, minFar;
+  int32_t n, start, sp;
+  uint32_t tp, tn;
+  Best<1> best;
+
+  __device__ __forceinline__ void bind(const uint4* nb, const float4* pb, uint32_t node_off, uint32_t ref_off) {
+    nodes = nb + 2 * (size_t)node_off;
+    pts = pb + ref_off;
+  }
+  __device__ __forceinline__ float res_d2() const { return best.v[0]; }
+  __device__ __forceinline__ int32_t res_id() const { return best.id[0]; }
+
+  __device__ __forceinline__ void reset(float a, float b, float c) {
+    q0 = a;
+    q1 = b;
+    q2 = c;
+    off0 = off1 = off2 = rd = 0.f;
+    n = start = sp = 0;
+    tp = tn = 0;
+    best_init<1>(best);
+  }
+
+  __device__ __forceinline__ bool advance(FarStack& fs, float maxE2, float maxR2, const uint4*, const float4*) {
+    minFar = __builtin_inff();
+    uint4 a = nodes[2 * n], b = nodes[2 * n + 1];
+    int32_t pl = (int32_t)a.z;  // parent of the leaf the descent ends in
+    while ((a.y & 3u) != kLeaf) {
+      const uint32_t cd = a.y & 3u;
+      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(a.x);
+      const float oc = sel3(cd, off0, off1, off2);
+      minFar = fminf(minFar, rd + (-oc * oc + no * no));
+      ++tn;
+      const bool right = no > 0.f;
+      const int32_t c = right ? (int32_t)(a.y >> 2) : n + 1;
+      const uint32_t cx = right ? b.y : a.w, cy = right ? b.z : b.x;
+      pl = n;
+      n = c;
+      if ((cy & 3u) == kLeaf) {  // leaf child: count and bucket start are already here
+        a.x = cx;
+        a.y = cy;
+        break;
+      }
+      const uint32_t cd2 = cy & 3u;
+      const float no2 = sel3(cd2, q0, q1, q2) - __uint_as_float(cx);
+      const float oc2 = sel3(cd2, off0, off1, off2);
+      minFar = fminf(minFar, rd + (-oc2 * oc2 + no2 * no2));
+      ++tn;
+      n = (no2 > 0.f) ? (int32_t)(cy >> 2) : c + 1;
+      a = nodes[2 * n];
+      b = nodes[2 * n + 1];
+      pl = (int32_t)a.z;
+    }
+    {
+      const uint32_t b0 = a.y >> 2, cnt = a.x;
+      float3 P[kLeafBatch];
+#pragma unroll
+      for (int i = 0; i < kLeafBatch; ++i)
+        if ((uint32_t)i < cnt) {
+          const float4 p = pts[b0 + i];
+          P[i] = make_float3(p.x, p.y, p.z);
+        }
+#pragma unroll
+      for (int i = 0; i < kLeafBatch; ++i)
+        if ((uint32_t)i < cnt) {
+          const float d0 = q0 - P[i].x, d1 = q1 - P[i].y, d2 = q2 - P[i].z;
+          float dist = 0.f;
+          dist += d0 * d0;
+          dist += d1 * d1;
+          dist += d2 * d2;
+          if (dist <= maxR2 && dist < best.v[0]) best_replace<1>(best, (int32_t)(b0 + i), dist);
+        }
+      for (uint32_t i = kLeafBatch; i < cnt; ++i) {
+        const float4 p = pts[b0 + i];
+        const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
+        float dist = 0.f;
+        dist += d0 * d0;
+        dist += d1 * d1;
+        dist += d2 * d2;
+        if (dist <= maxR2 && dist < best.v[0]) best_replace<1>(best, (int32_t)(b0 + i), dist);
+      }
+      tp += cnt;
+    }
+    int32_t c = n, pc = pl;
+    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+    for (;;) {
+      if (c == start) {
+        if (sp == 0) return true;
+        --sp;
+        const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
+        rd = fs.rd[sp];
+        const float old = fs.old[sp];
+        if (pcd == 0) off0 = old;
+        else if (pcd == 1) off1 = old;
+        else off2 = old;
+        minFar = fs.mn[sp];
+        start = fs.start[sp];
+        c = fs.P[sp];
+        pc = fs.PP[sp];
+        if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+        continue;
+      }
+      const int32_t p = pc;
+      const uint4 pn = nodes[2 * p];
+      const uint32_t cd = pn.y & 3u;
+      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(pn.x);
+      const float oc = sel3(cd, off0, off1, off2);
+      const float rdf = rd + (-oc * oc + no * no);
+      if (rdf <= maxR2 && rdf * maxE2 < best.v[0]) {
+        const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
+        fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
+        fs.rd[sp] = rd;
+        fs.old[sp] = oc;
+        fs.mn[sp] = minFar;
+        fs.start[sp] = start;
+        fs.P[sp] = p;
+        fs.PP[sp] = (int32_t)pn.z;
+        ++sp;
+        if (cd == 0) off0 = no;
+        else if (cd == 1) off1 = no;
+        else off2 = no;
+        rd = rdf;
+        n = far;
+        start = far;
+        return false;
+      }
+      c = p;
+      pc = (int32_t)pn.z;
+    }
+  }
+};
+
 // 1-NN (the ICP matcher) as a one-load-per-step state machine: each iteration a lane issues
 // exactly one 16-byte load -- a node record or a bucket point, chosen per lane -- and then
 // advances its own phase (descent / bucket / climb), so lanes in different phases of their
@@ -728,36 +869,40 @@ constexpr uint32_t kInfBits = 0x7f800000u;
 // ---- TrimmedDist limit = exact k-th smallest finite d2, k = (size_t)(float(n) * ratio)
 // (getDistsQuantile), as a radix select on the float bits (non-negative floats
 // order like their bit patterns) spread over the whole chip:
-//   k_sel_hist    per 1024 readings: LDS histogram of digit 1 (bits 31..21) -> global
+//   k_sel_hist    per 4096 readings: LDS histogram of digit 1 (bits 31..21) -> global
 //   k_sel_find1   per pair: n = #finite, k, bin b1 holding rank k, rank r1 inside it
-//   k_sel_compact per 1024 readings: the values of bin b1 -> per-pair candidate list
+//   k_sel_compact per 4096 readings: the values of bin b1 -> per-pair candidate list
 //   k_sel_final   per pair: digits 2 (bits 20..10) and 3 (bits 9..0) over the candidates
 __global__ __launch_bounds__(256) void k_sel_hist(BlockMap m, const PairDesc* __restrict__ pd,
                                                   const PairState* __restrict__ st, const float* __restrict__ d2,
                                                   uint32_t* __restrict__ hist1) {
   const int pair = m.pair[blockIdx.x];
   if (!st[pair].active) return;
-  __shared__ uint32_t h[4][kHistBins];  // one sub-histogram per wave (LDS atomic conflicts)
+  __shared__ uint32_t h[2][kHistBins];  // one sub-histogram per wave pair (LDS atomic conflicts)
   const int t = threadIdx.x;
-  for (int i = t; i < 4 * kHistBins; i += 256) (&h[0][0])[i] = 0;
-  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2 * kHistBins / 256; ++i) (&h[0][0])[t + 256 * i] = 0;
   const PairDesc& d = pd[pair];
   const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
-  uint32_t* mine = h[t >> 6];
   const uint32_t j0 = m.start[blockIdx.x];
+  uint32_t v[kSelPerThread];
 #pragma unroll
-  for (int u = 0; u < kReducePerThread; ++u) {
+  for (int u = 0; u < kSelPerThread; ++u) {
     const uint32_t j = j0 + t + 256u * u;
-    if (j < d.n_read) {
-      const uint32_t v = bits[j];
-      if (v != kInfBits) atomicAdd(&mine[v >> 21], 1u);
-    }
+    v[u] = j < d.n_read ? bits[j] : kInfBits;
   }
   __syncthreads();
+  uint32_t* mine = h[t >> 7];
+#pragma unroll
+  for (int u = 0; u < kSelPerThread; ++u)
+    if (v[u] != kInfBits) atomicAdd(&mine[v[u] >> 21], 1u);
+  __syncthreads();
   uint32_t* g = hist1 + (size_t)pair * kHistBins;
-  for (int i = t; i < kHistBins; i += 256) {
-    const uint32_t c = h[0][i] + h[1][i] + h[2][i] + h[3][i];
-    if (c) atomicAdd(&g[i], c);
+#pragma unroll
+  for (int i = 0; i < kHistBins / 256; ++i) {
+    const int b = t + 256 * i;
+    const uint32_t c = h[0][b] + h[1][b];
+    if (c) atomicAdd(&g[b], c);
   }
 }
 
@@ -825,17 +970,17 @@ __global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc*
   const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint32_t j0 = m.start[blockIdx.x];
-  uint32_t v[kReducePerThread];
-  uint64_t mk[kReducePerThread];
-  uint32_t mine = 0;  // this wave's hits
+  uint32_t v[kSelPerThread];
 #pragma unroll
-  for (int u = 0; u < kReducePerThread; ++u) {
+  for (int u = 0; u < kSelPerThread; ++u) {
     const uint32_t j = j0 + t + 256u * u;
     v[u] = j < d.n_read ? bits[j] : kInfBits;
-    mk[u] = __ballot(v[u] != kInfBits && (v[u] >> 21) == b1);
-    mine += (uint32_t)__popcll(mk[u]);
   }
-  // one atomic per block (the per-pair counter is shared by ~120 blocks)
+  uint32_t mine = 0;  // this wave's hits
+#pragma unroll
+  for (int u = 0; u < kSelPerThread; ++u)
+    mine += (uint32_t)__popcll(__ballot(v[u] != kInfBits && (v[u] >> 21) == b1));
+  // one atomic per block (the per-pair counter is shared by ~30 blocks)
   if (lane == 0) wcount[w] = mine;
   __syncthreads();
   if (t == 0) {
@@ -843,12 +988,16 @@ __global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc*
     base = tot ? atomicAdd(&cand_cnt[pair], tot) : 0u;
   }
   __syncthreads();
+  if (!wcount[w]) return;
   uint32_t o = base;
   for (int k = 0; k < w; ++k) o += wcount[k];
+  const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
-  for (int u = 0; u < kReducePerThread; ++u) {
-    if ((mk[u] >> lane) & 1ull) cand[d.read_off + o + (uint32_t)__popcll(mk[u] & ((1ull << lane) - 1ull))] = v[u];
-    o += (uint32_t)__popcll(mk[u]);
+  for (int u = 0; u < kSelPerThread; ++u) {
+    const bool hit = v[u] != kInfBits && (v[u] >> 21) == b1;
+    const uint64_t mk = __ballot(hit);
+    if (hit) cand[d.read_off + o + (uint32_t)__popcll(mk & below)] = v[u];
+    o += (uint32_t)__popcll(mk);
   }
 }
 
@@ -1229,23 +1378,26 @@ void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const Pa
                         uint32_t* ctr) {
   k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr);
 }
-// NN engine for the 1-NN kernels: 1 = Trav<1> (default), 0 = SM0; AICP_NN_ENGINE overrides
+// NN engine of the ICP matcher: 2 = Trav2 (default), 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
 // (design experiments, tools/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:
 // Trav<1> 230 us per NN launch, SM0 436 us (profiles/README.md).
 static int nn_engine() {
   static int e = -1;
   if (e < 0) {
     const char* v = getenv("AICP_NN_ENGINE");
-    e = (v && v[0] == '0') ? 0 : 1;
+    e = (v && v[0] == '0') ? 0 : (v && v[0] == '1') ? 1 : 2;
   }
   return e;
 }
 
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st, const ActiveList* al,
-                   const float4* read_c, const uint4* nodes, const int32_t* parent, const float4* bpts,
+                   const float4* read_c, const uint4* nodes, const uint4* sup, const int32_t* parent,
+                   const float4* bpts,
                    int32_t* match, float* d2, uint32_t* touched, uint32_t* ctr, const IcpParams& prm) {
   const int g = persistent_grid(grid_items);
-  if (nn_engine() == 1)
+  if (nn_engine() == 2 && sup)
+    k_icp_nn<Trav2><<<g, 256, 0, s>>>(pd, st, al, read_c, sup, parent, bpts, match, d2, touched, ctr, prm);
+  else if (nn_engine() >= 1)
     k_icp_nn<Trav<1>><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, match, d2, touched, ctr, prm);
   else
     k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, match, d2, touched, ctr, prm);
@@ -1278,7 +1430,7 @@ bool launch_knn_generic(hipStream_t s, uint32_t nq, const float4* q, const uint4
   const int g = persistent_grid((int)nq);
   switch (k) {
     case 1:
-      if (nn_engine() == 1)
+      if (nn_engine() >= 1)
         k_knn1_generic<Trav<1>><<<g, 256, 0, s>>>(nq, q, nodes, bpts, maxE2, maxR2, ids, d2, touched, ctr);
       else
         k_knn1_generic<SM0><<<g, 256, 0, s>>>(nq, q, nodes, bpts, maxE2, maxR2, ids, d2, touched, ctr);

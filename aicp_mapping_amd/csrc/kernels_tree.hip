@@ -837,6 +837,33 @@ static hipError_t scan_u32(hipStream_t s, void* temp, size_t temp_bytes, const u
   return rocprim::exclusive_scan(temp, bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), s);
 }
 
+__global__ __launch_bounds__(256) void k_super_nodes(int n_refs, uint32_t cap, const PairDesc* __restrict__ rd,
+                                                     const uint4* __restrict__ nodes, uint4* __restrict__ sup) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t total = rd[n_refs - 1].node_off + rd[n_refs - 1].n_nodes;
+  if (g >= total || g >= cap) return;
+  int lo = 0, hi = n_refs - 1;  // the reference owning node g (node_off ascending)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (rd[mid].node_off <= g) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint32_t base = rd[lo].node_off;
+  const uint4 a = nodes[g];
+  uint4 s0 = make_uint4(a.x, a.y, a.z, 0u), s1 = make_uint4(0u, 0u, 0u, 0u);
+  if ((a.y & 3u) != kLeaf) {
+    const uint4 L = nodes[g + 1], R = nodes[base + (a.y >> 2)];
+    s0.w = L.x;
+    s1 = make_uint4(L.y, R.x, R.y, 0u);
+  }
+  sup[2 * (size_t)g] = s0;
+  sup[2 * (size_t)g + 1] = s1;
+}
+
+void launch_super_nodes(hipStream_t s, int n_refs, uint32_t cap, const PairDesc* rd, const uint4* nodes, uint4* sup) {
+  if (n_refs > 0 && cap > 0) k_super_nodes<<<(cap + 255) / 256, 256, 0, s>>>(n_refs, cap, rd, nodes, sup);
+}
+
 void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd) {
   k_pairs_from_refs<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, rd);
 }
