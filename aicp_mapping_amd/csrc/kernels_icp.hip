@@ -119,17 +119,23 @@ struct Trav {
   // The climb follows the parent index stored in each node record (one load per level).
   __device__ __forceinline__ bool advance(FarStack& fs, float maxE2, float maxR2, const uint4*, const float4*) {
     minFar = __builtin_inff();
-    uint4 nd = nodes[n];
+    // the descent reads the first 8 bytes of each record (cut, cd | right); the leaf's parent
+    // is the node the descent came from (the climb reads whole records)
+    const uint2* nodes2 = reinterpret_cast<const uint2*>(nodes);
+    uint2 nd = nodes2[2 * n];
+    int32_t pl = -1;
     while ((nd.y & 3u) != kLeaf) {
       const uint32_t cd = nd.y & 3u;
       const float no = sel3(cd, q0, q1, q2) - __uint_as_float(nd.x);
       const float oc = sel3(cd, off0, off1, off2);
       const float rdf = rd + (-oc * oc + no * no);
       minFar = fminf(minFar, rdf);
+      pl = n;
       n = (no > 0.f) ? (int32_t)(nd.y >> 2) : n + 1;
       ++tn;
-      nd = nodes[n];
+      nd = nodes2[2 * n];
     }
+    if (pl < 0) pl = (int32_t)nodes[n].z;  // the descent started at a leaf
     {
       // bucket: the first kLeafBatch points are loaded before any is used (one round trip
       // instead of one per point), then scanned in order
@@ -162,7 +168,7 @@ struct Trav {
       }
       tp += cnt;
     }
-    int32_t c = n, pc = (int32_t)nd.z;
+    int32_t c = n, pc = pl;
     if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
     for (;;) {
       if (c == start) {
