@@ -47,6 +47,49 @@ def make_pairs(n_readings, ref_every, n_points, seed):
             for pr in sy.make_sequence(n_readings, ref_every, n_points, seed=seed)]
 
 
+def _c5_pair(seed_points):
+    from aicp_mapping_amd import synthetic as sy
+
+    seed, n = seed_points
+    pr = sy.make_pair(n, n, seed=seed)
+    return dict(ref=pr.ref, read=pr.read, ref_origin=pr.ref_origin, read_origin=pr.read_origin, T_gt=pr.T_gt)
+
+
+def make_c5_pairs(n_total, n_points, rank, world):
+    """C5: independent pairs, seeds 1000..; rank g takes pairs i = g mod G
+    (sharding.shard_pairs). Generated in a process pool (16 workers: the box's CPU share)."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    from aicp_mapping_amd import sharding as sh
+
+    mine = sh.shard_pairs(n_total, world, rank)
+    with ProcessPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        return list(ex.map(_c5_pair, [(1000 + i, n_points) for i in mine], chunksize=4))
+
+
+def make_c4_pairs(n_readings, n_points, map_points, crop, seed):
+    """C4 localization-only: a resident map of map_points points over the whole
+    scene; reading i (N points, sensor moving along x) registers against the map points within
+    +-crop m of its prior position (the cropped map, M ~ 250k); overlap fixed at 50 % => r = 0.5.
+    The crop is input preparation here (an axis-aligned box around the prior position)."""
+    from aicp_mapping_amd import synthetic as sy
+
+    seq = sy.make_sequence(n_readings, n_readings, n_points, seed=seed)
+    scene = sy.make_scene(seed)
+    rng = np.random.default_rng(seed * 7919 + 77)
+    mp = sy.sample_scene(scene, rng, np.array([0.0, 0.0, 0.7]), half=40.0)
+    if len(mp) > map_points:
+        mp = mp[rng.choice(len(mp), size=map_points, replace=False)]
+    mp = mp.astype(np.float32)
+    out = []
+    for i, pr in enumerate(seq):
+        o = np.array([(i + 1) * 0.3, 0.0, 0.7])  # prior position of reading i (make_sequence's path)
+        m = np.all(np.abs(mp - o.astype(np.float32)) <= crop, axis=1)
+        ref = np.ascontiguousarray(mp[m])
+        out.append(dict(ref=ref, read=pr.read, ref_origin=o, read_origin=pr.read_origin, T_gt=pr.T_gt))
+    return out, len(mp)
+
+
 def cpu_baseline(pairs, res, budget_s):
     """The oracle (single-thread C++ restatement of the libpointmatcher chain) on a bounded sample
     of the same workload: whole pairs (overlap + ratio + ICP), as many as fit the budget."""
@@ -89,9 +132,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=64, help="readings (pairs) per step per GPU")
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="BASELINE.json workload (default c2: the metric's configuration)")
+    ap.add_argument("--pairs", type=int, default=None, help="readings (pairs) per step per GPU")
     ap.add_argument("--ref-every", type=int, default=5, help="readings per reference window")
-    ap.add_argument("--points", type=int, default=120000)
+    ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -111,8 +156,34 @@ def main():
     from aicp_mapping_amd import sharding as sh
 
     res = float(np.float32(0.2))  # octomapResolution read as<float> (yaml_configurator.cpp:81)
-    # each rank streams its own C2 sequence (seed 1 + rank): weak scaling over independent pairs
-    pairs = make_pairs(args.pairs, args.ref_every, args.points, seed=1 + rank)
+    cfg = L.default_config()
+    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+    extra = {}
+    if args.config in ("c2", "c3"):
+        args.pairs = args.pairs or 64
+        args.points = args.points or (120000 if args.config == "c2" else 600000)
+        # each rank streams its own sequence (seed 1 + rank): weak scaling over independent pairs
+        pairs = make_pairs(args.pairs, args.ref_every, args.points, seed=1 + rank)
+        workload = ("%s: %s batch_size=80 clouds, N=M=%d, frame-to-reference sequence of %d readings, "
+                    "reference updated every %d" % (args.config.upper(), "ANYmal VLP-16" if args.config == "c2"
+                                                    else "KITTI HDL-64", args.points, args.pairs, args.ref_every))
+    elif args.config == "c4":
+        args.pairs = args.pairs or 64
+        args.points = args.points or 120000
+        pairs, n_map = make_c4_pairs(args.pairs, args.points, 1000000, 15.0, seed=1 + rank)
+        cfg = L.default_config(trimmed_ratio=0.5)  # overlap fixed at 50 % (app.cpp:123-127)
+        flags = L.AICP_RUN_ICP
+        extra = {"map_points": n_map, "mean_ref_points": int(np.mean([len(p["ref"]) for p in pairs]))}
+        workload = ("C4: localization-only, %d-pt map cropped to +-15 m per reading, %d VLP-16 readings of "
+                    "N=%d, r=0.5" % (n_map, args.pairs, args.points))
+    else:
+        args.points = args.points or 60000
+        n_total = args.pairs or 1024
+        pairs = make_c5_pairs(n_total, args.points, rank, world)
+        args.pairs = len(pairs)
+        extra = {"pairs_total": n_total}
+        workload = "C5: %d independent KITTI-like pairs, N=M=%d, seeds 1000.., sharded i mod G" % (
+            n_total, args.points)
     order = os.environ.get("AICP_BENCH_READ_ORDER")  # experiment: host-side reading order
     if order:
         rng = np.random.default_rng(0)
@@ -131,8 +202,6 @@ def main():
     n_refs = len({id(p["ref"]) for p in pairs})
     ctx = L.Context(local_rank)
     batch = ctx.upload(pairs)
-    cfg = L.default_config()
-    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
 
     def gather():
         if dist is None:
@@ -180,7 +249,7 @@ def main():
     st = batch.stats_dicts()
 
     if rank == 0:
-        total_pairs = args.pairs * args.steps * world
+        total_pairs = (extra.get("pairs_total") or args.pairs * world) * args.steps
         value = total_pairs / elapsed
         avg_launch_ms = nn_ms / max(1, nn_launches)
         achieved = (nn_bytes / max(1, nn_launches)) / (avg_launch_ms * 1e-3) / 1e9 if nn_launches else 0.0
@@ -194,18 +263,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "c5" else "weak",
             "vs_baseline": None,
             "dtype": "f32 (point arithmetic; 6x6/3x3 reductions and solves in f64)",
             "data": "synthetic (seeded planar scene per SURVEY §8(d); no recordings in the reference)",
             "config": {
-                "workload": "C2: ANYmal VLP-16 batch_size=80 clouds, N=M=%d, frame-to-reference sequence of %d "
-                            "readings, reference updated every %d" % (args.points, args.pairs, args.ref_every),
+                "workload": workload,
                 "pairs_per_step_per_gpu": args.pairs,
                 "references_per_step_per_gpu": n_refs,
                 "chain": "icp_autotuned_default.yaml (SurfaceNormal knn20, KDTree knn1 eps3.16, "
                          "TrimmedDist auto-tuned, PointToPlane, Counter20 + Differential)",
-                "overlap": "octree-equivalent voxel sets at 0.2 m",
+                "overlap": "octree-equivalent voxel sets at 0.2 m" if flags & L.AICP_RUN_OVERLAP
+                           else "fixed 50 %% (r = %.2f)" % cfg.trimmed_ratio,
+                **extra,
                 "parallelism": "independent pairs sharded over ranks, RCCL all_gather of T",
             },
             "icp_iters_per_s": round(iters_total / elapsed, 1),
