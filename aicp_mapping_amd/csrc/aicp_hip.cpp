@@ -269,7 +269,8 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     }
     red += d.n_red_blk;
     wo += p.n_read;
-    if (ro >= (1ull << 31) || wo >= (1ull << 31)) FAIL(AICP_ERR_UNSUPPORTED, "batch too large");
+    // reference positions travel as 28-bit fields in the NN kernel's bucket exchange (Trav2C)
+    if (ro >= (1ull << 28) || wo >= (1ull << 31)) FAIL(AICP_ERR_UNSUPPORTED, "batch too large");
     if (p.init_T)
       std::memcpy(d.Tin, p.init_T, 64);
     else

@@ -358,6 +358,206 @@ struct Trav2 {
   }
 };
 
+// Trav2 with the bucket scan done by the wave cooperatively. The per-lane bucket loads of Trav2
+// put up to 64 distinct cache lines into each load instruction, and the TA/TCP processes
+// gathers at a rate set by distinct lines per instruction (profiles/r01_gather_bench.txt: 64
+// lines -> 4-27 instr/CU/us, 8-16 lines -> 40-140). Here lanes 8g..8g+7 (an "octet") load the
+// 8 points of one owner's bucket together -- one 128-byte run, 1-2 lines -- and compute their
+// distances to the owner's query; a min over the octet (DPP) and the lowest lane holding it
+// (ballot) give the owner the result of libnabo's in-order scan (first strictly smaller d^2
+// wins). Eight rounds serve the octet's eight owners, so one load instruction covers eight
+// buckets in <= 16 lines. The split into descend() / (wave-wide bucket) / climb() keeps the
+// visit order, counts and results of Trav2.
+struct Trav2C {
+  const uint4* nodes;
+  uint32_t pbase;  // the pair's first bucket point (bpts index)
+  float q0, q1, q2;
+  float off0, off1, off2, rd, minFar;
+  int32_t n, start, sp, pl;
+  uint32_t lb0, lcnt;  // bucket of the leaf the last descent ended in
+  uint32_t tp, tn;
+  Best<1> best;
+
+  __device__ __forceinline__ void bind(const uint4* nb, const float4*, uint32_t node_off, uint32_t ref_off) {
+    nodes = nb + 2 * (size_t)node_off;
+    pbase = ref_off;
+  }
+  __device__ __forceinline__ float res_d2() const { return best.v[0]; }
+  __device__ __forceinline__ int32_t res_id() const { return best.id[0]; }
+
+  __device__ __forceinline__ void reset(float a, float b, float c) {
+    q0 = a;
+    q1 = b;
+    q2 = c;
+    off0 = off1 = off2 = rd = 0.f;
+    n = start = sp = 0;
+    tp = tn = 0;
+    best_init<1>(best);
+  }
+
+  __device__ __forceinline__ void descend() {
+    minFar = __builtin_inff();
+    uint4 a = nodes[2 * n], b = nodes[2 * n + 1];
+    pl = (int32_t)a.z;
+    while ((a.y & 3u) != kLeaf) {
+      const uint32_t cd = a.y & 3u;
+      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(a.x);
+      const float oc = sel3(cd, off0, off1, off2);
+      minFar = fminf(minFar, rd + (-oc * oc + no * no));
+      ++tn;
+      const bool right = no > 0.f;
+      const int32_t c = right ? (int32_t)(a.y >> 2) : n + 1;
+      const uint32_t cx = right ? b.y : a.w, cy = right ? b.z : b.x;
+      pl = n;
+      n = c;
+      if ((cy & 3u) == kLeaf) {
+        a.x = cx;
+        a.y = cy;
+        break;
+      }
+      const uint32_t cd2 = cy & 3u;
+      const float no2 = sel3(cd2, q0, q1, q2) - __uint_as_float(cx);
+      const float oc2 = sel3(cd2, off0, off1, off2);
+      minFar = fminf(minFar, rd + (-oc2 * oc2 + no2 * no2));
+      ++tn;
+      n = (no2 > 0.f) ? (int32_t)(cy >> 2) : c + 1;
+      a = nodes[2 * n];
+      b = nodes[2 * n + 1];
+      pl = (int32_t)a.z;
+    }
+    lb0 = a.y >> 2;
+    lcnt = a.x;
+  }
+
+  // bucket points beyond the first kLeafBatch (bucket sizes above libnabo's default 8), in order
+  __device__ __forceinline__ void bucket_tail(const float4* __restrict__ pts, float maxR2) {
+    for (uint32_t i = kLeafBatch; i < lcnt; ++i) {
+      const float4 p = pts[pbase + lb0 + i];
+      const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
+      float dist = 0.f;
+      dist += d0 * d0;
+      dist += d1 * d1;
+      dist += d2 * d2;
+      if (dist <= maxR2 && dist < best.v[0]) best_replace<1>(best, (int32_t)(lb0 + i), dist);
+    }
+    tp += lcnt;
+  }
+
+  __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
+    int32_t c = n, pc = pl;
+    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+    for (;;) {
+      if (c == start) {
+        if (sp == 0) return true;
+        --sp;
+        const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
+        rd = fs.rd[sp];
+        const float old = fs.old[sp];
+        if (pcd == 0) off0 = old;
+        else if (pcd == 1) off1 = old;
+        else off2 = old;
+        minFar = fs.mn[sp];
+        start = fs.start[sp];
+        c = fs.P[sp];
+        pc = fs.PP[sp];
+        if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+        continue;
+      }
+      const int32_t p = pc;
+      const uint4 pn = nodes[2 * p];
+      const uint32_t cd = pn.y & 3u;
+      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(pn.x);
+      const float oc = sel3(cd, off0, off1, off2);
+      const float rdf = rd + (-oc * oc + no * no);
+      if (rdf <= maxR2 && rdf * maxE2 < best.v[0]) {
+        const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
+        fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
+        fs.rd[sp] = rd;
+        fs.old[sp] = oc;
+        fs.mn[sp] = minFar;
+        fs.start[sp] = start;
+        fs.P[sp] = p;
+        fs.PP[sp] = (int32_t)pn.z;
+        ++sp;
+        if (cd == 0) off0 = no;
+        else if (cd == 1) off1 = no;
+        else off2 = no;
+        rd = rdf;
+        n = far;
+        start = far;
+        return false;
+      }
+      c = p;
+      pc = (int32_t)pn.z;
+    }
+  }
+};
+
+template <class E>
+struct is_coop {
+  static constexpr bool value = false;
+};
+template <>
+struct is_coop<Trav2C> {
+  static constexpr bool value = true;
+};
+
+// DPP row controls (gfx9): quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
+
+__device__ __forceinline__ float octet_min(float v) {
+  v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kDppXor1, 0xF, 0xF, false)));
+  v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kDppXor2, 0xF, 0xF, false)));
+  v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kDppHalfMirror, 0xF, 0xF, false)));
+  return v;
+}
+
+// Wave-wide cooperative scan of the first kLeafBatch points of every active lane's bucket
+// (Trav2C). Called by all 64 lanes in wave-uniform control flow; `act` = the lane has a
+// bucket this round. xch = this wave's 64 exchange slots in LDS.
+__device__ __forceinline__ void coop_bucket(Trav2C& t, bool act, const float4* __restrict__ pts, float maxR2,
+                                            float4* xch) {
+  const int lane = threadIdx.x & 63;
+  const int oct = lane & ~7, i = lane & 7;
+  const uint32_t cnt = act ? min(t.lcnt, (uint32_t)kLeafBatch) : 0u;
+  xch[lane] = make_float4(t.q0, t.q1, t.q2, __uint_as_float(((t.pbase + t.lb0) << 4) | cnt));
+  __builtin_amdgcn_wave_barrier();
+  // only the owners' bucket words stay live across the loads; their queries are re-read from
+  // LDS when used (keeps the kernel at <= 64 VGPRs, 8 waves/SIMD)
+  float3 P[kLeafBatch];
+#pragma unroll
+  for (int j = 0; j < kLeafBatch; ++j) {
+    const uint32_t w = __float_as_uint(xch[oct + j].w);
+    if ((uint32_t)i < (w & 15u)) {
+      const float4 p = pts[(w >> 4) + i];
+      P[j] = make_float3(p.x, p.y, p.z);
+    }
+  }
+  float res_d = __builtin_inff();
+  uint32_t res_i = 0;
+#pragma unroll
+  for (int j = 0; j < kLeafBatch; ++j) {
+    float dist = __builtin_inff();
+    const float4 Q = xch[oct + j];
+    if ((uint32_t)i < (__float_as_uint(Q.w) & 15u)) {
+      const float d0 = Q.x - P[j].x, d1 = Q.y - P[j].y, d2 = Q.z - P[j].z;
+      float d = 0.f;
+      d += d0 * d0;
+      d += d1 * d1;
+      d += d2 * d2;
+      if (d <= maxR2) dist = d;
+    }
+    const float m = octet_min(dist);
+    const uint32_t hit = (uint32_t)(__ballot(dist == m) >> oct) & 0xFFu;
+    if (i == j) {
+      res_d = m;
+      res_i = (uint32_t)__builtin_ctz(hit | 0x100u);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // every lane's reads of xch precede the next round's writes
+  if (act && res_d < t.best.v[0]) best_replace<1>(t.best, (int32_t)(t.lb0 + res_i), res_d);
+}
+
 // 1-NN (the ICP matcher) as a one-load-per-step state machine: each iteration a lane issues
 // exactly one 16-byte load -- a node record or a bucket point, chosen per lane -- and then
 // advances its own phase (descent / bucket / climb), so lanes in different phases of their
@@ -549,9 +749,22 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       pool += min(avail, (uint32_t)__popcll(needm));
     }
     if (__ballot(has) == 0) break;
-    if (has && t.advance(fs, maxE2, maxR2, nodes, pts)) {
-      done(my, t);
-      has = false;
+    if constexpr (is_coop<Eng>::value) {
+      __shared__ float4 xch_all[kNNBlock];
+      if (has) t.descend();
+      coop_bucket(t, has, pts, maxR2, xch_all + (threadIdx.x & ~63));
+      if (has) {
+        t.bucket_tail(pts, maxR2);
+        if (t.climb(fs, maxE2, maxR2)) {
+          done(my, t);
+          has = false;
+        }
+      }
+    } else {
+      if (has && t.advance(fs, maxE2, maxR2, nodes, pts)) {
+        done(my, t);
+        has = false;
+      }
     }
   }
 }
@@ -788,7 +1001,8 @@ __device__ __forceinline__ void apply_cols(const float4& c0, const float4& c1, c
 // NN kernel: also stores the query's touch counts (inner nodes << 16 | bucket points, each
 // saturated at 65535) for the reduce kernel to sum per pair without atomics.
 template <class Eng>
-__global__ __launch_bounds__(256) void k_icp_nn(const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_icp_nn(
+                                                const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
                                                 const ActiveList* __restrict__ al,
                                                 const float4* __restrict__ read_c,
                                                 const uint4* __restrict__ nodes,
@@ -1384,14 +1598,14 @@ void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const Pa
                         uint32_t* ctr) {
   k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr);
 }
-// NN engine of the ICP matcher: 2 = Trav2 (default), 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
+// NN engine of the ICP matcher: 3 = Trav2C (default), 2 = Trav2, 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
 // (design experiments, tools/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:
 // Trav<1> 230 us per NN launch, SM0 436 us (profiles/README.md).
 static int nn_engine() {
   static int e = -1;
   if (e < 0) {
     const char* v = getenv("AICP_NN_ENGINE");
-    e = (v && v[0] == '0') ? 0 : (v && v[0] == '1') ? 1 : 2;
+    e = (v && v[0] >= '0' && v[0] <= '3') ? v[0] - '0' : 3;
   }
   return e;
 }
@@ -1401,7 +1615,9 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
                    const float4* bpts,
                    int32_t* match, float* d2, uint32_t* touched, uint32_t* ctr, const IcpParams& prm) {
   const int g = persistent_grid(grid_items);
-  if (nn_engine() == 2 && sup)
+  if (nn_engine() == 3 && sup)
+    k_icp_nn<Trav2C><<<g, 256, 0, s>>>(pd, st, al, read_c, sup, parent, bpts, match, d2, touched, ctr, prm);
+  else if (nn_engine() == 2 && sup)
     k_icp_nn<Trav2><<<g, 256, 0, s>>>(pd, st, al, read_c, sup, parent, bpts, match, d2, touched, ctr, prm);
   else if (nn_engine() >= 1)
     k_icp_nn<Trav<1>><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, match, d2, touched, ctr, prm);
