@@ -136,6 +136,7 @@ struct SubSeg {
 struct TreeCtl {
   uint32_t nseg[kFarStack + 2];  // segments per global level
   uint32_t n_small;              // SubSeg entries
+  uint32_t n_big;                // of which above kSubMax points (planned build too shallow)
   int32_t error;
 };
 

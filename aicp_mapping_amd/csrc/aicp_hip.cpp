@@ -88,7 +88,9 @@ struct TreeBufs {
   DevBuf W0, W1, segof0, segof1, seg0, seg1, flag, X1, X2, posL, posR, ev, valid, subs, ecnt, sums, pdepth, ctl,
       scan;
   PinBuf pin_ctl;
-  TreeWork tw{};  // device_trees_begin -> device_trees_end
+  TreeWork tw{};    // device_trees_begin -> device_trees_end
+  int planned = 0;  // global levels enqueued without host polling (0: polled build)
+  int needed = 0;   // global levels the last planned build actually used
   void release_all() {
     for (DevBuf* b : {&W0, &W1, &segof0, &segof1, &seg0, &seg1, &flag, &X1, &X2, &posL, &posR, &ev, &valid, &subs,
                       &ecnt, &sums, &pdepth, &ctl, &scan})
@@ -399,18 +401,31 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
   return AICP_OK;
 }
 
-// global levels (host polls), wave subtrees, node records; see device_trees_begin
+// Global levels, wave subtrees, node records; see device_trees_begin. plan > 0: enqueue
+// `plan` global levels without any host read-back (the whole build is asynchronous) plus an
+// async copy of the control block, checked after the batch by device_trees_check; plan = 0:
+// the host polls the next level's segment count from level 4 on (fallback when a planned
+// build turned out too shallow).
 int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out) {
+                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan) {
   const size_t n = (size_t)total;
   const TreeWork& w = T.tw;
   float4* bpts = bpts_out.as<float4>();
   TreeCtl* hctl = T.pin_ctl.as<TreeCtl>();
-  // global levels until every remaining segment fits one wave's LDS (kSubMax points); the
-  // host polls the next level's segment count from level 4 on
+  T.planned = 0;
+  if (plan > 0) {
+    plan = std::min(plan, kFarStack - 2);
+    for (int level = 0; level < plan; ++level)
+      TCHK(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket, level == plan - 1));
+    TCHK(launch_tree_subtrees(s, (uint32_t)n, w, bpts, bucket));
+    TCHK(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
+    TCHK(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
+    T.planned = plan;
+    return AICP_OK;
+  }
   bool done = false;
   for (int level = 0; level < kFarStack - 1 && !done; ++level) {
-    TCHK(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket));
+    TCHK(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket, false));
     if (level >= 4 || level == kFarStack - 2) {
       TCHK(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
       TCHK(hipStreamSynchronize(s));
@@ -418,7 +433,7 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
     }
   }
   if (!done) TFAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
-  TCHK(launch_tree_subtrees(s, (uint32_t)n, hctl->n_small, w, bpts, bucket));
+  TCHK(launch_tree_subtrees(s, (uint32_t)n, w, bpts, bucket));
   TCHK(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
   TCHK(hipMemcpyAsync(&hctl->error, &w.ctl->error, 4, hipMemcpyDeviceToHost, s));
   TCHK(hipStreamSynchronize(s));
@@ -427,9 +442,39 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
   return AICP_OK;
 }
 
+// After the stream of a planned build has completed: its errors (the control block was copied
+// back asynchronously at the end of the build). Segments left above kSubMax points at the last
+// planned level were finished by the subtree kernel's global path, so the tree is complete.
+int device_trees_check(TreeBufs& T, std::string& err) {
+  if (!T.planned) return AICP_OK;
+  const TreeCtl* hctl = T.pin_ctl.as<TreeCtl>();
+  int used = 0;
+  while (used < kFarStack + 1 && hctl->nseg[used]) ++used;
+  // oversized segments at the last planned level: plan deeper next time
+  T.needed = hctl->n_big ? std::min(kFarStack - 3, T.planned + 2) : used;
+  if (hctl->error & 1) TFAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
+  if (hctl->error) TFAIL(AICP_ERR_HIP, "kd-tree construction overflow " + std::to_string(hctl->error));
+  return AICP_OK;
+}
+
+// Global levels to enqueue for clouds of at most n_max points: segments above kSubMax points
+// halve per level on balanced data; sliding-midpoint splits can peel off small slices, so the
+// plan keeps a margin and never goes below what the previous build of this tree needed.
+// AICP_TREE_PLAN=k forces k levels (tests: a too-shallow plan); AICP_TREE_PLAN=0 selects the
+// host-polled build (A/B measurements).
+int plan_levels(uint64_t n_max, const TreeBufs& T) {
+  if (const char* e = std::getenv("AICP_TREE_PLAN")) {
+    const int v = std::atoi(e);
+    return v > 0 ? std::min(kFarStack - 2, v) : 0;
+  }
+  int l = 0;
+  while (((uint64_t)kSubMax << l) < n_max) ++l;
+  return std::min(kFarStack - 2, std::max(l + 4, T.needed + 1));
+}
+
 // the centred reference's matcher tree and the pairs' frames, on stream3 (worker thread)
 int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dDesc, PairDesc* dRdesc,
-                  std::string& err) {
+                  int plan, std::string& err) {
   hipStream_t s3 = ctx->stream3;
   const size_t R = B->rdesc.size();
   TCHK(hipSetDevice(ctx->device));  // the current device is per host thread
@@ -439,7 +484,7 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
   int rc = device_trees_begin(ctx->tb[1], err, s3, R, B->total_ref, dRdesc, B->ref_raw.as<float4>(), 1, bucket,
                               ctx->bpts, ctx->nodes);
   if (rc) return rc;
-  rc = device_trees_end(ctx->tb[1], err, s3, R, B->total_ref, dRdesc, bucket, ctx->bpts, ctx->nodes);
+  rc = device_trees_end(ctx->tb[1], err, s3, R, B->total_ref, dRdesc, bucket, ctx->bpts, ctx->nodes, plan);
   if (rc) return rc;
   // two-level node records for the matcher (Trav2)
   const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);
@@ -584,14 +629,32 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(hipEventRecord(ctx->ev[8], s2));
     HIPC(hipMemcpyAsync(ctx->rdesc_raw.p, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s2));
     launch_init_state(s2, (int)R, ctx->rdesc_raw.as<PairDesc>(), dRstate);
-    // s3 (worker thread, it polls its own tree levels): centroid, centred reference, matcher
-    // tree, pair frames
-    worker = std::thread([&] { wrc = matcher_trees(ctx, B, cfg->bucket_size, dDesc, dRdesc, werr); });
+    uint64_t n_ref_max = 0;
+    for (const PairDesc& r : B->rdesc) n_ref_max = std::max<uint64_t>(n_ref_max, r.n_ref);
+    // s3 (worker thread; it still polls its levels in a polled redo): centroid, centred
+    // reference, matcher tree, pair frames
+    const int plan1 = plan_levels(n_ref_max, ctx->tb[1]);
+    worker = std::thread([&, plan1] { wrc = matcher_trees(ctx, B, cfg->bucket_size, dDesc, dRdesc, plan1, werr); });
     // SurfaceNormal runs on the reference as given, before the centring (ICP::compute,
     // SURVEY A.1 steps 1-2): its own libnabo tree over the raw coordinates first
     rc = device_trees_begin(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(),
                             B->ref_raw.as<float4>(), 0, cfg->bucket_size, ctx->bpts_raw, ctx->nodes_raw);
     if (rc) return join_worker(rc);
+    // s2: raw tree levels + subtrees, SurfaceNormal, all enqueued before the host waits for
+    // the overlap's key boxes
+    rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), cfg->bucket_size,
+                          ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0]));
+    if (rc) return join_worker(rc);
+    // normals on the raw tree (bucket order of that tree)
+    HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
+    HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
+    uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
+    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
+    if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, ctx->rdesc_raw.as<PairDesc>(), dRstate,
+                        ctx->nodes_raw.as<uint4>(), nullptr, ctx->bpts_raw.as<float4>(), ctx->nrm_raw.as<float4>(),
+                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
+      FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
+    HIPC(hipEventRecord(ctx->ev[10], s2));
   }
   // overlap: size the voxel maps from the key boxes, then mark
   uint64_t bm_bytes = 0;
@@ -637,20 +700,6 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   IcpParams prm{};
   int nn_launches = 0;
   if (doIcp) {
-    // s2: raw tree levels + subtrees, SurfaceNormal
-    rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), cfg->bucket_size,
-                          ctx->bpts_raw, ctx->nodes_raw);
-    if (rc) return join_worker(rc);
-    // normals on the raw tree (bucket order of that tree)
-    HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
-    HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
-    uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
-    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
-    if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, ctx->rdesc_raw.as<PairDesc>(), dRstate,
-                        ctx->nodes_raw.as<uint4>(), nullptr, ctx->bpts_raw.as<float4>(), ctx->nrm_raw.as<float4>(),
-                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
-      FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
-    HIPC(hipEventRecord(ctx->ev[10], s2));
     // the matcher tree (s3) must be complete, and the worker done with ctx->bpts / nodes
     rc = join_worker(AICP_OK);
     if (rc) return rc;
@@ -718,6 +767,11 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   if (doIcp) HIPC(hipMemcpyAsync(ctx->pin_out.p, ctx->outT.p, P * 64, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(pdC, dDesc, P * sizeof(PairDesc), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  if (doIcp) {  // planned tree builds: errors recorded on the device
+    rc = device_trees_check(ctx->tb[0], ctx->err);
+    if (!rc) rc = device_trees_check(ctx->tb[1], ctx->err);
+    if (rc) return rc;
+  }
   // results
   const PairState* hs = ctx->pin_state.as<PairState>();
   int first_err = AICP_OK;
@@ -792,7 +846,7 @@ int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, Pa
   int rc = device_trees_begin(ctx->tb[0], ctx->err, s, 1, n, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8,
                               ctx->bpts, ctx->nodes);
   if (rc) return rc;
-  rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, n, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes);
+  rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, n, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes, 0);
   if (rc) return rc;
   HIPC(hipMemcpyAsync(&d, ctx->desc.p, sizeof(d), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));

@@ -87,10 +87,12 @@ void launch_super_nodes(hipStream_t s, int n_refs, uint32_t cap, const PairDesc*
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
                                int center, const TreeWork& w, float4* bpts, int bucket);
 // one level: nodes at depth `level` are split (their children get depth level + 1)
+// last: the final planned level -- children above kSubMax points also go to the subtree
+// kernel (its global-memory path) instead of a next level
 hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const TreeWork& w, float4* bpts,
-                             int bucket);
-// subtrees of the segments with <= kSubMax points, one wave each (n_small read back by the host)
-hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, uint32_t n_small, const TreeWork& w, float4* bpts,
+                             int bucket, bool last);
+// subtrees of the segments with <= kSubMax points, one wave each (grid-stride over the device count)
+hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts,
                                 int bucket);
 // node records (preorder) and PairDesc node_off / n_nodes / tree_depth
 hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const TreeWork& w,

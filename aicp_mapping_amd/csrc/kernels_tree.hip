@@ -70,15 +70,47 @@ __device__ __forceinline__ bool wave_seg_minmax(int key, float& mn, float& mx) {
   return lane == 63 || kn != key;
 }
 
+// Whole-wave reductions (all 64 lanes active) on DPP row operations: quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror reduce each 16-lane row in registers; the four row results are
+// combined from scalar readlanes. No LDS round trips (the ds_bpermute shuffles they replace
+// cost ~6 dependent LDS-latency steps per reduction).
+template <class T, class Op>
+__device__ __forceinline__ T wave_reduce_dpp(T v, Op op) {
+  static_assert(sizeof(T) == 4, "32-bit values");
+  auto dpp = [](T x, int ctl) -> T {
+    int i;
+    __builtin_memcpy(&i, &x, 4);
+    int r;
+    switch (ctl) {
+      case 0: r = __builtin_amdgcn_mov_dpp(i, 0xB1, 0xF, 0xF, false); break;
+      case 1: r = __builtin_amdgcn_mov_dpp(i, 0x4E, 0xF, 0xF, false); break;
+      case 2: r = __builtin_amdgcn_mov_dpp(i, 0x141, 0xF, 0xF, false); break;
+      default: r = __builtin_amdgcn_mov_dpp(i, 0x140, 0xF, 0xF, false); break;
+    }
+    T y;
+    __builtin_memcpy(&y, &r, 4);
+    return y;
+  };
+  v = op(v, dpp(v, 0));
+  v = op(v, dpp(v, 1));
+  v = op(v, dpp(v, 2));
+  v = op(v, dpp(v, 3));
+  int i;
+  __builtin_memcpy(&i, &v, 4);
+  const int a = __builtin_amdgcn_readlane(i, 0), b = __builtin_amdgcn_readlane(i, 16),
+            c = __builtin_amdgcn_readlane(i, 32), d = __builtin_amdgcn_readlane(i, 48);
+  T ta, tb, tc, td;
+  __builtin_memcpy(&ta, &a, 4);
+  __builtin_memcpy(&tb, &b, 4);
+  __builtin_memcpy(&tc, &c, 4);
+  __builtin_memcpy(&td, &d, 4);
+  return op(op(ta, tb), op(tc, td));
+}
 __device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce_dpp(v, [](float a, float b) { return fminf(a, b); });
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce_dpp(v, [](float a, float b) { return fmaxf(a, b); });
 }
 
 // Block-wide min/max of (mn, mx) for a block whose valid threads share one key; the result
@@ -461,7 +493,7 @@ __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t*
 
 // split: left-count rule, node event of this segment, children: leaf events, wave-subtree
 // segments (count <= kSubMax) or next-level segments
-__global__ __launch_bounds__(256) void k_tr_split(int level, uint32_t total, TreeSeg* seg, TreeSeg* next,
+__global__ __launch_bounds__(256) void k_tr_split(int level, int last, uint32_t total, TreeSeg* seg, TreeSeg* next,
                                                   SubSeg* subs, TreeCtl* ctl, const uint32_t* __restrict__ X2,
                                                   NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
                                                   int32_t* pair_depth, int bucket, uint32_t max_seg) {
@@ -508,7 +540,8 @@ __global__ __launch_bounds__(256) void k_tr_split(int level, uint32_t total, Tre
       g.child[side] = -1;
       continue;
     }
-    if (cc <= (uint32_t)kSubMax) {
+    if (cc <= (uint32_t)kSubMax || last) {  // last planned level: oversized ones too (global path)
+      if (cc > (uint32_t)kSubMax) atomicAdd(&ctl->n_big, 1u);
       const uint32_t ni = atomicAdd(&ctl->n_small, 1u);
       if (ni >= max_seg) {
         atomicOr(&ctl->error, 4);
@@ -602,14 +635,12 @@ __device__ __forceinline__ uint32_t popc_lt(uint64_t m) {
 }
 
 __device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce_dpp(v, [](uint32_t a, uint32_t b) { return a + b; });
 }
 
 // one Hoare pass over local [lo_b, end) with boundary br: elements with pred in [lo_b, br)
-template <class Pred>
-__device__ __forceinline__ void wave_hoare(float4* pts, uint16_t* posA, uint16_t* posB, uint32_t lo_b, uint32_t br,
+template <class PosT, class Pred>
+__device__ __forceinline__ void wave_hoare(float4* pts, PosT* posA, PosT* posB, uint32_t lo_b, uint32_t br,
                                            uint32_t end, Pred pred) {
   const int lane = threadIdx.x & 63;
   uint32_t ra = 0, rb = 0;
@@ -619,8 +650,8 @@ __device__ __forceinline__ void wave_hoare(float4* pts, uint16_t* posA, uint16_t
     const bool pr = ok && pred(pts[j]);
     const bool ml = ok && j < br && !pr, mr = ok && j >= br && pr;
     const uint64_t ma = __ballot(ml), mb = __ballot(mr);
-    if (ml) posA[ra + popc_lt(ma)] = (uint16_t)j;
-    if (mr) posB[rb + popc_lt(mb)] = (uint16_t)j;
+    if (ml) posA[ra + popc_lt(ma)] = (PosT)j;
+    if (mr) posB[rb + popc_lt(mb)] = (PosT)j;
     ra += (uint32_t)__popcll(ma);
     rb += (uint32_t)__popcll(mb);
   }
@@ -635,19 +666,14 @@ __device__ __forceinline__ void wave_hoare(float4* pts, uint16_t* posA, uint16_t
   __syncthreads();
 }
 
-__global__ __launch_bounds__(64) void k_tr_subtree(uint32_t total, const TreeCtl* __restrict__ ctl,
-                                                   const SubSeg* __restrict__ subs, const float4* __restrict__ W,
-                                                   float4* __restrict__ bpts, NodeEvent* ev, uint8_t* valid,
-                                                   uint32_t* ecnt, int32_t* pair_depth, int bucket) {
-  __shared__ float4 pts[kSubMax];
-  __shared__ uint16_t posA[kSubMax / 2], posB[kSubMax / 2];
-  __shared__ SubNode stk[kFarStack];
-  if (blockIdx.x >= ctl->n_small) return;
-  const SubSeg g = subs[blockIdx.x];
+// One segment's whole subtree, depth first, by one wave. pts = the segment's points (LDS copy,
+// or the segment's range of bpts in place for an oversized segment), posA / posB = partition
+// scratch of the segment's size (LDS, or the free per-level position arrays).
+template <class PosT>
+__device__ void subtree_build(const SubSeg& g, uint32_t total, float4* pts, PosT* posA, PosT* posB, SubNode* stk,
+                              NodeEvent* ev, uint8_t* valid, uint32_t* ecnt, int32_t* pair_depth, int bucket) {
   const int lane = threadIdx.x;
   const uint32_t gf = g.f;
-  for (uint32_t j = lane; j < g.c; j += 64) pts[j] = W[gf + j];
-  __syncthreads();
   SubNode nd;
   nd.lf = 0;
   nd.lc = g.c;
@@ -732,8 +758,38 @@ __global__ __launch_bounds__(64) void k_tr_subtree(uint32_t total, const TreeCtl
     nd = L;
   }
   __syncthreads();
-  for (uint32_t j = lane; j < g.c; j += 64) bpts[gf + j] = pts[j];
   if (lane == 0 && pair_depth[g.pair] < maxd) atomicMax(&pair_depth[g.pair], maxd);
+}
+
+// Grid-stride over the small segments (the grid does not depend on their count, which only
+// the device knows). A segment above kSubMax points -- left over when the planned number of
+// global levels was too small for the data -- is finished in place in global memory with the
+// same routine: slower, same tree.
+__global__ __launch_bounds__(64) void k_tr_subtree(uint32_t total, const TreeCtl* __restrict__ ctl,
+                                                   const SubSeg* __restrict__ subs, const float4* __restrict__ W,
+                                                   float4* __restrict__ bpts, uint32_t* __restrict__ posL,
+                                                   uint32_t* __restrict__ posR, NodeEvent* ev, uint8_t* valid,
+                                                   uint32_t* ecnt, int32_t* pair_depth, int bucket) {
+  __shared__ float4 pts[kSubMax];
+  __shared__ uint16_t posA[kSubMax / 2], posB[kSubMax / 2];
+  __shared__ SubNode stk[kFarStack];
+  const uint32_t n_small = ctl->n_small;
+  const int lane = threadIdx.x;
+  for (uint32_t si = blockIdx.x; si < n_small; si += gridDim.x) {
+    __syncthreads();  // the previous segment's last LDS reads precede this one's loads
+    const SubSeg g = subs[si];
+    const uint32_t gf = g.f;
+    if (g.c <= (uint32_t)kSubMax) {
+      for (uint32_t j = lane; j < g.c; j += 64) pts[j] = W[gf + j];
+      __syncthreads();
+      subtree_build<uint16_t>(g, total, pts, posA, posB, stk, ev, valid, ecnt, pair_depth, bucket);
+      for (uint32_t j = lane; j < g.c; j += 64) bpts[gf + j] = pts[j];
+    } else {
+      for (uint32_t j = lane; j < g.c; j += 64) bpts[gf + j] = W[gf + j];
+      __syncthreads();
+      subtree_build<uint32_t>(g, total, bpts + gf, posL + gf, posR + gf, stk, ev, valid, ecnt, pair_depth, bucket);
+    }
+  }
 }
 
 // ---- node records --------------------------------------------------------------------------
@@ -894,7 +950,7 @@ hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairD
 }
 
 hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const TreeWork& w, float4* bpts,
-                             int bucket) {
+                             int bucket, bool last) {
   const int a = level & 1, b = a ^ 1;
   TreeSeg* seg = w.seg[a];
   TreeSeg* next = w.seg[b];
@@ -909,17 +965,20 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR, w.W[1], w.flag);
   e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X2, (size_t)total + 1);
   if (e != hipSuccess) return e;
-  k_tr_split<<<gs, 256, 0, s>>>(level, total, seg, next, w.subs, w.ctl, w.X2, w.ev, w.valid, w.ecnt, w.pair_depth,
+  k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.ctl, w.X2, w.ev, w.valid, w.ecnt, w.pair_depth,
                                 bucket, (uint32_t)w.max_seg);
   k_tr_pos<<<gp, 256, 0, s>>>(total, 2, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR);
   k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR, w.W[0], w.segof[b], bpts);
   return hipGetLastError();
 }
 
-hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, uint32_t n_small, const TreeWork& w, float4* bpts,
-                                int bucket) {
-  if (n_small) k_tr_subtree<<<n_small, 64, 0, s>>>(total, w.ctl, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt,
-                                                   w.pair_depth, bucket);
+// grid: an upper bound of the small-segment count (<= total / (bucket + 1) + pairs), capped;
+// the kernel strides over the device-side count
+hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts, int bucket) {
+  const size_t bound = std::min<size_t>(w.max_seg, (size_t)total / (size_t)(bucket + 1) + (size_t)w.n_pairs + 1);
+  const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, 16384));
+  k_tr_subtree<<<g, 64, 0, s>>>(total, w.ctl, w.subs, w.W[0], bpts, w.posL, w.posR, w.ev, w.valid, w.ecnt,
+                                w.pair_depth, bucket);
   return hipGetLastError();
 }
 

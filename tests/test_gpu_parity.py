@@ -268,6 +268,26 @@ def test_batch_deterministic_and_order_independent(ctx, L):
     np.testing.assert_array_equal(Ta[1], Tc[0])
 
 
+@pytest.mark.parametrize("plan", ["1", "2", "0"])
+def test_planned_tree_build(ctx, L, monkeypatch, plan):
+    """The kd-trees are built with a planned number of global levels and no host read-back.
+    A plan too shallow for the data (1 or 2 levels here) leaves segments above the wave-LDS
+    size, which the subtree kernel finishes in global memory; "0" is the host-polled build.
+    Every variant must give the default build's transforms, depths and touch counts."""
+    prs = [sy.make_pair(30000, 30000, seed=70 + i) for i in range(2)]
+    pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
+    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+    Ta, sa, rca = ctx.align_batch(pairs, flags=flags, resolution=RES)
+    monkeypatch.setenv("AICP_TREE_PLAN", plan)
+    Tb, sb, rcb = ctx.align_batch(pairs, flags=flags, resolution=RES)
+    monkeypatch.delenv("AICP_TREE_PLAN")
+    assert rca == rcb == 0
+    np.testing.assert_array_equal(Ta, Tb)
+    for a, b in zip(sa, sb):
+        assert (a["iterations"], a["tree_depth"], a["nn_points_touched"], a["nn_nodes_touched"]) == \
+               (b["iterations"], b["tree_depth"], b["nn_points_touched"], b["nn_nodes_touched"])
+
+
 def test_resident_batch_full_size_round_trip(ctx, L):
     """C2 size (N = M = 120k): properties at full size (recovers T_gt, repeatable)."""
     prs = [sy.make_pair(120000, 120000, seed=100 + i) for i in range(2)]
