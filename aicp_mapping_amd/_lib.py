@@ -27,7 +27,7 @@ EXPORTS = [
     "aicp_hip_create", "aicp_hip_destroy", "aicp_hip_last_error", "aicp_hip_version",
     "aicp_hip_default_config", "aicp_hip_parse_pm_yaml", "aicp_hip_replace_ratio_config_file",
     "aicp_hip_autotune_ratio", "aicp_hip_register", "aicp_hip_register_batch",
-    "aicp_hip_overlap", "aicp_hip_overlap_batch", "aicp_hip_align_batch", "aicp_hip_transform",
+    "aicp_hip_overlap", "aicp_hip_overlap_batch", "aicp_hip_align_batch", "aicp_hip_transform", "aicp_hip_crop_box",
     "aicp_hip_batch_upload", "aicp_hip_batch_run", "aicp_hip_batch_free",
     "aicp_hip_last_nn_timing", "aicp_hip_last_phase_ms", "aicp_hip_knn", "aicp_hip_normals",
     "aicp_hip_dists_quantile", "aicp_hip_solve6",
@@ -120,6 +120,7 @@ def _load():
     L.aicp_hip_overlap_batch.argtypes = [vp, pp, sz, C.c_double, fp, stp]
     L.aicp_hip_align_batch.argtypes = [vp, cfgp, pp, sz, C.c_double, C.c_int, fp, stp]
     L.aicp_hip_transform.argtypes = [vp, fp, fp, sz, sz, fp]
+    L.aicp_hip_crop_box.argtypes = [vp, fp, sz, sz, C.c_float, C.c_float, fp, fp, C.POINTER(C.c_size_t), fp]
     L.aicp_hip_batch_upload.argtypes = [vp, pp, sz, C.POINTER(vp)]
     L.aicp_hip_batch_run.argtypes = [vp, vp, cfgp, C.c_double, C.c_int, fp, stp]
     L.aicp_hip_batch_free.argtypes = [vp, vp]
@@ -315,6 +316,19 @@ class Context:
         rc = lib.aicp_hip_transform(self.h, _fptr(t), _fptr(pts), pts.shape[0], pts.shape[1] * 4, _fptr(out))
         self.check(rc)
         return out
+
+    def crop_box(self, pts, mn, mx, origin):
+        """getPointsInOrientedBox (filteringUtils.cpp:619-637) on device: returns (kept xyz in
+        input order, box angles rx, ry, rz). origin is a 4x4 row-major pose (Matrix4f values)."""
+        pts = as_points(pts)
+        o = np.ascontiguousarray(np.asarray(origin, np.float32).reshape(4, 4).T.reshape(16))
+        out = np.zeros((pts.shape[0], 3), np.float32)
+        m = C.c_size_t(0)
+        rpy = np.zeros(3, np.float32)
+        rc = lib.aicp_hip_crop_box(self.h, _fptr(pts), pts.shape[0], pts.shape[1] * 4, mn, mx, _fptr(o),
+                                   _fptr(out), C.byref(m), _fptr(rpy))
+        self.check(rc)
+        return out[:m.value].copy(), rpy
 
 
 class ResidentBatch:

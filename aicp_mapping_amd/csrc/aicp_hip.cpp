@@ -995,6 +995,93 @@ int aicp_hip_transform(aicp_hip_ctx* ctx, const float T[16], const float* in, si
   return AICP_OK;
 }
 
+// Box frame of getPointsInOrientedBox (filteringUtils.cpp:619-637): Eigen eulerAngles(0,1,2)
+// of origin.R, pcl::getTransformation(0,0,0,rx,ry,rz) = Rz Ry Rx, Affine3f::inverse() by
+// cofactors, and CropBox's fuzzy isIdentity() skip. Scalar float setup on the host; the
+// per-point test runs in k_crop_count / k_crop_scatter.
+static void crop_box_frame(const float origin[16], float inv[9], float t[3], float rpy[3]) {
+  auto R = [&](int r, int c) { return origin[c * 4 + r]; };
+  float a0 = std::atan2(R(1, 2), R(2, 2)), a1;
+  const float c2 = std::sqrt(R(0, 0) * R(0, 0) + R(0, 1) * R(0, 1));
+  if (a0 > 0.f) {
+    a0 -= float(M_PI);
+    a1 = std::atan2(-R(0, 2), -c2);
+  } else {
+    a1 = std::atan2(-R(0, 2), c2);
+  }
+  const float s1 = std::sin(a0), c1 = std::cos(a0);
+  const float a2 = std::atan2(s1 * R(2, 0) - c1 * R(1, 0), c1 * R(1, 1) - s1 * R(2, 1));
+  rpy[0] = -a0;
+  rpy[1] = -a1;
+  rpy[2] = -a2;
+  for (int q = 0; q < 3; ++q) t[q] = origin[12 + q];
+  for (int q = 0; q < 9; ++q) inv[q] = (q % 4 == 0) ? 1.f : 0.f;
+  if (rpy[0] == 0.f && rpy[1] == 0.f && rpy[2] == 0.f) return;
+  const float A = std::cos(rpy[2]), B = std::sin(rpy[2]), C = std::cos(rpy[1]), D = std::sin(rpy[1]),
+              E = std::cos(rpy[0]), F = std::sin(rpy[0]);
+  const float DE = D * E, DF = D * F;
+  const float m[3][3] = {{A * C, A * DF - B * E, B * F + A * DE}, {B * C, A * E + B * DF, B * DE - A * F},
+                         {-D, C * F, C * E}};
+  const float k00 = m[1][1] * m[2][2] - m[1][2] * m[2][1], k10 = m[1][2] * m[2][0] - m[1][0] * m[2][2],
+              k20 = m[1][0] * m[2][1] - m[1][1] * m[2][0];
+  const float id = 1.f / (m[0][0] * k00 + m[0][1] * k10 + m[0][2] * k20);
+  const float w[9] = {k00 * id,
+                      (m[0][2] * m[2][1] - m[0][1] * m[2][2]) * id,
+                      (m[0][1] * m[1][2] - m[0][2] * m[1][1]) * id,
+                      k10 * id,
+                      (m[0][0] * m[2][2] - m[0][2] * m[2][0]) * id,
+                      (m[0][2] * m[1][0] - m[0][0] * m[1][2]) * id,
+                      k20 * id,
+                      (m[0][1] * m[2][0] - m[0][0] * m[2][1]) * id,
+                      (m[0][0] * m[1][1] - m[0][1] * m[1][0]) * id};
+  bool ident = true;
+  for (int q = 0; q < 9; ++q)
+    ident = ident && (q % 4 == 0 ? std::fabs(w[q] - 1.f) <= 1e-5f * std::fmin(std::fabs(w[q]), 1.f)
+                                 : std::fabs(w[q]) <= 1e-5f);
+  if (!ident)
+    for (int q = 0; q < 9; ++q) inv[q] = w[q];
+}
+
+int aicp_hip_crop_box(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, float mn, float mx,
+                      const float origin[16], float* out, size_t* out_n, float* rpy_out) {
+  if (!ctx || !pts || !origin || !out || !out_n || stride < 12) return AICP_ERR_INVALID;
+  if (n > (size_t)INT32_MAX) return AICP_ERR_INVALID;
+  float inv[9], t[3], rpy[3];
+  crop_box_frame(origin, inv, t, rpy);
+  if (rpy_out)
+    for (int q = 0; q < 3; ++q) rpy_out[q] = rpy[q];
+  *out_n = 0;
+  if (n == 0) return AICP_OK;
+  HIPC(hipSetDevice(ctx->device));
+  const size_t tiles = aicp::crop_tiles(n);
+  const size_t tile_bytes = (2 * tiles * 4 + 255) & ~size_t(255);
+  HIPC(ensure(ctx->scratch, 256 + tile_bytes + 2 * n * 16));
+  HIPC(ensure(ctx->pin_io, n * 16 + 16));
+  float* h = ctx->pin_io.as<float>();
+  pack_xyz4(pts, n, stride, h);
+  char* d = ctx->scratch.as<char>();
+  uint32_t* total = (uint32_t*)d;
+  uint32_t* tcnt = (uint32_t*)(d + 256);
+  uint32_t* toff = tcnt + tiles;
+  float4* din = (float4*)(d + 256 + tile_bytes);
+  float4* dout = din + n;
+  HIPC(hipMemcpyAsync(din, h, n * 16, hipMemcpyHostToDevice, ctx->stream));
+  aicp::launch_crop_box(ctx->stream, (int)n, inv, t, mn, mx, din, tcnt, toff, total, dout);
+  HIPC(hipGetLastError());
+  uint32_t m = 0;
+  HIPC(hipMemcpyAsync(&m, total, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  if (m > n) {
+    ctx->err = "crop: kept count exceeds the input";
+    return AICP_ERR_HIP;
+  }
+  if (m) HIPC(hipMemcpy(h, dout, (size_t)m * 16, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < m; ++i)
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
+  *out_n = m;
+  return AICP_OK;
+}
+
 int aicp_hip_last_nn_timing(const aicp_hip_ctx* ctx, int* n_launches, double* total_ms, double* bytes,
                             uint64_t* queries) {
   if (!ctx) return AICP_ERR_INVALID;

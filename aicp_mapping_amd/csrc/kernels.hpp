@@ -56,6 +56,11 @@ bool launch_knn_generic(hipStream_t s, uint32_t nq, const float4* q, const uint4
                         float maxR2, int32_t* ids, float* d2, unsigned long long* touched,
                         uint32_t* ctr);
 void launch_transform(hipStream_t s, int n, const float* T, const float4* in, float4* out);
+// kernels_crop.hip: order-preserving oriented box crop (getPointsInOrientedBox).
+size_t crop_tiles(size_t n);
+void launch_crop_box(hipStream_t s, int n, const float inv[9], const float t[3], float mn, float mx,
+                     const float4* pts, uint32_t* tile_cnt, uint32_t* tile_off, uint32_t* total,
+                     float4* out);
 void launch_solve6(hipStream_t s, const double* A, const double* b, double* x, int32_t* path);
 
 // ---- kd-tree construction (kernels_tree.hip) ---------------------------------------------

@@ -130,6 +130,15 @@ int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg,
 int aicp_hip_transform(aicp_hip_ctx* ctx, const float T[16], const float* in, size_t n,
                        size_t stride, float* out /* packed xyz, 3*n */);
 
+/* Localization-only map crop, getPointsInOrientedBox (aicp_core/src/utils/filteringUtils.cpp:619-637,
+ * called at app.cpp:41-51): pcl::CropBox with the cube [min, max]^3, rotation =
+ * origin.R.eulerAngles(0,1,2) and translation = origin.t (origin: Matrix4f, col-major). Kept
+ * points are written packed xyz in input order to out (capacity n points); *out_n = count.
+ * Non-finite points are dropped. rpy_out (nullable) receives the box angles. */
+int aicp_hip_crop_box(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, float min,
+                      float max, const float origin[16], float* out /* 3*n */, size_t* out_n,
+                      float* rpy_out /* 3, nullable */);
+
 /* ---- device-resident batches (inputs uploaded once, run many times) ----------------------- */
 int aicp_hip_batch_upload(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs,
                           aicp_hip_batch** out);

@@ -1264,3 +1264,95 @@ float ao_autotune_ratio(float overlap_percent) {
 }
 
 }  // extern "C"
+
+/* ---------------------------------------------------------------- box crop --
+ * getPointsInOrientedBox, filteringUtils.cpp:619-637, through its [ext] dependencies:
+ *  - Eigen 3.3 MatrixBase::eulerAngles(0,1,2) (Geometry/EulerAngles.h): angles (a,b,c) with
+ *    R = Rx(a) Ry(b) Rz(c), a in [0, pi];
+ *  - pcl::CropBox<PointXYZ>::applyFilter (filters/impl/crop_box.hpp, PCL 1.8): translation
+ *    subtracted first, then the inverse of pcl::getTransformation(0,0,0, rx,ry,rz)
+ *    (= Rz(rz) Ry(ry) Rx(rx), note the reversed order against eulerAngles) applied with
+ *    pcl::transformPoint; kept iff min <= local <= max on every axis; non-finite points dropped.
+ * Float throughout, like PointXYZ and Affine3f. Parity unpinned against PCL/Eigen (neither is
+ * in the image); the device path is checked against this restatement. */
+namespace {
+void euler_012(const float R[3][3], float res[3]) {
+  const int i = 0, j = 1, k = 2;  // a0 = 0, a1 = 1 -> odd = 0
+  res[0] = std::atan2(R[j][k], R[k][k]);
+  const float c2 = std::sqrt(R[i][i] * R[i][i] + R[i][j] * R[i][j]);
+  if (res[0] > 0.f) {
+    res[0] -= float(M_PI);
+    res[1] = std::atan2(-R[i][k], -c2);
+  } else {
+    res[1] = std::atan2(-R[i][k], c2);
+  }
+  const float s1 = std::sin(res[0]), c1 = std::cos(res[0]);
+  res[2] = std::atan2(s1 * R[k][i] - c1 * R[j][i], c1 * R[j][j] - s1 * R[k][j]);
+  for (int q = 0; q < 3; ++q) res[q] = -res[q];
+}
+
+void crop_inverse(const float rpy[3], float inv[3][3]) {
+  // pcl::getTransformation(0,0,0, roll, pitch, yaw)
+  const float A = std::cos(rpy[2]), B = std::sin(rpy[2]), C = std::cos(rpy[1]), D = std::sin(rpy[1]),
+              E = std::cos(rpy[0]), F = std::sin(rpy[0]);
+  const float DE = D * E, DF = D * F;
+  const float m[3][3] = {{A * C, A * DF - B * E, B * F + A * DE},
+                         {B * C, A * E + B * DF, B * DE - A * F},
+                         {-D, C * F, C * E}};
+  // Affine3f::inverse(): linear().inverse() by cofactors
+  const float c00 = m[1][1] * m[2][2] - m[1][2] * m[2][1];
+  const float c10 = m[1][2] * m[2][0] - m[1][0] * m[2][2];
+  const float c20 = m[1][0] * m[2][1] - m[1][1] * m[2][0];
+  const float det = m[0][0] * c00 + m[0][1] * c10 + m[0][2] * c20;
+  const float id = 1.f / det;
+  inv[0][0] = c00 * id;
+  inv[1][0] = c10 * id;
+  inv[2][0] = c20 * id;
+  inv[0][1] = (m[0][2] * m[2][1] - m[0][1] * m[2][2]) * id;
+  inv[1][1] = (m[0][0] * m[2][2] - m[0][2] * m[2][0]) * id;
+  inv[2][1] = (m[0][1] * m[2][0] - m[0][0] * m[2][1]) * id;
+  inv[0][2] = (m[0][1] * m[1][2] - m[0][2] * m[1][1]) * id;
+  inv[1][2] = (m[0][2] * m[1][0] - m[0][0] * m[1][2]) * id;
+  inv[2][2] = (m[0][0] * m[1][1] - m[0][1] * m[1][0]) * id;
+}
+}  // namespace
+
+extern "C" int ao_crop_box(const float* pts, int64_t n, int64_t stride, float mn, float mx,
+                           const float origin[16], float* out, int64_t* out_n, float* rpy_out) {
+  if (!pts || !origin || !out || !out_n || stride < 3) return 2;
+  float R[3][3];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) R[r][c] = origin[c * 4 + r];
+  const float t[3] = {origin[12], origin[13], origin[14]};
+  float rpy[3];
+  euler_012(R, rpy);
+  if (rpy_out)
+    for (int q = 0; q < 3; ++q) rpy_out[q] = rpy[q];
+  float inv[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  const bool rot = rpy[0] != 0.f || rpy[1] != 0.f || rpy[2] != 0.f;
+  if (rot) crop_inverse(rpy, inv);
+  // `!inverse_transform.matrix().isIdentity()` (Eigen fuzzy test, float precision 1e-5)
+  bool ident = true;
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      ident = ident && (r == c ? std::fabs(inv[r][c] - 1.f) <= 1e-5f * std::fmin(std::fabs(inv[r][c]), 1.f)
+                               : std::fabs(inv[r][c]) <= 1e-5f);
+  if (ident)
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) inv[r][c] = r == c ? 1.f : 0.f;
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = pts + i * stride;
+    if (!std::isfinite(p[0]) || !std::isfinite(p[1]) || !std::isfinite(p[2])) continue;
+    const float x = p[0] - t[0], y = p[1] - t[1], z = p[2] - t[2];
+    float l[3];
+    for (int r = 0; r < 3; ++r) l[r] = ((inv[r][0] * x + inv[r][1] * y) + inv[r][2] * z) + 0.f;
+    if (l[0] < mn || l[1] < mn || l[2] < mn || l[0] > mx || l[1] > mx || l[2] > mx) continue;
+    out[3 * m] = p[0];
+    out[3 * m + 1] = p[1];
+    out[3 * m + 2] = p[2];
+    ++m;
+  }
+  *out_n = m;
+  return 0;
+}

@@ -110,6 +110,12 @@ int64_t ao_ray_keys(const float origin[3], const float end[3], double resolution
 float ao_autotune_ratio(float overlap_percent);
 float ao_quantize_ratio(float ratio);
 
+/* getPointsInOrientedBox (filteringUtils.cpp:619-637): pcl::CropBox with min/max cube,
+ * rotation = origin.R.eulerAngles(0,1,2), translation = origin.t. origin is col-major float[16]
+ * (Matrix4f). Kept points in input order; out_n = count. rpy_out (nullable) = the angles. */
+int ao_crop_box(const float* pts, int64_t n, int64_t stride_floats, float mn, float mx,
+                const float origin[16], float* out_xyz, int64_t* out_n, float* rpy_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -105,6 +105,8 @@ def lib():
         L.ao_autotune_ratio.restype = C.c_float
         L.ao_quantize_ratio.argtypes = [C.c_float]
         L.ao_quantize_ratio.restype = C.c_float
+        L.ao_crop_box.argtypes = [fp, C.c_int64, C.c_int64, C.c_float, C.c_float, fp, fp,
+                                  C.POINTER(C.c_int64), fp]
         _lib = L
     return _lib
 
@@ -240,3 +242,15 @@ def autotune_ratio(overlap_percent):
 
 def quantize_ratio(r):
     return lib().ao_quantize_ratio(r)
+
+
+def crop_box(pts, mn, mx, origin):
+    """getPointsInOrientedBox restatement (filteringUtils.cpp:619-637): (kept xyz, rpy)."""
+    p = _pts(pts)
+    o = np.ascontiguousarray(np.asarray(origin, np.float32).reshape(4, 4).T.reshape(16))
+    out = np.zeros((p.shape[0], 3), np.float32)
+    m = C.c_int64(0)
+    rpy = np.zeros(3, np.float32)
+    rc = lib().ao_crop_box(_f(p), p.shape[0], p.shape[1], mn, mx, _f(o), _f(out), C.byref(m), _f(rpy))
+    assert rc == 0
+    return out[:m.value].copy(), rpy
