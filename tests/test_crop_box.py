@@ -4,7 +4,7 @@ aicp_core/src/utils/filteringUtils.cpp:619-637, pcl::CropBox around the prior po
 CPU: the oracle's Eigen eulerAngles(0,1,2) restatement reproduces the rotation, and the crop
 matches an independent float64 numpy restatement away from the box faces. GPU: the device crop
 is bit-exact (same points, same order) with the oracle, including NaNs, empty and ragged tile
-sizes, and at the C4 map size (1M points). Parity against PCL itself is unpinned (PCL and
+sizes, and at C4 map size (~690k points). Parity against PCL itself is unpinned (PCL and
 Eigen are not in the image; no reference fixture covers the crop).
 """
 import math
@@ -100,7 +100,8 @@ def test_crop_box_bit_exact(oracle, n, k):
 
 @pytest.mark.gpu
 def test_crop_box_c4_map_size(oracle):
-    """C4: the 1M-point resident map cropped to +-15 m around a prior pose (app.cpp:41-51)."""
+    """C4-size map (make_pair asks for 1M points; 688 682 remain inside its 30 m sampling box)
+    cropped to +-15 m around a prior pose (app.cpp:41-51)."""
     import aicp_mapping_amd._lib as L
 
     pr = sy.make_pair(1_000_000, 10, seed=8)
@@ -112,3 +113,15 @@ def test_crop_box_c4_map_size(oracle):
         ctx.close()
     exp, _ = oracle.crop_box(pr.ref, -15.0, 15.0, T)
     assert 0 < len(exp) < len(pr.ref) and np.array_equal(got, exp)
+
+
+def test_bench_c4_crop_is_reference_crop(oracle):
+    """bench.py's C4 input preparation (axis-aligned +-15 m box around the prior position)
+    equals getPointsInOrientedBox with an identity-rotation pose, point for point."""
+    P = np.random.default_rng(12).uniform(-40, 40, size=(50000, 3)).astype(np.float32)
+    o = np.array([0.9, 0.0, 0.7])
+    m = np.all(np.abs(P - o.astype(np.float32)) <= 15.0, axis=1)
+    T = np.eye(4)
+    T[:3, 3] = o
+    kept, rpy = oracle.crop_box(P, -15.0, 15.0, T)
+    assert not np.any(rpy) and np.array_equal(kept, P[m])
