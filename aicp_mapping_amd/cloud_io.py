@@ -344,3 +344,28 @@ def process_from_file(directory: str):
         except (OSError, CloudFormatError):
             return
         yield p, cloud.xyz
+
+
+def recorded_sequence_pairs(directory: str, ref_every: int = 5, max_readings: int | None = None):
+    """Frame-to-reference pairs from a recorded directory, in App's windowing: the first cloud
+    is the first reference (app.cpp:300-313); each later cloud is a reading registered against
+    the current reference, and the reference is replaced by the reading that closes every
+    `ref_every` readings (reference_update_frequency, app.cpp:383-391; the replacement here is
+    the recorded cloud, not the corrected one). Origins are the recorded pose translations
+    (octrees_overlap.cpp:184,229-230). Returns dicts in the bench / ResidentBatch layout
+    (T_gt = None: recordings carry no ground truth)."""
+    pairs = []
+    ref = ref_pose = None
+    n_read = 0
+    for p, xyz in process_from_file(directory):
+        if ref is None:
+            ref, ref_pose = xyz, p.pose
+            continue
+        pairs.append(dict(ref=ref, read=xyz, ref_origin=ref_pose[:3, 3].copy(),
+                          read_origin=p.pose[:3, 3].copy(), T_gt=None))
+        n_read += 1
+        if max_readings is not None and n_read >= max_readings:
+            break
+        if n_read % ref_every == 0:
+            ref, ref_pose = xyz, p.pose
+    return pairs

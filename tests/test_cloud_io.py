@@ -196,3 +196,24 @@ def test_recorded_directory_registers_like_oracle(tmp_path, oracle):
                                                            normals_on_centered=0))
     r, t = sy.rot_err(T1, T)
     assert r < 1e-6 and t < 1e-5
+
+
+def test_recorded_sequence_pairs_windowing(tmp_path):
+    """App's frame-to-reference windowing over a recording: cloud 0 is the first reference;
+    the reference moves to the reading that closes every `ref_every` readings."""
+    clouds = [sy.make_pair(800, 10, seed=40 + i).ref for i in range(12)]
+    poses = []
+    for i in range(12):
+        T = np.eye(4)
+        T[:3, 3] = (0.5 * i, 0.0, 0.7)
+        poses.append(T)
+    write_recording(tmp_path, clouds, poses)
+    pairs = io.recorded_sequence_pairs(str(tmp_path), ref_every=5)
+    assert len(pairs) == 11
+    ref_idx = [0] * 5 + [5] * 5 + [10]
+    for j, (p, r) in enumerate(zip(pairs, ref_idx)):
+        assert np.array_equal(p["read"], clouds[j + 1]) and np.array_equal(p["ref"], clouds[r])
+        assert np.allclose(p["ref_origin"], (0.5 * r, 0, 0.7)) and p["T_gt"] is None
+    # readings of one window share one reference array (the device shares its tree and normals)
+    assert len({id(p["ref"]) for p in pairs}) == 3
+    assert len(io.recorded_sequence_pairs(str(tmp_path), 5, max_readings=4)) == 4
