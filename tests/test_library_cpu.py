@@ -226,3 +226,16 @@ def test_gloo_world2_gather_records():
         np.testing.assert_array_equal(out[:, 16], [10 + i for i in order])
         np.testing.assert_allclose(out[:, 0], [1 + i for i in order])
         assert m == 2.0 and s == 3.0
+
+
+def test_as_points_pcl_layouts(L):
+    """PointXYZ (16 B), PointXYZRGB (32 B) and PointXYZRGBNormal (48 B) rows pass through with
+    their stride; other widths are refused."""
+    import numpy as np
+
+    for w in (3, 4, 8, 12):
+        a = np.zeros((5, w), np.float32)
+        assert L.as_points(a) is a
+    for w in (2, 5, 16):
+        with pytest.raises(ValueError):
+            L.as_points(np.zeros((5, w), np.float32))
