@@ -10,7 +10,9 @@
 //                           inner: x = cut (float bits), y = cd | right << 2, z = parent
 //                           leaf : x = bucket count,     y = 3  | bucket_start << 2, z = parent
 //                         (16 B: a node record and a bucket point load with one instruction)
-//   parent    int32[ΣW]   parent node (-1 at the root), used by the kNN (normals) climb
+//                         w = depth
+//   tl        uint4[Σ(4M + 1)] matcher tree as two-level treelet records (kernels_tree.hip)
+//   ptl       uint32[Σ(4M + 1)] per treelet: node id of its root's parent
 //   match     int32[ΣN]   bucket position of the NN of each reading point
 //   d2        float[ΣN]   squared NN distance
 // Bucket positions are local to the pair (ref_off added by the kernels).
@@ -55,6 +57,7 @@ struct PairDesc {
   int32_t tree_depth;
   int32_t ref_id;               // index of the pair's (deduplicated) reference cloud
   int32_t ogroup;               // overlap group: distinct (reference cloud, reference origin)
+  uint32_t tl_off, tl_cap;      // matcher treelets (kernels_tree.hip): first record, records allotted
   double ref_origin[3], read_origin[3];
 };
 

@@ -131,7 +131,9 @@ struct aicp_hip_ctx {
   std::string err;
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
       ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
-      nrm_raw, inv, gdesc, gstate, sup, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp;
+      nrm_raw, inv, gdesc, gstate, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, tl, ptl, tl_flag,
+      tl_rank, tl_temp;
+  uint64_t tl_total = 0;  // matcher treelet records allotted for this batch (0: no treelets, Trav<1>)
   TreeBufs tb[2];  // [0] raw-coordinate tree (stream2), [1] centred matcher tree (stream3)
   PinBuf pin_desc, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
   std::vector<hipEvent_t> nn_ev;
@@ -453,7 +455,7 @@ int device_trees_check(TreeBufs& T, std::string& err) {
   // oversized segments at the last planned level: plan deeper next time
   T.needed = hctl->n_big ? std::min(kFarStack - 3, T.planned + 2) : used;
   if (hctl->error & 1) TFAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
-  if (hctl->error) TFAIL(AICP_ERR_HIP, "kd-tree construction overflow " + std::to_string(hctl->error));
+  if (hctl->error & ~4) TFAIL(AICP_ERR_HIP, "kd-tree construction overflow " + std::to_string(hctl->error));
   return AICP_OK;
 }
 
@@ -486,10 +488,22 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
   if (rc) return rc;
   rc = device_trees_end(ctx->tb[1], err, s3, R, B->total_ref, dRdesc, bucket, ctx->bpts, ctx->nodes, plan);
   if (rc) return rc;
-  // two-level node records for the matcher (Trav2)
-  const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);
-  TCHK(ensure(ctx->sup, (size_t)cap * 32));
-  launch_super_nodes(s3, (int)R, cap, dRdesc, ctx->nodes.as<uint4>(), ctx->sup.as<uint4>());
+  // treelet records of the matcher trees (Trav2C), then the control block again: k_tl_check
+  // reports into its error word, checked after the batch
+  if (ctx->tl_total) {
+    const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);  // node records allotted
+    const size_t tb = tree_scan_temp_bytes((size_t)cap + 1);
+    TCHK(ensure(ctx->tl, ctx->tl_total * 16));
+    TCHK(ensure(ctx->ptl, ctx->tl_total * 4));
+    TCHK(ensure(ctx->tl_flag, ((size_t)cap + 1) * 4));
+    TCHK(ensure(ctx->tl_rank, ((size_t)cap + 1) * 4));
+    TCHK(ensure(ctx->tl_temp, tb));
+    TreeBufs& T = ctx->tb[1];
+    TCHK(launch_treelets(s3, (int)R, cap, dRdesc, ctx->nodes.as<uint4>(), bucket, ctx->tl_flag.as<uint32_t>(),
+                         ctx->tl_rank.as<uint32_t>(), ctx->tl_temp.p, tb, ctx->tl.as<uint4>(),
+                         ctx->ptl.as<uint32_t>(), T.tw.ctl));
+    TCHK(hipMemcpyAsync(T.pin_ctl.p, T.tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
+  }
   launch_pairs_from_refs(s3, (int)B->P, dDesc, dRdesc);
   TCHK(hipEventRecord(ctx->ev[3], s3));
   return AICP_OK;
@@ -624,6 +638,18 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     dRdesc = ctx->rdesc.as<PairDesc>();
     dRstate = ctx->rstate.as<PairState>();
     std::memcpy(ctx->pin_rdesc.p, B->rdesc.data(), R * sizeof(PairDesc));
+    // matcher treelet records allotted per reference (kernels_tree.hip: at most 1 + 4 per inner
+    // node at even depth); leaf slots hold a 4-bit count, so larger buckets use Trav<1>
+    ctx->tl_total = 0;
+    if (cfg->bucket_size <= 15) {
+      for (size_t r = 0; r < R; ++r) {
+        PairDesc& rd = ctx->pin_rdesc.as<PairDesc>()[r];
+        rd.tl_off = (uint32_t)ctx->tl_total;
+        rd.tl_cap = (uint32_t)(4 * (uint64_t)rd.n_ref + 4);
+        ctx->tl_total += rd.tl_cap;
+      }
+      if (ctx->tl_total >= (1ull << 32)) ctx->tl_total = 0;  // offsets do not fit: Trav<1>
+    }
     HIPC(ensure(ctx->rdesc_raw, R * sizeof(PairDesc)));
     HIPC(hipStreamWaitEvent(s2, ctx->ev[7], 0));
     HIPC(hipEventRecord(ctx->ev[8], s2));
@@ -742,8 +768,9 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     for (int it = 0; it < cfg->max_iter; ++it) {
       launch_active_list(s, (int)P, dDesc, dState, dAl, dCtr);
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it], s));
-      launch_icp_nn(s, (int)B->total_read, dDesc, dState, dAl, readc, nodes, ctx->sup.as<uint4>(), parent, bpts,
-                    ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm);
+      launch_icp_nn(s, (int)B->total_read, dDesc, dState, dAl, readc, nodes,
+                    ctx->tl_total ? ctx->tl.as<uint4>() : nullptr, parent, bpts,
+                    ctx->tl_total ? ctx->ptl.as<uint32_t>() : nullptr, ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm);
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it + 1], s));
       ++nn_launches;
       launch_icp_select(s, B->m_sel, (int)P, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
@@ -771,6 +798,8 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     rc = device_trees_check(ctx->tb[0], ctx->err);
     if (!rc) rc = device_trees_check(ctx->tb[1], ctx->err);
     if (rc) return rc;
+    if (ctx->tl_total && (ctx->tb[1].pin_ctl.as<TreeCtl>()->error & 4))
+      FAIL(AICP_ERR_HIP, "matcher treelets exceed their allotment");
   }
   // results
   const PairState* hs = ctx->pin_state.as<PairState>();
@@ -893,7 +922,8 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
                     &ctx->state, &ctx->touch, &ctx->slab, &ctx->bitmap, &ctx->outT, &ctx->scratch, &ctx->active,
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
-                    &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->sup, &ctx->gdesc, &ctx->gstate})
+                    &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->gdesc, &ctx->gstate, &ctx->tl, &ctx->ptl,
+                    &ctx->tl_flag, &ctx->tl_rank, &ctx->tl_temp})
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,

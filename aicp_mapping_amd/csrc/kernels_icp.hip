@@ -217,169 +217,34 @@ struct Trav {
   }
 };
 
-// 1-NN (the ICP matcher) over two-level node records: record n of the matcher tree carries,
-// besides its own {cut, cd | right, parent}, the {x, y} words of both children (k_super_nodes,
-// 32 bytes = two loads from one cache line issued together). A descent step therefore decides
-// two levels -- the node's and the chosen child's -- per round trip: the descent, ~70 % of the
-// dependent loads of a query (tools/travstats.cpp: 18.3 of 26), takes half as many. Visit
-// order, far tests, counts and results are Trav<1>'s (libnabo recurseKnn).
-struct Trav2 {
-  const uint4* nodes;  // super records: [2n] = {x, y, parent, left.x}, [2n + 1] = {left.y, right.x, right.y, 0}
-  const float4* pts;
-  float q0, q1, q2;
-  float off0, off1, off2, rd, minFar;
-  int32_t n, start, sp;
-  uint32_t tp, tn;
-  Best<1> best;
-
-  __device__ __forceinline__ void bind(const uint4* nb, const float4* pb, uint32_t node_off, uint32_t ref_off) {
-    nodes = nb + 2 * (size_t)node_off;
-    pts = pb + ref_off;
-  }
-  __device__ __forceinline__ float res_d2() const { return best.v[0]; }
-  __device__ __forceinline__ int32_t res_id() const { return best.id[0]; }
-
-  __device__ __forceinline__ void reset(float a, float b, float c) {
-    q0 = a;
-    q1 = b;
-    q2 = c;
-    off0 = off1 = off2 = rd = 0.f;
-    n = start = sp = 0;
-    tp = tn = 0;
-    best_init<1>(best);
-  }
-
-  __device__ __forceinline__ bool advance(FarStack& fs, float maxE2, float maxR2, const uint4*, const float4*) {
-    minFar = __builtin_inff();
-    uint4 a = nodes[2 * n], b = nodes[2 * n + 1];
-    int32_t pl = (int32_t)a.z;  // parent of the leaf the descent ends in
-    while ((a.y & 3u) != kLeaf) {
-      const uint32_t cd = a.y & 3u;
-      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(a.x);
-      const float oc = sel3(cd, off0, off1, off2);
-      minFar = fminf(minFar, rd + (-oc * oc + no * no));
-      ++tn;
-      const bool right = no > 0.f;
-      const int32_t c = right ? (int32_t)(a.y >> 2) : n + 1;
-      const uint32_t cx = right ? b.y : a.w, cy = right ? b.z : b.x;
-      pl = n;
-      n = c;
-      if ((cy & 3u) == kLeaf) {  // leaf child: count and bucket start are already here
-        a.x = cx;
-        a.y = cy;
-        break;
-      }
-      const uint32_t cd2 = cy & 3u;
-      const float no2 = sel3(cd2, q0, q1, q2) - __uint_as_float(cx);
-      const float oc2 = sel3(cd2, off0, off1, off2);
-      minFar = fminf(minFar, rd + (-oc2 * oc2 + no2 * no2));
-      ++tn;
-      n = (no2 > 0.f) ? (int32_t)(cy >> 2) : c + 1;
-      a = nodes[2 * n];
-      b = nodes[2 * n + 1];
-      pl = (int32_t)a.z;
-    }
-    {
-      const uint32_t b0 = a.y >> 2, cnt = a.x;
-      float3 P[kLeafBatch];
-#pragma unroll
-      for (int i = 0; i < kLeafBatch; ++i)
-        if ((uint32_t)i < cnt) {
-          const float4 p = pts[b0 + i];
-          P[i] = make_float3(p.x, p.y, p.z);
-        }
-#pragma unroll
-      for (int i = 0; i < kLeafBatch; ++i)
-        if ((uint32_t)i < cnt) {
-          const float d0 = q0 - P[i].x, d1 = q1 - P[i].y, d2 = q2 - P[i].z;
-          float dist = 0.f;
-          dist += d0 * d0;
-          dist += d1 * d1;
-          dist += d2 * d2;
-          if (dist <= maxR2 && dist < best.v[0]) best_replace<1>(best, (int32_t)(b0 + i), dist);
-        }
-      for (uint32_t i = kLeafBatch; i < cnt; ++i) {
-        const float4 p = pts[b0 + i];
-        const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
-        float dist = 0.f;
-        dist += d0 * d0;
-        dist += d1 * d1;
-        dist += d2 * d2;
-        if (dist <= maxR2 && dist < best.v[0]) best_replace<1>(best, (int32_t)(b0 + i), dist);
-      }
-      tp += cnt;
-    }
-    int32_t c = n, pc = pl;
-    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
-    for (;;) {
-      if (c == start) {
-        if (sp == 0) return true;
-        --sp;
-        const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
-        rd = fs.rd[sp];
-        const float old = fs.old[sp];
-        if (pcd == 0) off0 = old;
-        else if (pcd == 1) off1 = old;
-        else off2 = old;
-        minFar = fs.mn[sp];
-        start = fs.start[sp];
-        c = fs.P[sp];
-        pc = fs.PP[sp];
-        if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
-        continue;
-      }
-      const int32_t p = pc;
-      const uint4 pn = nodes[2 * p];
-      const uint32_t cd = pn.y & 3u;
-      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(pn.x);
-      const float oc = sel3(cd, off0, off1, off2);
-      const float rdf = rd + (-oc * oc + no * no);
-      if (rdf <= maxR2 && rdf * maxE2 < best.v[0]) {
-        const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
-        fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
-        fs.rd[sp] = rd;
-        fs.old[sp] = oc;
-        fs.mn[sp] = minFar;
-        fs.start[sp] = start;
-        fs.P[sp] = p;
-        fs.PP[sp] = (int32_t)pn.z;
-        ++sp;
-        if (cd == 0) off0 = no;
-        else if (cd == 1) off1 = no;
-        else off2 = no;
-        rd = rdf;
-        n = far;
-        start = far;
-        return false;
-      }
-      c = p;
-      pc = (int32_t)pn.z;
-    }
-  }
-};
-
-// Trav2 with the bucket scan done by the wave cooperatively. The per-lane bucket loads of Trav2
-// put up to 64 distinct cache lines into each load instruction, and the TA/TCP processes
-// gathers at a rate set by distinct lines per instruction (profiles/r01_gather_bench.txt: 64
-// lines -> 4-27 instr/CU/us, 8-16 lines -> 40-140). Here lanes 8g..8g+7 (an "octet") load the
-// 8 points of one owner's bucket together -- one 128-byte run, 1-2 lines -- and compute their
-// distances to the owner's query; a min over the octet (DPP) and the lowest lane holding it
-// (ballot) give the owner the result of libnabo's in-order scan (first strictly smaller d^2
-// wins). Eight rounds serve the octet's eight owners, so one load instruction covers eight
-// buckets in <= 16 lines. The split into descend() / (wave-wide bucket) / climb() keeps the
-// visit order, counts and results of Trav2.
+// 1-NN (the ICP matcher) over the matcher tree's treelets (kernels_tree.hip: a node and its two
+// children in one 16-byte record, the grandchildren's treelets at base + 0..3). A node is named
+// by treelet << 2 | slot (slot 0 the treelet's root, 1 / 2 its left / right child), so the
+// root is 0. One record load decides two levels of a descent; the climb steps inside a record
+// without a load and into the parent treelet through ptl (loaded with the record). The records hold no parent, child or
+// redundant copies (about 5 B per node against 32 B for two-level node records), so the trees
+// of the references an XCD serves stay in its L2.
+//
+// The bucket scan is done by the wave cooperatively: lanes 8g..8g+7 (an "octet") read the 8
+// points of one owner's bucket together -- one 128-byte run -- and compute their distances to
+// the owner's query; a min over the octet (DPP) and the lowest lane holding it (ballot) give
+// the owner the result of libnabo's in-order scan (first strictly smaller d^2 wins). Eight
+// rounds serve the octet's eight owners. The split into descend() / (wave-wide bucket) /
+// climb() keeps libnabo recurseKnn's visit order, far tests and counts.
 struct Trav2C {
-  const uint4* nodes;
-  uint32_t pbase;  // the pair's first bucket point (bpts index)
+  const uint4* tl;       // the pair's treelets
+  const uint32_t* ptl;   // the pair's treelet parents
+  uint32_t pbase;        // the pair's first bucket point
   float q0, q1, q2;
   float off0, off1, off2, rd, minFar;
-  int32_t n, start, sp, pl;
-  uint32_t lb0, lcnt;  // bucket of the leaf the last descent ended in
+  int32_t n, start, sp, pl;  // node ids; pl: parent of the node the last descent ended in
+  uint32_t lb0, lcnt;        // bucket of the leaf the last descent ended in
   uint32_t tp, tn;
   Best<1> best;
 
-  __device__ __forceinline__ void bind(const uint4* nb, const float4*, uint32_t node_off, uint32_t ref_off) {
-    nodes = nb + 2 * (size_t)node_off;
+  __device__ __forceinline__ void bind(const uint4* t, const uint32_t* b, uint32_t tl_off, uint32_t ref_off) {
+    tl = t + tl_off;
+    ptl = b + tl_off;
     pbase = ref_off;
   }
   __device__ __forceinline__ float res_d2() const { return best.v[0]; }
@@ -391,42 +256,54 @@ struct Trav2C {
     q2 = c;
     off0 = off1 = off2 = rd = 0.f;
     n = start = sp = 0;
+    pl = -1;
     tp = tn = 0;
     best_init<1>(best);
   }
 
+  __device__ __forceinline__ static uint32_t slot_word(const uint4& r, uint32_t s) {
+    return s == 0 ? r.x : (s == 1 ? r.y : r.z);
+  }
+
+  // one inner slot: fold its far bound into minFar, return true if the query goes right
+  __device__ __forceinline__ bool decide(uint32_t w, uint32_t cd) {
+    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
+    const float oc = sel3(cd, off0, off1, off2);
+    minFar = fminf(minFar, rd + (-oc * oc + no * no));
+    ++tn;
+    return no > 0.f;
+  }
+
+  // a descent from n: the root slot of each treelet, then the chosen child's slot, one record
+  // load per two levels (a descent that starts at a child slot skips the first root step)
   __device__ __forceinline__ void descend() {
     minFar = __builtin_inff();
-    uint4 a = nodes[2 * n], b = nodes[2 * n + 1];
-    pl = (int32_t)a.z;
-    while ((a.y & 3u) != kLeaf) {
-      const uint32_t cd = a.y & 3u;
-      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(a.x);
-      const float oc = sel3(cd, off0, off1, off2);
-      minFar = fminf(minFar, rd + (-oc * oc + no * no));
-      ++tn;
-      const bool right = no > 0.f;
-      const int32_t c = right ? (int32_t)(a.y >> 2) : n + 1;
-      const uint32_t cx = right ? b.y : a.w, cy = right ? b.z : b.x;
+    uint32_t T = (uint32_t)n >> 2, s = (uint32_t)n & 3u;
+    uint4 r = tl[T];
+    uint32_t w = r.x, cd = r.w & 3u;
+    if (s == 0 && cd != kLeaf) {
+      s = decide(w, cd) ? 2u : 1u;
       pl = n;
-      n = c;
-      if ((cy & 3u) == kLeaf) {
-        a.x = cx;
-        a.y = cy;
-        break;
-      }
-      const uint32_t cd2 = cy & 3u;
-      const float no2 = sel3(cd2, q0, q1, q2) - __uint_as_float(cx);
-      const float oc2 = sel3(cd2, off0, off1, off2);
-      minFar = fminf(minFar, rd + (-oc2 * oc2 + no2 * no2));
-      ++tn;
-      n = (no2 > 0.f) ? (int32_t)(cy >> 2) : c + 1;
-      a = nodes[2 * n];
-      b = nodes[2 * n + 1];
-      pl = (int32_t)a.z;
+      n = (int32_t)(T << 2 | s);
     }
-    lb0 = a.y >> 2;
-    lcnt = a.x;
+    while (s != 0) {
+      w = s == 1 ? r.y : r.z;
+      cd = (r.w >> (2 * s)) & 3u;
+      if (cd == kLeaf) break;
+      const bool right = decide(w, cd);
+      pl = n;
+      T = (r.w >> 6) + 2 * (s - 1) + (right ? 1u : 0u);
+      n = (int32_t)(T << 2);
+      r = tl[T];
+      w = r.x;
+      cd = r.w & 3u;
+      if (cd == kLeaf) break;
+      s = decide(w, cd) ? 2u : 1u;
+      pl = n;
+      n = (int32_t)(T << 2 | s);
+    }
+    lb0 = w & 0x0FFFFFFFu;
+    lcnt = w >> 28;
   }
 
   // bucket points beyond the first kLeafBatch (bucket sizes above libnabo's default 8), in order
@@ -445,6 +322,9 @@ struct Trav2C {
 
   __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
     int32_t c = n, pc = pl;
+    uint32_t cT = 0xffffffffu;  // treelet whose record cr (and root parent cpp) is held
+    uint4 cr;
+    int32_t cpp = -1;
     if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
     for (;;) {
       if (c == start) {
@@ -464,20 +344,30 @@ struct Trav2C {
         continue;
       }
       const int32_t p = pc;
-      const uint4 pn = nodes[2 * p];
-      const uint32_t cd = pn.y & 3u;
-      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(pn.x);
+      const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
+      if (T != cT) {  // the record and its root's parent, one round trip per treelet
+        cT = T;
+        cr = tl[T];
+        cpp = (int32_t)ptl[T];
+      }
+      const uint4 r = cr;
+      const int32_t pp = s != 0 ? (int32_t)(T << 2) : cpp;  // parent of p
+      const uint32_t w = slot_word(r, s), cd = (r.w >> (2 * s)) & 3u;
+      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
       const float oc = sel3(cd, off0, off1, off2);
       const float rdf = rd + (-oc * oc + no * no);
       if (rdf <= maxR2 && rdf * maxE2 < best.v[0]) {
-        const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
+        // far child = the left one when the query is right of the cut
+        const uint32_t fr = no > 0.f ? 0u : 1u;
+        const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr))
+                                   : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
         fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
         fs.rd[sp] = rd;
         fs.old[sp] = oc;
         fs.mn[sp] = minFar;
         fs.start[sp] = start;
         fs.P[sp] = p;
-        fs.PP[sp] = (int32_t)pn.z;
+        fs.PP[sp] = pp;
         ++sp;
         if (cd == 0) off0 = no;
         else if (cd == 1) off1 = no;
@@ -485,10 +375,11 @@ struct Trav2C {
         rd = rdf;
         n = far;
         start = far;
+        pl = p;
         return false;
       }
       c = p;
-      pc = (int32_t)pn.z;
+      pc = pp;
     }
   }
 };
@@ -1001,13 +892,17 @@ __device__ __forceinline__ void apply_cols(const float4& c0, const float4& c1, c
 // NN kernel: also stores the query's touch counts (inner nodes << 16 | bucket points, each
 // saturated at 65535) for the reduce kernel to sum per pair without atomics.
 template <class Eng>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_icp_nn(
+#ifndef AICP_NN_WAVES
+#define AICP_NN_WAVES 8  // waves per SIMD the NN kernel is compiled for (VGPR budget 512 / waves)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAVES))) void k_icp_nn(
                                                 const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
                                                 const ActiveList* __restrict__ al,
                                                 const float4* __restrict__ read_c,
                                                 const uint4* __restrict__ nodes,
                                                 const int32_t* __restrict__ parent,
-                                                const float4* __restrict__ bpts, int32_t* __restrict__ match,
+                                                const float4* __restrict__ bpts, const uint32_t* __restrict__ ptl,
+                                                int32_t* __restrict__ match,
                                                 float* __restrict__ d2out, uint32_t* __restrict__ touched,
                                                 uint32_t* ctr, IcpParams prm) {
   const uint32_t total = al->total;
@@ -1030,13 +925,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         const PairDesc& d = pd[c_pair];
         c_n = __builtin_amdgcn_readfirstlane(d.n_read);
         c_read = __builtin_amdgcn_readfirstlane(d.read_off);
-        c_node = __builtin_amdgcn_readfirstlane(d.node_off);
+        if constexpr (is_coop<Eng>::value) c_node = __builtin_amdgcn_readfirstlane(d.tl_off);
+        else c_node = __builtin_amdgcn_readfirstlane(d.node_off);
         c_ref = __builtin_amdgcn_readfirstlane(d.ref_off);
       },
       [&](uint32_t s, Eng& t) {
         const uint32_t j = s - c_lo;
         if (j >= c_n) return false;  // padding slot
-        t.bind(nodes, bpts, c_node, c_ref);
+        if constexpr (is_coop<Eng>::value) t.bind(nodes, ptl, c_node, c_ref);
+        else t.bind(nodes, bpts, c_node, c_ref);
         qidx = c_read + j;
         const float4 r = read_c[qidx];
         const float4* Tp = reinterpret_cast<const float4*>(st[c_pair].T);
@@ -1547,7 +1444,7 @@ __global__ __launch_bounds__(64) void k_solve6(const double* A, const double* b,
 // ------------------------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------------------------
-static int persistent_grid(int n_items) {
+static int persistent_grid(int n_items, int blocks_per_cu = 8) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1557,7 +1454,7 @@ static int persistent_grid(int n_items) {
   }
   // every work group (blockIdx % kXcdGroups) needs at least one block: a multiple of 8
   int want = (n_items + 255) / 256;
-  if (want > cus * 8) want = cus * 8;
+  if (want > cus * blocks_per_cu) want = cus * blocks_per_cu;
   return (want + kXcdGroups - 1) / kXcdGroups * kXcdGroups;
 }
 
@@ -1598,31 +1495,30 @@ void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const Pa
                         uint32_t* ctr) {
   k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr);
 }
-// NN engine of the ICP matcher: 3 = Trav2C (default), 2 = Trav2, 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
+// NN engine of the ICP matcher: 3 = Trav2C (default), 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
 // (design experiments, tools/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:
 // Trav<1> 230 us per NN launch, SM0 436 us (profiles/README.md).
 static int nn_engine() {
   static int e = -1;
   if (e < 0) {
     const char* v = getenv("AICP_NN_ENGINE");
-    e = (v && v[0] >= '0' && v[0] <= '3') ? v[0] - '0' : 3;
+    e = (v && (v[0] == '0' || v[0] == '1' || v[0] == '3')) ? v[0] - '0' : 3;
   }
   return e;
 }
 
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st, const ActiveList* al,
-                   const float4* read_c, const uint4* nodes, const uint4* sup, const int32_t* parent,
-                   const float4* bpts,
-                   int32_t* match, float* d2, uint32_t* touched, uint32_t* ctr, const IcpParams& prm) {
-  const int g = persistent_grid(grid_items);
-  if (nn_engine() == 3 && sup)
-    k_icp_nn<Trav2C><<<g, 256, 0, s>>>(pd, st, al, read_c, sup, parent, bpts, match, d2, touched, ctr, prm);
-  else if (nn_engine() == 2 && sup)
-    k_icp_nn<Trav2><<<g, 256, 0, s>>>(pd, st, al, read_c, sup, parent, bpts, match, d2, touched, ctr, prm);
+                   const float4* read_c, const uint4* nodes, const uint4* tl, const int32_t* parent,
+                   const float4* bpts, const uint32_t* ptl, int32_t* match, float* d2, uint32_t* touched,
+                   uint32_t* ctr, const IcpParams& prm) {
+  const int g = persistent_grid(grid_items, AICP_NN_WAVES);
+  if (nn_engine() == 3 && tl && ptl)
+    k_icp_nn<Trav2C><<<g, 256, 0, s>>>(pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
   else if (nn_engine() >= 1)
-    k_icp_nn<Trav<1>><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, match, d2, touched, ctr, prm);
+    k_icp_nn<Trav<1>><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, nullptr, match, d2, touched, ctr,
+                                        prm);
   else
-    k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, match, d2, touched, ctr, prm);
+    k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, nullptr, match, d2, touched, ctr, prm);
 }
 void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* pd, PairState* st, const float* d2,
                        uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt) {

@@ -806,10 +806,10 @@ __global__ __launch_bounds__(256) void k_tr_emit(uint32_t total, const NodeEvent
   const uint32_t par = e.parent_depth < 0 ? 0xffffffffu : (uint32_t)e.parent_depth + S[e.parent_f + 1] - base;
   uint4 r;
   if (e.cd == (int32_t)kLeaf) {
-    r = make_uint4(e.c, kLeaf | ((e.f - ro) << 2), par, 0u);
+    r = make_uint4(e.c, kLeaf | ((e.f - ro) << 2), par, (uint32_t)e.depth);
   } else {
     const uint32_t right = (uint32_t)e.depth + 1 + S[e.f + e.left + 1] - base;
-    r = make_uint4(e.cut_bits, (uint32_t)e.cd | (right << 2), par, 0u);
+    r = make_uint4(e.cut_bits, (uint32_t)e.cd | (right << 2), par, (uint32_t)e.depth);
   }
   if (pre >= 2 * total + 2) {
     atomicOr(&ctl->error, 2);
@@ -840,6 +840,8 @@ __global__ void k_pairs_from_refs(int n_pairs, PairDesc* pd, const PairDesc* __r
   d.node_off = r.node_off;
   d.n_nodes = r.n_nodes;
   d.tree_depth = r.tree_depth;
+  d.tl_off = r.tl_off;
+  d.tl_cap = r.tl_cap;
   float Tmi[16];
   ident4(Tmi);
   for (int k = 0; k < 3; ++k) {
@@ -893,33 +895,113 @@ static hipError_t scan_u32(hipStream_t s, void* temp, size_t temp_bytes, const u
   return rocprim::exclusive_scan(temp, bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), s);
 }
 
-__global__ __launch_bounds__(256) void k_super_nodes(int n_refs, uint32_t cap, const PairDesc* __restrict__ rd,
-                                                     const uint4* __restrict__ nodes, uint4* __restrict__ sup) {
-  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t total = rd[n_refs - 1].node_off + rd[n_refs - 1].n_nodes;
-  if (g >= total || g >= cap) return;
+// ---- treelets: the matcher tree in two-level, pointer-light records (Trav2C) ----------------
+// The nodes at even depth are treelet roots. Treelet T = a root v and its two children, in one
+// 16-byte record {slot v, slot L, slot R, meta}: an inner slot holds the cut (float bits), a leaf
+// slot count << 28 | bucket start; meta = cd_v | cd_L << 2 | cd_R << 4 | base << 6 (cd 3 = leaf).
+// The (up to four) treelets rooted at v's grandchildren LL, LR, RL, RR sit at base + 0..3, so no
+// child pointer is stored. Slot 0 of a reference is the root's treelet; a treelet that has
+// grandchildren gets its block of 4 at base = 1 + 4 * rank, rank = its position among such
+// treelets in preorder (one scan), so every treelet's index follows from its grandparent's base
+// without a level-by-level pass. ptl[T] = the node id (treelet << 2 | slot) of the parent of T's
+// root, -1 for the root treelet (the climb's step out of a treelet). Indices are local to the
+// reference (PairDesc::tl_off, for tl and ptl).
+__device__ __forceinline__ int ref_of_node(const PairDesc* __restrict__ rd, int n_refs, uint32_t g) {
   int lo = 0, hi = n_refs - 1;  // the reference owning node g (node_off ascending)
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (rd[mid].node_off <= g) lo = mid;
     else hi = mid - 1;
   }
-  const uint32_t base = rd[lo].node_off;
-  const uint4 a = nodes[g];
-  uint4 s0 = make_uint4(a.x, a.y, a.z, 0u), s1 = make_uint4(0u, 0u, 0u, 0u);
-  if ((a.y & 3u) != kLeaf) {
-    const uint4 L = nodes[g + 1], R = nodes[base + (a.y >> 2)];
-    s0.w = L.x;
-    s1 = make_uint4(L.y, R.x, R.y, 0u);
+  return lo;
+}
+
+__device__ __forceinline__ bool tl_has_block(const uint4* __restrict__ nd, uint32_t v) {
+  const uint4 a = nd[v];
+  if ((a.w & 1u) || (a.y & 3u) == kLeaf) return false;  // odd depth or leaf: no treelet block
+  const uint4 L = nd[v + 1], R = nd[a.y >> 2];
+  return (L.y & 3u) != kLeaf || (R.y & 3u) != kLeaf;
+}
+
+__global__ __launch_bounds__(256) void k_tl_flag(int n_refs, uint32_t n, const PairDesc* __restrict__ rd,
+                                                 const uint4* __restrict__ nodes, uint32_t* __restrict__ flag) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g >= n) return;
+  const uint32_t total = rd[n_refs - 1].node_off + rd[n_refs - 1].n_nodes;
+  if (g >= total) {
+    flag[g] = 0;
+    return;
   }
-  sup[2 * (size_t)g] = s0;
-  sup[2 * (size_t)g + 1] = s1;
+  const PairDesc& r = rd[ref_of_node(rd, n_refs, g)];
+  flag[g] = tl_has_block(nodes + r.node_off, g - r.node_off) ? 1u : 0u;
 }
 
-void launch_super_nodes(hipStream_t s, int n_refs, uint32_t cap, const PairDesc* rd, const uint4* nodes, uint4* sup) {
-  if (n_refs > 0 && cap > 0) k_super_nodes<<<(cap + 255) / 256, 256, 0, s>>>(n_refs, cap, rd, nodes, sup);
+__device__ __forceinline__ uint32_t tl_slot(const uint4& a) {
+  return (a.y & 3u) == kLeaf ? (a.x << 28) | (a.y >> 2) : a.x;
 }
 
+__global__ __launch_bounds__(256) void k_tl_build(int n_refs, uint32_t cap, const PairDesc* __restrict__ rd,
+                                                  const uint4* __restrict__ nodes, const uint32_t* __restrict__ rank,
+                                                  uint4* __restrict__ tl, uint32_t* __restrict__ ptl) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t total = rd[n_refs - 1].node_off + rd[n_refs - 1].n_nodes;
+  if (g >= total || g >= cap) return;
+  const PairDesc& r = rd[ref_of_node(rd, n_refs, g)];
+  const uint4* nd = nodes + r.node_off;
+  const uint32_t v = g - r.node_off;
+  const uint4 a = nd[v];
+  if (a.w & 1u) return;  // odd depth: a slot of its parent's treelet
+  const uint32_t r0 = rank[r.node_off];
+  auto base_of = [&](uint32_t u) { return 1u + 4u * (rank[r.node_off + u] - r0); };
+  // treelet of an even-depth node u: 0 for the root, else its grandparent's base + k with
+  // k = 2 * (parent is the grandparent's right child) + (u is its parent's right child)
+  auto id_of = [&](uint32_t u) -> uint32_t {
+    if (u == 0) return 0u;
+    const uint32_t p = nd[u].z, gp = nd[p].z;
+    return base_of(gp) + 2u * (p != gp + 1 ? 1u : 0u) + (u != p + 1 ? 1u : 0u);
+  };
+  const uint32_t id = id_of(v);
+  if (id >= r.tl_cap) return;  // k_tl_check reports it
+  // parent of the treelet's root as a node id: the grandparent's treelet, slot of the parent
+  if (v == 0) {
+    ptl[r.tl_off + id] = 0xffffffffu;
+  } else {
+    const uint32_t p = a.z, gp = nd[p].z;
+    ptl[r.tl_off + id] = id_of(gp) << 2 | (p != gp + 1 ? 2u : 1u);
+  }
+  uint4 rec = make_uint4(tl_slot(a), 0u, 0u, a.y & 3u);
+  if ((a.y & 3u) != kLeaf) {
+    const uint4 L = nd[v + 1], R = nd[a.y >> 2];
+    rec.y = tl_slot(L);
+    rec.z = tl_slot(R);
+    rec.w |= ((L.y & 3u) << 2) | ((R.y & 3u) << 4);
+    if ((L.y & 3u) != kLeaf || (R.y & 3u) != kLeaf) rec.w |= base_of(v) << 6;
+  }
+  tl[r.tl_off + id] = rec;
+}
+
+// treelets used per reference within its allotment and addressable by the 26-bit base field;
+// leaf slots need count < 16 and bucket starts < 2^28
+__global__ void k_tl_check(int n_refs, const PairDesc* __restrict__ rd, const uint32_t* __restrict__ rank,
+                           int bucket, TreeCtl* ctl) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_refs) return;
+  const PairDesc& r = rd[i];
+  const uint32_t used = 1u + 4u * (rank[r.node_off + r.n_nodes] - rank[r.node_off]);
+  if (used > r.tl_cap || used >= (1u << 26) || bucket > 15 || r.n_ref >= (1u << 28)) atomicOr(&ctl->error, 4);
+}
+
+hipError_t launch_treelets(hipStream_t s, int n_refs, uint32_t cap, const PairDesc* rd, const uint4* nodes,
+                           int bucket, uint32_t* flag, uint32_t* rank, void* temp, size_t temp_bytes, uint4* tl,
+                           uint32_t* ptl, TreeCtl* ctl) {
+  if (n_refs <= 0 || cap == 0) return hipSuccess;
+  k_tl_flag<<<grid_of((size_t)cap + 1), 256, 0, s>>>(n_refs, cap + 1, rd, nodes, flag);
+  const hipError_t e = scan_u32(s, temp, temp_bytes, flag, rank, (size_t)cap + 1);
+  if (e != hipSuccess) return e;
+  k_tl_build<<<grid_of(cap), 256, 0, s>>>(n_refs, cap, rd, nodes, rank, tl, ptl);
+  k_tl_check<<<(n_refs + 63) / 64, 64, 0, s>>>(n_refs, rd, rank, bucket, ctl);
+  return hipGetLastError();
+}
 void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd) {
   k_pairs_from_refs<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, rd);
 }
