@@ -87,6 +87,16 @@ struct FarStack {
 };
 
 constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
+#ifndef AICP_NN_COOP
+#define AICP_NN_COOP 0  // Trav2C: 1 = cooperative octet bucket scan, 0 = each lane scans its own bucket
+#endif
+#ifndef AICP_NN_PREFMIN
+#define AICP_NN_PREFMIN 1  // Trav2C: per-depth running minimum of the far bounds in LDS (climb pruning)
+#endif
+constexpr int kPmDepth = 24;  // depths whose running minimum is kept (deeper levels climb unpruned)
+#ifndef AICP_NN_BUCKET_MIN
+#define AICP_NN_BUCKET_MIN 16  // Trav2S: lanes at a leaf before a cooperative bucket pass
+#endif
 
 template <int K>
 struct Trav {
@@ -231,6 +241,14 @@ struct Trav {
 // the owner the result of libnabo's in-order scan (first strictly smaller d^2 wins). Eight
 // rounds serve the octet's eight owners. The split into descend() / (wave-wide bucket) /
 // climb() keeps libnabo recurseKnn's visit order, far tests and counts.
+// one 16-byte treelet record as a single dwordx4: the empty asm keeps the compiler from narrowing
+// the load into the words used first plus a dependent load of the rest
+__device__ __forceinline__ uint4 ld_rec(const uint4* p) {
+  uint4 r = *p;
+  asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));
+  return r;
+}
+
 struct Trav2C {
   const uint4* tl;       // the pair's treelets
   const uint32_t* ptl;   // the pair's treelet parents
@@ -238,6 +256,8 @@ struct Trav2C {
   float q0, q1, q2;
   float off0, off1, off2, rd, minFar;
   int32_t n, start, sp, pl;  // node ids; pl: parent of the node the last descent ended in
+  int32_t dep;               // depth of n (descent) / of the node climbed from (climb)
+  uint16_t* pm;              // this lane's prefix-minimum column in LDS (AICP_NN_PREFMIN)
   uint32_t lb0, lcnt;        // bucket of the leaf the last descent ended in
   uint32_t tp, tn;
   Best<1> best;
@@ -257,6 +277,7 @@ struct Trav2C {
     off0 = off1 = off2 = rd = 0.f;
     n = start = sp = 0;
     pl = -1;
+    dep = 0;
     tp = tn = 0;
     best_init<1>(best);
   }
@@ -265,12 +286,20 @@ struct Trav2C {
     return s == 0 ? r.x : (s == 1 ? r.y : r.z);
   }
 
-  // one inner slot: fold its far bound into minFar, return true if the query goes right
+  // one inner slot: fold its far bound into minFar, return true if the query goes right. With
+  // AICP_NN_PREFMIN the running minimum after this level is kept per depth in LDS, rounded down
+  // to bf16 (the upper half of the float bits, exact for the skip test's direction): the climb
+  // then knows, before loading an ancestor, whether it or any level above it in this descent
+  // can still pass the far test.
   __device__ __forceinline__ bool decide(uint32_t w, uint32_t cd) {
     const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
     const float oc = sel3(cd, off0, off1, off2);
     minFar = fminf(minFar, rd + (-oc * oc + no * no));
     ++tn;
+#if AICP_NN_PREFMIN
+    if (dep < kPmDepth) pm[dep * kNNBlock] = (uint16_t)(__float_as_uint(minFar) >> 16);
+    ++dep;
+#endif
     return no > 0.f;
   }
 
@@ -279,7 +308,7 @@ struct Trav2C {
   __device__ __forceinline__ void descend() {
     minFar = __builtin_inff();
     uint32_t T = (uint32_t)n >> 2, s = (uint32_t)n & 3u;
-    uint4 r = tl[T];
+    uint4 r = ld_rec(tl + T);
     uint32_t w = r.x, cd = r.w & 3u;
     if (s == 0 && cd != kLeaf) {
       s = decide(w, cd) ? 2u : 1u;
@@ -294,7 +323,7 @@ struct Trav2C {
       pl = n;
       T = (r.w >> 6) + 2 * (s - 1) + (right ? 1u : 0u);
       n = (int32_t)(T << 2);
-      r = tl[T];
+      r = ld_rec(tl + T);
       w = r.x;
       cd = r.w & 3u;
       if (cd == kLeaf) break;
@@ -304,6 +333,29 @@ struct Trav2C {
     }
     lb0 = w & 0x0FFFFFFFu;
     lcnt = w >> 28;
+  }
+
+  // the whole bucket by this lane (AICP_NN_COOP 0): the first kLeafBatch points loaded before
+  // any is used, then scanned in order
+  __device__ __forceinline__ void bucket_lane(const float4* __restrict__ pts, float maxR2) {
+    float3 P[kLeafBatch];
+#pragma unroll
+    for (int i = 0; i < kLeafBatch; ++i)
+      if ((uint32_t)i < lcnt) {
+        const float4 p = pts[pbase + lb0 + i];
+        P[i] = make_float3(p.x, p.y, p.z);
+      }
+#pragma unroll
+    for (int i = 0; i < kLeafBatch; ++i)
+      if ((uint32_t)i < lcnt) {
+        const float d0 = q0 - P[i].x, d1 = q1 - P[i].y, d2 = q2 - P[i].z;
+        float dist = 0.f;
+        dist += d0 * d0;
+        dist += d1 * d1;
+        dist += d2 * d2;
+        if (dist <= maxR2 && dist < best.v[0]) best_replace<1>(best, (int32_t)(lb0 + i), dist);
+      }
+    bucket_tail(pts, maxR2);
   }
 
   // bucket points beyond the first kLeafBatch (bucket sizes above libnabo's default 8), in order
@@ -340,14 +392,27 @@ struct Trav2C {
         start = fs.start[sp];
         c = fs.P[sp];
         pc = fs.PP[sp];
+#if AICP_NN_PREFMIN
+        dep = (int32_t)((uint32_t)fs.F[sp] & 0x3fffffffu);
+#endif
         if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
         continue;
       }
       const int32_t p = pc;
+#if AICP_NN_PREFMIN
+      const int32_t dp = dep - 1;  // depth of p
+      if (dp < kPmDepth) {
+        const float bnd = __uint_as_float((uint32_t)pm[dp * kNNBlock] << 16);
+        if (!(bnd <= maxR2 && bnd * maxE2 < best.v[0])) {  // no level from start to p can pass
+          c = start;
+          continue;
+        }
+      }
+#endif
       const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
       if (T != cT) {  // the record and its root's parent, one round trip per treelet
         cT = T;
-        cr = tl[T];
+        cr = ld_rec(tl + T);
         cpp = (int32_t)ptl[T];
       }
       const uint4 r = cr;
@@ -361,7 +426,12 @@ struct Trav2C {
         const uint32_t fr = no > 0.f ? 0u : 1u;
         const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr))
                                    : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
+#if AICP_NN_PREFMIN
+        fs.F[sp] = (int32_t)((uint32_t)dp | (cd << 30));  // the far child is n; keep p's depth
+        dep = dp + 1;
+#else
         fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
+#endif
         fs.rd[sp] = rd;
         fs.old[sp] = oc;
         fs.mn[sp] = minFar;
@@ -380,7 +450,186 @@ struct Trav2C {
       }
       c = p;
       pc = pp;
+#if AICP_NN_PREFMIN
+      dep = dp;
+#endif
     }
+  }
+};
+
+// Trav2C's traversal as a per-lane state machine ("if-if"): every iteration of the persistent
+// loop each lane takes one step of its own phase -- a descent step (one treelet record, up to two
+// levels) or a climb step (one record: the node and, for a child slot, its treelet root) -- with
+// one record load instruction shared by both phases. Lanes that reach a leaf wait until enough of
+// the wave is at a leaf (or nothing else can step) and then scan their buckets in one
+// cooperative pass. While-while loops make a wave wait for its slowest lane at every phase; here
+// a lane's dependent chain advances every round trip (tools/wavesim.cpp: 23 instead of 41 round
+// trips per 64 queries). Visit order, far tests, counts and results are Trav2C's.
+enum : int32_t { kPhDesc = 0, kPhLeaf = 1, kPhClimb = 2 };
+
+struct Trav2S {
+  const uint4* tl;
+  const uint32_t* ptl;
+  uint32_t pbase;
+  float q0, q1, q2;
+  float off0, off1, off2, rd, minFar;
+  int32_t n, start, sp, pl;  // descent: current node, climb frame start, far-stack depth, parent of n
+  int32_t c, pc;             // climb: node climbed from, node to test next
+  int32_t ph;
+  uint32_t lb0, lcnt;
+  uint32_t tp, tn;
+  Best<1> best;
+
+  __device__ __forceinline__ void bind(const uint4* t, const uint32_t* b, uint32_t tl_off, uint32_t ref_off) {
+    tl = t + tl_off;
+    ptl = b + tl_off;
+    pbase = ref_off;
+  }
+  __device__ __forceinline__ float res_d2() const { return best.v[0]; }
+  __device__ __forceinline__ int32_t res_id() const { return best.id[0]; }
+
+  __device__ __forceinline__ void reset(float a, float b, float cc) {
+    q0 = a;
+    q1 = b;
+    q2 = cc;
+    off0 = off1 = off2 = rd = 0.f;
+    minFar = __builtin_inff();
+    n = start = sp = 0;
+    pl = -1;
+    c = pc = 0;
+    ph = kPhDesc;
+    tp = tn = 0;
+    best_init<1>(best);
+  }
+
+  __device__ __forceinline__ bool decide(uint32_t w, uint32_t cd) {
+    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
+    const float oc = sel3(cd, off0, off1, off2);
+    minFar = fminf(minFar, rd + (-oc * oc + no * no));
+    ++tn;
+    return no > 0.f;
+  }
+
+  // the record this lane needs this round: its descent node's or its next climb node's treelet
+  __device__ __forceinline__ uint32_t need() const { return (uint32_t)(ph == kPhDesc ? n : pc) >> 2; }
+
+  // one descent step with n's record: up to two levels, then the next treelet or the leaf
+  __device__ __forceinline__ void desc_step(const uint4& r) {
+    const uint32_t T = (uint32_t)n >> 2;
+    uint32_t s = (uint32_t)n & 3u, w, cd;
+    if (s == 0) {
+      w = r.x;
+      cd = r.w & 3u;
+      if (cd == kLeaf) {
+        lb0 = w & 0x0FFFFFFFu;
+        lcnt = w >> 28;
+        ph = kPhLeaf;
+        return;
+      }
+      s = decide(w, cd) ? 2u : 1u;
+      pl = n;
+      n = (int32_t)(T << 2 | s);
+    }
+    w = s == 1 ? r.y : r.z;
+    cd = (r.w >> (2 * s)) & 3u;
+    if (cd == kLeaf) {
+      lb0 = w & 0x0FFFFFFFu;
+      lcnt = w >> 28;
+      ph = kPhLeaf;
+      return;
+    }
+    const bool right = decide(w, cd);
+    pl = n;
+    n = (int32_t)(((r.w >> 6) + 2 * (s - 1) + (right ? 1u : 0u)) << 2);
+  }
+
+  __device__ __forceinline__ void bucket_tail(const float4* __restrict__ pts, float maxR2) {
+    for (uint32_t i = kLeafBatch; i < lcnt; ++i) {
+      const float4 p = pts[pbase + lb0 + i];
+      const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
+      float dist = 0.f;
+      dist += d0 * d0;
+      dist += d1 * d1;
+      dist += d2 * d2;
+      if (dist <= maxR2 && dist < best.v[0]) best_replace<1>(best, (int32_t)(lb0 + i), dist);
+    }
+    tp += lcnt;
+  }
+
+  // after the bucket: climb from the leaf unless no ancestor's far bound can pass
+  __device__ __forceinline__ void start_climb(float maxE2, float maxR2) {
+    c = n;
+    pc = pl;
+    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+    ph = kPhClimb;
+  }
+
+  // frames whose climb reached their start are popped without loads; true when the query is done
+  __device__ __forceinline__ bool climb_pops(FarStack& fs, float maxE2, float maxR2) {
+    while (c == start) {
+      if (sp == 0) return true;
+      --sp;
+      const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
+      rd = fs.rd[sp];
+      const float old = fs.old[sp];
+      if (pcd == 0) off0 = old;
+      else if (pcd == 1) off1 = old;
+      else off2 = old;
+      minFar = fs.mn[sp];
+      start = fs.start[sp];
+      c = fs.P[sp];
+      pc = fs.PP[sp];
+      if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+    }
+    return false;
+  }
+
+  // far test of node p (slot s of the record r); on a pass, push the frame and start the far
+  // descent. pp = p's parent.
+  __device__ __forceinline__ bool far_test(FarStack& fs, const uint4& r, int32_t p, uint32_t s, int32_t pp,
+                                           float maxE2, float maxR2) {
+    const uint32_t T = (uint32_t)p >> 2;
+    const uint32_t w = s == 0 ? r.x : (s == 1 ? r.y : r.z), cd = (r.w >> (2 * s)) & 3u;
+    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
+    const float oc = sel3(cd, off0, off1, off2);
+    const float rdf = rd + (-oc * oc + no * no);
+    if (!(rdf <= maxR2 && rdf * maxE2 < best.v[0])) return false;
+    const uint32_t fr = no > 0.f ? 0u : 1u;  // far child = the left one when the query is right of the cut
+    const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
+    fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
+    fs.rd[sp] = rd;
+    fs.old[sp] = oc;
+    fs.mn[sp] = minFar;
+    fs.start[sp] = start;
+    fs.P[sp] = p;
+    fs.PP[sp] = pp;
+    ++sp;
+    if (cd == 0) off0 = no;
+    else if (cd == 1) off1 = no;
+    else off2 = no;
+    rd = rdf;
+    n = far;
+    start = far;
+    pl = p;
+    minFar = __builtin_inff();
+    ph = kPhDesc;
+    return true;
+  }
+
+  // one climb step with pc's record r and its treelet root's parent rootpp: node pc, and if pc
+  // is a child slot and the climb goes on, its treelet root (same record)
+  __device__ __forceinline__ void climb_step(FarStack& fs, const uint4& r, int32_t rootpp, float maxE2,
+                                             float maxR2) {
+    const int32_t p = pc;
+    const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
+    const int32_t pp = s != 0 ? (int32_t)(T << 2) : rootpp;
+    if (far_test(fs, r, p, s, pp, maxE2, maxR2)) return;
+    c = p;
+    pc = pp;
+    if (s == 0 || c == start) return;
+    if (far_test(fs, r, pp, 0, rootpp, maxE2, maxR2)) return;
+    c = pp;
+    pc = rootpp;
   }
 };
 
@@ -390,6 +639,18 @@ struct is_coop {
 };
 template <>
 struct is_coop<Trav2C> {
+  static constexpr bool value = true;
+};
+template <>
+struct is_coop<Trav2S> {
+  static constexpr bool value = true;
+};
+template <class E>
+struct is_sm {
+  static constexpr bool value = false;
+};
+template <>
+struct is_sm<Trav2S> {
   static constexpr bool value = true;
 };
 
@@ -406,7 +667,8 @@ __device__ __forceinline__ float octet_min(float v) {
 // Wave-wide cooperative scan of the first kLeafBatch points of every active lane's bucket
 // (Trav2C). Called by all 64 lanes in wave-uniform control flow; `act` = the lane has a
 // bucket this round. xch = this wave's 64 exchange slots in LDS.
-__device__ __forceinline__ void coop_bucket(Trav2C& t, bool act, const float4* __restrict__ pts, float maxR2,
+template <class Eng>
+__device__ __forceinline__ void coop_bucket(Eng& t, bool act, const float4* __restrict__ pts, float maxR2,
                                             float4* xch) {
   const int lane = threadIdx.x & 63;
   const int oct = lane & ~7, i = lane & 7;
@@ -640,12 +902,45 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       pool += min(avail, (uint32_t)__popcll(needm));
     }
     if (__ballot(has) == 0) break;
-    if constexpr (is_coop<Eng>::value) {
-      __shared__ float4 xch_all[kNNBlock];
+    if constexpr (is_sm<Eng>::value) {
+      __shared__ float4 xch_sm[kNNBlock];
+      const bool leaf = has && t.ph == kPhLeaf;
+      const uint32_t n_leaf = (uint32_t)__popcll(__ballot(leaf));
+      const uint32_t n_step = (uint32_t)__popcll(__ballot(has && t.ph != kPhLeaf));
+      if (n_leaf != 0 && (n_leaf >= (uint32_t)AICP_NN_BUCKET_MIN || n_step == 0)) {
+        coop_bucket(t, leaf, pts, maxR2, xch_sm + (threadIdx.x & ~63));
+        if (leaf) {
+          t.bucket_tail(pts, maxR2);
+          t.start_climb(maxE2, maxR2);
+        }
+      }
+      if (has && t.ph == kPhClimb && t.climb_pops(fs, maxE2, maxR2)) {
+        done(my, t);
+        has = false;
+      }
+      if (has && t.ph != kPhLeaf) {
+        const uint32_t T = t.need();
+        const uint4 r = ld_rec(t.tl + T);
+        const int32_t rootpp = (int32_t)t.ptl[T];
+        if (t.ph == kPhDesc) t.desc_step(r);
+        else t.climb_step(fs, r, rootpp, maxE2, maxR2);
+      }
+    } else if constexpr (is_coop<Eng>::value) {
+#if AICP_NN_PREFMIN
+      __shared__ uint16_t pm_lds[kPmDepth * kNNBlock];
+      t.pm = pm_lds + threadIdx.x;
+#endif
       if (has) t.descend();
+#if AICP_NN_COOP
+      __shared__ float4 xch_all[kNNBlock];
       coop_bucket(t, has, pts, maxR2, xch_all + (threadIdx.x & ~63));
+#endif
       if (has) {
+#if AICP_NN_COOP
         t.bucket_tail(pts, maxR2);
+#else
+        t.bucket_lane(pts, maxR2);
+#endif
         if (t.climb(fs, maxE2, maxR2)) {
           done(my, t);
           has = false;
@@ -1495,14 +1790,14 @@ void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const Pa
                         uint32_t* ctr) {
   k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr);
 }
-// NN engine of the ICP matcher: 3 = Trav2C (default), 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
+// NN engine of the ICP matcher: 4 = Trav2S, 3 = Trav2C (default), 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
 // (design experiments, tools/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:
 // Trav<1> 230 us per NN launch, SM0 436 us (profiles/README.md).
 static int nn_engine() {
   static int e = -1;
   if (e < 0) {
     const char* v = getenv("AICP_NN_ENGINE");
-    e = (v && (v[0] == '0' || v[0] == '1' || v[0] == '3')) ? v[0] - '0' : 3;
+    e = (v && (v[0] == '0' || v[0] == '1' || v[0] == '3' || v[0] == '4')) ? v[0] - '0' : 3;
   }
   return e;
 }
@@ -1512,7 +1807,9 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
                    const float4* bpts, const uint32_t* ptl, int32_t* match, float* d2, uint32_t* touched,
                    uint32_t* ctr, const IcpParams& prm) {
   const int g = persistent_grid(grid_items, AICP_NN_WAVES);
-  if (nn_engine() == 3 && tl && ptl)
+  if (nn_engine() == 4 && tl && ptl)
+    k_icp_nn<Trav2S><<<g, 256, 0, s>>>(pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
+  else if (nn_engine() == 3 && tl && ptl)
     k_icp_nn<Trav2C><<<g, 256, 0, s>>>(pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
   else if (nn_engine() >= 1)
     k_icp_nn<Trav<1>><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, nullptr, match, d2, touched, ctr,

@@ -183,6 +183,49 @@ int main(int argc, char** argv) {
       printf("  rounds histogram:"); for (int i = 1; i < 10; ++i) printf(" %d:%.1f%%", i, 100.0 * hr[i] / N); printf("\n");
     }
   }
+  // "if-if" replay: every iteration each lane takes one step of its own phase (a descent record,
+  // a climb load); lanes at a leaf wait until at least B lanes are at leaves (or no lane can step),
+  // then one cooperative bucket pass (1 tick, 8 instructions) serves all of them.
+  for (int g = 0; g < 1; ++g)
+    for (int B : {1, 8, 16, 32, 64}) {
+      size_t next = 0;
+      struct Lane { int q = -1; size_t r = 0; int ph = 0; int k = 0; };  // ph 0 descent, 1 at leaf, 2 climb
+      std::vector<Lane> L(64);
+      double ticks = 0, ins = 0, lanesteps = 0;
+      for (;;) {
+        bool any = false, refill = false;
+        for (auto& l : L) {
+          if (l.q < 0 && next < (size_t)N) { l.q = (int)next++; l.r = 0; l.ph = 0; l.k = 0; refill = true; }
+          if (l.q >= 0) any = true;
+        }
+        if (!any) break;
+        if (refill) ins += 1;
+        int atleaf = 0, stepping = 0;
+        for (auto& l : L) if (l.q >= 0) { if (l.ph == 1) ++atleaf; else ++stepping; }
+        if (atleaf > 0 && (atleaf >= B || stepping == 0)) {
+          ticks += 1; ins += 8;
+          for (auto& l : L) if (l.q >= 0 && l.ph == 1) { l.ph = 2; l.k = 0; }
+        }
+        // one step for every lane in descent or climb
+        bool d = false, c = false;
+        for (auto& l : L) {
+          if (l.q < 0) continue;
+          const Round& R = Q[g][l.q][l.r];
+          if (l.ph == 0) { d = true; lanesteps++; if (++l.k >= R.desc) { l.ph = 1; } }
+          else if (l.ph == 2) {
+            if (l.k < R.climb) { c = true; lanesteps++; ++l.k; }
+            if (l.k >= R.climb) {
+              l.r++; l.k = 0;
+              if (l.r >= Q[g][l.q].size()) l.q = -1; else l.ph = 0;
+            }
+          }
+        }
+        if (d || c) ticks += 1;
+        ins += (d ? 1 : 0) + (c ? 1 : 0);
+      }
+      const double W = N / 64.0;
+      printf("if-if B %2d: ticks per 64 queries %.1f, instructions %.1f, lane utilisation %.2f\n", B, ticks / W, ins / W, lanesteps / (64.0 * ticks));
+    }
   // wave replay of the current kernel (descent to the leaf, cooperative bucket, climb), counting
   // wave-instructions and distinct 128-B lines (TA tag work) per phase
   for (int g = 0; g < 2; ++g) {
