@@ -176,8 +176,9 @@ def _fptr(a):
 def as_points(p) -> np.ndarray:
     """float32 array of shape (N, W), C-contiguous, xyz in the first 3 floats of each row:
     W = 3 packed, 4 = pcl::PointXYZ (16 B), 8 = PointXYZRGB (32 B), 12 = PointXYZRGBNormal (48 B)
-    (the registerClouds overloads, abstract_registrator.hpp:10-12). The row stride is passed
-    through the C-ABI, so no copy is made for these layouts."""
+    (the point types of the registerClouds overloads, abstract_registrator.hpp:10-12; the
+    XYZRGBNormal overload is a no-op in the reference, see registration.HipRegistration). The
+    row stride is passed through the C-ABI, so no copy is made for these layouts."""
     a = np.ascontiguousarray(p, dtype=np.float32)
     if a.ndim != 2 or a.shape[1] not in (3, 4, 8, 12):
         raise ValueError("points must be (N, 3|4|8|12) float32 rows (PointXYZ / XYZRGB / XYZRGBNormal)")

@@ -711,6 +711,16 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     for (size_t g = 0; g < G; ++g)
       if (!size_map(ctx->pin_gstate.as<PairState>()[g], ho[P + g]))
         FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
+    // all maps of the batch at once: at most half the free device memory (beyond what the
+    // arena already holds), so a few far outlier points fail this batch with a clear error
+    // instead of an allocation failure
+    size_t free_b = 0, total_b = 0;
+    HIPC(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t limit = ctx->bitmap.cap + free_b / 2;
+    if (bm_bytes > limit)
+      FAIL(AICP_ERR_UNSUPPORTED, "overlap voxel maps need " + std::to_string(bm_bytes >> 20) + " MiB, more than " +
+                                     std::to_string(limit >> 20) +
+                                     " MiB available: far outlier points? crop the clouds or split the batch");
     HIPC(ensure(ctx->bitmap, bm_bytes));
     HIPC(hipMemcpyAsync(ctx->ovl.p, ho, (P + G) * sizeof(OvlDesc), hipMemcpyHostToDevice, s));
     HIPC(hipEventRecord(ctx->ev[6], s));

@@ -10,8 +10,10 @@ Reference interfaces (zbqq/aicp_mapping):
   App::computeOverlap / computeRegistration / runAicpPipeline
                         aicp_core/src/registration/app.cpp:112-141,187-247
 
-Same method names, argument meaning and error behaviour: clouds are (N, 3) or (N, 4) float32
-arrays (pcl::PointXYZ layout), transforms 4x4 row-major numpy (Eigen::Matrix4f values), a
+Same method names, argument meaning and error behaviour: clouds are float32 rows of width 3
+(packed xyz), 4, 8 or 12 (pcl::PointXYZ / PointXYZRGB / PointXYZRGBNormal, 16 / 32 / 48 B; the
+XYZRGBNormal overload is the reference's no-op stub, pointmatcher_registration.cpp:35-44),
+transforms 4x4 row-major numpy (Eigen::Matrix4f values), a
 ConvergenceError propagates exactly where libpointmatcher's would (uncaught at app.cpp:210),
 an unknown registration type prints an error and yields None.
 """
@@ -88,7 +90,7 @@ class HipRegistration(AbstractRegistrator):
 
     def __init__(self, params: RegistrationParams, ctx: Context | None = None):
         self.params_ = params
-        self.ctx = ctx or default_context()
+        self._ctx = ctx
         self.cfg = _lib.default_config()
         self.stats = None
         self._read = None
@@ -107,13 +109,26 @@ class HipRegistration(AbstractRegistrator):
             raise _lib.AicpError(rc, f"unsupported chain in {path}")
         self.cfg = cfg
 
+    @property
+    def ctx(self) -> Context:  # the HIP context is created on first use
+        if self._ctx is None:
+            self._ctx = default_context()
+        return self._ctx
+
     def updateConfigParams(self, config_name: str):
         self.params_.pointmatcher.configFileName = config_name
 
     def registerClouds(self, cloud_ref, cloud_read, final_transform=None):
-        """Returns T (4x4); if final_transform (4x4 array) is given it is filled in place."""
+        """Returns T (4x4); if final_transform (4x4 array) is given it is filled in place.
+
+        PointXYZRGBNormal rows (width 12): the reference's overload is a commented-out stub
+        (pointmatcher_registration.cpp:35-44) that leaves final_transform as it is, and so does
+        this one (returns final_transform unchanged, None if not given). The C-ABI itself reads
+        48-byte rows like any other stride (aicp_pair.ref_stride)."""
         ref = _lib.as_points(cloud_ref)
         read = _lib.as_points(cloud_read)
+        if ref.shape[1] == 12 or read.shape[1] == 12:
+            return final_transform
         self.applyConfig()
         T, stats, rc = self.ctx.align_batch([dict(ref=ref, read=read)], self.cfg, flags=AICP_RUN_ICP,
                                             raise_on_error=False)

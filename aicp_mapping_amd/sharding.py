@@ -42,15 +42,40 @@ def pack_records(T: np.ndarray, iterations, inlier_ratio) -> np.ndarray:
     return rec
 
 
-def gather_records(rec: np.ndarray, dist, device="cpu") -> np.ndarray:
-    """All-gather equally sized per-rank record blocks; returns (world * P, 18) in rank order."""
+def gather_records(rec: np.ndarray, dist, device="cpu", pair_index=None) -> np.ndarray:
+    """All-gather per-rank record blocks of any size; returns (n_total, 18) ordered by global
+    pair index.
+
+    Ranks may hold different pair counts (i mod G with n_total % G != 0, or LPT shards), and a
+    collective needs equal shapes, so every block is padded to the largest count. Each row
+    carries its global pair index in an extra column (-1 on padding rows); the padding is
+    dropped and the rows sorted by index after the gather. pair_index: the global index of each
+    local row (default: rank-major, i.e. the counts of lower ranks + 0..P-1)."""
     import torch
 
-    t = torch.from_numpy(np.ascontiguousarray(rec, dtype=np.float32)).to(device)
-    world = dist.get_world_size()
+    rec = np.ascontiguousarray(rec, dtype=np.float32).reshape(-1, RECORD_FLOATS)
+    n = rec.shape[0]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    cnt = torch.tensor([n], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    counts = [int(c.item()) for c in counts]
+    if pair_index is None:
+        pair_index = sum(counts[:rank]) + np.arange(n)
+    pair_index = np.asarray(pair_index, dtype=np.int64)
+    if pair_index.shape != (n,):
+        raise ValueError("one pair index per record")
+    m = max(counts)
+    buf = np.full((m, RECORD_FLOATS + 1), -1.0, np.float64)
+    buf[:n, :RECORD_FLOATS] = rec
+    buf[:n, RECORD_FLOATS] = pair_index
+    t = torch.from_numpy(buf).to(device)
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t)
-    return torch.cat(out, 0).cpu().numpy()
+    allr = torch.cat(out, 0).cpu().numpy()
+    allr = allr[allr[:, RECORD_FLOATS] >= 0]
+    allr = allr[np.argsort(allr[:, RECORD_FLOATS], kind="stable")]
+    return allr[:, :RECORD_FLOATS].astype(np.float32)
 
 
 def max_over_ranks(value: float, dist, device="cpu") -> float:

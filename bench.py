@@ -90,9 +90,11 @@ def make_c4_pairs(n_readings, n_points, map_points, crop, seed):
     return out, len(mp)
 
 
-def cpu_baseline(pairs, res, budget_s):
+def cpu_baseline(pairs, res, budget_s, cfg_ratio, run_overlap, workload):
     """The oracle (single-thread C++ restatement of the libpointmatcher chain) on a bounded sample
-    of the same workload: whole pairs (overlap + ratio + ICP), as many as fit the budget."""
+    of the same workload as the GPU run: whole pairs, as many as fit the budget. With the overlap
+    (C2, C3, C5) each pair runs overlap -> auto-tuned ratio -> ICP like the device; without it
+    (C4: localization against the map, overlap fixed) ICP runs at the configured ratio."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
 
@@ -102,8 +104,10 @@ def cpu_baseline(pairs, res, budget_s):
     Ts = []
     t0 = time.perf_counter()
     for p in pairs:
-        ov, _ = po.overlap(p["ref"], p["ref_origin"], p["read"], p["read_origin"], res)
-        ratio = po.autotune_ratio(ov)
+        ratio = cfg_ratio
+        if run_overlap:
+            ov, _ = po.overlap(p["ref"], p["ref_origin"], p["read"], p["read_origin"], res)
+            ratio = po.autotune_ratio(ov)
         rc, T, st = po.icp(p["ref"], p["read"], po.default_config(trimmed_ratio=ratio))
         Ts.append(T)
         done += 1
@@ -111,9 +115,11 @@ def cpu_baseline(pairs, res, budget_s):
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
+    steps = "overlap + ratio + ICP" if run_overlap else "ICP at r = %.2f" % cfg_ratio
     return dict(value=done / dt, unit="aligned_clouds/s", cores=1, kind="port",
-                sample=f"{done} C2 pair(s) (N=M={pairs[0]['ref'].shape[0]}) end to end on 1 host core "
-                       f"({cpu_model()}, nproc {os.cpu_count()}); {iters} ICP iterations in {dt:.1f} s",
+                sample=f"first {done} pair(s) of [{workload}] ({steps}, N={pairs[0]['read'].shape[0]}, "
+                       f"M={pairs[0]['ref'].shape[0]}) on 1 host core ({cpu_model()}, nproc {os.cpu_count()}); "
+                       f"{iters} ICP iterations in {dt:.1f} s",
                 icp_iters_per_s=iters / dt), Ts
 
 
@@ -216,12 +222,17 @@ def main():
     ctx = L.Context(local_rank)
     batch = ctx.upload(pairs)
 
+    # global index of each local pair for the result gather (C5: the i mod G shard; the other
+    # configs: every rank its own sequence, rank-major)
+    pair_index = (sh.shard_pairs(extra["pairs_total"], world, rank) if args.config == "c5" and not args.data
+                  else None)
+
     def gather():
         if dist is None:
             return None
         st = batch.stats
         rec = sh.pack_records(batch.outT, [s.iterations for s in st], [s.inlier_ratio for s in st])
-        return sh.gather_records(rec, dist, device="cuda")
+        return sh.gather_records(rec, dist, device="cuda", pair_index=pair_index)
 
     def sync():
         if dist is not None:
@@ -305,7 +316,7 @@ def main():
                         "synthetic pairs; the oracle reproduces the same transforms (parity_vs_oracle)"}
             if errs else None,
             "roofline": {
-                "kernel": "k_icp_nn (transform + libnabo-order 1-NN + digit-1 histogram)",
+                "kernel": "k_icp_nn (transform + libnabo-order 1-NN over treelets + bucket scan)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -318,7 +329,8 @@ def main():
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            cb, Ts = cpu_baseline(pairs, res, args.cpu_budget)
+            cb, Ts = cpu_baseline(pairs, res, args.cpu_budget, float(cfg.trimmed_ratio),
+                                  bool(flags & L.AICP_RUN_OVERLAP), workload)
             out["cpu_baseline"] = cb
             # parity of this run's transforms against the oracle's (reference normal semantics)
             pe = [sy.rot_err(To, Tg) for To, Tg in zip(Ts, batch.transforms())]

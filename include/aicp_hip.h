@@ -78,7 +78,8 @@ typedef struct {
 typedef struct {
   const float* ref;      /* reference cloud, x,y,z at ref_stride bytes            */
   uint64_t n_ref;
-  uint64_t ref_stride;   /* bytes between points; 12 (packed) or 16 (PointXYZ)   */
+  uint64_t ref_stride;   /* bytes between points: 12 packed, 16 / 32 / 48 =      */
+                         /* pcl::PointXYZ / PointXYZRGB / PointXYZRGBNormal rows   */
   const float* read;     /* reading cloud                                         */
   uint64_t n_read;
   uint64_t read_stride;

@@ -141,6 +141,32 @@ def test_overlap_identical_clouds_is_100(ctx, L):
     assert st[0]["overlap_percent"] == 100.0
 
 
+def test_overlap_far_outlier(ctx, oracle, L):
+    """One return 300 m away (a long ray, a wide key box): counts still equal the oracle's."""
+    pr = sy.make_pair(6000, 6000, seed=31)
+    read = np.vstack([pr.read, [[300.0, 2.0, 1.0]]]).astype(np.float32)
+    _, st, rc = ctx.align_batch([dict(ref=pr.ref, read=read, ref_origin=pr.ref_origin,
+                                      read_origin=pr.read_origin)], flags=L.AICP_RUN_OVERLAP, resolution=RES)
+    ov, cnt = oracle.overlap(pr.ref, pr.ref_origin, read, pr.read_origin, RES)
+    assert rc == 0
+    assert st[0]["overlap_keys"] == [int(c) for c in cnt]
+
+
+def test_overlap_extreme_outlier_refused_cleanly(ctx, L):
+    """A return kilometres away in every axis would need a voxel map beyond the device's memory:
+    the batch fails with AICP_ERR_UNSUPPORTED and a message, and the context keeps working."""
+    pr = sy.make_pair(3000, 3000, seed=32)
+    read = np.vstack([pr.read, [[5000.0, 5000.0, 5000.0]]]).astype(np.float32)
+    _, _, rc = ctx.align_batch([dict(ref=pr.ref, read=read, ref_origin=pr.ref_origin,
+                                     read_origin=pr.read_origin)], flags=L.AICP_RUN_OVERLAP,
+                               resolution=RES, raise_on_error=False)
+    assert rc == L.AICP_ERR_UNSUPPORTED
+    assert "voxel map" in ctx.last_error()
+    _, st, rc = ctx.align_batch([dict(ref=pr.ref, read=pr.read, ref_origin=pr.ref_origin,
+                                      read_origin=pr.read_origin)], flags=L.AICP_RUN_OVERLAP, resolution=RES)
+    assert rc == 0 and st[0]["overlap_percent"] > 0
+
+
 # ---------------------------------------------------------------- whole ICP ---------------
 def _icp_case(ctx, oracle, pr, ratio, eps=3.16, T0=None):
     cfg = ctx_cfg = None

@@ -187,7 +187,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, n_pairs):
     import torch.distributed as dist
 
     from aicp_mapping_amd import sharding as sh
@@ -195,36 +195,43 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        idx = sh.shard_pairs(6, world, rank)
+        idx = sh.shard_pairs(n_pairs, world, rank)
         T = np.stack([np.eye(4, dtype=np.float32).T.reshape(-1) + i for i in idx])
         rec = sh.pack_records(T, [10 + i for i in idx], [0.5 + 0.01 * i for i in idx])
-        out = sh.gather_records(rec, dist)
+        by_index = sh.gather_records(rec, dist, pair_index=idx)
+        rank_major = sh.gather_records(rec, dist)
         m = sh.max_over_ranks(float(rank + 1), dist)
         s = sh.sum_over_ranks(float(rank + 1), dist)
-        q.put((rank, out, m, s))
+        q.put((rank, by_index, rank_major, m, s))
     finally:
         dist.destroy_process_group()
 
 
-def test_gloo_world2_gather_records():
+@pytest.mark.parametrize("n_pairs", [6, 5])
+def test_gloo_world2_gather_records(n_pairs):
+    """Result records of independent pairs gathered over 2 ranks, also when the i mod G split
+    leaves the ranks with different pair counts (5 pairs: 3 + 2, padded for the collective)."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, n_pairs)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(2)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, out, m, s in res:
-        assert out.shape == (6, 18)
-        # rank order: rank 0's pairs {0,2,4}, then rank 1's {1,3,5}
-        order = [0, 2, 4, 1, 3, 5]
-        np.testing.assert_array_equal(out[:, 16], [10 + i for i in order])
-        np.testing.assert_allclose(out[:, 0], [1 + i for i in order])
+    for rank, by_index, rank_major, m, s in res:
+        assert by_index.shape == (n_pairs, 18) and rank_major.shape == (n_pairs, 18)
+        # with the shard's pair indices: global pair order
+        np.testing.assert_array_equal(by_index[:, 16], [10 + i for i in range(n_pairs)])
+        np.testing.assert_allclose(by_index[:, 0], [1 + i for i in range(n_pairs)])
+        np.testing.assert_allclose(by_index[:, 17], [0.5 + 0.01 * i for i in range(n_pairs)], rtol=1e-6)
+        # default: rank-major (rank 0's pairs 0, 2, 4, then rank 1's 1, 3, ...)
+        order = list(range(0, n_pairs, 2)) + list(range(1, n_pairs, 2))
+        np.testing.assert_array_equal(rank_major[:, 16], [10 + i for i in order])
         assert m == 2.0 and s == 3.0
 
 
@@ -239,3 +246,18 @@ def test_as_points_pcl_layouts(L):
     for w in (2, 5, 16):
         with pytest.raises(ValueError):
             L.as_points(np.zeros((5, w), np.float32))
+
+
+def test_xyzrgbnormal_register_is_reference_noop():
+    """registerClouds over PointXYZRGBNormal rows leaves final_transform unchanged, as the
+    reference's commented-out overload does (pointmatcher_registration.cpp:35-44); no device
+    work is started (runs without a GPU)."""
+    from aicp_mapping_amd import registration as R
+
+    reg = R.create_registrator(R.RegistrationParams(type="HIP"))
+    pts = np.zeros((100, 12), np.float32)
+    T = np.arange(16, dtype=np.float32).reshape(4, 4)
+    out = reg.registerClouds(pts, pts, T)
+    assert out is T and np.array_equal(T, np.arange(16, dtype=np.float32).reshape(4, 4))
+    assert reg.registerClouds(pts, pts) is None
+    assert reg._ctx is None
