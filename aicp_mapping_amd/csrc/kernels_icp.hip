@@ -93,7 +93,7 @@ constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #ifndef AICP_NN_PREFMIN
 #define AICP_NN_PREFMIN 0  // Trav2C: per-depth running minimum of the far bounds in LDS (climb pruning; off: C2 -1 %, C4 +20 %)
 #endif
-constexpr int kPmDepth = 24;  // depths whose running minimum is kept (deeper levels climb unpruned)
+[[maybe_unused]] constexpr int kPmDepth = 24;  // depths whose running minimum is kept (deeper levels climb unpruned)
 #ifndef AICP_NN_BUCKET_MIN
 #define AICP_NN_BUCKET_MIN 16  // Trav2S: lanes at a leaf before a cooperative bucket pass
 #endif
@@ -249,12 +249,20 @@ __device__ __forceinline__ uint4 ld_rec(const uint4* p) {
   return r;
 }
 
+// Running minimum of far bounds: every bound is rd + (-off^2 + no^2) with |no| >= |off| (the
+// region shrinks away from the query), so it is >= 0 and a signed integer minimum of the float
+// bits is the float minimum (one v_min_i32, no NaN canonicalisation). A negative bound, if
+// rounding ever produced one, only makes the minimum negative, i.e. forces the exact climb.
+__device__ __forceinline__ float min_bound(float a, float b) {
+  return __int_as_float(min(__float_as_int(a), __float_as_int(b)));
+}
+
 struct Trav2C {
   const uint4* tl;       // the pair's treelets
   const uint32_t* ptl;   // the pair's treelet parents
   uint32_t pbase;        // the pair's first bucket point
   float q0, q1, q2;
-  float off0, off1, off2, rd, minFar;
+  float noc0, noc1, noc2, rd, minFar;  // noc = -(off * off) per axis (libnabo's off[] enters only so)
   int32_t n, start, sp, pl;  // node ids; pl: parent of the node the last descent ended in
   int32_t dep;               // depth of n (descent) / of the node climbed from (climb)
   uint16_t* pm;              // this lane's prefix-minimum column in LDS (AICP_NN_PREFMIN)
@@ -274,7 +282,7 @@ struct Trav2C {
     q0 = a;
     q1 = b;
     q2 = c;
-    off0 = off1 = off2 = rd = 0.f;
+    noc0 = noc1 = noc2 = rd = 0.f;
     n = start = sp = 0;
     pl = -1;
     dep = 0;
@@ -293,8 +301,7 @@ struct Trav2C {
   // can still pass the far test.
   __device__ __forceinline__ bool decide(uint32_t w, uint32_t cd) {
     const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
-    const float oc = sel3(cd, off0, off1, off2);
-    minFar = fminf(minFar, rd + (-oc * oc + no * no));
+    minFar = min_bound(minFar, rd + (sel3(cd, noc0, noc1, noc2) + no * no));
     ++tn;
 #if AICP_NN_PREFMIN
     if (dep < kPmDepth) pm[dep * kNNBlock] = (uint16_t)(__float_as_uint(minFar) >> 16);
@@ -385,9 +392,9 @@ struct Trav2C {
         const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
         rd = fs.rd[sp];
         const float old = fs.old[sp];
-        if (pcd == 0) off0 = old;
-        else if (pcd == 1) off1 = old;
-        else off2 = old;
+        if (pcd == 0) noc0 = old;
+        else if (pcd == 1) noc1 = old;
+        else noc2 = old;
         minFar = fs.mn[sp];
         start = fs.start[sp];
         c = fs.P[sp];
@@ -419,8 +426,8 @@ struct Trav2C {
       const int32_t pp = s != 0 ? (int32_t)(T << 2) : cpp;  // parent of p
       const uint32_t w = slot_word(r, s), cd = (r.w >> (2 * s)) & 3u;
       const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
-      const float oc = sel3(cd, off0, off1, off2);
-      const float rdf = rd + (-oc * oc + no * no);
+      const float oc = sel3(cd, noc0, noc1, noc2);
+      const float rdf = rd + (oc + no * no);
       if (rdf <= maxR2 && rdf * maxE2 < best.v[0]) {
         // far child = the left one when the query is right of the cut
         const uint32_t fr = no > 0.f ? 0u : 1u;
@@ -439,9 +446,10 @@ struct Trav2C {
         fs.P[sp] = p;
         fs.PP[sp] = pp;
         ++sp;
-        if (cd == 0) off0 = no;
-        else if (cd == 1) off1 = no;
-        else off2 = no;
+        const float nn = -no * no;
+        if (cd == 0) noc0 = nn;
+        else if (cd == 1) noc1 = nn;
+        else noc2 = nn;
         rd = rdf;
         n = far;
         start = far;
