@@ -790,6 +790,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       launch_icp_update(s, (int)P, dDesc, dState, ctx->slab.as<double>(), prm);
     }
     launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
+    if (std::getenv("AICP_NN_PROF_DUMP")) {
+      HIPC(hipStreamSynchronize(s));
+      nn_prof_dump();
+    }
   } else {
     HIPC(hipEventRecord(ctx->ev[8], s));
     HIPC(hipEventRecord(ctx->ev[10], s));

@@ -50,6 +50,9 @@ void launch_icp_update(hipStream_t s, int n_pairs, const PairDesc* pd, PairState
 void launch_finalize(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
                      float* outT);
 
+// AICP_NN_PROF builds: print and reset the NN kernel's per-phase cycle shares (stderr)
+void nn_prof_dump();
+
 // ---- kernel-level entry points ----------------------------------------------------------
 bool launch_knn_generic(hipStream_t s, uint32_t nq, const float4* q, const uint4* nodes,
                         const int32_t* parent, const float4* bpts, int k, float maxE2,

@@ -18,6 +18,8 @@
 // covariance / eigen work per point).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include <cstdlib>
 
 #include "aicp_common.hpp"
@@ -79,11 +81,15 @@ __device__ __forceinline__ float sel3(uint32_t cd, float a, float b, float c) {
 
 // Far-descent stack: the only dynamically indexed state (private/scratch memory, touched only
 // on far descents); kept apart from Trav so the rest of the traversal stays in registers.
+// One 32-byte frame per far descent, so a push or pop moves 16-byte scratch words instead of
+// seven separate dwords (NN launch -5 %).
+struct FarFrame {
+  int32_t F;
+  float rd, old, mn;
+  int32_t start, P, PP, pad;  // P: node whose far child began the frame, PP: its parent
+};
 struct FarStack {
-  int32_t F[kFarStack];
-  float rd[kFarStack], old[kFarStack], mn[kFarStack];
-  int32_t start[kFarStack];
-  int32_t P[kFarStack], PP[kFarStack];  // node whose far child began the frame, and its parent
+  FarFrame f[kFarStack];
 };
 
 constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
@@ -184,16 +190,16 @@ struct Trav {
       if (c == start) {
         if (sp == 0) return true;
         --sp;
-        const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
-        rd = fs.rd[sp];
-        const float old = fs.old[sp];
+        const uint32_t pcd = (uint32_t)fs.f[sp].F >> 30;
+        rd = fs.f[sp].rd;
+        const float old = fs.f[sp].old;
         if (pcd == 0) off0 = old;
         else if (pcd == 1) off1 = old;
         else off2 = old;
-        minFar = fs.mn[sp];
-        start = fs.start[sp];
-        c = fs.P[sp];
-        pc = fs.PP[sp];
+        minFar = fs.f[sp].mn;
+        start = fs.f[sp].start;
+        c = fs.f[sp].P;
+        pc = fs.f[sp].PP;
         if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
         continue;
       }
@@ -205,13 +211,13 @@ struct Trav {
       const float rdf = rd + (-oc * oc + no * no);
       if (rdf <= maxR2 && rdf * maxE2 < best.v[K - 1]) {
         const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
-        fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
-        fs.rd[sp] = rd;
-        fs.old[sp] = oc;
-        fs.mn[sp] = minFar;
-        fs.start[sp] = start;
-        fs.P[sp] = p;
-        fs.PP[sp] = (int32_t)pn.z;
+        fs.f[sp].F = (int32_t)((uint32_t)far | (cd << 30));
+        fs.f[sp].rd = rd;
+        fs.f[sp].old = oc;
+        fs.f[sp].mn = minFar;
+        fs.f[sp].start = start;
+        fs.f[sp].P = p;
+        fs.f[sp].PP = (int32_t)pn.z;
         ++sp;
         if (cd == 0) off0 = no;
         else if (cd == 1) off1 = no;
@@ -389,18 +395,18 @@ struct Trav2C {
       if (c == start) {
         if (sp == 0) return true;
         --sp;
-        const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
-        rd = fs.rd[sp];
-        const float old = fs.old[sp];
+        const uint32_t pcd = (uint32_t)fs.f[sp].F >> 30;
+        rd = fs.f[sp].rd;
+        const float old = fs.f[sp].old;
         if (pcd == 0) noc0 = old;
         else if (pcd == 1) noc1 = old;
         else noc2 = old;
-        minFar = fs.mn[sp];
-        start = fs.start[sp];
-        c = fs.P[sp];
-        pc = fs.PP[sp];
+        minFar = fs.f[sp].mn;
+        start = fs.f[sp].start;
+        c = fs.f[sp].P;
+        pc = fs.f[sp].PP;
 #if AICP_NN_PREFMIN
-        dep = (int32_t)((uint32_t)fs.F[sp] & 0x3fffffffu);
+        dep = (int32_t)((uint32_t)fs.f[sp].F & 0x3fffffffu);
 #endif
         if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
         continue;
@@ -434,17 +440,17 @@ struct Trav2C {
         const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr))
                                    : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
 #if AICP_NN_PREFMIN
-        fs.F[sp] = (int32_t)((uint32_t)dp | (cd << 30));  // the far child is n; keep p's depth
+        fs.f[sp].F = (int32_t)((uint32_t)dp | (cd << 30));  // the far child is n; keep p's depth
         dep = dp + 1;
 #else
-        fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
+        fs.f[sp].F = (int32_t)((uint32_t)far | (cd << 30));
 #endif
-        fs.rd[sp] = rd;
-        fs.old[sp] = oc;
-        fs.mn[sp] = minFar;
-        fs.start[sp] = start;
-        fs.P[sp] = p;
-        fs.PP[sp] = pp;
+        fs.f[sp].rd = rd;
+        fs.f[sp].old = oc;
+        fs.f[sp].mn = minFar;
+        fs.f[sp].start = start;
+        fs.f[sp].P = p;
+        fs.f[sp].PP = pp;
         ++sp;
         const float nn = -no * no;
         if (cd == 0) noc0 = nn;
@@ -577,16 +583,16 @@ struct Trav2S {
     while (c == start) {
       if (sp == 0) return true;
       --sp;
-      const uint32_t pcd = (uint32_t)fs.F[sp] >> 30;
-      rd = fs.rd[sp];
-      const float old = fs.old[sp];
+      const uint32_t pcd = (uint32_t)fs.f[sp].F >> 30;
+      rd = fs.f[sp].rd;
+      const float old = fs.f[sp].old;
       if (pcd == 0) off0 = old;
       else if (pcd == 1) off1 = old;
       else off2 = old;
-      minFar = fs.mn[sp];
-      start = fs.start[sp];
-      c = fs.P[sp];
-      pc = fs.PP[sp];
+      minFar = fs.f[sp].mn;
+      start = fs.f[sp].start;
+      c = fs.f[sp].P;
+      pc = fs.f[sp].PP;
       if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
     }
     return false;
@@ -604,13 +610,13 @@ struct Trav2S {
     if (!(rdf <= maxR2 && rdf * maxE2 < best.v[0])) return false;
     const uint32_t fr = no > 0.f ? 0u : 1u;  // far child = the left one when the query is right of the cut
     const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
-    fs.F[sp] = (int32_t)((uint32_t)far | (cd << 30));
-    fs.rd[sp] = rd;
-    fs.old[sp] = oc;
-    fs.mn[sp] = minFar;
-    fs.start[sp] = start;
-    fs.P[sp] = p;
-    fs.PP[sp] = pp;
+    fs.f[sp].F = (int32_t)((uint32_t)far | (cd << 30));
+    fs.f[sp].rd = rd;
+    fs.f[sp].old = oc;
+    fs.f[sp].mn = minFar;
+    fs.f[sp].start = start;
+    fs.f[sp].P = p;
+    fs.f[sp].PP = pp;
     ++sp;
     if (cd == 0) off0 = no;
     else if (cd == 1) off1 = no;
@@ -822,13 +828,13 @@ struct SM0 {
       if (rdf <= R && rdf * E < bestd) {
         const int32_t far = (no > 0.f) ? n + 1 : (int32_t)(v.y >> 2);
         const int k = sp;
-        fs.F[k] = (int32_t)((uint32_t)far | (cd << 30));
-        fs.rd[k] = rd;
-        fs.old[k] = oc;
-        fs.mn[k] = minFar;
-        fs.start[k] = start;
-        fs.P[k] = n;
-        fs.PP[k] = (int32_t)v.z;
+        fs.f[k].F = (int32_t)((uint32_t)far | (cd << 30));
+        fs.f[k].rd = rd;
+        fs.f[k].old = oc;
+        fs.f[k].mn = minFar;
+        fs.f[k].start = start;
+        fs.f[k].P = n;
+        fs.f[k].PP = (int32_t)v.z;
         sp = k + 1;
         set_off(cd, no);
         rd = rdf;
@@ -849,16 +855,23 @@ struct SM0 {
       }
       if (sp == 0) return true;
       const int k = --sp;
-      rd = fs.rd[k];
-      set_off((uint32_t)fs.F[k] >> 30, fs.old[k]);
-      minFar = fs.mn[k];
-      start = fs.start[k];
-      c = fs.P[k];
-      pc = fs.PP[k];
+      rd = fs.f[k].rd;
+      set_off((uint32_t)fs.f[k].F >> 30, fs.f[k].old);
+      minFar = fs.f[k].mn;
+      start = fs.f[k].start;
+      c = fs.f[k].P;
+      pc = fs.f[k].PP;
       if (!(minFar <= R && minFar * E < bestd)) c = start;
     }
   }
 };
+
+#ifndef AICP_NN_PROF
+#define AICP_NN_PROF 0  // diagnostic builds: per-phase s_memtime cycles of the persistent waves
+#endif
+#if AICP_NN_PROF
+__device__ unsigned long long g_nn_prof[8];
+#endif
 
 // Persistent waves with XCD-affine work: the slot space [0, total) is cut into kXcdGroups
 // contiguous ranges (64-slot aligned) and group g is served only by blocks with
@@ -885,6 +898,20 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
   bool has = false;
   uint32_t pool = 0, pool_end = 0, my = 0;
   bool exhausted = false;
+#if AICP_NN_PROF
+  uint64_t pf_t = __builtin_amdgcn_s_memtime(), pf_fill = 0, pf_desc = 0, pf_buck = 0, pf_climb = 0, pf_rounds = 0,
+           pf_lanes = 0;
+#define AICP_PF(acc)                                    \
+  do {                                                  \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+    acc += now_ - pf_t;                                 \
+    pf_t = now_;                                        \
+  } while (0)
+#else
+#define AICP_PF(acc) \
+  do {               \
+  } while (0)
+#endif
   for (;;) {
     for (;;) {
       const uint64_t needm = __ballot(!has);
@@ -910,6 +937,11 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       pool += min(avail, (uint32_t)__popcll(needm));
     }
     if (__ballot(has) == 0) break;
+    AICP_PF(pf_fill);
+#if AICP_NN_PROF
+    ++pf_rounds;
+    pf_lanes += __popcll(__ballot(has));
+#endif
     if constexpr (is_sm<Eng>::value) {
       __shared__ float4 xch_sm[kNNBlock];
       const bool leaf = has && t.ph == kPhLeaf;
@@ -939,6 +971,7 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       t.pm = pm_lds + threadIdx.x;
 #endif
       if (has) t.descend();
+      AICP_PF(pf_desc);
 #if AICP_NN_COOP
       __shared__ float4 xch_all[kNNBlock];
       coop_bucket(t, has, pts, maxR2, xch_all + (threadIdx.x & ~63));
@@ -949,11 +982,13 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
 #else
         t.bucket_lane(pts, maxR2);
 #endif
-        if (t.climb(fs, maxE2, maxR2)) {
-          done(my, t);
-          has = false;
-        }
       }
+      AICP_PF(pf_buck);
+      if (has && t.climb(fs, maxE2, maxR2)) {
+        done(my, t);
+        has = false;
+      }
+      AICP_PF(pf_climb);
     } else {
       if (has && t.advance(fs, maxE2, maxR2, nodes, pts)) {
         done(my, t);
@@ -961,6 +996,16 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       }
     }
   }
+#if AICP_NN_PROF
+  if (lane == 0) {
+    atomicAdd(&g_nn_prof[0], (unsigned long long)pf_fill);
+    atomicAdd(&g_nn_prof[1], (unsigned long long)pf_desc);
+    atomicAdd(&g_nn_prof[2], (unsigned long long)pf_buck);
+    atomicAdd(&g_nn_prof[3], (unsigned long long)pf_climb);
+    atomicAdd(&g_nn_prof[4], (unsigned long long)pf_rounds);
+    atomicAdd(&g_nn_prof[5], (unsigned long long)pf_lanes);
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1825,6 +1870,20 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
   else
     k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, nullptr, match, d2, touched, ctr, prm);
 }
+void nn_prof_dump() {
+#if AICP_NN_PROF
+  unsigned long long h[8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_nn_prof), sizeof(h)) == hipSuccess) {
+    const double tot = (double)(h[0] + h[1] + h[2] + h[3]);
+    fprintf(stderr, "nn_prof: fill %.1f%% descent %.1f%% bucket %.1f%% climb %.1f%% | rounds %llu, mean active lanes %.1f\n",
+            100.0 * h[0] / tot, 100.0 * h[1] / tot, 100.0 * h[2] / tot, 100.0 * h[3] / tot, h[4],
+            h[4] ? (double)h[5] / h[4] : 0.0);
+  }
+  unsigned long long z[8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_nn_prof), z, sizeof(z));
+#endif
+}
+
 void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* pd, PairState* st, const float* d2,
                        uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt) {
   if (!m.n_blocks) return;
