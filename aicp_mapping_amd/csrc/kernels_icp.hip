@@ -100,6 +100,9 @@ constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #define AICP_NN_PREFMIN 0  // Trav2C: per-depth running minimum of the far bounds in LDS (climb pruning; off: C2 -1 %, C4 +20 %)
 #endif
 [[maybe_unused]] constexpr int kPmDepth = 24;  // depths whose running minimum is kept (deeper levels climb unpruned)
+#ifndef AICP_NN_CLIMB2
+#define AICP_NN_CLIMB2 1  // Trav2C: climb one treelet (record + parent, up to two levels) per iteration
+#endif
 #ifndef AICP_NN_BUCKET_MIN
 #define AICP_NN_BUCKET_MIN 16  // Trav2S: lanes at a leaf before a cooperative bucket pass
 #endif
@@ -385,6 +388,76 @@ struct Trav2C {
     tp += lcnt;
   }
 
+#if AICP_NN_CLIMB2
+  // far test of node p (slot s of record r, parent pp); on a pass: push the frame, start the far
+  // descent and return true
+  __device__ __forceinline__ bool far_push(FarStack& fs, const uint4& r, int32_t p, uint32_t s, int32_t pp,
+                                           float maxE2, float maxR2) {
+    const uint32_t T = (uint32_t)p >> 2;
+    const uint32_t w = slot_word(r, s), cd = (r.w >> (2 * s)) & 3u;
+    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
+    const float oc = sel3(cd, noc0, noc1, noc2);
+    const float rdf = rd + (oc + no * no);
+    if (!(rdf <= maxR2 && rdf * maxE2 < best.v[0])) return false;
+    const uint32_t fr = no > 0.f ? 0u : 1u;  // far child = the left one when the query is right of the cut
+    const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
+    FarFrame& f = fs.f[sp];
+    f.F = (int32_t)((uint32_t)far | (cd << 30));
+    f.rd = rd;
+    f.old = oc;
+    f.mn = minFar;
+    f.start = start;
+    f.P = p;
+    f.PP = pp;
+    ++sp;
+    const float nn = -no * no;
+    if (cd == 0) noc0 = nn;
+    else if (cd == 1) noc1 = nn;
+    else noc2 = nn;
+    rd = rdf;
+    n = far;
+    start = far;
+    pl = p;
+    return true;
+  }
+
+  // the climb one treelet per iteration: one record (and its root's parent) per round trip, the
+  // node and, for a child slot, the treelet root above it
+  __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
+    int32_t c = n, pc = pl;
+    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+    for (;;) {
+      if (c == start) {
+        if (sp == 0) return true;
+        --sp;
+        const FarFrame f = fs.f[sp];
+        const uint32_t pcd = (uint32_t)f.F >> 30;
+        rd = f.rd;
+        if (pcd == 0) noc0 = f.old;
+        else if (pcd == 1) noc1 = f.old;
+        else noc2 = f.old;
+        minFar = f.mn;
+        start = f.start;
+        c = f.P;
+        pc = f.PP;
+        if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+        continue;
+      }
+      const int32_t p = pc;
+      const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
+      const uint4 r = ld_rec(tl + T);
+      const int32_t rootpp = (int32_t)ptl[T];
+      const int32_t root = (int32_t)(T << 2);
+      if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2)) return false;
+      c = p;
+      pc = s != 0 ? root : rootpp;
+      if (s == 0 || c == start) continue;
+      if (far_push(fs, r, root, 0, rootpp, maxE2, maxR2)) return false;
+      c = root;
+      pc = rootpp;
+    }
+  }
+#else
   __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
     int32_t c = n, pc = pl;
     uint32_t cT = 0xffffffffu;  // treelet whose record cr (and root parent cpp) is held
@@ -469,6 +542,7 @@ struct Trav2C {
 #endif
     }
   }
+#endif
 };
 
 // Trav2C's traversal as a per-lane state machine ("if-if"): every iteration of the persistent
