@@ -91,6 +91,12 @@ struct FarFrame {
 struct FarStack {
   FarFrame f[kFarStack];
 };
+// the same frame in LDS, 24 bytes: P (node ids < 2^30) shares its word with cd
+struct LdsFrame {
+  int32_t Pcd;
+  float rd, old, mn;
+  int32_t start, PP;
+};
 
 constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #ifndef AICP_NN_COOP
@@ -104,7 +110,7 @@ constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #define AICP_NN_CLIMB2 1  // Trav2C: climb one treelet (record + parent, up to two levels) per iteration
 #endif
 #ifndef AICP_NN_LDS_FRAMES
-#define AICP_NN_LDS_FRAMES 2  // Trav2C: innermost far-descent frames kept in LDS (32 B each per lane)
+#define AICP_NN_LDS_FRAMES 3  // Trav2C: innermost far-descent frames kept in LDS (24 B each per lane)
 #endif
 #ifndef AICP_NN_BUCKET_MIN
 #define AICP_NN_BUCKET_MIN 16  // Trav2S: lanes at a leaf before a cooperative bucket pass
@@ -279,7 +285,7 @@ struct Trav2C {
   int32_t dep;               // depth of n (descent) / of the node climbed from (climb)
   uint16_t* pm;              // this lane's prefix-minimum column in LDS (AICP_NN_PREFMIN)
   uint32_t lb0, lcnt;        // bucket of the leaf the last descent ended in
-  FarFrame* lf;              // this lane's LDS frames (AICP_NN_LDS_FRAMES, stride kNNBlock)
+  LdsFrame* lf;              // this lane's LDS frames (AICP_NN_LDS_FRAMES, stride kNNBlock)
   uint32_t tp, tn;
   Best<1> best;
 
@@ -405,11 +411,10 @@ struct Trav2C {
     if (!(rdf <= maxR2 && rdf * maxE2 < best.v[0])) return false;
     const uint32_t fr = no > 0.f ? 0u : 1u;  // far child = the left one when the query is right of the cut
     const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
-    const FarFrame fr_new{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, 0};
     // the innermost frames live in LDS (no scratch traffic: scratch frames are written back
     // to HBM through L2), deeper nesting in the scratch stack
-    if (sp < AICP_NN_LDS_FRAMES) lf[sp * kNNBlock] = fr_new;
-    else fs.f[sp] = fr_new;
+    if (sp < AICP_NN_LDS_FRAMES) lf[sp * kNNBlock] = LdsFrame{(int32_t)((uint32_t)p | (cd << 30)), rd, oc, minFar, start, pp};
+    else fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, 0};
     ++sp;
     const float nn = -no * no;
     if (cd == 0) noc0 = nn;
@@ -431,7 +436,13 @@ struct Trav2C {
       if (c == start) {
         if (sp == 0) return true;
         --sp;
-        const FarFrame f = sp < AICP_NN_LDS_FRAMES ? lf[sp * kNNBlock] : fs.f[sp];
+        FarFrame f;
+        if (sp < AICP_NN_LDS_FRAMES) {
+          const LdsFrame g = lf[sp * kNNBlock];
+          f = FarFrame{g.Pcd, g.rd, g.old, g.mn, g.start, g.Pcd & 0x3fffffff, g.PP, 0};
+        } else {
+          f = fs.f[sp];
+        }
         const uint32_t pcd = (uint32_t)f.F >> 30;
         rd = f.rd;
         if (pcd == 0) noc0 = f.old;
@@ -1061,7 +1072,7 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       AICP_PF(pf_buck);
 #if AICP_NN_LDS_FRAMES > 0
       if constexpr (is_coop<Eng>::value && !is_sm<Eng>::value) {
-        __shared__ FarFrame lds_frames[AICP_NN_LDS_FRAMES * kNNBlock];
+        __shared__ LdsFrame lds_frames[AICP_NN_LDS_FRAMES * kNNBlock];
         t.lf = lds_frames + threadIdx.x;
       }
 #endif
