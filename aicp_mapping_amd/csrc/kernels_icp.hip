@@ -112,6 +112,10 @@ constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #ifndef AICP_NN_LDS_FRAMES
 #define AICP_NN_LDS_FRAMES 3  // Trav2C: innermost far-descent frames kept in LDS (24 B each per lane)
 #endif
+#ifndef AICP_KNN_LDS_FRAMES
+#define AICP_KNN_LDS_FRAMES 6  // k_knn_ids (SurfaceNormal kNN): far frames per lane kept in LDS
+#endif
+constexpr int kKnnLdsFrames = AICP_KNN_LDS_FRAMES;
 #ifndef AICP_NN_BUCKET_MIN
 #define AICP_NN_BUCKET_MIN 16  // Trav2S: lanes at a leaf before a cooperative bucket pass
 #endif
@@ -125,6 +129,8 @@ struct Trav {
   int32_t n, start, sp;
   uint32_t tp, tn;
   Best<K> best;
+  LdsFrame* lf = nullptr;  // innermost far frames in LDS (stride kNNBlock), nlf of them
+  int32_t nlf = 0;
 
   __device__ __forceinline__ void bind(const uint4* nb, const float4* pb, uint32_t node_off, uint32_t ref_off) {
     nodes = nb + node_off;
@@ -202,16 +208,23 @@ struct Trav {
       if (c == start) {
         if (sp == 0) return true;
         --sp;
-        const uint32_t pcd = (uint32_t)fs.f[sp].F >> 30;
-        rd = fs.f[sp].rd;
-        const float old = fs.f[sp].old;
+        FarFrame f;
+        if (sp < nlf) {
+          const LdsFrame g = lf[sp * kNNBlock];
+          f = FarFrame{g.Pcd, g.rd, g.old, g.mn, g.start, g.Pcd & 0x3fffffff, g.PP, 0};
+        } else {
+          f = fs.f[sp];
+        }
+        const uint32_t pcd = (uint32_t)f.F >> 30;
+        rd = f.rd;
+        const float old = f.old;
         if (pcd == 0) off0 = old;
         else if (pcd == 1) off1 = old;
         else off2 = old;
-        minFar = fs.f[sp].mn;
-        start = fs.f[sp].start;
-        c = fs.f[sp].P;
-        pc = fs.f[sp].PP;
+        minFar = f.mn;
+        start = f.start;
+        c = f.P;
+        pc = f.PP;
         if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
         continue;
       }
@@ -223,13 +236,8 @@ struct Trav {
       const float rdf = rd + (-oc * oc + no * no);
       if (rdf <= maxR2 && rdf * maxE2 < best.v[K - 1]) {
         const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
-        fs.f[sp].F = (int32_t)((uint32_t)far | (cd << 30));
-        fs.f[sp].rd = rd;
-        fs.f[sp].old = oc;
-        fs.f[sp].mn = minFar;
-        fs.f[sp].start = start;
-        fs.f[sp].P = p;
-        fs.f[sp].PP = (int32_t)pn.z;
+        if (sp < nlf) lf[sp * kNNBlock] = LdsFrame{(int32_t)((uint32_t)p | (cd << 30)), rd, oc, minFar, start, (int32_t)pn.z};
+        else fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, (int32_t)pn.z, 0};
         ++sp;
         if (cd == 0) off0 = no;
         else if (cd == 1) off1 = no;
@@ -1238,6 +1246,9 @@ __global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, co
                                                  const int32_t* __restrict__ parent,
                                                  const float4* __restrict__ bpts,
                                                  int32_t* __restrict__ ids, uint32_t* ctr) {
+  // innermost far frames in LDS (the exact kNN nests far descents often; scratch frames are
+  // written back to HBM): 4 blocks of 256 per CU at this kernel's VGPR count
+  __shared__ LdsFrame knn_frames[(kKnnLdsFrames > 0 ? kKnnLdsFrames : 1) * kNNBlock];
   int cur = -1;
   uint32_t cur_end = 0, cur_off = 0;
   persistent_xcd<Trav<K>>(
@@ -1253,6 +1264,8 @@ __global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, co
         t.pts = bpts + d.ref_off;
         const float4 q = bpts[s];
         t.reset(q.x, q.y, q.z);
+        t.lf = knn_frames + threadIdx.x;
+        t.nlf = kKnnLdsFrames;
         return true;
       },
       [&](uint32_t s, Trav<K>& t) {
