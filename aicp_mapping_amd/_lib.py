@@ -30,7 +30,7 @@ EXPORTS = [
     "aicp_hip_overlap", "aicp_hip_overlap_batch", "aicp_hip_align_batch", "aicp_hip_transform", "aicp_hip_crop_box",
     "aicp_hip_batch_upload", "aicp_hip_batch_run", "aicp_hip_batch_free",
     "aicp_hip_last_nn_timing", "aicp_hip_last_phase_ms", "aicp_hip_knn", "aicp_hip_normals",
-    "aicp_hip_dists_quantile", "aicp_hip_solve6",
+    "aicp_hip_dists_quantile", "aicp_hip_solve6", "aicp_hip_default_prefilter", "aicp_hip_prefilter",
 ]
 
 
@@ -84,6 +84,19 @@ class Pair(C.Structure):
     ]
 
 
+class PrefilterParams(C.Structure):
+    _fields_ = [
+        ("leaf_size", C.c_float),
+        ("normal_k", C.c_int32),
+        ("neighbours", C.c_int32),
+        ("min_cluster_size", C.c_int32),
+        ("max_cluster_size", C.c_int32),
+        ("smoothness_rad", C.c_float),
+        ("curvature_threshold", C.c_float),
+        ("viewpoint", C.c_float * 3),
+    ]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
@@ -131,6 +144,10 @@ def _load():
     L.aicp_hip_normals.argtypes = [vp, fp, sz, sz, C.c_int, fp, ip]
     L.aicp_hip_dists_quantile.argtypes = [vp, fp, sz, C.c_float, fp]
     L.aicp_hip_solve6.argtypes = [vp, dp, dp, dp, ip]
+    L.aicp_hip_default_prefilter.argtypes = [C.POINTER(PrefilterParams)]
+    L.aicp_hip_default_prefilter.restype = None
+    L.aicp_hip_prefilter.argtypes = [vp, C.POINTER(PrefilterParams), fp, sz, sz, fp, C.POINTER(C.c_size_t), fp, ip,
+                                     C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
     return L
 
 
@@ -205,6 +222,19 @@ def make_pair(ref, read, ref_origin=(0, 0, 0), read_origin=(0, 0, 0), init_T=Non
         p.ref_origin[k] = float(ref_origin[k])
         p.read_origin[k] = float(read_origin[k])
     return p, keep
+
+
+def default_prefilter(**kw) -> PrefilterParams:
+    """filteringUtils.cpp:12,22,27-34 (aicp_hip_default_prefilter); keyword overrides."""
+    p = PrefilterParams()
+    lib.aicp_hip_default_prefilter(C.byref(p))
+    for k, v in kw.items():
+        if k == "viewpoint":
+            for i in range(3):
+                p.viewpoint[i] = float(v[i])
+        else:
+            setattr(p, k, v)
+    return p
 
 
 class Context:
@@ -333,6 +363,28 @@ class Context:
                                    _fptr(out), C.byref(m), _fptr(rpy))
         self.check(rc)
         return out[:m.value].copy(), rpy
+
+    def prefilter(self, pts, params=None, details=False):
+        """regionGrowingUniformPlaneSegmentationFilter (filteringUtils.cpp:5-45) on device.
+        Returns the kept points (clusters concatenated), or with details=True a dict with
+        out, sampled (V, 8) {x, y, z, curvature, nx, ny, nz, 0}, labels (V,) and n_clusters."""
+        pts = as_points(pts)
+        n = pts.shape[0]
+        prm = params or default_prefilter()
+        out = np.zeros((max(n, 1), 3), np.float32)
+        m, ns, nc = C.c_size_t(0), C.c_size_t(0), C.c_size_t(0)
+        sampled = np.zeros((max(n, 1), 8), np.float32) if details else None
+        labels = np.zeros(max(n, 1), np.int32) if details else None
+        rc = lib.aicp_hip_prefilter(self.h, C.byref(prm), _fptr(pts), n, pts.shape[1] * 4, _fptr(out), C.byref(m),
+                                    _fptr(sampled) if details else None,
+                                    labels.ctypes.data_as(C.POINTER(C.c_int32)) if details else None,
+                                    C.byref(ns), C.byref(nc))
+        self.check(rc)
+        if not details:
+            return out[:m.value].copy()
+        V = ns.value
+        return dict(out=out[:m.value].copy(), sampled=sampled[:V].copy(), labels=labels[:V].copy(),
+                    n_clusters=nc.value)
 
 
 class ResidentBatch:

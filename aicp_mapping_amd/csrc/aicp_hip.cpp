@@ -132,7 +132,7 @@ struct aicp_hip_ctx {
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
       ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
       nrm_raw, inv, gdesc, gstate, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, tl, ptl, tl_flag,
-      tl_rank, tl_temp;
+      tl_rank, tl_temp, pf_a, pf_b;
   uint64_t tl_total = 0;  // matcher treelet records allotted for this batch (0: no treelets, Trav<1>)
   TreeBufs tb[2];  // [0] raw-coordinate tree (stream2), [1] centred matcher tree (stream3)
   PinBuf pin_desc, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
@@ -937,7 +937,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
                     &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->gdesc, &ctx->gstate, &ctx->tl, &ctx->ptl,
-                    &ctx->tl_flag, &ctx->tl_rank, &ctx->tl_temp})
+                    &ctx->tl_flag, &ctx->tl_rank, &ctx->tl_temp, &ctx->pf_a, &ctx->pf_b})
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
@@ -1266,6 +1266,161 @@ int aicp_hip_solve6(aicp_hip_ctx* ctx, const double* A, const double* b, double*
   int32_t path = 0;
   HIPC(hipMemcpy(&path, d + 384, 4, hipMemcpyDeviceToHost));
   if (out_path) *out_path = path;
+  return AICP_OK;
+}
+
+void aicp_hip_default_prefilter(aicp_prefilter_params* p) {
+  if (!p) return;
+  *p = aicp_prefilter_params{};
+  p->leaf_size = 0.08f;  // filteringUtils.cpp:12
+  p->normal_k = 30;      // :22
+  p->neighbours = 15;    // :30
+  p->min_cluster_size = 50;
+  p->max_cluster_size = 1000000;
+  p->smoothness_rad = (float)(3.0 / 180.0 * M_PI);  // :33 (setSmoothnessThreshold(float))
+  p->curvature_threshold = 1.0f;
+}
+
+// VoxelGrid -> NormalEstimation -> RegionGrowing on the device (kernels_prefilter.hip). Host
+// syncs: after the voxel grid (sampled count sizes the tree), per round of four propagation
+// launches (fixed-point test), and the final counts.
+int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, const float* pts, size_t n,
+                       size_t stride, float* out, size_t* out_n, float* sampled, int32_t* labels, size_t* n_sampled,
+                       size_t* n_clusters) {
+  if (!ctx || !prm || !out || !out_n || (n && !pts) || stride < 12 || (stride % 4)) return AICP_ERR_INVALID;
+  if (n >= (1ull << 31)) return AICP_ERR_INVALID;
+  if (!(prm->leaf_size > 0.f) || !std::isfinite(prm->leaf_size)) FAIL(AICP_ERR_INVALID, "leaf size must be > 0");
+  const int K = prm->normal_k, NB = prm->neighbours;
+  if (K != 10 && K != 20 && K != 30) FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
+  if (NB < 1 || NB > kPfMaxNbrs || NB > K) FAIL(AICP_ERR_UNSUPPORTED, "neighbours must be 1..min(16, normal_k)");
+  *out_n = 0;
+  if (n_sampled) *n_sampled = 0;
+  if (n_clusters) *n_clusters = 0;
+  if (n == 0) return AICP_OK;
+  HIPC(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  // ---- scratch of the voxel grid and the extraction: ctl | pts4[n] | 9 x (n + 1) words | temp
+  const size_t wn = (n + 1 + 63) & ~size_t(63);
+  const size_t temp_b = pf_temp_bytes(n + 1);
+  const size_t off_pts = 256, off_w = off_pts + n * 16, off_temp = off_w + 9 * wn * 4;
+  HIPC(ensure(ctx->pf_a, off_temp + temp_b));
+  char* A = ctx->pf_a.as<char>();
+  PfCtl* dctl = (PfCtl*)A;
+  float4* pts4 = (float4*)(A + off_pts);
+  uint32_t* wb = (uint32_t*)(A + off_w);
+  PfWork W{wb, wb + wn, wb + 2 * wn, wb + 3 * wn, wb + 4 * wn, wb + 5 * wn, wb + 6 * wn, wb + 7 * wn, wb + 8 * wn,
+           A + off_temp, temp_b};
+  HIPC(ensure(ctx->ref1, n * 16));
+  HIPC(ensure(ctx->pin_io, n * 16 + 64));
+  pack_xyz4(pts, n, stride, ctx->pin_io.as<float>());
+  HIPC(hipMemcpyAsync(pts4, ctx->pin_io.p, n * 16, hipMemcpyHostToDevice, s));
+  PfCtl hc{};
+  for (int k = 0; k < 3; ++k) hc.lo[k] = 0xFFFFFFFFu;
+  HIPC(hipMemcpyAsync(dctl, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
+  HIPC(launch_pf_voxel(s, (uint32_t)n, pts4, 1.f / prm->leaf_size, dctl, W, ctx->ref1.as<float4>()));
+  HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  if (hc.passthrough && hc.n_bad)
+    FAIL(AICP_ERR_UNSUPPORTED, "voxel grid overflows 32-bit indices and the cloud has non-finite points");
+  const uint32_t V = hc.n_fin ? hc.n_vox : 0u;
+  if (n_sampled) *n_sampled = V;
+  if (V == 0) return AICP_OK;
+  // ---- kd-tree of the sampled cloud and its exact kNN (libnabo order, eps 0, self included)
+  PairDesc d{};
+  d.n_ref = V;
+  d.ratio = 0.5f;
+  ident4(d.Tin);
+  HIPC(ensure(ctx->desc, sizeof(PairDesc)));
+  HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
+  int rc = device_trees_begin(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8,
+                              ctx->bpts, ctx->nodes);
+  if (rc) return rc;
+  rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes, 0);
+  if (rc) return rc;
+  HIPC(ensure(ctx->match, (size_t)V * K * 4));
+  HIPC(ensure(ctx->d2, (size_t)V * K * 4));
+  HIPC(ensure(ctx->scratch, 16 + kCtrWords * 4));
+  HIPC(hipMemsetAsync(ctx->scratch.p, 0, 16 + kCtrWords * 4, s));
+  const float4* bpts = ctx->bpts.as<float4>();
+  if (!launch_knn_generic(s, V, bpts, ctx->nodes.as<uint4>(), nullptr, bpts, K, 1.f, __builtin_inff(),
+                          ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->scratch.as<unsigned long long>(),
+                          (uint32_t*)(ctx->scratch.as<char>() + 16)))
+    FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
+  HIPC(hipGetLastError());
+  // ---- per sampled point: inv, nrm (float4), nbp (16), ckey, cval, nob, order_of, em, label,
+  // cluster_of, out4 (float4)
+  const size_t vn = ((size_t)V + 63) & ~size_t(63);
+  HIPC(ensure(ctx->pf_b, vn * 4 * (1 + 4 + kPfMaxNbrs + 7 + 4) + 256));
+  uint32_t* B = ctx->pf_b.as<uint32_t>();
+  uint32_t* inv = B;
+  float4* nrm = (float4*)(B + vn);
+  int32_t* nbp = (int32_t*)(B + 5 * vn);
+  uint32_t* ckey = B + (5 + kPfMaxNbrs) * vn;
+  uint32_t* cval = ckey + vn;
+  uint32_t* nob = cval + vn;
+  uint32_t* order_of = nob + vn;
+  uint32_t* em = order_of + vn;
+  uint32_t* label = em + vn;
+  int32_t* cluster_of = (int32_t*)(label + vn);
+  float4* out4 = (float4*)(cluster_of + vn);
+  uint32_t* flags = (uint32_t*)(out4 + vn);
+  const float vp[3] = {prm->viewpoint[0], prm->viewpoint[1], prm->viewpoint[2]};
+  if (!launch_pf_normals(s, V, K, NB, bpts, ctx->ref1.as<float4>(), ctx->match.as<int32_t>(), ctx->d2.as<float>(),
+                         inv, vp, nrm, nbp, ckey, cval))
+    FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
+  // validatePoint: cosine_threshold = cosf(theta_threshold_)
+  const float cos_thr = (float)std::cos((double)prm->smoothness_rad);
+  HIPC(launch_pf_order(s, V, NB, W, ckey, cval, inv, nrm, nbp, cos_thr, prm->curvature_threshold, nob, order_of, em,
+                       label));
+  // ---- min-label propagation to the fixed point: rounds of four launches, until a launch
+  // changes no label (labels only decrease, so this ends; V launches bound any schedule)
+  constexpr int R = 4;
+  uint32_t hf[R];
+  for (uint64_t launches = 0;; launches += R) {
+    if (launches > (uint64_t)V + 2 * R) FAIL(AICP_ERR_HIP, "region growing did not reach its fixed point");
+    HIPC(hipMemsetAsync(flags, 0, R * 4, s));
+    for (int r = 0; r < R; ++r) launch_rg_tiles(s, V, NB, nbp, em, nob, label, flags + r);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(hf, flags, R * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (!hf[R - 1]) break;
+  }
+  launch_rg_count_inf(s, V, label, dctl);
+  HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  if (hc.n_inf) launch_rg_phaseb(s, V, NB, nbp, em, nob, label);
+  HIPC(launch_rg_extract(s, V, (uint32_t)std::max(prm->min_cluster_size, 0),
+                         (uint32_t)std::max(prm->max_cluster_size, 0), label, inv, ctx->ref1.as<float4>(), W, out4,
+                         cluster_of, dctl));
+  HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  if (hc.n_out > V || hc.n_clusters > V) FAIL(AICP_ERR_HIP, "pre-filter: inconsistent cluster counts");
+  float* h = ctx->pin_io.as<float>();
+  if (hc.n_out) HIPC(hipMemcpy(h, out4, (size_t)hc.n_out * 16, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < hc.n_out; ++i)
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
+  *out_n = hc.n_out;
+  if (n_clusters) *n_clusters = hc.n_clusters;
+  if (labels) HIPC(hipMemcpy(labels, cluster_of, (size_t)V * 4, hipMemcpyDeviceToHost));
+  if (sampled) {
+    std::vector<float> P(4 * (size_t)V), N(4 * (size_t)V);
+    std::vector<uint32_t> I(V);
+    HIPC(hipMemcpy(P.data(), ctx->ref1.p, (size_t)V * 16, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(N.data(), nrm, (size_t)V * 16, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(I.data(), inv, (size_t)V * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < V; ++i) {
+      float* o = sampled + 8 * i;
+      const float* nb = &N[4 * (size_t)I[i]];
+      o[0] = P[4 * i];
+      o[1] = P[4 * i + 1];
+      o[2] = P[4 * i + 2];
+      o[3] = nb[3];
+      o[4] = nb[0];
+      o[5] = nb[1];
+      o[6] = nb[2];
+      o[7] = 0.f;
+    }
+  }
   return AICP_OK;
 }
 

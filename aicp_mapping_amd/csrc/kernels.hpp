@@ -133,4 +133,45 @@ void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* 
 void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
                        int set_ratio);
 
+// ---- pre-filter (kernels_prefilter.hip): regionGrowingUniformPlaneSegmentationFilter -------
+constexpr int kPfMaxNbrs = 16;  // RegionGrowing neighbours per point (edge mask bits)
+struct PfCtl {                  // device control block; lo = 0xFFFFFFFF, everything else 0 at start
+  uint32_t lo[3], hi[3];        // order-preserving bits of the finite points' min / max
+  uint32_t n_fin, n_bad;        // finite / non-finite input points
+  int32_t minb[3];              // VoxelGrid min_b_
+  uint32_t mul1, mul2;          // divb_mul_[1], divb_mul_[2]
+  float inv;                    // inverse leaf size
+  uint32_t passthrough;         // PCL's integer-overflow guard fired: the cloud passes unfiltered
+  uint32_t n_vox;               // sampled points V
+  uint32_t n_inf;               // points left for k_rg_phaseb
+  uint32_t n_seg, n_clusters, n_out;
+};
+struct PfWork {  // scratch, n (+1) words each
+  uint32_t *k0, *k1, *v0, *v1, *flag, *scan, *keep, *kpts, *koff;
+  void* temp;
+  size_t temp_bytes;
+};
+size_t pf_temp_bytes(size_t n);
+// VoxelGrid: ctl->n_vox centroids into sampled (ascending voxel index)
+hipError_t launch_pf_voxel(hipStream_t s, uint32_t n, const float4* pts, float inv, PfCtl* ctl, const PfWork& w,
+                           float4* sampled);
+// NormalEstimation from the kNN of the sampled tree (bucket order); k in {10, 20, 30}
+bool launch_pf_normals(hipStream_t s, uint32_t V, int k, int nnb, const float4* bpts, const float4* sampled,
+                       const int32_t* ids, const float* d2, uint32_t* inv, const float vp[3], float4* nrm,
+                       int32_t* nbp, uint32_t* ckey, uint32_t* cval);
+// seed order, edge masks and initial labels
+hipError_t launch_pf_order(hipStream_t s, uint32_t V, int nnb, const PfWork& w, const uint32_t* ckey,
+                           const uint32_t* cval, const uint32_t* inv, const float4* nrm, const int32_t* nbp,
+                           float cos_thr, float curv_thr, uint32_t* nob, uint32_t* order_of, uint32_t* em,
+                           uint32_t* label);
+void launch_rg_tiles(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, const uint32_t* nob,
+                     uint32_t* label, uint32_t* changed);
+void launch_rg_count_inf(hipStream_t s, uint32_t V, const uint32_t* label, PfCtl* ctl);
+void launch_rg_phaseb(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, const uint32_t* nob,
+                      uint32_t* label);
+// clusters of min..max points: out (creation order, ascending index), cluster of every point
+hipError_t launch_rg_extract(hipStream_t s, uint32_t V, uint32_t min_size, uint32_t max_size, const uint32_t* label,
+                             const uint32_t* inv, const float4* sampled, const PfWork& w, float4* out,
+                             int32_t* cluster_of, PfCtl* ctl);
+
 }  // namespace aicp

@@ -97,6 +97,16 @@ struct LdsFrame {
   float rd, old, mn;
   int32_t start, PP;
 };
+// the NN kernel's LDS frame, 20 bytes (four per lane fit 20 KB per 256-lane block, 8 blocks per
+// CU): PP (< 2^30) shares its word with cd; P itself is only compared with start, so its place is
+// the sign bit of mn, set when P == start (a negative mn, possible by rounding, is stored as +0:
+// both force the exact climb).
+struct NnLdsFrame {
+  int32_t PPcd;
+  float rd, old;
+  int32_t start;
+  float mnf;
+};
 
 constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #ifndef AICP_NN_COOP
@@ -110,7 +120,7 @@ constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #define AICP_NN_CLIMB2 1  // Trav2C: climb one treelet (record + parent, up to two levels) per iteration
 #endif
 #ifndef AICP_NN_LDS_FRAMES
-#define AICP_NN_LDS_FRAMES 3  // Trav2C: innermost far-descent frames kept in LDS (24 B each per lane)
+#define AICP_NN_LDS_FRAMES 3  // Trav2C: innermost far-descent frames kept in LDS (20 B each per lane; 4 measured no faster)
 #endif
 #ifndef AICP_KNN_LDS_FRAMES
 #define AICP_KNN_LDS_FRAMES 6  // k_knn_ids (SurfaceNormal kNN): far frames per lane kept in LDS
@@ -293,7 +303,7 @@ struct Trav2C {
   int32_t dep;               // depth of n (descent) / of the node climbed from (climb)
   uint16_t* pm;              // this lane's prefix-minimum column in LDS (AICP_NN_PREFMIN)
   uint32_t lb0, lcnt;        // bucket of the leaf the last descent ended in
-  LdsFrame* lf;              // this lane's LDS frames (AICP_NN_LDS_FRAMES, stride kNNBlock)
+  NnLdsFrame* lf;            // this lane's LDS frames (AICP_NN_LDS_FRAMES, stride kNNBlock)
   uint32_t tp, tn;
   Best<1> best;
 
@@ -421,7 +431,9 @@ struct Trav2C {
     const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
     // the innermost frames live in LDS (no scratch traffic: scratch frames are written back
     // to HBM through L2), deeper nesting in the scratch stack
-    if (sp < AICP_NN_LDS_FRAMES) lf[sp * kNNBlock] = LdsFrame{(int32_t)((uint32_t)p | (cd << 30)), rd, oc, minFar, start, pp};
+    if (sp < AICP_NN_LDS_FRAMES)
+      lf[sp * kNNBlock] = NnLdsFrame{(int32_t)(((uint32_t)pp & 0x3fffffffu) | (cd << 30)), rd, oc, start,
+                                     __int_as_float(max(__float_as_int(minFar), 0) | (p == start ? (int32_t)0x80000000 : 0))};
     else fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, 0};
     ++sp;
     const float nn = -no * no;
@@ -446,8 +458,11 @@ struct Trav2C {
         --sp;
         FarFrame f;
         if (sp < AICP_NN_LDS_FRAMES) {
-          const LdsFrame g = lf[sp * kNNBlock];
-          f = FarFrame{g.Pcd, g.rd, g.old, g.mn, g.start, g.Pcd & 0x3fffffff, g.PP, 0};
+          // P only matters through P == start (the sign bit of mn); any other id != start will do
+          const NnLdsFrame g = lf[sp * kNNBlock];
+          const int32_t mi = __float_as_int(g.mnf);
+          f = FarFrame{g.PPcd, g.rd, g.old, __int_as_float(mi & 0x7fffffff), g.start, mi < 0 ? g.start : -2,
+                       g.PPcd & 0x3fffffff, 0};
         } else {
           f = fs.f[sp];
         }
@@ -1080,7 +1095,7 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       AICP_PF(pf_buck);
 #if AICP_NN_LDS_FRAMES > 0
       if constexpr (is_coop<Eng>::value && !is_sm<Eng>::value) {
-        __shared__ LdsFrame lds_frames[AICP_NN_LDS_FRAMES * kNNBlock];
+        __shared__ NnLdsFrame lds_frames[AICP_NN_LDS_FRAMES * kNNBlock];
         t.lf = lds_frames + threadIdx.x;
       }
 #endif

@@ -140,6 +140,33 @@ int aicp_hip_crop_box(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stri
                       float max, const float origin[16], float* out /* 3*n */, size_t* out_n,
                       float* rpy_out /* 3, nullable */);
 
+/* Pre-filter regionGrowingUniformPlaneSegmentationFilter (aicp_core/src/utils/filteringUtils.cpp:5-45,
+ * called at app.cpp:109,295,491 and app_ros.cpp:309; the XYZRGBNormal overload :51-103 adds the
+ * viewpoint, the sampled cloud with normals and the clusters): pcl::VoxelGrid (leaf 0.08) ->
+ * pcl::NormalEstimation (k 30) -> pcl::RegionGrowing (15 neighbours, 3 deg, curvature 1.0,
+ * clusters of 50..1e6 points). Rules for PCL's unspecified orders: DESIGN.md §4.4. */
+typedef struct {
+  float leaf_size;           /* VoxelGrid leaf, all three axes (0.08) */
+  int32_t normal_k;          /* NormalEstimation k: 10, 20 or 30 (30) */
+  int32_t neighbours;        /* RegionGrowing neighbours, <= min(16, normal_k) (15) */
+  int32_t min_cluster_size;  /* 50 */
+  int32_t max_cluster_size;  /* 1000000 */
+  float smoothness_rad;      /* 3.0 / 180.0 * M_PI as float */
+  float curvature_threshold; /* 1.0 */
+  float viewpoint[3];        /* NormalEstimation viewpoint ((0,0,0): the first overload) */
+} aicp_prefilter_params;
+void aicp_hip_default_prefilter(aicp_prefilter_params* out);
+/* out: the clusters' points concatenated (clusters in creation order, each in sampled-cloud
+ * order), packed xyz, capacity n points; *out_n = count. Optional (nullable, capacity n):
+ * sampled = 8 floats per sampled point {x, y, z, curvature, nx, ny, nz, 0}; labels = cluster of
+ * each sampled point (-1: in no kept cluster). A cloud whose voxel grid would overflow 32-bit
+ * indices passes unfiltered (as in PCL), which requires finite points (else
+ * AICP_ERR_UNSUPPORTED). */
+int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, const float* pts, size_t n,
+                       size_t stride, float* out /* 3*n */, size_t* out_n, float* sampled /* 8*n */,
+                       int32_t* labels /* n */, size_t* n_sampled /* nullable */,
+                       size_t* n_clusters /* nullable */);
+
 /* ---- device-resident batches (inputs uploaded once, run many times) ----------------------- */
 int aicp_hip_batch_upload(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs,
                           aicp_hip_batch** out);

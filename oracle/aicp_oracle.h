@@ -116,6 +116,26 @@ float ao_quantize_ratio(float ratio);
 int ao_crop_box(const float* pts, int64_t n, int64_t stride_floats, float mn, float mx,
                 const float origin[16], float* out_xyz, int64_t* out_n, float* rpy_out);
 
+/* Pre-filter regionGrowingUniformPlaneSegmentationFilter (filteringUtils.cpp:5-45): VoxelGrid ->
+ * NormalEstimation -> RegionGrowing, restated in prefilter_oracle.cpp (rules for PCL's unspecified
+ * orders there). sampled: optional, 8 floats per sampled point {x, y, z, curvature, nx, ny, nz,
+ * cluster}; labels: optional, cluster per sampled point (-1: none); out: 3 floats per kept point,
+ * clusters concatenated. All capacities n. Returns 0, 2 (invalid), 3 (PCL would pass a cloud with
+ * non-finite points through unfiltered). */
+typedef struct {
+  float leaf;
+  int32_t normal_k;
+  int32_t neighbours;
+  int32_t min_cluster;
+  int32_t max_cluster;
+  float cos_smoothness; /* cosf(theta) of validatePoint */
+  float curvature;
+  float viewpoint[3];
+} ao_prefilter_params;
+int ao_prefilter(const float* pts, int64_t n, int64_t stride_floats, const ao_prefilter_params* prm,
+                 float* sampled, int32_t* labels, int64_t* n_sampled, int64_t* n_clusters, float* out,
+                 int64_t* n_out);
+
 #ifdef __cplusplus
 }
 #endif

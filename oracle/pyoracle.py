@@ -17,8 +17,8 @@ LIB_PATH = os.path.join(HERE, "libaicp_oracle.so")
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "aicp_oracle.cpp")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("aicp_oracle.cpp", "prefilter_oracle.cpp", "aicp_oracle.h")]
+    if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -70,6 +70,27 @@ def default_config(**kw) -> IcpConfig:
     return c
 
 
+class PrefilterParams(C.Structure):
+    _fields_ = [
+        ("leaf", C.c_float),
+        ("normal_k", C.c_int32),
+        ("neighbours", C.c_int32),
+        ("min_cluster", C.c_int32),
+        ("max_cluster", C.c_int32),
+        ("cos_smoothness", C.c_float),
+        ("curvature", C.c_float),
+        ("viewpoint", C.c_float * 3),
+    ]
+
+
+def prefilter_params(leaf=0.08, normal_k=30, neighbours=15, min_cluster=50, max_cluster=1000000,
+                     smoothness_rad=3.0 / 180.0 * np.pi, curvature=1.0, viewpoint=(0.0, 0.0, 0.0)):
+    """filteringUtils.cpp:12,22,27-34. validatePoint compares with cosf(theta) of the float theta."""
+    cos_s = np.float32(np.cos(np.float64(np.float32(smoothness_rad))))
+    return PrefilterParams(leaf, normal_k, neighbours, min_cluster, max_cluster, float(cos_s), curvature,
+                           (C.c_float * 3)(*viewpoint))
+
+
 _lib = None
 
 
@@ -107,6 +128,8 @@ def lib():
         L.ao_quantize_ratio.restype = C.c_float
         L.ao_crop_box.argtypes = [fp, C.c_int64, C.c_int64, C.c_float, C.c_float, fp, fp,
                                   C.POINTER(C.c_int64), fp]
+        L.ao_prefilter.argtypes = [fp, C.c_int64, C.c_int64, C.POINTER(PrefilterParams), fp, ip,
+                                   C.POINTER(C.c_int64), C.POINTER(C.c_int64), fp, C.POINTER(C.c_int64)]
         _lib = L
     return _lib
 
@@ -254,3 +277,24 @@ def crop_box(pts, mn, mx, origin):
     rc = lib().ao_crop_box(_f(p), p.shape[0], p.shape[1], mn, mx, _f(o), _f(out), C.byref(m), _f(rpy))
     assert rc == 0
     return out[:m.value].copy(), rpy
+
+
+def prefilter(pts, params=None):
+    """regionGrowingUniformPlaneSegmentationFilter (filteringUtils.cpp:5-45, 51-103) on the CPU.
+    Returns dict(out=(n_out, 3) kept points, clusters concatenated; sampled=(V, 8) {x, y, z,
+    curvature, nx, ny, nz, cluster}; labels=(V,) cluster or -1; n_clusters)."""
+    p = _pts(pts)
+    n = p.shape[0]
+    prm = params or prefilter_params()
+    sampled = np.zeros((max(n, 1), 8), np.float32)
+    labels = np.zeros(max(n, 1), np.int32)
+    out = np.zeros((max(n, 1), 3), np.float32)
+    ns, nc, no = C.c_int64(), C.c_int64(), C.c_int64()
+    rc = lib().ao_prefilter(_f(p), n, p.shape[1], C.byref(prm), _f(sampled),
+                            labels.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(ns), C.byref(nc), _f(out),
+                            C.byref(no))
+    if rc:
+        raise RuntimeError(f"ao_prefilter failed ({rc})")
+    V = ns.value
+    return dict(out=out[:no.value].copy(), sampled=sampled[:V].copy(), labels=labels[:V].copy(),
+                n_clusters=nc.value)
