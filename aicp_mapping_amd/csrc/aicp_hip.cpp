@@ -142,6 +142,7 @@ struct aicp_hip_ctx {
   double last_nn_ms = 0, last_nn_bytes = 0;
   uint64_t last_queries = 0;
   double last_phase[5] = {0, 0, 0, 0, 0};
+  int last_pf_passes = 0;  // propagation passes of the last pre-filter
 };
 
 #define HIPC(x)                                                                   \
@@ -1338,19 +1339,17 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes, 0);
   if (rc) return rc;
   HIPC(ensure(ctx->match, (size_t)V * K * 4));
-  HIPC(ensure(ctx->d2, (size_t)V * K * 4));
-  HIPC(ensure(ctx->scratch, 16 + kCtrWords * 4));
-  HIPC(hipMemsetAsync(ctx->scratch.p, 0, 16 + kCtrWords * 4, s));
+  HIPC(ensure(ctx->ctrs, kCtrWords * 4));
+  HIPC(hipMemsetAsync(ctx->ctrs.p, 0, kCtrWords * 4, s));
   const float4* bpts = ctx->bpts.as<float4>();
-  if (!launch_knn_generic(s, V, bpts, ctx->nodes.as<uint4>(), nullptr, bpts, K, 1.f, __builtin_inff(),
-                          ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->scratch.as<unsigned long long>(),
-                          (uint32_t*)(ctx->scratch.as<char>() + 16)))
+  if (!launch_knn_ids(s, 1, V, ctx->desc.as<PairDesc>(), ctx->nodes.as<uint4>(), bpts, K, ctx->match.as<int32_t>(),
+                      ctx->ctrs.as<uint32_t>()))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   HIPC(hipGetLastError());
   // ---- per sampled point: inv, nrm (float4), nbp (16), ckey, cval, nob, order_of, em, label,
   // cluster_of, out4 (float4)
   const size_t vn = ((size_t)V + 63) & ~size_t(63);
-  HIPC(ensure(ctx->pf_b, vn * 4 * (1 + 4 + kPfMaxNbrs + 7 + 4) + 256));
+  HIPC(ensure(ctx->pf_b, vn * 4 * (1 + 4 + kPfMaxNbrs + 8 + 4) + 256));
   uint32_t* B = ctx->pf_b.as<uint32_t>();
   uint32_t* inv = B;
   float4* nrm = (float4*)(B + vn);
@@ -1363,28 +1362,32 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   uint32_t* label = em + vn;
   int32_t* cluster_of = (int32_t*)(label + vn);
   float4* out4 = (float4*)(cluster_of + vn);
-  uint32_t* flags = (uint32_t*)(out4 + vn);
+  uint32_t* comp = (uint32_t*)(out4 + vn);
+  uint32_t* flags = comp + vn;
   const float vp[3] = {prm->viewpoint[0], prm->viewpoint[1], prm->viewpoint[2]};
-  if (!launch_pf_normals(s, V, K, NB, bpts, ctx->ref1.as<float4>(), ctx->match.as<int32_t>(), ctx->d2.as<float>(),
-                         inv, vp, nrm, nbp, ckey, cval))
+  if (!launch_pf_normals(s, V, K, NB, bpts, ctx->ref1.as<float4>(), ctx->match.as<int32_t>(), inv, vp, nrm, nbp,
+                         ckey, cval))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   // validatePoint: cosine_threshold = cosf(theta_threshold_)
   const float cos_thr = (float)std::cos((double)prm->smoothness_rad);
   HIPC(launch_pf_order(s, V, NB, W, ckey, cval, inv, nrm, nbp, cos_thr, prm->curvature_threshold, nob, order_of, em,
                        label));
-  // ---- min-label propagation to the fixed point: rounds of four launches, until a launch
-  // changes no label (labels only decrease, so this ends; V launches bound any schedule)
-  constexpr int R = 4;
+  // ---- min-label propagation to the fixed point: union-find over mutual edges, then passes
+  // until one changes no label (labels only decrease, so this ends; V passes bound any schedule)
+  launch_rg_components(s, V, NB, nbp, em, comp, label);
+  constexpr int R = 2;
   uint32_t hf[R];
   for (uint64_t launches = 0;; launches += R) {
     if (launches > (uint64_t)V + 2 * R) FAIL(AICP_ERR_HIP, "region growing did not reach its fixed point");
     HIPC(hipMemsetAsync(flags, 0, R * 4, s));
-    for (int r = 0; r < R; ++r) launch_rg_tiles(s, V, NB, nbp, em, nob, label, flags + r);
+    for (int r = 0; r < R; ++r) launch_rg_iter(s, V, NB, nbp, em, nob, comp, label, flags + r);
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(hf, flags, R * 4, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+    ctx->last_pf_passes = (int)(launches + R);
     if (!hf[R - 1]) break;
   }
+  launch_rg_settle(s, V, comp, label);
   launch_rg_count_inf(s, V, label, dctl);
   HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));

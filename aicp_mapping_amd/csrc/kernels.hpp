@@ -31,6 +31,10 @@ void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState
 bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
                     int32_t* ids, uint32_t* ctr);
+// the kNN of every reference point in its own tree (bucket order in and out: ids are bucket
+// positions of the pair's tree, -1 past the cloud size); eps 0, self included
+bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr);
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
                         ActiveList* al, uint32_t* ctr);
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st,
@@ -156,16 +160,21 @@ size_t pf_temp_bytes(size_t n);
 hipError_t launch_pf_voxel(hipStream_t s, uint32_t n, const float4* pts, float inv, PfCtl* ctl, const PfWork& w,
                            float4* sampled);
 // NormalEstimation from the kNN of the sampled tree (bucket order); k in {10, 20, 30}
+// ids: launch_knn_ids output (bucket positions)
 bool launch_pf_normals(hipStream_t s, uint32_t V, int k, int nnb, const float4* bpts, const float4* sampled,
-                       const int32_t* ids, const float* d2, uint32_t* inv, const float vp[3], float4* nrm,
-                       int32_t* nbp, uint32_t* ckey, uint32_t* cval);
+                       const int32_t* ids, uint32_t* inv, const float vp[3], float4* nrm, int32_t* nbp, uint32_t* ckey,
+                       uint32_t* cval);
 // seed order, edge masks and initial labels
 hipError_t launch_pf_order(hipStream_t s, uint32_t V, int nnb, const PfWork& w, const uint32_t* ckey,
                            const uint32_t* cval, const uint32_t* inv, const float4* nrm, const int32_t* nbp,
                            float cos_thr, float curv_thr, uint32_t* nob, uint32_t* order_of, uint32_t* em,
                            uint32_t* label);
-void launch_rg_tiles(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, const uint32_t* nob,
-                     uint32_t* label, uint32_t* changed);
+// union-find over mutual edges: comp[x] = component root, roots start at their members' minimum
+void launch_rg_components(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, uint32_t* comp,
+                          uint32_t* label);
+void launch_rg_iter(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, const uint32_t* nob,
+                    const uint32_t* comp, uint32_t* label, uint32_t* changed);
+void launch_rg_settle(hipStream_t s, uint32_t V, const uint32_t* comp, uint32_t* label);
 void launch_rg_count_inf(hipStream_t s, uint32_t V, const uint32_t* label, PfCtl* ctl);
 void launch_rg_phaseb(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, const uint32_t* nob,
                       uint32_t* label);

@@ -1959,6 +1959,18 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   }
   return true;
 }
+bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr) {
+  if (!total_ref) return true;
+  const int g = persistent_grid((int)total_ref);
+  switch (knn) {
+    case 10: k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr); break;
+    case 20: k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr); break;
+    case 30: k_knn_ids<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr); break;
+    default: return false;
+  }
+  return true;
+}
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st, ActiveList* al,
                         uint32_t* ctr) {
   k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr);

@@ -4,10 +4,10 @@
 //   VoxelGrid 0.08 m   k_pf_minmax -> k_pf_grid -> k_pf_keys -> radix sort (voxel index, point)
 //                      -> k_pf_heads + scan -> k_pf_centroid (one thread per voxel, input order)
 //   NormalEstimation   the device kd-tree of the sampled cloud (kernels_tree.hip), exact libnabo
-//   k = 30             kNN (k_knn_generic, eps 0, self included), k_pf_normals: neighbours
+//   k = 30             kNN (k_knn_ids, eps 0, self included), k_pf_normals: neighbours
 //                      sorted by (d2, id), PCL's float covariance, eigen33 and viewpoint flip
 //   RegionGrowing      k_pf_order (seed order: curvature, index), k_pf_edges (smoothness mask of
-//   15 nbrs, 3 deg,    the 15 nearest), k_rg_tiles (min-label propagation, see below),
+//   15 nbrs, 3 deg,    the 15 nearest), k_uf_* + k_rg_iter (min-label propagation, see below),
 //   curvature 1.0      k_rg_phaseb, k_rg_extract* (clusters of 50..1e6 points, creation order)
 //
 // RegionGrowing as min-label propagation. PCL grows one region at a time from the unlabelled
@@ -19,9 +19,11 @@
 // minimal such s is itself a seed: an earlier seed reaching it would reach y through it.) That
 // fixed point is computed by monotone atomic minima along the valid edges of prop points, with
 // pointer jumping (label[x] = min(label[x], label[node(label[x])]), valid because the node of a
-// label is a prop point reaching x). Work runs in the kd-tree's bucket order so that a tile of
-// 1024 consecutive nodes is a compact patch: each k_rg_tiles block relaxes its tile's edges in
-// LDS to a local fixed point, then pushes labels across tile borders through global atomics.
+// label is a prop point reaching x). Plain propagation moves a label one kNN radius per pass, so a
+// plane-wide region would take hundreds of passes; mutual edges (x -> y and y -> x, both prop)
+// are first merged by union-find (k_uf_*), every member of such a component reaches every
+// other, and k_rg_iter passes labels member <-> root as well as along the edges, which leaves a
+// handful of passes for the one-way edges between components.
 // Non-prop points that no prop point reaches (curvature above the threshold: rounding cases
 // only, as PCL's curvature is <= 1/3) are seeds after every prop point and are grown one level
 // by k_rg_phaseb in seed order. tests/test_prefilter.py checks the labels against the oracle's
@@ -43,7 +45,6 @@ namespace aicp {
 namespace {
 
 constexpr uint32_t kInf = 0xFFFFFFFFu;
-constexpr int kTile = 1024;  // k_rg_tiles nodes per block
 
 __device__ __forceinline__ uint32_t f2ord(float f) {  // order-preserving float -> u32
   const uint32_t b = __float_as_uint(f);
@@ -56,42 +57,46 @@ __device__ __forceinline__ bool finite3(const float4& p) {
 
 // ---- VoxelGrid -------------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void k_pf_minmax(uint32_t n, const float4* __restrict__ pts, PfCtl* ctl) {
-  uint32_t lo0 = kInf, lo1 = kInf, lo2 = kInf, hi0 = 0, hi1 = 0, hi2 = 0, fin = 0, bad = 0;
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+// one block of 1024 threads per 64 Ki points; LDS reduction, one set of atomics per block (not
+// per wave: the eight words are shared by the whole grid)
+__global__ __launch_bounds__(1024) void k_pf_minmax(uint32_t n, const float4* __restrict__ pts, PfCtl* ctl) {
+  __shared__ uint32_t red[16][8];
+  uint32_t v[8] = {kInf, kInf, kInf, 0u, 0u, 0u, 0u, 0u};  // lo xyz, hi xyz, finite, non-finite
+  for (uint32_t i = blockIdx.x * 1024u + threadIdx.x; i < n; i += gridDim.x * 1024u) {
     const float4 p = pts[i];
     if (!finite3(p)) {
-      ++bad;
+      ++v[7];
       continue;
     }
-    ++fin;
-    lo0 = min(lo0, f2ord(p.x));
-    lo1 = min(lo1, f2ord(p.y));
-    lo2 = min(lo2, f2ord(p.z));
-    hi0 = max(hi0, f2ord(p.x));
-    hi1 = max(hi1, f2ord(p.y));
-    hi2 = max(hi2, f2ord(p.z));
+    ++v[6];
+    v[0] = min(v[0], f2ord(p.x));
+    v[1] = min(v[1], f2ord(p.y));
+    v[2] = min(v[2], f2ord(p.z));
+    v[3] = max(v[3], f2ord(p.x));
+    v[4] = max(v[4], f2ord(p.y));
+    v[5] = max(v[5], f2ord(p.z));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    lo0 = min(lo0, (uint32_t)__shfl_xor((int)lo0, o, 64));
-    lo1 = min(lo1, (uint32_t)__shfl_xor((int)lo1, o, 64));
-    lo2 = min(lo2, (uint32_t)__shfl_xor((int)lo2, o, 64));
-    hi0 = max(hi0, (uint32_t)__shfl_xor((int)hi0, o, 64));
-    hi1 = max(hi1, (uint32_t)__shfl_xor((int)hi1, o, 64));
-    hi2 = max(hi2, (uint32_t)__shfl_xor((int)hi2, o, 64));
-    fin += __shfl_xor(fin, o, 64);
-    bad += __shfl_xor(bad, o, 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t w = (uint32_t)__shfl_xor((int)v[k], o, 64);
+      v[k] = k < 3 ? min(v[k], w) : (k < 6 ? max(v[k], w) : v[k] + w);
+    }
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMin(&ctl->lo[0], lo0);
-    atomicMin(&ctl->lo[1], lo1);
-    atomicMin(&ctl->lo[2], lo2);
-    atomicMax(&ctl->hi[0], hi0);
-    atomicMax(&ctl->hi[1], hi1);
-    atomicMax(&ctl->hi[2], hi2);
-    atomicAdd(&ctl->n_fin, fin);
-    atomicAdd(&ctl->n_bad, bad);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[wave][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int k = threadIdx.x;
+    uint32_t r = red[0][k];
+    for (int w = 1; w < 16; ++w) r = k < 3 ? min(r, red[w][k]) : (k < 6 ? max(r, red[w][k]) : r + red[w][k]);
+    if (k < 3) atomicMin(&ctl->lo[k], r);
+    else if (k < 6) atomicMax(&ctl->hi[k - 3], r);
+    else if (k == 6) atomicAdd(&ctl->n_fin, r);
+    else atomicAdd(&ctl->n_bad, r);
   }
 }
 
@@ -275,31 +280,46 @@ __device__ __forceinline__ void eigen33(const float cov[9], float& lambda, float
   nz = __fdiv_rn(v[2], sl);
 }
 
-// One bucket position j: the K nearest (libnabo order, ties in visit order) sorted by (d2, id),
+// One bucket position j: the K nearest (libnabo order, ties in visit order; given as bucket
+// positions, d2 recomputed with libnabo's expression) sorted by (d2, sampled id),
 // computePointNormal on them (computeMeanAndCovarianceMatrix's nine float sums in neighbour
 // order, solvePlaneParameters), flipNormalTowardsViewpoint; then the seed-sort key (curvature,
 // by sampled index) and the first `nnb` neighbours as bucket positions.
 template <int K>
 __global__ __launch_bounds__(256) void k_pf_normals(uint32_t V, int nnb, const float4* __restrict__ bpts,
                                                     const float4* __restrict__ sampled, const int32_t* __restrict__ ids,
-                                                    const float* __restrict__ d2, const uint32_t* __restrict__ inv,
+                                                    const uint32_t* __restrict__ inv,
                                                     float vpx, float vpy, float vpz, float4* __restrict__ nrm,
                                                     int32_t* __restrict__ nbp, uint32_t* __restrict__ ckey,
                                                     uint32_t* __restrict__ cval) {
   const uint32_t j = blockIdx.x * 256u + threadIdx.x;
   if (j >= V) return;
+  const float4 p = bpts[j];
   float d[K];
   int32_t id[K];
 #pragma unroll
   for (int t = 0; t < K; ++t) {
-    id[t] = ids[(size_t)j * K + t];
-    d[t] = d2[(size_t)j * K + t];
-    if (id[t] < 0) {
+    const int32_t b = ids[(size_t)j * K + t];
+    if (b < 0) {
       id[t] = 0x7fffffff;
       d[t] = __builtin_inff();
+    } else {
+      const float4 q = bpts[b];
+      const float e0 = p.x - q.x, e1 = p.y - q.y, e2 = p.z - q.z;
+      float dist = 0.f;
+      dist += e0 * e0;
+      dist += e1 * e1;
+      dist += e2 * e2;
+      d[t] = dist;
+      id[t] = __float_as_int(q.w);
     }
   }
-  // insertion sort by (d2, id) on registers (compile-time indices only)
+  // libnabo's list is ascending in d2 with ties in visit order: sort by (d2, id) only when a tie
+  // is out of order (insertion sort on registers, compile-time indices only)
+  bool ordered = true;
+#pragma unroll
+  for (int t = 1; t < K; ++t) ordered = ordered && (d[t - 1] < d[t] || (d[t - 1] == d[t] && id[t - 1] <= id[t]));
+  if (!ordered)
 #pragma unroll
   for (int a = 1; a < K; ++a)
 #pragma unroll
@@ -329,7 +349,6 @@ __global__ __launch_bounds__(256) void k_pf_normals(uint32_t V, int nnb, const f
       a8 += q.z;
       ++cnt;
     }
-  const float4 p = bpts[j];
   float nx, ny, nz, curv;
   if (cnt < 3) {
     nx = ny = nz = curv = __builtin_nanf("");
@@ -412,54 +431,137 @@ __global__ __launch_bounds__(256) void k_pf_edges(uint32_t V, int nnb, const flo
   label[x] = prop ? order_of[x] : kInf;
 }
 
-// One block per tile of kTile consecutive nodes: load labels (one pointer jump each), relax the
-// tile's internal edges in LDS to a fixed point, write back and push across tile borders with
-// global atomic minima. changed = 1 when any global label decreased.
-__global__ __launch_bounds__(kTile) void k_rg_tiles(uint32_t V, int nnb, const int32_t* __restrict__ nbp,
-                                                    const uint32_t* __restrict__ em, const uint32_t* __restrict__ nob,
-                                                    uint32_t* label, uint32_t* changed) {
-  __shared__ uint32_t L[kTile];
-  const uint32_t base = blockIdx.x * (uint32_t)kTile;
-  const uint32_t x = base + threadIdx.x;
+// Union-find over mutual edges: x -> y and y -> x both valid, x and y both prop. Such points
+// reach each other, so a component shares one label, and a label reaching any member reaches
+// all of them: the propagation adds the member <-> root shortcuts (k_rg_iter), which turns the
+// plane-wide wavefront of plain label propagation (one kNN radius per pass) into a few passes.
+// par[v] <= v always (a root is hung under a smaller root), loads bypass the vector L1 so that a
+// failed CAS is never retried against a stale root.
+__device__ __forceinline__ uint32_t uf_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t uf_root(uint32_t* par, uint32_t x) {
+  uint32_t p = uf_ld(par + x);
+  while (p != x) {
+    const uint32_t g = uf_ld(par + p);
+    if (g == p) return p;
+    par[x] = g;  // path halving; g is still an ancestor of x whatever other threads do
+    x = p;
+    p = g;
+  }
+  return x;
+}
+
+// atomicMin(&label[r], l) for the active lanes of a wave, one atomic per distinct r: the lanes
+// of a big component all target its root, and per-lane atomics on one word serialise (the
+// k_uf_compress of a 600 k-point cloud took 1.1 ms that way). Returns true if this lane's
+// target decreased.
+__device__ __forceinline__ bool wave_min_to(uint32_t* label, uint32_t r, uint32_t l, bool active) {
+  bool dec = false;
+  unsigned long long pending = __ballot(active);
+  while (pending) {
+    const int lead = __ffsll((long long)pending) - 1;
+    const uint32_t r0 = (uint32_t)__shfl((int)r, lead, 64);
+    const bool mine = active && r == r0;
+    uint32_t m = mine ? l : kInf;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    bool d = false;
+    if ((int)(threadIdx.x & 63) == lead) d = m < atomicMin(&label[r0], m);
+    d = __shfl((int)d, lead, 64) != 0;
+    dec = dec || (mine && d);
+    pending &= ~__ballot(mine);
+  }
+  return dec;
+}
+
+__global__ __launch_bounds__(256) void k_uf_init(uint32_t V, uint32_t* __restrict__ par) {
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (x < V) par[x] = x;
+}
+
+__global__ __launch_bounds__(256) void k_uf_hook(uint32_t V, int nnb, const int32_t* __restrict__ nbp,
+                                                 const uint32_t* __restrict__ em, uint32_t* par) {
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (x >= V) return;
+  const uint32_t m = em[x];
+  if (!((m >> 16) & 1u)) return;
+  for (int t = 0; t < nnb; ++t) {
+    if (!((m >> t) & 1u)) continue;
+    const int32_t y = nbp[(size_t)x * kPfMaxNbrs + t];
+    if (y <= (int32_t)x) continue;  // each mutual edge once, from its smaller end
+    const uint32_t my = em[y];
+    if (!((my >> 16) & 1u)) continue;
+    bool back = false;
+    for (int u = 0; u < nnb && !back; ++u) back = ((my >> u) & 1u) && nbp[(size_t)y * kPfMaxNbrs + u] == (int32_t)x;
+    if (!back) continue;
+    uint32_t a = x, b = (uint32_t)y;
+    for (;;) {
+      uint32_t ra = uf_root(par, a), rb = uf_root(par, b);
+      if (ra == rb) break;
+      if (ra < rb) {
+        const uint32_t t2 = ra;
+        ra = rb;
+        rb = t2;
+      }
+      if (atomicCAS(&par[ra], ra, rb) == ra) break;
+      a = ra;
+      b = rb;
+    }
+  }
+}
+
+// components -> comp[x] (the root); each root starts at the smallest initial label of its members
+__global__ __launch_bounds__(256) void k_uf_compress(uint32_t V, uint32_t* par, uint32_t* label) {
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
   const bool in = x < V;
-  uint32_t m = in ? em[x] : 0u;
-  const bool prop = (m >> 16) & 1u;
-  m &= prop ? 0xFFFFu : 0u;
-  uint32_t l = in ? label[x] : kInf;
-  if (l != kInf) l = min(l, label[nob[l]]);
-  L[threadIdx.x] = l;
-  int32_t nb[kPfMaxNbrs];
-#pragma unroll
-  for (int t = 0; t < kPfMaxNbrs; ++t) nb[t] = (m >> t) & 1u ? nbp[(size_t)x * kPfMaxNbrs + t] : -1;
-  __syncthreads();
-  for (;;) {
-    int any = 0;
-    if (m) {
-      const uint32_t lx = L[threadIdx.x];
-#pragma unroll
-      for (int t = 0; t < kPfMaxNbrs; ++t) {
-        const uint32_t r = (uint32_t)nb[t] - base;
-        if (nb[t] >= 0 && r < (uint32_t)kTile && lx < L[r]) {
-          atomicMin(&L[r], lx);
-          any = 1;
-        }
-      }
-    }
-    if (!__syncthreads_or(any)) break;
-  }
-  int ch = 0;
+  uint32_t r = 0, l = kInf;
   if (in) {
-    const uint32_t lx = L[threadIdx.x];
-    if (lx < atomicMin(&label[x], lx)) ch = 1;
-    if (m) {
-#pragma unroll
-      for (int t = 0; t < kPfMaxNbrs; ++t) {
-        const uint32_t r = (uint32_t)nb[t] - base;
-        if (nb[t] >= 0 && r >= (uint32_t)kTile && lx < label[nb[t]] && lx < atomicMin(&label[nb[t]], lx)) ch = 1;
-      }
+    r = uf_root(par, x);
+    par[x] = r;
+    l = label[x];
+  }
+  wave_min_to(label, r, l, in && r != x && l != kInf);
+}
+
+// One pass of the propagation: prop x takes min(own, root's, pointer jump), gives it to its root,
+// and pushes it along its valid edges to y and y's root. changed = 1 when any label decreased.
+__global__ __launch_bounds__(256) void k_rg_iter(uint32_t V, int nnb, const int32_t* __restrict__ nbp,
+                                                 const uint32_t* __restrict__ em, const uint32_t* __restrict__ nob,
+                                                 const uint32_t* __restrict__ comp, uint32_t* label,
+                                                 uint32_t* changed) {
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  int ch = 0;
+  const uint32_t m = x < V ? em[x] : 0u;
+  const bool prop = (m >> 16) & 1u;
+  uint32_t r = 0, l = kInf, lr = kInf;
+  if (prop) {
+    r = comp[x];
+    const uint32_t lx = label[x];
+    lr = label[r];
+    l = min(lx, lr);
+    l = min(l, label[nob[l]]);
+    if (l < lx && l < atomicMin(&label[x], l)) ch = 1;
+  }
+  if (wave_min_to(label, r, l, prop && l < lr)) ch = 1;
+  if (prop) {
+    for (int t = 0; t < nnb; ++t) {
+      if (!((m >> t) & 1u)) continue;
+      const int32_t y = nbp[(size_t)x * kPfMaxNbrs + t];
+      if (l < label[y] && l < atomicMin(&label[y], l)) ch = 1;
+      const uint32_t ry = comp[y];
+      if (l < label[ry] && l < atomicMin(&label[ry], l)) ch = 1;
     }
   }
-  if (__syncthreads_or(ch) && threadIdx.x == 0) *changed = 1u;
+  if (__any(ch) && (threadIdx.x & 63) == 0) *changed = 1u;
+}
+
+// members adopt their root's final label (non-prop points are their own components)
+__global__ __launch_bounds__(256) void k_rg_settle(uint32_t V, const uint32_t* __restrict__ comp, uint32_t* label) {
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (x >= V) return;
+  const uint32_t lr = label[comp[x]];
+  if (lr < label[x]) label[x] = lr;
 }
 
 __global__ __launch_bounds__(256) void k_rg_count_inf(uint32_t V, const uint32_t* __restrict__ label, PfCtl* ctl) {
@@ -591,7 +693,7 @@ size_t pf_temp_bytes(size_t n) {
 hipError_t launch_pf_voxel(hipStream_t s, uint32_t n, const float4* pts, float inv, PfCtl* ctl, const PfWork& w,
                            float4* sampled) {
   if (n == 0) return hipSuccess;
-  k_pf_minmax<<<min(blocks_for(n), 2048u), 256, 0, s>>>(n, pts, ctl);
+  k_pf_minmax<<<min((n + 65535u) / 65536u, 1024u), 1024, 0, s>>>(n, pts, ctl);
   k_pf_grid<<<1, 64, 0, s>>>(ctl, inv);
   k_pf_keys<<<blocks_for(n), 256, 0, s>>>(n, pts, ctl, w.k0, w.v0);
   hipError_t e = sort_u32(s, w.temp, w.temp_bytes, w.k0, w.k1, w.v0, w.v1, n);
@@ -604,14 +706,14 @@ hipError_t launch_pf_voxel(hipStream_t s, uint32_t n, const float4* pts, float i
 }
 
 bool launch_pf_normals(hipStream_t s, uint32_t V, int k, int nnb, const float4* bpts, const float4* sampled,
-                       const int32_t* ids, const float* d2, uint32_t* inv, const float vp[3], float4* nrm,
-                       int32_t* nbp, uint32_t* ckey, uint32_t* cval) {
+                       const int32_t* ids, uint32_t* inv, const float vp[3], float4* nrm, int32_t* nbp, uint32_t* ckey,
+                       uint32_t* cval) {
   if (V == 0) return true;
   k_pf_inv<<<blocks_for(V), 256, 0, s>>>(V, bpts, inv);
   switch (k) {
-    case 10: k_pf_normals<10><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, d2, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
-    case 20: k_pf_normals<20><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, d2, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
-    case 30: k_pf_normals<30><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, d2, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
+    case 10: k_pf_normals<10><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
+    case 20: k_pf_normals<20><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
+    case 30: k_pf_normals<30><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
     default: return false;
   }
   return true;
@@ -629,9 +731,21 @@ hipError_t launch_pf_order(hipStream_t s, uint32_t V, int nnb, const PfWork& w, 
   return hipGetLastError();
 }
 
-void launch_rg_tiles(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, const uint32_t* nob,
-                     uint32_t* label, uint32_t* changed) {
-  if (V) k_rg_tiles<<<(V + kTile - 1) / kTile, kTile, 0, s>>>(V, nnb, nbp, em, nob, label, changed);
+void launch_rg_components(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, uint32_t* comp,
+                          uint32_t* label) {
+  if (!V) return;
+  k_uf_init<<<blocks_for(V), 256, 0, s>>>(V, comp);
+  k_uf_hook<<<blocks_for(V), 256, 0, s>>>(V, nnb, nbp, em, comp);
+  k_uf_compress<<<blocks_for(V), 256, 0, s>>>(V, comp, label);
+}
+
+void launch_rg_iter(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, const uint32_t* nob,
+                    const uint32_t* comp, uint32_t* label, uint32_t* changed) {
+  if (V) k_rg_iter<<<blocks_for(V), 256, 0, s>>>(V, nnb, nbp, em, nob, comp, label, changed);
+}
+
+void launch_rg_settle(hipStream_t s, uint32_t V, const uint32_t* comp, uint32_t* label) {
+  if (V) k_rg_settle<<<blocks_for(V), 256, 0, s>>>(V, comp, label);
 }
 
 void launch_rg_count_inf(hipStream_t s, uint32_t V, const uint32_t* label, PfCtl* ctl) {
