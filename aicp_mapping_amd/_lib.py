@@ -31,6 +31,7 @@ EXPORTS = [
     "aicp_hip_batch_upload", "aicp_hip_batch_run", "aicp_hip_batch_free",
     "aicp_hip_last_nn_timing", "aicp_hip_last_phase_ms", "aicp_hip_knn", "aicp_hip_normals",
     "aicp_hip_dists_quantile", "aicp_hip_solve6", "aicp_hip_default_prefilter", "aicp_hip_prefilter",
+    "aicp_hip_last_prefilter_stats",
 ]
 
 
@@ -97,6 +98,22 @@ class PrefilterParams(C.Structure):
     ]
 
 
+class PrefilterStats(C.Structure):
+    _fields_ = [
+        ("voxel_ms", C.c_double),
+        ("normals_ms", C.c_double),
+        ("segment_ms", C.c_double),
+        ("device_ms", C.c_double),
+        ("wall_ms", C.c_double),
+        ("knn_ms", C.c_double),
+        ("knn_queries", C.c_uint64),
+        ("knn_points_touched", C.c_uint64),
+        ("knn_nodes_touched", C.c_uint64),
+        ("propagation_passes", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
@@ -148,6 +165,7 @@ def _load():
     L.aicp_hip_default_prefilter.restype = None
     L.aicp_hip_prefilter.argtypes = [vp, C.POINTER(PrefilterParams), fp, sz, sz, fp, C.POINTER(C.c_size_t), fp, ip,
                                      C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+    L.aicp_hip_last_prefilter_stats.argtypes = [vp, C.POINTER(PrefilterStats)]
     return L
 
 
@@ -363,6 +381,11 @@ class Context:
                                    _fptr(out), C.byref(m), _fptr(rpy))
         self.check(rc)
         return out[:m.value].copy(), rpy
+
+    def last_prefilter_stats(self):
+        st = PrefilterStats()
+        self.check(lib.aicp_hip_last_prefilter_stats(self.h, C.byref(st)))
+        return {k: getattr(st, k) for k, _ in PrefilterStats._fields_ if k != "pad"}
 
     def prefilter(self, pts, params=None, details=False):
         """regionGrowingUniformPlaneSegmentationFilter (filteringUtils.cpp:5-45) on device.

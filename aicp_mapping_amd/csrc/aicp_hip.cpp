@@ -142,7 +142,8 @@ struct aicp_hip_ctx {
   double last_nn_ms = 0, last_nn_bytes = 0;
   uint64_t last_queries = 0;
   double last_phase[5] = {0, 0, 0, 0, 0};
-  int last_pf_passes = 0;  // propagation passes of the last pre-filter
+  aicp_prefilter_stats last_pf{};  // timing and kNN counts of the last pre-filter
+  hipEvent_t pf_ev[8] = {};
 };
 
 #define HIPC(x)                                                                   \
@@ -947,6 +948,8 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
   for (auto e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto e : ctx->pf_ev)
+    if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
@@ -1297,9 +1300,14 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   *out_n = 0;
   if (n_sampled) *n_sampled = 0;
   if (n_clusters) *n_clusters = 0;
+  ctx->last_pf = aicp_prefilter_stats{};
   if (n == 0) return AICP_OK;
+  const auto t_wall = std::chrono::steady_clock::now();
   HIPC(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
+  for (auto& e : ctx->pf_ev)
+    if (!e) HIPC(hipEventCreate(&e));
+  hipEvent_t* E = ctx->pf_ev;  // 0 uploaded, 1 voxels, 2 kNN start, 3 kNN end, 4 normals, 5 clusters
   // ---- scratch of the voxel grid and the extraction: ctl | pts4[n] | 9 x (n + 1) words | temp
   const size_t wn = (n + 1 + 63) & ~size_t(63);
   const size_t temp_b = pf_temp_bytes(n + 1);
@@ -1318,7 +1326,9 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   PfCtl hc{};
   for (int k = 0; k < 3; ++k) hc.lo[k] = 0xFFFFFFFFu;
   HIPC(hipMemcpyAsync(dctl, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
+  HIPC(hipEventRecord(E[0], s));
   HIPC(launch_pf_voxel(s, (uint32_t)n, pts4, 1.f / prm->leaf_size, dctl, W, ctx->ref1.as<float4>()));
+  HIPC(hipEventRecord(E[1], s));
   HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   if (hc.passthrough && hc.n_bad)
@@ -1339,13 +1349,16 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes, 0);
   if (rc) return rc;
   HIPC(ensure(ctx->match, (size_t)V * K * 4));
-  HIPC(ensure(ctx->ctrs, kCtrWords * 4));
-  HIPC(hipMemsetAsync(ctx->ctrs.p, 0, kCtrWords * 4, s));
+  HIPC(ensure(ctx->ctrs, kCtrWords * 4 + 16));
+  HIPC(hipMemsetAsync(ctx->ctrs.p, 0, kCtrWords * 4 + 16, s));
   const float4* bpts = ctx->bpts.as<float4>();
+  unsigned long long* dtouch = (unsigned long long*)(ctx->ctrs.as<uint32_t>() + kCtrWords);
+  HIPC(hipEventRecord(E[2], s));
   if (!launch_knn_ids(s, 1, V, ctx->desc.as<PairDesc>(), ctx->nodes.as<uint4>(), bpts, K, ctx->match.as<int32_t>(),
-                      ctx->ctrs.as<uint32_t>()))
+                      ctx->ctrs.as<uint32_t>(), dtouch))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   HIPC(hipGetLastError());
+  HIPC(hipEventRecord(E[3], s));
   // ---- per sampled point: inv, nrm (float4), nbp (16), ckey, cval, nob, order_of, em, label,
   // cluster_of, out4 (float4)
   const size_t vn = ((size_t)V + 63) & ~size_t(63);
@@ -1368,6 +1381,7 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   if (!launch_pf_normals(s, V, K, NB, bpts, ctx->ref1.as<float4>(), ctx->match.as<int32_t>(), inv, vp, nrm, nbp,
                          ckey, cval))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
+  HIPC(hipEventRecord(E[4], s));
   // validatePoint: cosine_threshold = cosf(theta_threshold_)
   const float cos_thr = (float)std::cos((double)prm->smoothness_rad);
   HIPC(launch_pf_order(s, V, NB, W, ckey, cval, inv, nrm, nbp, cos_thr, prm->curvature_threshold, nob, order_of, em,
@@ -1384,7 +1398,7 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(hf, flags, R * 4, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    ctx->last_pf_passes = (int)(launches + R);
+    ctx->last_pf.propagation_passes = (int)(launches + R);
     if (!hf[R - 1]) break;
   }
   launch_rg_settle(s, V, comp, label);
@@ -1395,8 +1409,20 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   HIPC(launch_rg_extract(s, V, (uint32_t)std::max(prm->min_cluster_size, 0),
                          (uint32_t)std::max(prm->max_cluster_size, 0), label, inv, ctx->ref1.as<float4>(), W, out4,
                          cluster_of, dctl));
+  HIPC(hipEventRecord(E[5], s));
   HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
+  unsigned long long ht[2] = {0, 0};
+  HIPC(hipMemcpyAsync(ht, dtouch, 16, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  aicp_prefilter_stats& ps = ctx->last_pf;
+  ps.voxel_ms = ev_ms(E[0], E[1]);
+  ps.normals_ms = ev_ms(E[1], E[4]);
+  ps.segment_ms = ev_ms(E[4], E[5]);
+  ps.device_ms = ev_ms(E[0], E[5]);
+  ps.knn_ms = ev_ms(E[2], E[3]);
+  ps.knn_queries = V;
+  ps.knn_points_touched = ht[0];
+  ps.knn_nodes_touched = ht[1];
   if (hc.n_out > V || hc.n_clusters > V) FAIL(AICP_ERR_HIP, "pre-filter: inconsistent cluster counts");
   float* h = ctx->pin_io.as<float>();
   if (hc.n_out) HIPC(hipMemcpy(h, out4, (size_t)hc.n_out * 16, hipMemcpyDeviceToHost));
@@ -1424,6 +1450,14 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
       o[7] = 0.f;
     }
   }
+  ctx->last_pf.wall_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wall).count();
+  return AICP_OK;
+}
+
+int aicp_hip_last_prefilter_stats(const aicp_hip_ctx* ctx, aicp_prefilter_stats* out) {
+  if (!ctx || !out) return AICP_ERR_INVALID;
+  *out = ctx->last_pf;
   return AICP_OK;
 }
 

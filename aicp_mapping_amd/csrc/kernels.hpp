@@ -32,9 +32,10 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
                     int32_t* ids, uint32_t* ctr);
 // the kNN of every reference point in its own tree (bucket order in and out: ids are bucket
-// positions of the pair's tree, -1 past the cloud size); eps 0, self included
+// positions of the pair's tree, -1 past the cloud size); eps 0, self included. touched
+// (nullable, zeroed): += touched points, inner nodes
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
-                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr);
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched);
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
                         ActiveList* al, uint32_t* ctr);
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st,

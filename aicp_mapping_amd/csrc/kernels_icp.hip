@@ -1260,10 +1260,12 @@ __global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, co
                                                  const uint4* __restrict__ nodes,
                                                  const int32_t* __restrict__ parent,
                                                  const float4* __restrict__ bpts,
-                                                 int32_t* __restrict__ ids, uint32_t* ctr) {
+                                                 int32_t* __restrict__ ids, uint32_t* ctr,
+                                                 unsigned long long* touched) {
   // innermost far frames in LDS (the exact kNN nests far descents often; scratch frames are
   // written back to HBM): 4 blocks of 256 per CU at this kernel's VGPR count
   __shared__ LdsFrame knn_frames[(kKnnLdsFrames > 0 ? kKnnLdsFrames : 1) * kNNBlock];
+  uint32_t tp = 0, tn = 0;
   int cur = -1;
   uint32_t cur_end = 0, cur_off = 0;
   persistent_xcd<Trav<K>>(
@@ -1286,7 +1288,21 @@ __global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, co
       [&](uint32_t s, Trav<K>& t) {
 #pragma unroll
         for (int i = 0; i < K; ++i) ids[(size_t)s * K + i] = (t.best.v[i] != __builtin_inff()) ? t.best.id[i] : -1;
+        tp += t.tp;
+        tn += t.tn;
       });
+  if (touched) {  // touched points / inner nodes (the algorithmic bytes of the roofline), optional
+    unsigned long long a = tp, b = tn;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o, 64);
+      b += __shfl_xor(b, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&touched[0], a);
+      atomicAdd(&touched[1], b);
+    }
+  }
 }
 
 template <int K>
@@ -1943,15 +1959,15 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   const int g = persistent_grid((int)total_ref), gu = (int)((total_ref + 255) / 256);
   switch (knn) {
     case 10:
-      k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr);
+      k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr, nullptr);
       k_normals_from_ids<10><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
       break;
     case 20:
-      k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr);
+      k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr, nullptr);
       k_normals_from_ids<20><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
       break;
     case 30:
-      k_knn_ids<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr);
+      k_knn_ids<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr, nullptr);
       k_normals_from_ids<30><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
       break;
     default:
@@ -1960,13 +1976,13 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   return true;
 }
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
-                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr) {
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched) {
   if (!total_ref) return true;
   const int g = persistent_grid((int)total_ref);
   switch (knn) {
-    case 10: k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr); break;
-    case 20: k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr); break;
-    case 30: k_knn_ids<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr); break;
+    case 10: k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr, touched); break;
+    case 20: k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr, touched); break;
+    case 30: k_knn_ids<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr, touched); break;
     default: return false;
   }
   return true;

@@ -167,6 +167,22 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
                        int32_t* labels /* n */, size_t* n_sampled /* nullable */,
                        size_t* n_clusters /* nullable */);
 
+/* Timing of the last aicp_hip_prefilter (HIP events on the context stream). */
+typedef struct {
+  double voxel_ms;          /* VoxelGrid: bounds, keys, sort, centroids */
+  double normals_ms;        /* kd-tree of the sampled cloud, kNN, normals */
+  double segment_ms;        /* RegionGrowing: seed order, union-find, propagation (with its host
+                               round trips), cluster extraction */
+  double device_ms;         /* input uploaded -> clusters ready */
+  double wall_ms;           /* the whole call: host packing, PCIe both ways */
+  double knn_ms;            /* the kNN kernel alone */
+  uint64_t knn_queries;     /* sampled points */
+  uint64_t knn_points_touched, knn_nodes_touched;
+  int32_t propagation_passes;
+  int32_t pad;
+} aicp_prefilter_stats;
+int aicp_hip_last_prefilter_stats(const aicp_hip_ctx* ctx, aicp_prefilter_stats* out);
+
 /* ---- device-resident batches (inputs uploaded once, run many times) ----------------------- */
 int aicp_hip_batch_upload(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs,
                           aicp_hip_batch** out);
