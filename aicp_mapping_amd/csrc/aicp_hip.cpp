@@ -1362,7 +1362,7 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   // ---- per sampled point: inv, nrm (float4), nbp (16), ckey, cval, nob, order_of, em, label,
   // cluster_of, out4 (float4)
   const size_t vn = ((size_t)V + 63) & ~size_t(63);
-  HIPC(ensure(ctx->pf_b, vn * 4 * (1 + 4 + kPfMaxNbrs + 8 + 4) + 256));
+  HIPC(ensure(ctx->pf_b, vn * 4 * (1 + 4 + kPfMaxNbrs + 8 + 4 + 2) + 256));
   uint32_t* B = ctx->pf_b.as<uint32_t>();
   uint32_t* inv = B;
   float4* nrm = (float4*)(B + vn);
@@ -1376,16 +1376,17 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   int32_t* cluster_of = (int32_t*)(label + vn);
   float4* out4 = (float4*)(cluster_of + vn);
   uint32_t* comp = (uint32_t*)(out4 + vn);
-  uint32_t* flags = comp + vn;
+  uint2* kth = (uint2*)(comp + vn);
+  uint32_t* flags = (uint32_t*)(kth + vn);
   const float vp[3] = {prm->viewpoint[0], prm->viewpoint[1], prm->viewpoint[2]};
   if (!launch_pf_normals(s, V, K, NB, bpts, ctx->ref1.as<float4>(), ctx->match.as<int32_t>(), inv, vp, nrm, nbp,
-                         ckey, cval))
+                         kth, ckey, cval))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   HIPC(hipEventRecord(E[4], s));
   // validatePoint: cosine_threshold = cosf(theta_threshold_)
   const float cos_thr = (float)std::cos((double)prm->smoothness_rad);
-  HIPC(launch_pf_order(s, V, NB, W, ckey, cval, inv, nrm, nbp, cos_thr, prm->curvature_threshold, nob, order_of, em,
-                       label));
+  HIPC(launch_pf_order(s, V, NB, W, ckey, cval, inv, bpts, nrm, nbp, kth, cos_thr, prm->curvature_threshold, nob,
+                       order_of, em, label));
   // ---- min-label propagation to the fixed point: union-find over mutual edges, then passes
   // until one changes no label (labels only decrease, so this ends; V passes bound any schedule)
   launch_rg_components(s, V, NB, nbp, em, comp, label);

@@ -163,15 +163,15 @@ hipError_t launch_pf_voxel(hipStream_t s, uint32_t n, const float4* pts, float i
 // NormalEstimation from the kNN of the sampled tree (bucket order); k in {10, 20, 30}
 // ids: launch_knn_ids output (bucket positions)
 bool launch_pf_normals(hipStream_t s, uint32_t V, int k, int nnb, const float4* bpts, const float4* sampled,
-                       const int32_t* ids, uint32_t* inv, const float vp[3], float4* nrm, int32_t* nbp, uint32_t* ckey,
-                       uint32_t* cval);
+                       const int32_t* ids, uint32_t* inv, const float vp[3], float4* nrm, int32_t* nbp, uint2* kth,
+                       uint32_t* ckey, uint32_t* cval);
 // seed order, edge masks and initial labels
 hipError_t launch_pf_order(hipStream_t s, uint32_t V, int nnb, const PfWork& w, const uint32_t* ckey,
-                           const uint32_t* cval, const uint32_t* inv, const float4* nrm, const int32_t* nbp,
-                           float cos_thr, float curv_thr, uint32_t* nob, uint32_t* order_of, uint32_t* em,
-                           uint32_t* label);
-// union-find over mutual edges: comp[x] = component root, roots start at their members' minimum
-void launch_rg_components(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, uint32_t* comp,
+                           const uint32_t* cval, const uint32_t* inv, const float4* bpts, const float4* nrm,
+                           const int32_t* nbp, const uint2* kth, float cos_thr, float curv_thr, uint32_t* nob,
+                           uint32_t* order_of, uint32_t* em, uint32_t* label);
+// union-find over mutual edges (marked in em bits 17..): comp[x] = component root, roots start at their members' minimum
+void launch_rg_components(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, uint32_t* em, uint32_t* comp,
                           uint32_t* label);
 void launch_rg_iter(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, const uint32_t* nob,
                     const uint32_t* comp, uint32_t* label, uint32_t* changed);

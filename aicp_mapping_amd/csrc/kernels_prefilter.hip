@@ -290,8 +290,8 @@ __global__ __launch_bounds__(256) void k_pf_normals(uint32_t V, int nnb, const f
                                                     const float4* __restrict__ sampled, const int32_t* __restrict__ ids,
                                                     const uint32_t* __restrict__ inv,
                                                     float vpx, float vpy, float vpz, float4* __restrict__ nrm,
-                                                    int32_t* __restrict__ nbp, uint32_t* __restrict__ ckey,
-                                                    uint32_t* __restrict__ cval) {
+                                                    int32_t* __restrict__ nbp, uint2* __restrict__ kth,
+                                                    uint32_t* __restrict__ ckey, uint32_t* __restrict__ cval) {
   const uint32_t j = blockIdx.x * 256u + threadIdx.x;
   if (j >= V) return;
   const float4 p = bpts[j];
@@ -385,6 +385,16 @@ __global__ __launch_bounds__(256) void k_pf_normals(uint32_t V, int nnb, const f
     }
   }
   nrm[j] = make_float4(nx, ny, nz, curv);
+  // the last of the first nnb neighbours, (d2, sampled id): y is among x's nnb nearest iff
+  // (d2(x, y), id y) <= kth[x] (the mutual-edge test of k_pf_edges)
+  {
+    const int last = (nnb < cnt ? nnb : cnt) - 1;
+    uint2 k = make_uint2(0u, 0u);
+#pragma unroll
+    for (int t = 0; t < K; ++t)
+      if (t == last) k = make_uint2(__float_as_uint(d[t]), (uint32_t)id[t]);
+    kth[j] = k;
+  }
 #pragma unroll
   for (int t = 0; t < kPfMaxNbrs; ++t) {
     int32_t v = -1;
@@ -411,23 +421,38 @@ __global__ __launch_bounds__(256) void k_pf_rank(uint32_t V, const uint32_t* __r
 
 // validatePoint's smoothness test per edge x -> y (|n_y . n_x| < cos rejects, a NaN dot passes)
 // as a bit mask, bit 16 = prop (curvature not above the threshold); initial labels
-__global__ __launch_bounds__(256) void k_pf_edges(uint32_t V, int nnb, const float4* __restrict__ nrm,
-                                                  const int32_t* __restrict__ nbp, const uint32_t* __restrict__ order_of,
+__global__ __launch_bounds__(256) void k_pf_edges(uint32_t V, int nnb, const float4* __restrict__ bpts,
+                                                  const float4* __restrict__ nrm, const int32_t* __restrict__ nbp,
+                                                  const uint2* __restrict__ kth, const uint32_t* __restrict__ order_of,
                                                   float cos_thr, float curv_thr, uint32_t* __restrict__ em,
                                                   uint32_t* __restrict__ label) {
   const uint32_t x = blockIdx.x * 256u + threadIdx.x;
   if (x >= V) return;
   const float4 n = nrm[x];
-  uint32_t m = 0;
+  const float4 p = bpts[x];
+  const bool prop = !(n.w > curv_thr);
+  uint32_t m = 0, mm = 0;
   for (int t = 0; t < nnb; ++t) {
     const int32_t y = nbp[(size_t)x * kPfMaxNbrs + t];
     if (y < 0) break;
     const float4 ny = nrm[y];
     const float dot = fabsf(ny.x * n.x + (ny.y * n.y + ny.z * n.z));
-    if (!(dot < cos_thr)) m |= 1u << t;
+    if (dot < cos_thr) continue;
+    m |= 1u << t;
+    // mutual: y prop too and x among y's nnb nearest, by y's (d2, id) order (d2 is symmetric)
+    if (prop && !(ny.w > curv_thr)) {
+      const float4 q = bpts[y];
+      const float e0 = q.x - p.x, e1 = q.y - p.y, e2 = q.z - p.z;
+      float d = 0.f;
+      d += e0 * e0;
+      d += e1 * e1;
+      d += e2 * e2;
+      const uint2 k = kth[y];
+      const float kd = __uint_as_float(k.x);
+      if (d < kd || (d == kd && __float_as_uint(p.w) <= k.y)) mm |= 1u << t;
+    }
   }
-  const bool prop = !(n.w > curv_thr);
-  em[x] = m | (prop ? 1u << 16 : 0u);
+  em[x] = m | (prop ? 1u << 16 : 0u) | (mm << 17);
   label[x] = prop ? order_of[x] : kInf;
 }
 
@@ -435,15 +460,17 @@ __global__ __launch_bounds__(256) void k_pf_edges(uint32_t V, int nnb, const flo
 // reach each other, so a component shares one label, and a label reaching any member reaches
 // all of them: the propagation adds the member <-> root shortcuts (k_rg_iter), which turns the
 // plane-wide wavefront of plain label propagation (one kNN radius per pass) into a few passes.
-// par[v] <= v always (a root is hung under a smaller root), loads bypass the vector L1 so that a
-// failed CAS is never retried against a stale root.
-__device__ __forceinline__ uint32_t uf_ld(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// par[v] <= v always (a root is hung under a smaller root).
+// Plain (L1-cacheable) loads: every find ends at its root, and the root of a plane-wide
+// component is one word read by every thread, which an L1-bypassing load turns into a hot
+// spot in one L2 channel. A stale cached parent is always an older ancestor (parents only move
+// up, par[v] <= v), so finds stay correct; a CAS that fails because its "root" was hooked in
+// the meantime returns the real parent, and the hook continues from there (k_uf_hook), so a
+// stale line never makes it spin.
 __device__ __forceinline__ uint32_t uf_root(uint32_t* par, uint32_t x) {
-  uint32_t p = uf_ld(par + x);
+  uint32_t p = par[x];
   while (p != x) {
-    const uint32_t g = uf_ld(par + p);
+    const uint32_t g = par[p];
     if (g == p) return p;
     par[x] = g;  // path halving; g is still an ancestor of x whatever other threads do
     x = p;
@@ -475,26 +502,64 @@ __device__ __forceinline__ bool wave_min_to(uint32_t* label, uint32_t r, uint32_
   return dec;
 }
 
-__global__ __launch_bounds__(256) void k_uf_init(uint32_t V, uint32_t* __restrict__ par) {
-  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
-  if (x < V) par[x] = x;
+// tile-local union-find in LDS: the mutual edges inside each tile of 1024 consecutive bucket
+// positions (a compact patch), flattened into par as global ids. The global hook then sees only
+// the edges that cross tiles.
+__device__ __forceinline__ uint32_t lds_root(uint32_t* lp, uint32_t x) {
+  uint32_t p = lp[x];
+  while (p != x) {
+    const uint32_t g = lp[p];
+    if (g == p) return p;
+    lp[x] = g;
+    x = p;
+    p = g;
+  }
+  return x;
+}
+constexpr int kUfTile = 1024;
+__global__ __launch_bounds__(kUfTile) void k_uf_tile(uint32_t V, int nnb, const int32_t* __restrict__ nbp,
+                                                     const uint32_t* __restrict__ em, uint32_t* __restrict__ par) {
+  __shared__ uint32_t lp[kUfTile];
+  const uint32_t base = blockIdx.x * (uint32_t)kUfTile, x = base + threadIdx.x;
+  lp[threadIdx.x] = threadIdx.x;
+  __syncthreads();
+  const uint32_t mm = x < V ? em[x] >> 17 : 0u;
+  for (int t = 0; t < nnb; ++t) {
+    if (!((mm >> t) & 1u)) continue;
+    const int32_t y = nbp[(size_t)x * kPfMaxNbrs + t];
+    const uint32_t r = (uint32_t)y - base;
+    if (y <= (int32_t)x || r >= (uint32_t)kUfTile) continue;
+    uint32_t a = threadIdx.x, b = r;
+    for (;;) {
+      uint32_t ra = lds_root(lp, a), rb = lds_root(lp, b);
+      if (ra == rb) break;
+      if (ra < rb) {
+        const uint32_t t2 = ra;
+        ra = rb;
+        rb = t2;
+      }
+      const uint32_t old = atomicCAS(&lp[ra], ra, rb);
+      if (old == ra) break;
+      a = old;
+      b = rb;
+    }
+  }
+  __syncthreads();
+  if (x < V) par[x] = base + lds_root(lp, threadIdx.x);
 }
 
+// hook the mutual edges that cross tiles, each from its smaller end; roots are read through
+// uf_root, so an edge inside one tree costs no CAS
 __global__ __launch_bounds__(256) void k_uf_hook(uint32_t V, int nnb, const int32_t* __restrict__ nbp,
                                                  const uint32_t* __restrict__ em, uint32_t* par) {
   const uint32_t x = blockIdx.x * 256u + threadIdx.x;
   if (x >= V) return;
-  const uint32_t m = em[x];
-  if (!((m >> 16) & 1u)) return;
+  const uint32_t mm = em[x] >> 17;
+  if (!mm) return;
   for (int t = 0; t < nnb; ++t) {
-    if (!((m >> t) & 1u)) continue;
+    if (!((mm >> t) & 1u)) continue;
     const int32_t y = nbp[(size_t)x * kPfMaxNbrs + t];
-    if (y <= (int32_t)x) continue;  // each mutual edge once, from its smaller end
-    const uint32_t my = em[y];
-    if (!((my >> 16) & 1u)) continue;
-    bool back = false;
-    for (int u = 0; u < nnb && !back; ++u) back = ((my >> u) & 1u) && nbp[(size_t)y * kPfMaxNbrs + u] == (int32_t)x;
-    if (!back) continue;
+    if (y <= (int32_t)x || (uint32_t)y / kUfTile == x / kUfTile) continue;  // once; tile edges are done
     uint32_t a = x, b = (uint32_t)y;
     for (;;) {
       uint32_t ra = uf_root(par, a), rb = uf_root(par, b);
@@ -504,8 +569,9 @@ __global__ __launch_bounds__(256) void k_uf_hook(uint32_t V, int nnb, const int3
         ra = rb;
         rb = t2;
       }
-      if (atomicCAS(&par[ra], ra, rb) == ra) break;
-      a = ra;
+      const uint32_t old = atomicCAS(&par[ra], ra, rb);
+      if (old == ra) break;
+      a = old;  // ra was hooked meanwhile: continue from its real parent
       b = rb;
     }
   }
@@ -706,35 +772,35 @@ hipError_t launch_pf_voxel(hipStream_t s, uint32_t n, const float4* pts, float i
 }
 
 bool launch_pf_normals(hipStream_t s, uint32_t V, int k, int nnb, const float4* bpts, const float4* sampled,
-                       const int32_t* ids, uint32_t* inv, const float vp[3], float4* nrm, int32_t* nbp, uint32_t* ckey,
-                       uint32_t* cval) {
+                       const int32_t* ids, uint32_t* inv, const float vp[3], float4* nrm, int32_t* nbp, uint2* kth,
+                       uint32_t* ckey, uint32_t* cval) {
   if (V == 0) return true;
   k_pf_inv<<<blocks_for(V), 256, 0, s>>>(V, bpts, inv);
   switch (k) {
-    case 10: k_pf_normals<10><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
-    case 20: k_pf_normals<20><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
-    case 30: k_pf_normals<30><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, ckey, cval); break;
+    case 10: k_pf_normals<10><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, kth, ckey, cval); break;
+    case 20: k_pf_normals<20><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, kth, ckey, cval); break;
+    case 30: k_pf_normals<30><<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, sampled, ids, inv, vp[0], vp[1], vp[2], nrm, nbp, kth, ckey, cval); break;
     default: return false;
   }
   return true;
 }
 
 hipError_t launch_pf_order(hipStream_t s, uint32_t V, int nnb, const PfWork& w, const uint32_t* ckey,
-                           const uint32_t* cval, const uint32_t* inv, const float4* nrm, const int32_t* nbp,
-                           float cos_thr, float curv_thr, uint32_t* nob, uint32_t* order_of, uint32_t* em,
-                           uint32_t* label) {
+                           const uint32_t* cval, const uint32_t* inv, const float4* bpts, const float4* nrm,
+                           const int32_t* nbp, const uint2* kth, float cos_thr, float curv_thr, uint32_t* nob,
+                           uint32_t* order_of, uint32_t* em, uint32_t* label) {
   if (V == 0) return hipSuccess;
   const hipError_t e = sort_u32(s, w.temp, w.temp_bytes, ckey, w.k1, cval, w.v1, V);
   if (e != hipSuccess) return e;
   k_pf_rank<<<blocks_for(V), 256, 0, s>>>(V, w.v1, inv, nob, order_of);
-  k_pf_edges<<<blocks_for(V), 256, 0, s>>>(V, nnb, nrm, nbp, order_of, cos_thr, curv_thr, em, label);
+  k_pf_edges<<<blocks_for(V), 256, 0, s>>>(V, nnb, bpts, nrm, nbp, kth, order_of, cos_thr, curv_thr, em, label);
   return hipGetLastError();
 }
 
-void launch_rg_components(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, const uint32_t* em, uint32_t* comp,
+void launch_rg_components(hipStream_t s, uint32_t V, int nnb, const int32_t* nbp, uint32_t* em, uint32_t* comp,
                           uint32_t* label) {
   if (!V) return;
-  k_uf_init<<<blocks_for(V), 256, 0, s>>>(V, comp);
+  k_uf_tile<<<(V + kUfTile - 1) / kUfTile, kUfTile, 0, s>>>(V, nnb, nbp, em, comp);
   k_uf_hook<<<blocks_for(V), 256, 0, s>>>(V, nnb, nbp, em, comp);
   k_uf_compress<<<blocks_for(V), 256, 0, s>>>(V, comp, label);
 }

@@ -311,9 +311,13 @@ __global__ __launch_bounds__(256) void k_tr_center(int n_pairs, uint32_t total, 
     float mn = ok ? v[k] : __builtin_inff(), mx = ok ? v[k] : -__builtin_inff();
     if (uniform) {
       block_minmax(mn, mx);
+      // one cloud spans thousands of blocks: skip the atomic when the box already holds the
+      // bound (a read costs no serialisation on the six shared words; a stale read only
+      // lets an unnecessary atomic through)
       if (threadIdx.x == 0) {
-        atomicMin(&seg[p_first].bmn[k], ord_enc(mn));
-        atomicMax(&seg[p_first].bmx[k], ord_enc(mx));
+        const uint32_t emn = ord_enc(mn), emx = ord_enc(mx);
+        if (emn < seg[p_first].bmn[k]) atomicMin(&seg[p_first].bmn[k], emn);
+        if (emx > seg[p_first].bmx[k]) atomicMax(&seg[p_first].bmx[k], emx);
       }
     } else {
       const bool lastl = wave_seg_minmax(pair, mn, mx);
@@ -383,9 +387,10 @@ __global__ __launch_bounds__(256) void k_tr_minmax(uint32_t total, const int32_t
   float mn = s >= 0 ? v : __builtin_inff(), mx = s >= 0 ? v : -__builtin_inff();
   if (uniform) {
     block_minmax(mn, mx);
-    if (threadIdx.x == 0) {
-      atomicMin(&seg[s_first].lo, ord_enc(mn));
-      atomicMax(&seg[s_first].hi, ord_enc(mx));
+    if (threadIdx.x == 0) {  // top levels: thousands of blocks per segment; see k_tr_center
+      const uint32_t emn = ord_enc(mn), emx = ord_enc(mx);
+      if (emn < seg[s_first].lo) atomicMin(&seg[s_first].lo, emn);
+      if (emx > seg[s_first].hi) atomicMax(&seg[s_first].hi, emx);
     }
     return;
   }
