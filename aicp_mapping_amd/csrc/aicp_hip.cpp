@@ -463,17 +463,29 @@ int device_trees_check(TreeBufs& T, std::string& err) {
 
 // Global levels to enqueue for clouds of at most n_max points: segments above kSubMax points
 // halve per level on balanced data; sliding-midpoint splits can peel off small slices, so the
-// plan keeps a margin and never goes below what the previous build of this tree needed.
+// first plan keeps a margin, and later plans follow what the previous build of this tree used
+// (every planned level costs its launches and two full-length scans even when no segment is
+// left: C2 with 8 instead of 11 levels, +2 %).
 // AICP_TREE_PLAN=k forces k levels (tests: a too-shallow plan); AICP_TREE_PLAN=0 selects the
 // host-polled build (A/B measurements).
-int plan_levels(uint64_t n_max, const TreeBufs& T) {
+int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean = false) {
   if (const char* e = std::getenv("AICP_TREE_PLAN")) {
     const int v = std::atoi(e);
     return v > 0 ? std::min(kFarStack - 2, v) : 0;
   }
   int l = 0;
   while (((uint64_t)kSubMax << l) < n_max) ++l;
-  return std::min(kFarStack - 2, std::max(l + 4, T.needed + 1));
+  // lean: the balanced estimate + 1, whatever the previous build used; the few segments still
+  // above kSubMax go to the subtree kernel's global path (used for the raw-coordinate tree on
+  // the critical stream: C2 +2 %, the leftovers cost less than the full-length levels)
+  if (lean) {
+    const char* e = std::getenv("AICP_TREE_LEAN");
+    if (!e || std::atoi(e) != 0) return std::min(kFarStack - 2, l + 1);
+  }
+  // with a previous build of this tree: the levels it used (a cloud that needs more leaves a few
+  // segments above kSubMax to the subtree kernel's global path once, and the next plan grows);
+  // without one: a margin of 4 levels over the balanced estimate
+  return std::min(kFarStack - 2, T.needed > 0 ? std::max(l + 1, T.needed) : l + 4);
 }
 
 // the centred reference's matcher tree and the pairs' frames, on stream3 (worker thread)
@@ -496,14 +508,14 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
     const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);  // node records allotted
     const size_t tb = tree_scan_temp_bytes((size_t)cap + 1);
     TCHK(ensure(ctx->tl, ctx->tl_total * 16));
-    TCHK(ensure(ctx->ptl, ctx->tl_total * 4));
+    TCHK(ensure(ctx->ptl, ctx->tl_total * 8));  // treelet links {parent, grandparent}
     TCHK(ensure(ctx->tl_flag, ((size_t)cap + 1) * 4));
     TCHK(ensure(ctx->tl_rank, ((size_t)cap + 1) * 4));
     TCHK(ensure(ctx->tl_temp, tb));
     TreeBufs& T = ctx->tb[1];
     TCHK(launch_treelets(s3, (int)R, cap, dRdesc, ctx->nodes.as<uint4>(), bucket, ctx->tl_flag.as<uint32_t>(),
                          ctx->tl_rank.as<uint32_t>(), ctx->tl_temp.p, tb, ctx->tl.as<uint4>(),
-                         ctx->ptl.as<uint32_t>(), T.tw.ctl));
+                         ctx->ptl.as<uint2>(), T.tw.ctl));
     TCHK(hipMemcpyAsync(T.pin_ctl.p, T.tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
   }
   launch_pairs_from_refs(s3, (int)B->P, dDesc, dRdesc);
@@ -671,7 +683,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     // s2: raw tree levels + subtrees, SurfaceNormal, all enqueued before the host waits for
     // the overlap's key boxes
     rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), cfg->bucket_size,
-                          ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0]));
+                          ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0], true));
     if (rc) return join_worker(rc);
     // normals on the raw tree (bucket order of that tree)
     HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
@@ -782,7 +794,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it], s));
       launch_icp_nn(s, (int)B->total_read, dDesc, dState, dAl, readc, nodes,
                     ctx->tl_total ? ctx->tl.as<uint4>() : nullptr, parent, bpts,
-                    ctx->tl_total ? ctx->ptl.as<uint32_t>() : nullptr, ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm);
+                    ctx->tl_total ? ctx->ptl.as<uint2>() : nullptr, ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm);
       if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it + 1], s));
       ++nn_launches;
       launch_icp_select(s, B->m_sel, (int)P, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),

@@ -40,7 +40,7 @@ void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const Pa
                         ActiveList* al, uint32_t* ctr);
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st,
                    const ActiveList* al, const float4* read_c, const uint4* nodes, const uint4* tl,
-                   const int32_t* parent, const float4* bpts, const uint32_t* ptl, int32_t* match, float* d2,
+                   const int32_t* parent, const float4* bpts, const uint2* ptl, int32_t* match, float* d2,
                    uint32_t* touched, uint32_t* ctr, const IcpParams& prm);
 // TrimmedDist limit per active pair. m: blocks of kNNBlock * kReducePerThread readings;
 // hist1: n_pairs * kHistBins zeroed words, cand: total_read words, cand_cnt: n_pairs zeroed
@@ -99,7 +99,7 @@ size_t tree_scan_temp_bytes(size_t n);
 // words each; temp: tree_scan_temp_bytes(cap + 1); errors into ctl->error (bit 4)
 hipError_t launch_treelets(hipStream_t s, int n_refs, uint32_t cap, const PairDesc* rd, const uint4* nodes,
                            int bucket, uint32_t* flag, uint32_t* rank, void* temp, size_t temp_bytes, uint4* tl,
-                           uint32_t* ptl, TreeCtl* ctl);
+                           uint2* link, TreeCtl* ctl);
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
                                int center, const TreeWork& w, float4* bpts, int bucket);
 // one level: nodes at depth `level` are split (their children get depth level + 1)

@@ -119,6 +119,9 @@ constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #ifndef AICP_NN_CLIMB2
 #define AICP_NN_CLIMB2 1  // Trav2C: climb one treelet (record + parent, up to two levels) per iteration
 #endif
+#ifndef AICP_NN_CLIMB4
+#define AICP_NN_CLIMB4 0  // Trav2C (with CLIMB2): two treelets per climb round trip through the treelet links (measured 6 % slower: the extra records are mostly not needed)
+#endif
 #ifndef AICP_NN_LDS_FRAMES
 #define AICP_NN_LDS_FRAMES 3  // Trav2C: innermost far-descent frames kept in LDS (20 B each per lane; 4 measured no faster)
 #endif
@@ -295,7 +298,7 @@ __device__ __forceinline__ float min_bound(float a, float b) {
 
 struct Trav2C {
   const uint4* tl;       // the pair's treelets
-  const uint32_t* ptl;   // the pair's treelet parents
+  const uint2* ptl;      // the pair's treelet links {parent of the root, parent of the parent treelet's root}
   uint32_t pbase;        // the pair's first bucket point
   float q0, q1, q2;
   float noc0, noc1, noc2, rd, minFar;  // noc = -(off * off) per axis (libnabo's off[] enters only so)
@@ -307,7 +310,7 @@ struct Trav2C {
   uint32_t tp, tn;
   Best<1> best;
 
-  __device__ __forceinline__ void bind(const uint4* t, const uint32_t* b, uint32_t tl_off, uint32_t ref_off) {
+  __device__ __forceinline__ void bind(const uint4* t, const uint2* b, uint32_t tl_off, uint32_t ref_off) {
     tl = t + tl_off;
     ptl = b + tl_off;
     pbase = ref_off;
@@ -447,6 +450,80 @@ struct Trav2C {
     return true;
   }
 
+#if AICP_NN_CLIMB4
+  // far tests of node p (slot s of record r) and, for a child slot, of the treelet root above
+  // it: true on a far push; else c / pc advance to the highest node tested / its parent (stopping
+  // at start)
+  __device__ __forceinline__ bool climb_treelet(FarStack& fs, const uint4& r, int32_t p, int32_t rootpp, int32_t& c,
+                                                int32_t& pc, float maxE2, float maxR2) {
+    const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
+    const int32_t root = (int32_t)(T << 2);
+    if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2)) return true;
+    c = p;
+    pc = s != 0 ? root : rootpp;
+    if (s == 0 || c == start) return false;
+    if (far_push(fs, r, root, 0, rootpp, maxE2, maxR2)) return true;
+    c = root;
+    pc = rootpp;
+    return false;
+  }
+
+  // the climb two treelets (up to four levels) per round trip: the links {parent of the
+  // treelet's root, parent of the parent treelet's root} name the next two treelets before
+  // their records arrive. After a descent or a frame pop the first step knows only the node to
+  // test, so it loads one record and its link.
+  __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
+    int32_t c = n, pc = pl;
+    int32_t px = 0;
+    bool have_px = false;  // px: parent node of pc's treelet's root
+    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+    for (;;) {
+      if (c == start) {
+        if (sp == 0) return true;
+        --sp;
+        FarFrame f;
+        if (sp < AICP_NN_LDS_FRAMES) {
+          const NnLdsFrame g = lf[sp * kNNBlock];
+          const int32_t mi = __float_as_int(g.mnf);
+          f = FarFrame{g.PPcd, g.rd, g.old, __int_as_float(mi & 0x7fffffff), g.start, mi < 0 ? g.start : -2,
+                       g.PPcd & 0x3fffffff, 0};
+        } else {
+          f = fs.f[sp];
+        }
+        const uint32_t pcd = (uint32_t)f.F >> 30;
+        rd = f.rd;
+        if (pcd == 0) noc0 = f.old;
+        else if (pcd == 1) noc1 = f.old;
+        else noc2 = f.old;
+        minFar = f.mn;
+        start = f.start;
+        c = f.P;
+        pc = f.PP;
+        have_px = false;
+        if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+        continue;
+      }
+      const uint32_t X = (uint32_t)pc >> 2;
+      if (!have_px) {
+        const uint4 r = ld_rec(tl + X);
+        const uint2 lk = ptl[X];
+        if (climb_treelet(fs, r, pc, (int32_t)lk.x, c, pc, maxE2, maxR2)) return false;
+        px = (int32_t)lk.y;
+        have_px = c != start;
+        continue;
+      }
+      // pc in treelet X, px = parent of X's root in treelet Y (px < 0: X is the root treelet)
+      const uint4 rx = ld_rec(tl + X);
+      const uint32_t Y = (uint32_t)max(px, 0) >> 2;
+      const uint4 ry = ld_rec(tl + Y);
+      const uint2 ly = ptl[Y];
+      if (climb_treelet(fs, rx, pc, px, c, pc, maxE2, maxR2)) return false;
+      if (c == start || px < 0) continue;  // px < 0: X's root is the tree root, so c == start there
+      if (climb_treelet(fs, ry, px, (int32_t)ly.x, c, pc, maxE2, maxR2)) return false;
+      px = (int32_t)ly.y;
+    }
+  }
+#else
   // the climb one treelet per iteration: one record (and its root's parent) per round trip, the
   // node and, for a child slot, the treelet root above it
   __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
@@ -481,7 +558,7 @@ struct Trav2C {
       const int32_t p = pc;
       const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
       const uint4 r = ld_rec(tl + T);
-      const int32_t rootpp = (int32_t)ptl[T];
+      const int32_t rootpp = (int32_t)ptl[T].x;
       const int32_t root = (int32_t)(T << 2);
       if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2)) return false;
       c = p;
@@ -492,6 +569,7 @@ struct Trav2C {
       pc = rootpp;
     }
   }
+#endif  // AICP_NN_CLIMB4
 #else
   __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
     int32_t c = n, pc = pl;
@@ -534,7 +612,7 @@ struct Trav2C {
       if (T != cT) {  // the record and its root's parent, one round trip per treelet
         cT = T;
         cr = ld_rec(tl + T);
-        cpp = (int32_t)ptl[T];
+        cpp = (int32_t)ptl[T].x;
       }
       const uint4 r = cr;
       const int32_t pp = s != 0 ? (int32_t)(T << 2) : cpp;  // parent of p
@@ -592,7 +670,7 @@ enum : int32_t { kPhDesc = 0, kPhLeaf = 1, kPhClimb = 2 };
 
 struct Trav2S {
   const uint4* tl;
-  const uint32_t* ptl;
+  const uint2* ptl;
   uint32_t pbase;
   float q0, q1, q2;
   float off0, off1, off2, rd, minFar;
@@ -603,7 +681,7 @@ struct Trav2S {
   uint32_t tp, tn;
   Best<1> best;
 
-  __device__ __forceinline__ void bind(const uint4* t, const uint32_t* b, uint32_t tl_off, uint32_t ref_off) {
+  __device__ __forceinline__ void bind(const uint4* t, const uint2* b, uint32_t tl_off, uint32_t ref_off) {
     tl = t + tl_off;
     ptl = b + tl_off;
     pbase = ref_off;
@@ -1070,7 +1148,7 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       if (has && t.ph != kPhLeaf) {
         const uint32_t T = t.need();
         const uint4 r = ld_rec(t.tl + T);
-        const int32_t rootpp = (int32_t)t.ptl[T];
+        const int32_t rootpp = (int32_t)t.ptl[T].x;
         if (t.ph == kPhDesc) t.desc_step(r);
         else t.climb_step(fs, r, rootpp, maxE2, maxR2);
       }
@@ -1385,7 +1463,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
                                                 const float4* __restrict__ read_c,
                                                 const uint4* __restrict__ nodes,
                                                 const int32_t* __restrict__ parent,
-                                                const float4* __restrict__ bpts, const uint32_t* __restrict__ ptl,
+                                                const float4* __restrict__ bpts, const uint2* __restrict__ ptl,
                                                 int32_t* __restrict__ match,
                                                 float* __restrict__ d2out, uint32_t* __restrict__ touched,
                                                 uint32_t* ctr, IcpParams prm) {
@@ -2005,7 +2083,7 @@ static int nn_engine() {
 
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st, const ActiveList* al,
                    const float4* read_c, const uint4* nodes, const uint4* tl, const int32_t* parent,
-                   const float4* bpts, const uint32_t* ptl, int32_t* match, float* d2, uint32_t* touched,
+                   const float4* bpts, const uint2* ptl, int32_t* match, float* d2, uint32_t* touched,
                    uint32_t* ctr, const IcpParams& prm) {
   const int g = persistent_grid(grid_items, AICP_NN_WAVES);
   if (nn_engine() == 4 && tl && ptl)

@@ -908,9 +908,10 @@ static hipError_t scan_u32(hipStream_t s, void* temp, size_t temp_bytes, const u
 // child pointer is stored. Slot 0 of a reference is the root's treelet; a treelet that has
 // grandchildren gets its block of 4 at base = 1 + 4 * rank, rank = its position among such
 // treelets in preorder (one scan), so every treelet's index follows from its grandparent's base
-// without a level-by-level pass. ptl[T] = the node id (treelet << 2 | slot) of the parent of T's
-// root, -1 for the root treelet (the climb's step out of a treelet). Indices are local to the
-// reference (PairDesc::tl_off, for tl and ptl).
+// without a level-by-level pass. link[T].x = the node id (treelet << 2 | slot) of the parent of
+// T's root, -1 for the root treelet (the climb's step out of a treelet); link[T].y = the same for
+// the parent treelet (two treelets ahead). Indices are local to the reference (PairDesc::tl_off,
+// for tl and link).
 __device__ __forceinline__ int ref_of_node(const PairDesc* __restrict__ rd, int n_refs, uint32_t g) {
   int lo = 0, hi = n_refs - 1;  // the reference owning node g (node_off ascending)
   while (lo < hi) {
@@ -947,7 +948,7 @@ __device__ __forceinline__ uint32_t tl_slot(const uint4& a) {
 
 __global__ __launch_bounds__(256) void k_tl_build(int n_refs, uint32_t cap, const PairDesc* __restrict__ rd,
                                                   const uint4* __restrict__ nodes, const uint32_t* __restrict__ rank,
-                                                  uint4* __restrict__ tl, uint32_t* __restrict__ ptl) {
+                                                  uint4* __restrict__ tl, uint2* __restrict__ link) {
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
   const uint32_t total = rd[n_refs - 1].node_off + rd[n_refs - 1].n_nodes;
   if (g >= total || g >= cap) return;
@@ -967,13 +968,16 @@ __global__ __launch_bounds__(256) void k_tl_build(int n_refs, uint32_t cap, cons
   };
   const uint32_t id = id_of(v);
   if (id >= r.tl_cap) return;  // k_tl_check reports it
-  // parent of the treelet's root as a node id: the grandparent's treelet, slot of the parent
-  if (v == 0) {
-    ptl[r.tl_off + id] = 0xffffffffu;
-  } else {
-    const uint32_t p = a.z, gp = nd[p].z;
-    ptl[r.tl_off + id] = id_of(gp) << 2 | (p != gp + 1 ? 2u : 1u);
-  }
+  // parent of a treelet root u as a node id: the grandparent's treelet, slot of the parent
+  auto up_of = [&](uint32_t u) -> uint32_t {
+    if (u == 0) return 0xffffffffu;
+    const uint32_t p = nd[u].z, gp = nd[p].z;
+    return id_of(gp) << 2 | (p != gp + 1 ? 2u : 1u);
+  };
+  // link = {parent of this treelet's root, parent of the parent treelet's root}: the climb
+  // names two treelets ahead (kernels_icp.hip, AICP_NN_CLIMB4)
+  const uint32_t up = up_of(v);
+  link[r.tl_off + id] = make_uint2(up, v == 0 ? 0xffffffffu : up_of(nd[a.z].z));  // nd[a.z].z: the grandparent, root of the parent treelet
   uint4 rec = make_uint4(tl_slot(a), 0u, 0u, a.y & 3u);
   if ((a.y & 3u) != kLeaf) {
     const uint4 L = nd[v + 1], R = nd[a.y >> 2];
@@ -998,12 +1002,12 @@ __global__ void k_tl_check(int n_refs, const PairDesc* __restrict__ rd, const ui
 
 hipError_t launch_treelets(hipStream_t s, int n_refs, uint32_t cap, const PairDesc* rd, const uint4* nodes,
                            int bucket, uint32_t* flag, uint32_t* rank, void* temp, size_t temp_bytes, uint4* tl,
-                           uint32_t* ptl, TreeCtl* ctl) {
+                           uint2* link, TreeCtl* ctl) {
   if (n_refs <= 0 || cap == 0) return hipSuccess;
   k_tl_flag<<<grid_of((size_t)cap + 1), 256, 0, s>>>(n_refs, cap + 1, rd, nodes, flag);
   const hipError_t e = scan_u32(s, temp, temp_bytes, flag, rank, (size_t)cap + 1);
   if (e != hipSuccess) return e;
-  k_tl_build<<<grid_of(cap), 256, 0, s>>>(n_refs, cap, rd, nodes, rank, tl, ptl);
+  k_tl_build<<<grid_of(cap), 256, 0, s>>>(n_refs, cap, rd, nodes, rank, tl, link);
   k_tl_check<<<(n_refs + 63) / 64, 64, 0, s>>>(n_refs, rd, rank, bucket, ctl);
   return hipGetLastError();
 }
