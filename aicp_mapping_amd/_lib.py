@@ -31,7 +31,8 @@ EXPORTS = [
     "aicp_hip_batch_upload", "aicp_hip_batch_run", "aicp_hip_batch_free",
     "aicp_hip_last_nn_timing", "aicp_hip_last_phase_ms", "aicp_hip_knn", "aicp_hip_normals",
     "aicp_hip_dists_quantile", "aicp_hip_solve6", "aicp_hip_default_prefilter", "aicp_hip_prefilter",
-    "aicp_hip_last_prefilter_stats",
+    "aicp_hip_last_prefilter_stats", "aicp_hip_map_create", "aicp_hip_map_free", "aicp_hip_map_size",
+    "aicp_hip_map_download", "aicp_hip_map_crop", "aicp_hip_map_merge", "aicp_hip_map_prefilter",
 ]
 
 
@@ -166,6 +167,15 @@ def _load():
     L.aicp_hip_prefilter.argtypes = [vp, C.POINTER(PrefilterParams), fp, sz, sz, fp, C.POINTER(C.c_size_t), fp, ip,
                                      C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
     L.aicp_hip_last_prefilter_stats.argtypes = [vp, C.POINTER(PrefilterStats)]
+    szp = C.POINTER(C.c_size_t)
+    L.aicp_hip_map_create.argtypes = [vp, fp, sz, sz, C.POINTER(vp)]
+    L.aicp_hip_map_free.argtypes = [vp, vp]
+    L.aicp_hip_map_free.restype = None
+    L.aicp_hip_map_size.argtypes = [vp, szp]
+    L.aicp_hip_map_download.argtypes = [vp, vp, fp, sz, szp]
+    L.aicp_hip_map_crop.argtypes = [vp, vp, C.c_float, C.c_float, fp, fp, sz, szp]
+    L.aicp_hip_map_merge.argtypes = [vp, vp, fp, sz, sz, fp]
+    L.aicp_hip_map_prefilter.argtypes = [vp, vp, C.POINTER(PrefilterParams)]
     return L
 
 

@@ -123,6 +123,11 @@ struct aicp_hip_batch {
   BlockMap m_read{}, m_gref{}, m_red{}, m_sel{};
 };
 
+struct aicp_hip_map {  // a device-resident point cloud (float4, w = 1)
+  DevBuf pts;
+  size_t n = 0;
+};
+
 struct aicp_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -930,9 +935,10 @@ int aicp_hip_create(int device, aicp_hip_ctx** out) {
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
   if (!stream_prio_enabled()) prio_lo = prio_hi = 0;
+  const int prio3 = prio_hi;  // (measured: stream 3 at the low priority is no faster)
   if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio3) != hipSuccess) {
     for (hipStream_t q : {c->stream, c->stream2, c->stream3})
       if (q) (void)hipStreamDestroy(q);
     delete c;
@@ -1102,6 +1108,33 @@ static void crop_box_frame(const float origin[16], float inv[9], float t[3], flo
     for (int q = 0; q < 9; ++q) inv[q] = w[q];
 }
 
+// the crop kernels on n device points; kept points (input order) to host out, capacity cap
+static int crop_device(aicp_hip_ctx* ctx, const float4* din, size_t n, const float inv[9], const float t[3], float mn,
+                       float mx, float* out, size_t cap, size_t* out_n) {
+  const size_t tiles = aicp::crop_tiles(n);
+  const size_t tile_bytes = (2 * tiles * 4 + 255) & ~size_t(255);
+  HIPC(ensure(ctx->scratch, 256 + tile_bytes + n * 16));
+  HIPC(ensure(ctx->pin_io, n * 16 + 16));
+  char* d = ctx->scratch.as<char>();
+  uint32_t* total = (uint32_t*)d;
+  uint32_t* tcnt = (uint32_t*)(d + 256);
+  uint32_t* toff = tcnt + tiles;
+  float4* dout = (float4*)(d + 256 + tile_bytes);
+  aicp::launch_crop_box(ctx->stream, (int)n, inv, t, mn, mx, din, tcnt, toff, total, dout);
+  HIPC(hipGetLastError());
+  uint32_t m = 0;
+  HIPC(hipMemcpyAsync(&m, total, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  if (m > n) FAIL(AICP_ERR_HIP, "crop: kept count exceeds the input");
+  if (m > cap) FAIL(AICP_ERR_INVALID, "crop: output capacity too small");
+  float* h = ctx->pin_io.as<float>();
+  if (m) HIPC(hipMemcpy(h, dout, (size_t)m * 16, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < m; ++i)
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
+  *out_n = m;
+  return AICP_OK;
+}
+
 int aicp_hip_crop_box(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, float mn, float mx,
                       const float origin[16], float* out, size_t* out_n, float* rpy_out) {
   if (!ctx || !pts || !origin || !out || !out_n || stride < 12) return AICP_ERR_INVALID;
@@ -1113,33 +1146,11 @@ int aicp_hip_crop_box(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stri
   *out_n = 0;
   if (n == 0) return AICP_OK;
   HIPC(hipSetDevice(ctx->device));
-  const size_t tiles = aicp::crop_tiles(n);
-  const size_t tile_bytes = (2 * tiles * 4 + 255) & ~size_t(255);
-  HIPC(ensure(ctx->scratch, 256 + tile_bytes + 2 * n * 16));
+  HIPC(ensure(ctx->ref1, n * 16));
   HIPC(ensure(ctx->pin_io, n * 16 + 16));
-  float* h = ctx->pin_io.as<float>();
-  pack_xyz4(pts, n, stride, h);
-  char* d = ctx->scratch.as<char>();
-  uint32_t* total = (uint32_t*)d;
-  uint32_t* tcnt = (uint32_t*)(d + 256);
-  uint32_t* toff = tcnt + tiles;
-  float4* din = (float4*)(d + 256 + tile_bytes);
-  float4* dout = din + n;
-  HIPC(hipMemcpyAsync(din, h, n * 16, hipMemcpyHostToDevice, ctx->stream));
-  aicp::launch_crop_box(ctx->stream, (int)n, inv, t, mn, mx, din, tcnt, toff, total, dout);
-  HIPC(hipGetLastError());
-  uint32_t m = 0;
-  HIPC(hipMemcpyAsync(&m, total, 4, hipMemcpyDeviceToHost, ctx->stream));
-  HIPC(hipStreamSynchronize(ctx->stream));
-  if (m > n) {
-    ctx->err = "crop: kept count exceeds the input";
-    return AICP_ERR_HIP;
-  }
-  if (m) HIPC(hipMemcpy(h, dout, (size_t)m * 16, hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < m; ++i)
-    for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
-  *out_n = m;
-  return AICP_OK;
+  pack_xyz4(pts, n, stride, ctx->pin_io.as<float>());
+  HIPC(hipMemcpyAsync(ctx->ref1.p, ctx->pin_io.p, n * 16, hipMemcpyHostToDevice, ctx->stream));
+  return crop_device(ctx, ctx->ref1.as<float4>(), n, inv, t, mn, mx, out, n, out_n);
 }
 
 int aicp_hip_last_nn_timing(const aicp_hip_ctx* ctx, int* n_launches, double* total_ms, double* bytes,
@@ -1298,55 +1309,67 @@ void aicp_hip_default_prefilter(aicp_prefilter_params* p) {
 }
 
 // VoxelGrid -> NormalEstimation -> RegionGrowing on the device (kernels_prefilter.hip). Host
-// syncs: after the voxel grid (sampled count sizes the tree), per round of four propagation
+// syncs: after the voxel grid (sampled count sizes the tree), per round of two propagation
 // launches (fixed-point test), and the final counts.
-int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, const float* pts, size_t n,
-                       size_t stride, float* out, size_t* out_n, float* sampled, int32_t* labels, size_t* n_sampled,
-                       size_t* n_clusters) {
-  if (!ctx || !prm || !out || !out_n || (n && !pts) || stride < 12 || (stride % 4)) return AICP_ERR_INVALID;
-  if (n >= (1ull << 31)) return AICP_ERR_INVALID;
+struct PfRun {  // device results of pf_core
+  uint32_t V = 0, n_out = 0, n_clusters = 0;
+  const float4* out4 = nullptr;      // kept points, clusters concatenated
+  const float4* nrm = nullptr;       // normal + curvature, kd-tree bucket order
+  const uint32_t* inv = nullptr;     // sampled index -> bucket position
+  const int32_t* cluster_of = nullptr;
+};
+struct PfLayout {
+  PfCtl* ctl;
+  float4* pts4;  // the input, n points
+  PfWork W;
+};
+
+static int pf_check(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm) {
   if (!(prm->leaf_size > 0.f) || !std::isfinite(prm->leaf_size)) FAIL(AICP_ERR_INVALID, "leaf size must be > 0");
   const int K = prm->normal_k, NB = prm->neighbours;
   if (K != 10 && K != 20 && K != 30) FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   if (NB < 1 || NB > kPfMaxNbrs || NB > K) FAIL(AICP_ERR_UNSUPPORTED, "neighbours must be 1..min(16, normal_k)");
-  *out_n = 0;
-  if (n_sampled) *n_sampled = 0;
-  if (n_clusters) *n_clusters = 0;
-  ctx->last_pf = aicp_prefilter_stats{};
-  if (n == 0) return AICP_OK;
-  const auto t_wall = std::chrono::steady_clock::now();
-  HIPC(hipSetDevice(ctx->device));
-  hipStream_t s = ctx->stream;
-  for (auto& e : ctx->pf_ev)
-    if (!e) HIPC(hipEventCreate(&e));
-  hipEvent_t* E = ctx->pf_ev;  // 0 uploaded, 1 voxels, 2 kNN start, 3 kNN end, 4 normals, 5 clusters
-  // ---- scratch of the voxel grid and the extraction: ctl | pts4[n] | 9 x (n + 1) words | temp
+  return AICP_OK;
+}
+
+// scratch of the voxel grid and the extraction: ctl | pts4[n] | 9 x (n + 1) words | temp
+static int pf_layout(aicp_hip_ctx* ctx, size_t n, PfLayout* L) {
   const size_t wn = (n + 1 + 63) & ~size_t(63);
   const size_t temp_b = pf_temp_bytes(n + 1);
   const size_t off_pts = 256, off_w = off_pts + n * 16, off_temp = off_w + 9 * wn * 4;
   HIPC(ensure(ctx->pf_a, off_temp + temp_b));
   char* A = ctx->pf_a.as<char>();
-  PfCtl* dctl = (PfCtl*)A;
-  float4* pts4 = (float4*)(A + off_pts);
   uint32_t* wb = (uint32_t*)(A + off_w);
-  PfWork W{wb, wb + wn, wb + 2 * wn, wb + 3 * wn, wb + 4 * wn, wb + 5 * wn, wb + 6 * wn, wb + 7 * wn, wb + 8 * wn,
-           A + off_temp, temp_b};
+  L->ctl = (PfCtl*)A;
+  L->pts4 = (float4*)(A + off_pts);
+  L->W = PfWork{wb, wb + wn, wb + 2 * wn, wb + 3 * wn, wb + 4 * wn, wb + 5 * wn, wb + 6 * wn, wb + 7 * wn, wb + 8 * wn,
+                A + off_temp, temp_b};
+  return AICP_OK;
+}
+
+// the whole chain on n points already in the layout's pts4 (enqueued on ctx->stream)
+static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n, const PfLayout& Lo, PfRun* o) {
+  hipStream_t s = ctx->stream;
+  const int K = prm->normal_k, NB = prm->neighbours;
+  for (auto& e : ctx->pf_ev)
+    if (!e) HIPC(hipEventCreate(&e));
+  hipEvent_t* E = ctx->pf_ev;  // 0 input ready, 1 voxels, 2 kNN start, 3 kNN end, 4 normals, 5 clusters
+  PfCtl* dctl = Lo.ctl;
+  const PfWork& W = Lo.W;
   HIPC(ensure(ctx->ref1, n * 16));
-  HIPC(ensure(ctx->pin_io, n * 16 + 64));
-  pack_xyz4(pts, n, stride, ctx->pin_io.as<float>());
-  HIPC(hipMemcpyAsync(pts4, ctx->pin_io.p, n * 16, hipMemcpyHostToDevice, s));
   PfCtl hc{};
   for (int k = 0; k < 3; ++k) hc.lo[k] = 0xFFFFFFFFu;
   HIPC(hipMemcpyAsync(dctl, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
   HIPC(hipEventRecord(E[0], s));
-  HIPC(launch_pf_voxel(s, (uint32_t)n, pts4, 1.f / prm->leaf_size, dctl, W, ctx->ref1.as<float4>()));
+  HIPC(launch_pf_voxel(s, (uint32_t)n, Lo.pts4, 1.f / prm->leaf_size, dctl, W, ctx->ref1.as<float4>()));
   HIPC(hipEventRecord(E[1], s));
   HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   if (hc.passthrough && hc.n_bad)
     FAIL(AICP_ERR_UNSUPPORTED, "voxel grid overflows 32-bit indices and the cloud has non-finite points");
   const uint32_t V = hc.n_fin ? hc.n_vox : 0u;
-  if (n_sampled) *n_sampled = V;
+  *o = PfRun{};
+  o->V = V;
   if (V == 0) return AICP_OK;
   // ---- kd-tree of the sampled cloud and its exact kNN (libnabo order, eps 0, self included)
   PairDesc d{};
@@ -1372,7 +1395,7 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(E[3], s));
   // ---- per sampled point: inv, nrm (float4), nbp (16), ckey, cval, nob, order_of, em, label,
-  // cluster_of, out4 (float4)
+  // cluster_of, out4 (float4), comp, kth (uint2)
   const size_t vn = ((size_t)V + 63) & ~size_t(63);
   HIPC(ensure(ctx->pf_b, vn * 4 * (1 + 4 + kPfMaxNbrs + 8 + 4 + 2) + 256));
   uint32_t* B = ctx->pf_b.as<uint32_t>();
@@ -1437,32 +1460,188 @@ int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, cons
   ps.knn_points_touched = ht[0];
   ps.knn_nodes_touched = ht[1];
   if (hc.n_out > V || hc.n_clusters > V) FAIL(AICP_ERR_HIP, "pre-filter: inconsistent cluster counts");
-  float* h = ctx->pin_io.as<float>();
-  if (hc.n_out) HIPC(hipMemcpy(h, out4, (size_t)hc.n_out * 16, hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < hc.n_out; ++i)
-    for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
-  *out_n = hc.n_out;
-  if (n_clusters) *n_clusters = hc.n_clusters;
-  if (labels) HIPC(hipMemcpy(labels, cluster_of, (size_t)V * 4, hipMemcpyDeviceToHost));
-  if (sampled) {
-    std::vector<float> P(4 * (size_t)V), N(4 * (size_t)V);
-    std::vector<uint32_t> I(V);
-    HIPC(hipMemcpy(P.data(), ctx->ref1.p, (size_t)V * 16, hipMemcpyDeviceToHost));
-    HIPC(hipMemcpy(N.data(), nrm, (size_t)V * 16, hipMemcpyDeviceToHost));
-    HIPC(hipMemcpy(I.data(), inv, (size_t)V * 4, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < V; ++i) {
-      float* o = sampled + 8 * i;
-      const float* nb = &N[4 * (size_t)I[i]];
-      o[0] = P[4 * i];
-      o[1] = P[4 * i + 1];
-      o[2] = P[4 * i + 2];
-      o[3] = nb[3];
-      o[4] = nb[0];
-      o[5] = nb[1];
-      o[6] = nb[2];
-      o[7] = 0.f;
+  o->n_out = hc.n_out;
+  o->n_clusters = hc.n_clusters;
+  o->out4 = out4;
+  o->nrm = nrm;
+  o->inv = inv;
+  o->cluster_of = cluster_of;
+  return AICP_OK;
+}
+
+int aicp_hip_prefilter(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, const float* pts, size_t n,
+                       size_t stride, float* out, size_t* out_n, float* sampled, int32_t* labels, size_t* n_sampled,
+                       size_t* n_clusters) {
+  if (!ctx || !prm || !out || !out_n || (n && !pts) || stride < 12 || (stride % 4)) return AICP_ERR_INVALID;
+  if (n >= (1ull << 31)) return AICP_ERR_INVALID;
+  int rc = pf_check(ctx, prm);
+  if (rc) return rc;
+  *out_n = 0;
+  if (n_sampled) *n_sampled = 0;
+  if (n_clusters) *n_clusters = 0;
+  ctx->last_pf = aicp_prefilter_stats{};
+  if (n == 0) return AICP_OK;
+  const auto t_wall = std::chrono::steady_clock::now();
+  HIPC(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  PfLayout Lo;
+  rc = pf_layout(ctx, n, &Lo);
+  if (rc) return rc;
+  HIPC(ensure(ctx->pin_io, n * 16 + 64));
+  pack_xyz4(pts, n, stride, ctx->pin_io.as<float>());
+  HIPC(hipMemcpyAsync(Lo.pts4, ctx->pin_io.p, n * 16, hipMemcpyHostToDevice, s));
+  PfRun o;
+  rc = pf_core(ctx, prm, n, Lo, &o);
+  if (rc) return rc;
+  const uint32_t V = o.V;
+  if (n_sampled) *n_sampled = V;
+  if (V) {
+    float* h = ctx->pin_io.as<float>();
+    if (o.n_out) HIPC(hipMemcpy(h, o.out4, (size_t)o.n_out * 16, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < o.n_out; ++i)
+      for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
+    *out_n = o.n_out;
+    if (n_clusters) *n_clusters = o.n_clusters;
+    if (labels) HIPC(hipMemcpy(labels, o.cluster_of, (size_t)V * 4, hipMemcpyDeviceToHost));
+    if (sampled) {
+      std::vector<float> P(4 * (size_t)V), N(4 * (size_t)V);
+      std::vector<uint32_t> I(V);
+      HIPC(hipMemcpy(P.data(), ctx->ref1.p, (size_t)V * 16, hipMemcpyDeviceToHost));
+      HIPC(hipMemcpy(N.data(), o.nrm, (size_t)V * 16, hipMemcpyDeviceToHost));
+      HIPC(hipMemcpy(I.data(), o.inv, (size_t)V * 4, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < V; ++i) {
+        float* q = sampled + 8 * i;
+        const float* nb = &N[4 * (size_t)I[i]];
+        q[0] = P[4 * i];
+        q[1] = P[4 * i + 1];
+        q[2] = P[4 * i + 2];
+        q[3] = nb[3];
+        q[4] = nb[0];
+        q[5] = nb[1];
+        q[6] = nb[2];
+        q[7] = 0.f;
+      }
     }
   }
+  ctx->last_pf.wall_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wall).count();
+  return AICP_OK;
+}
+
+// ---- device-resident prior map (localization mode, app.cpp:41-51, 469-493) ------------------
+int aicp_hip_map_create(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, aicp_hip_map** out) {
+  if (!ctx || !out || (n && !pts) || stride < 12 || (stride % 4) || n > (size_t)INT32_MAX) return AICP_ERR_INVALID;
+  *out = nullptr;
+  HIPC(hipSetDevice(ctx->device));
+  aicp_hip_map* m = new aicp_hip_map();
+  if (n) {
+    const hipError_t e = ensure(m->pts, n * 16);
+    if (e != hipSuccess) {
+      delete m;
+      ctx->err = std::string("map allocation: ") + hipGetErrorString(e);
+      return AICP_ERR_HIP;
+    }
+    HIPC(ensure(ctx->pin_io, n * 16 + 16));
+    pack_xyz4(pts, n, stride, ctx->pin_io.as<float>());
+    HIPC(hipMemcpyAsync(m->pts.p, ctx->pin_io.p, n * 16, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+  }
+  m->n = n;
+  *out = m;
+  return AICP_OK;
+}
+
+void aicp_hip_map_free(aicp_hip_ctx* ctx, aicp_hip_map* map) {
+  if (!map) return;
+  if (ctx) (void)hipStreamSynchronize(ctx->stream);
+  release(map->pts);
+  delete map;
+}
+
+int aicp_hip_map_size(const aicp_hip_map* map, size_t* n) {
+  if (!map || !n) return AICP_ERR_INVALID;
+  *n = map->n;
+  return AICP_OK;
+}
+
+int aicp_hip_map_download(aicp_hip_ctx* ctx, const aicp_hip_map* map, float* out, size_t cap, size_t* out_n) {
+  if (!ctx || !map || !out_n || (map->n && !out)) return AICP_ERR_INVALID;
+  if (cap < map->n) FAIL(AICP_ERR_INVALID, "map download: output capacity too small");
+  HIPC(hipSetDevice(ctx->device));
+  *out_n = map->n;
+  if (!map->n) return AICP_OK;
+  HIPC(ensure(ctx->pin_io, map->n * 16));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  HIPC(hipMemcpy(ctx->pin_io.p, map->pts.p, map->n * 16, hipMemcpyDeviceToHost));
+  const float* h = ctx->pin_io.as<float>();
+  for (size_t i = 0; i < map->n; ++i)
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
+  return AICP_OK;
+}
+
+int aicp_hip_map_crop(aicp_hip_ctx* ctx, const aicp_hip_map* map, float mn, float mx, const float origin[16],
+                      float* out, size_t cap, size_t* out_n) {
+  if (!ctx || !map || !origin || !out_n || (cap && !out)) return AICP_ERR_INVALID;
+  float inv[9], t[3], rpy[3];
+  crop_box_frame(origin, inv, t, rpy);
+  *out_n = 0;
+  if (!map->n) return AICP_OK;
+  HIPC(hipSetDevice(ctx->device));
+  return crop_device(ctx, map->pts.as<float4>(), map->n, inv, t, mn, mx, out, cap, out_n);
+}
+
+int aicp_hip_map_merge(aicp_hip_ctx* ctx, aicp_hip_map* map, const float* pts, size_t n, size_t stride,
+                       const float T[16]) {
+  if (!ctx || !map || !T || (n && !pts) || stride < 12 || (stride % 4)) return AICP_ERR_INVALID;
+  if (map->n + n > (size_t)INT32_MAX) FAIL(AICP_ERR_INVALID, "map merge: more than 2^31 points");
+  if (!n) return AICP_OK;
+  HIPC(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const size_t need = (map->n + n) * 16;
+  if (need > map->pts.cap) {  // grow with copy (ensure() would drop the content)
+    DevBuf nb;
+    HIPC(ensure(nb, std::max(need, 2 * map->pts.cap)));
+    if (map->n) HIPC(hipMemcpyAsync(nb.p, map->pts.p, map->n * 16, hipMemcpyDeviceToDevice, s));
+    HIPC(hipStreamSynchronize(s));
+    release(map->pts);
+    map->pts = nb;
+  }
+  HIPC(ensure(ctx->scratch, 64 + n * 16));
+  HIPC(ensure(ctx->pin_io, n * 16 + 64));
+  float* h = ctx->pin_io.as<float>();
+  std::memcpy(h, T, 64);
+  pack_xyz4(pts, n, stride, h + 16);
+  char* d = ctx->scratch.as<char>();
+  HIPC(hipMemcpyAsync(d, h, 64 + n * 16, hipMemcpyHostToDevice, s));
+  // transformPointCloud (pcl 1.8, common/impl/transforms.hpp): x' = r00 x + r01 y + r02 z + t0
+  // in float, in that order (launch_transform: the same expression, no FMA)
+  launch_transform(s, (int)n, (const float*)d, (const float4*)(d + 64), map->pts.as<float4>() + map->n);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(s));
+  map->n += n;
+  return AICP_OK;
+}
+
+int aicp_hip_map_prefilter(aicp_hip_ctx* ctx, aicp_hip_map* map, const aicp_prefilter_params* prm) {
+  if (!ctx || !map || !prm) return AICP_ERR_INVALID;
+  int rc = pf_check(ctx, prm);
+  if (rc) return rc;
+  ctx->last_pf = aicp_prefilter_stats{};
+  if (!map->n) return AICP_OK;
+  const auto t_wall = std::chrono::steady_clock::now();
+  HIPC(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  PfLayout Lo;
+  rc = pf_layout(ctx, map->n, &Lo);
+  if (rc) return rc;
+  HIPC(hipMemcpyAsync(Lo.pts4, map->pts.p, map->n * 16, hipMemcpyDeviceToDevice, s));
+  PfRun o;
+  rc = pf_core(ctx, prm, map->n, Lo, &o);
+  if (rc) return rc;
+  // the map becomes the kept points (prior_map_->updateCloud(map_prefiltered), app.cpp:490-492)
+  if (o.V && o.n_out) HIPC(hipMemcpyAsync(map->pts.p, o.out4, (size_t)o.n_out * 16, hipMemcpyDeviceToDevice, s));
+  HIPC(hipStreamSynchronize(s));
+  map->n = o.V ? o.n_out : 0;
   ctx->last_pf.wall_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wall).count();
   return AICP_OK;

@@ -183,6 +183,28 @@ typedef struct {
 } aicp_prefilter_stats;
 int aicp_hip_last_prefilter_stats(const aicp_hip_ctx* ctx, aicp_prefilter_stats* out);
 
+/* ---- device-resident prior map (localization mode) ------------------------------------------
+ * App keeps prior_map_ and, per reading, crops it around the prior pose (setReference,
+ * app.cpp:41-51), appends the aligned reference reading every reference_update_frequency clouds
+ * (merge_aligned_clouds_to_map, app.cpp:469-483: *merged = *prior_map + *output, output =
+ * transformPointCloud(read_prefiltered, correction)) and pre-filters the whole map every 30
+ * clouds (app.cpp:485-493). The map stays in HBM: crop, merge and pre-filter run on it without
+ * re-uploading it. */
+typedef struct aicp_hip_map aicp_hip_map;
+int aicp_hip_map_create(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, aicp_hip_map** out);
+void aicp_hip_map_free(aicp_hip_ctx* ctx, aicp_hip_map* map);
+int aicp_hip_map_size(const aicp_hip_map* map, size_t* n);
+/* the map's points, packed xyz (capacity cap points) */
+int aicp_hip_map_download(aicp_hip_ctx* ctx, const aicp_hip_map* map, float* out, size_t cap, size_t* out_n);
+/* getPointsInOrientedBox on the map (aicp_hip_crop_box semantics), kept points to out */
+int aicp_hip_map_crop(aicp_hip_ctx* ctx, const aicp_hip_map* map, float min, float max, const float origin[16],
+                      float* out /* 3*cap */, size_t cap, size_t* out_n);
+/* map += T * pts (pcl::transformPointCloud, T column-major float[16]) */
+int aicp_hip_map_merge(aicp_hip_ctx* ctx, aicp_hip_map* map, const float* pts, size_t n, size_t stride,
+                       const float T[16]);
+/* map = regionGrowingUniformPlaneSegmentationFilter(map) (aicp_hip_prefilter on device data) */
+int aicp_hip_map_prefilter(aicp_hip_ctx* ctx, aicp_hip_map* map, const aicp_prefilter_params* prm);
+
 /* ---- device-resident batches (inputs uploaded once, run many times) ----------------------- */
 int aicp_hip_batch_upload(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs,
                           aicp_hip_batch** out);
