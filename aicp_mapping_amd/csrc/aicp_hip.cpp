@@ -137,7 +137,7 @@ struct aicp_hip_ctx {
   DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
       ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
       nrm_raw, inv, gdesc, gstate, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, tl, ptl, tl_flag,
-      tl_rank, tl_temp, pf_a, pf_b;
+      tl_rank, tl_temp, pf_a, pf_b, tl_raw, link_raw, tlr_flag, tlr_rank, tlr_temp;
   uint64_t tl_total = 0;  // matcher treelet records allotted for this batch (0: no treelets, Trav<1>)
   TreeBufs tb[2];  // [0] raw-coordinate tree (stream2), [1] centred matcher tree (stream3)
   PinBuf pin_desc, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
@@ -690,6 +690,26 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), cfg->bucket_size,
                           ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0], true));
     if (rc) return join_worker(rc);
+    // the raw tree as treelet records too (the kNN's engine, TravT); errors into its control
+    // block (bit 4), copied again and checked after the batch
+    const uint4* tl_raw = nullptr;
+    const uint2* link_raw = nullptr;
+    if (ctx->tl_total && knn_treelets_enabled()) {
+      const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);
+      const size_t tbb = tree_scan_temp_bytes((size_t)cap + 1);
+      HIPC(ensure(ctx->tl_raw, ctx->tl_total * 16));
+      HIPC(ensure(ctx->link_raw, ctx->tl_total * 8));
+      HIPC(ensure(ctx->tlr_flag, ((size_t)cap + 1) * 4));
+      HIPC(ensure(ctx->tlr_rank, ((size_t)cap + 1) * 4));
+      HIPC(ensure(ctx->tlr_temp, tbb));
+      TreeBufs& T0 = ctx->tb[0];
+      HIPC(launch_treelets(s2, (int)R, cap, ctx->rdesc_raw.as<PairDesc>(), ctx->nodes_raw.as<uint4>(), cfg->bucket_size,
+                           ctx->tlr_flag.as<uint32_t>(), ctx->tlr_rank.as<uint32_t>(), ctx->tlr_temp.p, tbb,
+                           ctx->tl_raw.as<uint4>(), ctx->link_raw.as<uint2>(), T0.tw.ctl));
+      HIPC(hipMemcpyAsync(T0.pin_ctl.p, T0.tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
+      tl_raw = ctx->tl_raw.as<uint4>();
+      link_raw = ctx->link_raw.as<uint2>();
+    }
     // normals on the raw tree (bucket order of that tree)
     HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
@@ -697,7 +717,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
     if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, ctx->rdesc_raw.as<PairDesc>(), dRstate,
                         ctx->nodes_raw.as<uint4>(), nullptr, ctx->bpts_raw.as<float4>(), ctx->nrm_raw.as<float4>(),
-                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
+                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr, tl_raw, link_raw))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
     HIPC(hipEventRecord(ctx->ev[10], s2));
   }
@@ -833,6 +853,8 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     if (rc) return rc;
     if (ctx->tl_total && (ctx->tb[1].pin_ctl.as<TreeCtl>()->error & 4))
       FAIL(AICP_ERR_HIP, "matcher treelets exceed their allotment");
+    if (ctx->tl_total && knn_treelets_enabled() && (ctx->tb[0].pin_ctl.as<TreeCtl>()->error & 4))
+      FAIL(AICP_ERR_HIP, "normal-tree treelets exceed their allotment");
   }
   // results
   const PairState* hs = ctx->pin_state.as<PairState>();
@@ -957,7 +979,8 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
                     &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->gdesc, &ctx->gstate, &ctx->tl, &ctx->ptl,
-                    &ctx->tl_flag, &ctx->tl_rank, &ctx->tl_temp, &ctx->pf_a, &ctx->pf_b})
+                    &ctx->tl_flag, &ctx->tl_rank, &ctx->tl_temp, &ctx->pf_a, &ctx->pf_b, &ctx->tl_raw,
+                    &ctx->link_raw, &ctx->tlr_flag, &ctx->tlr_rank, &ctx->tlr_temp})
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
@@ -1375,6 +1398,8 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   PairDesc d{};
   d.n_ref = V;
   d.ratio = 0.5f;
+  d.tl_off = 0;
+  d.tl_cap = 4 * V + 4;  // treelet records allotted (the kNN engine's tree format)
   ident4(d.Tin);
   HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
@@ -1383,6 +1408,19 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   if (rc) return rc;
   rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes, 0);
   if (rc) return rc;
+  const bool use_tl = knn_treelets_enabled();
+  if (use_tl) {
+    const uint32_t cap = 2 * V + 2;
+    const size_t tbb = tree_scan_temp_bytes((size_t)cap + 1);
+    HIPC(ensure(ctx->tl_raw, ((size_t)V * 4 + 4) * 16));
+    HIPC(ensure(ctx->link_raw, ((size_t)V * 4 + 4) * 8));
+    HIPC(ensure(ctx->tlr_flag, ((size_t)cap + 1) * 4));
+    HIPC(ensure(ctx->tlr_rank, ((size_t)cap + 1) * 4));
+    HIPC(ensure(ctx->tlr_temp, tbb));
+    HIPC(launch_treelets(s, 1, cap, ctx->desc.as<PairDesc>(), ctx->nodes.as<uint4>(), 8, ctx->tlr_flag.as<uint32_t>(),
+                         ctx->tlr_rank.as<uint32_t>(), ctx->tlr_temp.p, tbb, ctx->tl_raw.as<uint4>(),
+                         ctx->link_raw.as<uint2>(), ctx->tb[0].tw.ctl));
+  }
   HIPC(ensure(ctx->match, (size_t)V * K * 4));
   HIPC(ensure(ctx->ctrs, kCtrWords * 4 + 16));
   HIPC(hipMemsetAsync(ctx->ctrs.p, 0, kCtrWords * 4 + 16, s));
@@ -1390,7 +1428,8 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   unsigned long long* dtouch = (unsigned long long*)(ctx->ctrs.as<uint32_t>() + kCtrWords);
   HIPC(hipEventRecord(E[2], s));
   if (!launch_knn_ids(s, 1, V, ctx->desc.as<PairDesc>(), ctx->nodes.as<uint4>(), bpts, K, ctx->match.as<int32_t>(),
-                      ctx->ctrs.as<uint32_t>(), dtouch))
+                      ctx->ctrs.as<uint32_t>(), dtouch, use_tl ? ctx->tl_raw.as<uint4>() : nullptr,
+                      use_tl ? ctx->link_raw.as<uint2>() : nullptr))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(E[3], s));
@@ -1449,7 +1488,10 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
   unsigned long long ht[2] = {0, 0};
   HIPC(hipMemcpyAsync(ht, dtouch, 16, hipMemcpyDeviceToHost, s));
+  uint32_t tl_err = 0;
+  HIPC(hipMemcpyAsync(&tl_err, &ctx->tb[0].tw.ctl->error, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  if (tl_err & 4) FAIL(AICP_ERR_HIP, "pre-filter treelets exceed their allotment");
   aicp_prefilter_stats& ps = ctx->last_pf;
   ps.voxel_ms = ev_ms(E[0], E[1]);
   ps.normals_ms = ev_ms(E[1], E[4]);

@@ -28,14 +28,18 @@ void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const floa
 void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st);
 // SurfaceNormal of the reference points (bucket order); ids: scratch of total_ref * knn;
 // ctr: zeroed work counter. Returns false if knn is unsupported.
+// tl / link (nullable): the same trees as treelet records (launch_treelets, pd[].tl_off) for the
+// treelet kNN engine, used when knn_treelets_enabled() (AICP_KNN_TREELETS=1, A/B only)
+bool knn_treelets_enabled();
 bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
-                    int32_t* ids, uint32_t* ctr);
+                    int32_t* ids, uint32_t* ctr, const uint4* tl = nullptr, const uint2* link = nullptr);
 // the kNN of every reference point in its own tree (bucket order in and out: ids are bucket
 // positions of the pair's tree, -1 past the cloud size); eps 0, self included. touched
 // (nullable, zeroed): += touched points, inner nodes
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
-                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched);
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
+                    const uint4* tl = nullptr, const uint2* link = nullptr);
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
                         ActiveList* al, uint32_t* ctr);
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st,

@@ -658,6 +658,174 @@ struct Trav2C {
 #endif
 };
 
+// k-NN over the same treelet records (the SurfaceNormal and pre-filter kNN, eps 0): Trav2C's
+// descent (one record per two levels) and one-treelet climb with libnabo's k-best list
+// (IndexHeapBruteForceVector: the head is v[K-1]) instead of the 1-NN best. Visit order, far
+// tests and results are Trav<K>'s over the node records.
+template <int K>
+struct TravT {
+  const uint4* tl;
+  const uint2* ptl;
+  const float4* pts;
+  float q0, q1, q2;
+  float noc0, noc1, noc2, rd, minFar;
+  int32_t n, start, sp, pl;
+  uint32_t lb0, lcnt;
+  uint32_t tp, tn;
+  Best<K> best;
+  NnLdsFrame* lf = nullptr;
+  int32_t nlf = 0;
+
+  __device__ __forceinline__ void reset(float a, float b, float c) {
+    q0 = a;
+    q1 = b;
+    q2 = c;
+    noc0 = noc1 = noc2 = rd = 0.f;
+    n = start = sp = 0;
+    pl = -1;
+    tp = tn = 0;
+    best_init<K>(best);
+  }
+  __device__ __forceinline__ bool decide(uint32_t w, uint32_t cd) {
+    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
+    minFar = min_bound(minFar, rd + (sel3(cd, noc0, noc1, noc2) + no * no));
+    ++tn;
+    return no > 0.f;
+  }
+  __device__ __forceinline__ void descend() {
+    minFar = __builtin_inff();
+    uint32_t T = (uint32_t)n >> 2, s = (uint32_t)n & 3u;
+    uint4 r = ld_rec(tl + T);
+    uint32_t w = r.x, cd = r.w & 3u;
+    if (s == 0 && cd != kLeaf) {
+      s = decide(w, cd) ? 2u : 1u;
+      pl = n;
+      n = (int32_t)(T << 2 | s);
+    }
+    while (s != 0) {
+      w = s == 1 ? r.y : r.z;
+      cd = (r.w >> (2 * s)) & 3u;
+      if (cd == kLeaf) break;
+      const bool right = decide(w, cd);
+      pl = n;
+      T = (r.w >> 6) + 2 * (s - 1) + (right ? 1u : 0u);
+      n = (int32_t)(T << 2);
+      r = ld_rec(tl + T);
+      w = r.x;
+      cd = r.w & 3u;
+      if (cd == kLeaf) break;
+      s = decide(w, cd) ? 2u : 1u;
+      pl = n;
+      n = (int32_t)(T << 2 | s);
+    }
+    lb0 = w & 0x0FFFFFFFu;
+    lcnt = w >> 28;
+  }
+  __device__ __forceinline__ void bucket(float maxR2) {
+    float3 P[kLeafBatch];
+#pragma unroll
+    for (int i = 0; i < kLeafBatch; ++i)
+      if ((uint32_t)i < lcnt) {
+        const float4 p = pts[lb0 + i];
+        P[i] = make_float3(p.x, p.y, p.z);
+      }
+#pragma unroll
+    for (int i = 0; i < kLeafBatch; ++i)
+      if ((uint32_t)i < lcnt) {
+        const float d0 = q0 - P[i].x, d1 = q1 - P[i].y, d2 = q2 - P[i].z;
+        float dist = 0.f;
+        dist += d0 * d0;
+        dist += d1 * d1;
+        dist += d2 * d2;
+        if (dist <= maxR2 && dist < best.v[K - 1]) best_replace<K>(best, (int32_t)(lb0 + i), dist);
+      }
+    for (uint32_t i = kLeafBatch; i < lcnt; ++i) {
+      const float4 p = pts[lb0 + i];
+      const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
+      float dist = 0.f;
+      dist += d0 * d0;
+      dist += d1 * d1;
+      dist += d2 * d2;
+      if (dist <= maxR2 && dist < best.v[K - 1]) best_replace<K>(best, (int32_t)(lb0 + i), dist);
+    }
+    tp += lcnt;
+  }
+  __device__ __forceinline__ bool far_push(FarStack& fs, const uint4& r, int32_t p, uint32_t s, int32_t pp,
+                                           float maxE2, float maxR2) {
+    const uint32_t T = (uint32_t)p >> 2;
+    const uint32_t w = s == 0 ? r.x : (s == 1 ? r.y : r.z), cd = (r.w >> (2 * s)) & 3u;
+    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
+    const float oc = sel3(cd, noc0, noc1, noc2);
+    const float rdf = rd + (oc + no * no);
+    if (!(rdf <= maxR2 && rdf * maxE2 < best.v[K - 1])) return false;
+    const uint32_t fr = no > 0.f ? 0u : 1u;
+    const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
+    if (sp < nlf)
+      lf[sp * kNNBlock] = NnLdsFrame{(int32_t)(((uint32_t)pp & 0x3fffffffu) | (cd << 30)), rd, oc, start,
+                                     __int_as_float(max(__float_as_int(minFar), 0) | (p == start ? (int32_t)0x80000000 : 0))};
+    else
+      fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, 0};
+    ++sp;
+    const float nn = -no * no;
+    if (cd == 0) noc0 = nn;
+    else if (cd == 1) noc1 = nn;
+    else noc2 = nn;
+    rd = rdf;
+    n = far;
+    start = far;
+    pl = p;
+    return true;
+  }
+  __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
+    int32_t c = n, pc = pl;
+    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
+    for (;;) {
+      if (c == start) {
+        if (sp == 0) return true;
+        --sp;
+        FarFrame f;
+        if (sp < nlf) {
+          const NnLdsFrame g = lf[sp * kNNBlock];
+          const int32_t mi = __float_as_int(g.mnf);
+          f = FarFrame{g.PPcd, g.rd, g.old, __int_as_float(mi & 0x7fffffff), g.start, mi < 0 ? g.start : -2,
+                       g.PPcd & 0x3fffffff, 0};
+        } else {
+          f = fs.f[sp];
+        }
+        const uint32_t pcd = (uint32_t)f.F >> 30;
+        rd = f.rd;
+        if (pcd == 0) noc0 = f.old;
+        else if (pcd == 1) noc1 = f.old;
+        else noc2 = f.old;
+        minFar = f.mn;
+        start = f.start;
+        c = f.P;
+        pc = f.PP;
+        if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
+        continue;
+      }
+      const int32_t p = pc;
+      const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
+      const uint4 r = ld_rec(tl + T);
+      const int32_t rootpp = (int32_t)ptl[T].x;
+      const int32_t root = (int32_t)(T << 2);
+      if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2)) return false;
+      c = p;
+      pc = s != 0 ? root : rootpp;
+      if (s == 0 || c == start) continue;
+      if (far_push(fs, r, root, 0, rootpp, maxE2, maxR2)) return false;
+      c = root;
+      pc = rootpp;
+    }
+  }
+  // one round: a descent, its bucket and the climb to the next far descent; true when done
+  __device__ __forceinline__ bool advance(FarStack& fs, float maxE2, float maxR2, const uint4*, const float4*) {
+    descend();
+    bucket(maxR2);
+    return climb(fs, maxE2, maxR2);
+  }
+};
+
 // Trav2C's traversal as a per-lane state machine ("if-if"): every iteration of the persistent
 // loop each lane takes one step of its own phase -- a descent step (one treelet record, up to two
 // levels) or a climb step (one record: the node and, for a child slot, its treelet root) -- with
@@ -1334,7 +1502,15 @@ __device__ __forceinline__ int pair_of_ref(const PairDesc* __restrict__ pd, int 
 }
 
 template <int K>
-__global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
+#ifndef AICP_KNN_WAVES
+#define AICP_KNN_WAVES 0  // k_knn_ids: waves per SIMD to compile for (0: the compiler's choice)
+#endif
+#if AICP_KNN_WAVES > 0
+#define AICP_KNN_ATTR __attribute__((amdgpu_waves_per_eu(AICP_KNN_WAVES)))
+#else
+#define AICP_KNN_ATTR
+#endif
+__global__ __launch_bounds__(256) AICP_KNN_ATTR void k_knn_ids(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
                                                  const uint4* __restrict__ nodes,
                                                  const int32_t* __restrict__ parent,
                                                  const float4* __restrict__ bpts,
@@ -1370,6 +1546,59 @@ __global__ __launch_bounds__(256) void k_knn_ids(int n_pairs, uint32_t total, co
         tn += t.tn;
       });
   if (touched) {  // touched points / inner nodes (the algorithmic bytes of the roofline), optional
+    unsigned long long a = tp, b = tn;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o, 64);
+      b += __shfl_xor(b, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&touched[0], a);
+      atomicAdd(&touched[1], b);
+    }
+  }
+}
+
+// k_knn_ids over the treelet records (TravT<K>); pd[].tl_off locates each reference's records
+// occupancy of the node-record engine at each K (its register count sits just under the
+// 4 / 3 waves-per-SIMD steps; the treelet engine's few extra registers would cost a wave)
+template <int K>
+__global__ __launch_bounds__(256, (K <= 10 ? 5 : (K <= 20 ? 4 : 3))) void k_knn_ids_tl(int n_pairs, uint32_t total,
+                                                                 const PairDesc* __restrict__ pd,
+                                                                 const uint4* __restrict__ tl,
+                                                                 const uint2* __restrict__ link,
+                                                                 const float4* __restrict__ bpts,
+                                                                 int32_t* __restrict__ ids, uint32_t* ctr,
+                                                                 unsigned long long* touched) {
+  __shared__ NnLdsFrame knn_frames[(kKnnLdsFrames > 0 ? kKnnLdsFrames : 1) * kNNBlock];
+  uint32_t tp = 0, tn = 0;
+  int cur = -1;
+  uint32_t cur_end = 0, cur_off = 0;
+  persistent_xcd<TravT<K>>(
+      total, ctr, 1.f, __builtin_inff(), nullptr, bpts, [](uint32_t) {},
+      [&](uint32_t s, TravT<K>& t) {
+        if (cur < 0 || s < cur_off || s >= cur_end) {
+          cur = pair_of_ref(pd, n_pairs, s);
+          cur_off = pd[cur].ref_off;
+          cur_end = cur_off + pd[cur].n_ref;
+        }
+        const PairDesc& d = pd[cur];
+        t.tl = tl + d.tl_off;
+        t.ptl = link + d.tl_off;
+        t.pts = bpts + d.ref_off;
+        const float4 q = bpts[s];
+        t.reset(q.x, q.y, q.z);
+        t.lf = knn_frames + threadIdx.x;
+        t.nlf = kKnnLdsFrames;
+        return true;
+      },
+      [&](uint32_t s, TravT<K>& t) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) ids[(size_t)s * K + i] = (t.best.v[i] != __builtin_inff()) ? t.best.id[i] : -1;
+        tp += t.tp;
+        tn += t.tn;
+      });
+  if (touched) {
     unsigned long long a = tp, b = tn;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -2030,33 +2259,45 @@ void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const floa
 void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st) {
   k_init_state<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st);
 }
+// kNN over treelet records (TravT) only with AICP_KNN_TREELETS=1: measured no faster than the
+// node-record engine at equal occupancy (C2 normals and the pre-filter's k = 30 within 1 %), as
+// the k-best insertions, not the record loads, dominate these kernels
+bool knn_treelets_enabled() {
+  static int e = -1;
+  if (e < 0) {
+    const char* v = getenv("AICP_KNN_TREELETS");
+    e = (v && v[0] == '1') ? 1 : 0;
+  }
+  return e == 1;
+}
 bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
-                    int32_t* ids, uint32_t* ctr) {
+                    int32_t* ids, uint32_t* ctr, const uint4* tl, const uint2* link) {
   if (!total_ref) return true;
-  const int g = persistent_grid((int)total_ref), gu = (int)((total_ref + 255) / 256);
+  if (!launch_knn_ids(s, n_pairs, total_ref, pd, nodes, bpts, knn, ids, ctr, nullptr, tl, link)) return false;
+  const int gu = (int)((total_ref + 255) / 256);
   switch (knn) {
-    case 10:
-      k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr, nullptr);
-      k_normals_from_ids<10><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
-      break;
-    case 20:
-      k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr, nullptr);
-      k_normals_from_ids<20><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
-      break;
-    case 30:
-      k_knn_ids<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, parent, bpts, ids, ctr, nullptr);
-      k_normals_from_ids<30><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm);
-      break;
-    default:
-      return false;
+    case 10: k_normals_from_ids<10><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm); break;
+    case 20: k_normals_from_ids<20><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm); break;
+    case 30: k_normals_from_ids<30><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm); break;
+    default: return false;
   }
   return true;
 }
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
-                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched) {
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
+                    const uint4* tl, const uint2* link) {
   if (!total_ref) return true;
   const int g = persistent_grid((int)total_ref);
+  if (tl && link && knn_treelets_enabled()) {
+    switch (knn) {
+      case 10: k_knn_ids_tl<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, tl, link, bpts, ids, ctr, touched); break;
+      case 20: k_knn_ids_tl<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, tl, link, bpts, ids, ctr, touched); break;
+      case 30: k_knn_ids_tl<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, tl, link, bpts, ids, ctr, touched); break;
+      default: return false;
+    }
+    return true;
+  }
   switch (knn) {
     case 10: k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr, touched); break;
     case 20: k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr, touched); break;

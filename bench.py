@@ -398,6 +398,17 @@ def main():
         elapsed = sh.max_over_ranks(elapsed, dist, device="cuda")
         iters_total = int(sh.sum_over_ranks(float(iters_total), dist, device="cuda"))
 
+    # PCIe-inclusive rate (not `value`): the same step from host buffers, upload + run + free
+    # (aicp_hip_align_batch); rank 0 alone, after the timed loop
+    pcie = None
+    if rank == 0 and not args.data:
+        tp = time.perf_counter()
+        reps = max(1, min(3, args.steps))
+        for _ in range(reps):
+            ctx.align_batch(pairs, cfg, res, flags)
+        pcie = {"clouds_per_s": round(reps * args.pairs / (time.perf_counter() - tp), 3),
+                "note": "host xyz in -> T out per step: H2D of all clouds, run, D2H (aicp_hip_align_batch)"}
+
     # accuracy of the last step (synthetic ground truth)
     from aicp_mapping_amd import synthetic as sy
 
@@ -436,6 +447,7 @@ def main():
                 **extra,
                 "parallelism": "independent pairs sharded over ranks, RCCL all_gather of T",
             },
+            "pcie_inclusive": pcie,
             "icp_iters_per_s": round(iters_total / elapsed, 1),
             "mean_iterations": float(np.mean([s["iterations"] for s in st])),
             "phase_ms_per_step": dict(zip(["overlap_gpu (stream 1)", "normal_tree_and_normals_gpu (stream 2)",
