@@ -287,6 +287,16 @@ __device__ __forceinline__ uint4 ld_rec(const uint4* p) {
   asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));
   return r;
 }
+// a record and its treelet's parent link in one round trip: both loads are issued before the
+// empty asm makes the wave wait for them (ld_rec followed by a plain load would wait for the
+// record first and send the link load after it, a second dependent round trip per climb step)
+__device__ __forceinline__ uint4 ld_rec_up(const uint4* p, const uint2* l, int32_t& up) {
+  uint32_t u = l->x;
+  uint4 r = *p;
+  asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w), "+v"(u));
+  up = (int32_t)u;
+  return r;
+}
 
 // Running minimum of far bounds: every bound is rd + (-off^2 + no^2) with |no| >= |off| (the
 // region shrinks away from the query), so it is >= 0 and a signed integer minimum of the float
@@ -505,18 +515,22 @@ struct Trav2C {
       }
       const uint32_t X = (uint32_t)pc >> 2;
       if (!have_px) {
-        const uint4 r = ld_rec(tl + X);
-        const uint2 lk = ptl[X];
+        uint2 lk = ptl[X];
+        uint4 r = tl[X];
+        asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w), "+v"(lk.x), "+v"(lk.y));
         if (climb_treelet(fs, r, pc, (int32_t)lk.x, c, pc, maxE2, maxR2)) return false;
         px = (int32_t)lk.y;
         have_px = c != start;
         continue;
       }
       // pc in treelet X, px = parent of X's root in treelet Y (px < 0: X is the root treelet)
-      const uint4 rx = ld_rec(tl + X);
+      // three independent loads, one wait
       const uint32_t Y = (uint32_t)max(px, 0) >> 2;
-      const uint4 ry = ld_rec(tl + Y);
-      const uint2 ly = ptl[Y];
+      uint2 ly = ptl[Y];
+      uint4 rx = tl[X];
+      uint4 ry = tl[Y];
+      asm volatile("" : "+v"(rx.x), "+v"(rx.y), "+v"(rx.z), "+v"(rx.w), "+v"(ry.x), "+v"(ry.y), "+v"(ry.z),
+                   "+v"(ry.w), "+v"(ly.x), "+v"(ly.y));
       if (climb_treelet(fs, rx, pc, px, c, pc, maxE2, maxR2)) return false;
       if (c == start || px < 0) continue;  // px < 0: X's root is the tree root, so c == start there
       if (climb_treelet(fs, ry, px, (int32_t)ly.x, c, pc, maxE2, maxR2)) return false;
@@ -557,8 +571,8 @@ struct Trav2C {
       }
       const int32_t p = pc;
       const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
-      const uint4 r = ld_rec(tl + T);
-      const int32_t rootpp = (int32_t)ptl[T].x;
+      int32_t rootpp;
+      const uint4 r = ld_rec_up(tl + T, ptl + T, rootpp);
       const int32_t root = (int32_t)(T << 2);
       if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2)) return false;
       c = p;
@@ -611,8 +625,7 @@ struct Trav2C {
       const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
       if (T != cT) {  // the record and its root's parent, one round trip per treelet
         cT = T;
-        cr = ld_rec(tl + T);
-        cpp = (int32_t)ptl[T].x;
+        cr = ld_rec_up(tl + T, ptl + T, cpp);
       }
       const uint4 r = cr;
       const int32_t pp = s != 0 ? (int32_t)(T << 2) : cpp;  // parent of p
@@ -806,8 +819,8 @@ struct TravT {
       }
       const int32_t p = pc;
       const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
-      const uint4 r = ld_rec(tl + T);
-      const int32_t rootpp = (int32_t)ptl[T].x;
+      int32_t rootpp;
+      const uint4 r = ld_rec_up(tl + T, ptl + T, rootpp);
       const int32_t root = (int32_t)(T << 2);
       if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2)) return false;
       c = p;
@@ -1315,8 +1328,8 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       }
       if (has && t.ph != kPhLeaf) {
         const uint32_t T = t.need();
-        const uint4 r = ld_rec(t.tl + T);
-        const int32_t rootpp = (int32_t)t.ptl[T].x;
+        int32_t rootpp;
+        const uint4 r = ld_rec_up(t.tl + T, t.ptl + T, rootpp);
         if (t.ph == kPhDesc) t.desc_step(r);
         else t.climb_step(fs, r, rootpp, maxE2, maxR2);
       }
