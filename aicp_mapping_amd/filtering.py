@@ -45,6 +45,8 @@ def regionGrowingUniformPlaneSegmentationFilter(cloud_in, *args, ctx=None, param
       carry one colour.
 
     cloud_in: (N, 3|4|8|12) float32 rows. ctx: an aicp Context (default: one on device 0)."""
+    if len(args) > 2:
+        raise TypeError("expected (cloud_in[, cloud_out]) or (cloud_in, view_point, clusters)")
     c = _ctx(ctx)
     if len(args) == 2:
         view_point, clusters = args
@@ -67,8 +69,6 @@ def regionGrowingUniformPlaneSegmentationFilter(cloud_in, *args, ctx=None, param
             clusters.append(idx.astype(np.int32))
             out[idx, 8] = _cluster_rgb(k)
         return out
-    if len(args) > 1:
-        raise TypeError("expected (cloud_in[, cloud_out]) or (cloud_in, view_point, clusters)")
     kept = c.prefilter(cloud_in, params)
     if args and args[0] is not None:
         prev = np.asarray(args[0], np.float32).reshape(-1, 3)
