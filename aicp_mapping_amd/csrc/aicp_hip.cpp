@@ -148,6 +148,7 @@ struct aicp_hip_ctx {
   uint64_t last_queries = 0;
   double last_phase[5] = {0, 0, 0, 0, 0};
   aicp_prefilter_stats last_pf{};  // timing and kNN counts of the last pre-filter
+  aicp_hip_batch* oneshot = nullptr;  // buffers of aicp_hip_align_batch, kept across calls
   hipEvent_t pf_ev[8] = {};
 };
 
@@ -184,6 +185,41 @@ void pack_xyz(const float* src, uint64_t n, uint64_t stride_bytes, float* dst3) 
     dst3[3 * i + 2] = p[2];
   }
 }
+// Strided xyz -> float4 for many clouds at once, split into equal point ranges over host
+// threads (the packing, not the DMA, bounded the host-buffer path: one thread moves ~5 GB/s)
+struct PackSeg {
+  const float* src;
+  uint64_t n, stride;
+  float* dst4;
+};
+void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4);
+void pack_many(const std::vector<PackSeg>& segs) {
+  uint64_t total = 0;
+  for (const PackSeg& g : segs) total += g.n;
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const unsigned nt = total < (1u << 16) ? 1u : hw;
+  if (nt == 1) {
+    for (const PackSeg& g : segs) pack_xyz4(g.src, g.n, g.stride, g.dst4);
+    return;
+  }
+  auto work = [&](uint64_t lo, uint64_t hi) {  // global point range [lo, hi)
+    uint64_t base = 0;
+    for (const PackSeg& g : segs) {
+      const uint64_t a = std::max(lo, base), b = std::min(hi, base + g.n);
+      if (a < b) {
+        const char* src = reinterpret_cast<const char*>(g.src) + (a - base) * g.stride;
+        pack_xyz4(reinterpret_cast<const float*>(src), b - a, g.stride, g.dst4 + 4 * (a - base));
+      }
+      base += g.n;
+      if (base >= hi) break;
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, total * t / nt, total * (t + 1) / nt);
+  work(0, total / nt);
+  for (auto& x : th) x.join();
+}
+
 void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4) {
   const char* b = reinterpret_cast<const char*>(src);
   for (uint64_t i = 0; i < n; ++i) {
@@ -296,19 +332,23 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   // raw clouds as float4
   HIPC(ensure(B->ref_raw, ro * 16));
   HIPC(ensure(B->read_raw, wo * 16));
-  HIPC(ensure(ctx->pin_io, std::max(ro, wo) * 16));
-  float* st = ctx->pin_io.as<float>();
+  HIPC(ensure(ctx->pin_io, (ro + wo) * 16));  // references, then readings: the readings are
+  float* st = ctx->pin_io.as<float>();          // packed while the references' DMA runs
+  std::vector<PackSeg> segs;
   for (size_t r = 0; r < rep.size(); ++r) {
     const PairDesc& d = B->rdesc[r];
-    pack_xyz4(pairs[rep[r]].ref, d.n_ref, pairs[rep[r]].ref_stride, st + 4ull * d.ref_off);
+    segs.push_back(PackSeg{pairs[rep[r]].ref, d.n_ref, pairs[rep[r]].ref_stride, st + 4ull * d.ref_off});
   }
+  pack_many(segs);
   HIPC(hipMemcpyAsync(B->ref_raw.p, st, ro * 16, hipMemcpyHostToDevice, ctx->stream));
-  HIPC(hipStreamSynchronize(ctx->stream));
+  float* sw = st + 4ull * ro;
+  segs.clear();
   for (size_t i = 0; i < n; ++i) {
     const PairDesc& d = B->desc[i];
-    pack_xyz4(pairs[i].read, d.n_read, pairs[i].read_stride, st + 4ull * d.read_off);
+    segs.push_back(PackSeg{pairs[i].read, d.n_read, pairs[i].read_stride, sw + 4ull * d.read_off});
   }
-  HIPC(hipMemcpyAsync(B->read_raw.p, st, wo * 16, hipMemcpyHostToDevice, ctx->stream));
+  pack_many(segs);
+  HIPC(hipMemcpyAsync(B->read_raw.p, sw, wo * 16, hipMemcpyHostToDevice, ctx->stream));
   // block maps: [read pair][read start][ref pair][ref start][red pair][red start]
   const size_t nr = mr.pair.size(), nf = mf.pair.size(), nd = md.pair.size(), ns = ms.pair.size();
   const size_t words = 2 * (nr + nf + nd + ns);
@@ -983,6 +1023,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
                     &ctx->link_raw, &ctx->tlr_flag, &ctx->tlr_rank, &ctx->tlr_temp})
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
+  free_batch(ctx->oneshot);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
                     &ctx->pin_rdesc, &ctx->pin_gdesc, &ctx->pin_gstate})
     release(*b);
@@ -1028,12 +1069,14 @@ int aicp_hip_batch_run(aicp_hip_ctx* ctx, aicp_hip_batch* batch, const aicp_icp_
 
 int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
                          double resolution, int flags, float* out_T, aicp_icp_stats* stats) {
-  aicp_hip_batch* B = nullptr;
-  int rc = aicp_hip_batch_upload(ctx, pairs, n_pairs, &B);
+  if (!ctx) return AICP_ERR_INVALID;
+  HIPC(hipSetDevice(ctx->device));
+  // one-shot batches reuse the context's batch buffers (no device allocation per call)
+  if (!ctx->oneshot) ctx->oneshot = new aicp_hip_batch();
+  aicp_hip_batch* B = ctx->oneshot;
+  const int rc = upload_pairs(ctx, pairs, n_pairs, B);
   if (rc) return rc;
-  rc = aicp_hip_batch_run(ctx, B, cfg, resolution, flags, out_T, stats);
-  aicp_hip_batch_free(ctx, B);
-  return rc;
+  return aicp_hip_batch_run(ctx, B, cfg, resolution, flags, out_T, stats);
 }
 
 int aicp_hip_register_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
