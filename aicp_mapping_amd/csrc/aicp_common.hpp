@@ -24,7 +24,11 @@ namespace aicp {
 constexpr int kHistBins = 2048;     // radix-select digit 1/2 (11 bits)
 constexpr int kHist3Bins = 1024;    // digit 3 (10 bits)
 constexpr int kNNBlock = 256;       // NN / reduce kernel block
-constexpr int kReducePerThread = 4; // reading points per thread in the reduce kernel
+constexpr int kReducePerThread = 4; // reading points per thread and chunk in the reduce kernel
+#ifndef AICP_REDUCE_CHUNKS
+#define AICP_REDUCE_CHUNKS 1
+#endif
+constexpr int kReduceChunks = AICP_REDUCE_CHUNKS;  // chunks per reduce thread (2 and 4 measured no faster than 1)
 constexpr int kSelPerThread = 16;   // reading points per thread in the select passes
 constexpr int kRedCols = 30;        // 21 unique A entries + 6 b + kept + NN touch counts (2)
 constexpr int kFarStack = 48;       // max nested far descents (= max tree depth supported)

@@ -309,7 +309,8 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     d.read_off = (uint32_t)wo;
     d.n_read = (uint32_t)p.n_read;
     d.red_blk_off = red;
-    d.n_red_blk = (uint32_t)((p.n_read + kNNBlock * kReducePerThread - 1) / (kNNBlock * kReducePerThread));
+    constexpr uint32_t kRedBlk = kNNBlock * kReducePerThread * kReduceChunks;
+    d.n_red_blk = (uint32_t)((p.n_read + kRedBlk - 1) / kRedBlk);
     for (int k = 0; k < 3; ++k) {
       d.ref_origin[k] = p.ref_origin[k];
       d.read_origin[k] = p.read_origin[k];
@@ -323,7 +324,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     else
       ident4(d.Tin);
     mr.add((int)i, d.n_read, kNNBlock);
-    md.add((int)i, d.n_read, kNNBlock * kReducePerThread);
+    md.add((int)i, d.n_read, kNNBlock * kReducePerThread * kReduceChunks);
     ms.add((int)i, d.n_read, kNNBlock * kSelPerThread);
   }
   B->total_ref = ro;

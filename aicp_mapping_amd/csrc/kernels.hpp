@@ -46,7 +46,7 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
                    const ActiveList* al, const float4* read_c, const uint4* nodes, const uint4* tl,
                    const int32_t* parent, const float4* bpts, const uint2* ptl, int32_t* match, float* d2,
                    uint32_t* touched, uint32_t* ctr, const IcpParams& prm);
-// TrimmedDist limit per active pair. m: blocks of kNNBlock * kReducePerThread readings;
+// TrimmedDist limit per active pair. m: blocks of kNNBlock * kSelPerThread readings;
 // hist1: n_pairs * kHistBins zeroed words, cand: total_read words, cand_cnt: n_pairs zeroed
 // words (both left zeroed for the next call).
 void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* pd, PairState* st,

@@ -1967,11 +1967,16 @@ __device__ __forceinline__ double dpp_d(double v) {
 
 // Sum over the 64 lanes in a fixed order (quads, rows of 16 via rotations, then the row
 // broadcasts), valid in every lane: DPP moves instead of LDS-crossbar shuffles.
-__device__ __forceinline__ double wave_sum_d(double v) {
+// the sum over the lane's row of 16, valid in every lane of the row
+__device__ __forceinline__ double row_sum_d(double v) {
   v += dpp_d<0xB1>(v);  // quad_perm [1,0,3,2]
   v += dpp_d<0x4E>(v);  // quad_perm [2,3,0,1]
   v += dpp_d<0x124>(v); // row_ror:4
-  v += dpp_d<0x128>(v); // row_ror:8  -> every lane holds its row's sum
+  v += dpp_d<0x128>(v); // row_ror:8
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+  v = row_sum_d(v);
   const double r0 = __shfl(v, 0, 64), r1 = __shfl(v, 16, 64), r2 = __shfl(v, 32, 64), r3 = __shfl(v, 48, 64);
   return (r0 + r1) + (r2 + r3);
 }
@@ -1992,73 +1997,82 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
   double acc[kRedCols];
 #pragma unroll
   for (int i = 0; i < kRedCols; ++i) acc[i] = 0.0;
-  const uint32_t base = m.start[blockIdx.x];
   uint32_t tpts = 0, tnod = 0;
-  // all loads of the thread's readings first (independent), then the gathers of the kept
-  // ones, then the arithmetic: two round trips instead of three per reading
-  bool keep[kReducePerThread];
-  int32_t pos[kReducePerThread];
-  float4 r[kReducePerThread];
+  // kReduceChunks chunks of kReducePerThread readings per thread (the block's reduction below
+  // is paid once per kNNBlock * kReducePerThread * kReduceChunks readings). Per chunk: all
+  // loads of the thread's readings first (independent), then the gathers of the kept ones,
+  // then the arithmetic: two round trips instead of three per reading.
+  for (int ch = 0; ch < kReduceChunks; ++ch) {
+    const uint32_t base = m.start[blockIdx.x] + ch * kReducePerThread * kNNBlock;
+    bool keep[kReducePerThread];
+    int32_t pos[kReducePerThread];
+    float4 r[kReducePerThread];
 #pragma unroll
-  for (int it = 0; it < kReducePerThread; ++it) {
-    const uint32_t j = base + it * kNNBlock + threadIdx.x;
-    keep[it] = false;
-    pos[it] = 0;
-    if (j < d.n_read) {
-      const uint32_t tc = touched[d.read_off + j];
-      tpts += tc & 0xFFFFu;
-      tnod += tc >> 16;
-      keep[it] = d2[d.read_off + j] <= limit;
-      pos[it] = match[d.read_off + j];
-      r[it] = read_c[d.read_off + j];
+    for (int it = 0; it < kReducePerThread; ++it) {
+      const uint32_t j = base + it * kNNBlock + threadIdx.x;
+      keep[it] = false;
+      pos[it] = 0;
+      if (j < d.n_read) {
+        const uint32_t tc = touched[d.read_off + j];
+        tpts += tc & 0xFFFFu;
+        tnod += tc >> 16;
+        keep[it] = d2[d.read_off + j] <= limit;
+        pos[it] = match[d.read_off + j];
+        r[it] = read_c[d.read_off + j];
+      }
     }
-  }
-  float4 q[kReducePerThread], nr[kReducePerThread];
+    float4 q[kReducePerThread], nr[kReducePerThread];
 #pragma unroll
-  for (int it = 0; it < kReducePerThread; ++it)
-    if (keep[it]) {
-      q[it] = bpts[d.ref_off + pos[it]];
-      nr[it] = bnrm[d.ref_off + pos[it]];
+    for (int it = 0; it < kReducePerThread; ++it)
+      if (keep[it]) {
+        q[it] = bpts[d.ref_off + pos[it]];
+        nr[it] = bnrm[d.ref_off + pos[it]];
+      }
+#pragma unroll
+    for (int it = 0; it < kReducePerThread; ++it) {
+      if (!keep[it]) continue;
+      float p[3];
+      apply4(T, r[it].x, r[it].y, r[it].z, p);
+      const float4 n4 = nr[it];
+      float F[6];
+      F[0] = p[1] * n4.z - p[2] * n4.y;
+      F[1] = p[2] * n4.x - p[0] * n4.z;
+      F[2] = p[0] * n4.y - p[1] * n4.x;
+      F[3] = n4.x;
+      F[4] = n4.y;
+      F[5] = n4.z;
+      const float dl0 = p[0] - q[it].x, dl1 = p[1] - q[it].y, dl2 = p[2] - q[it].z;
+      float dot = dl0 * n4.x;
+      dot += dl1 * n4.y;
+      dot += dl2 * n4.z;
+      int c = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = a; b < 6; ++b) acc[c++] += (double)F[a] * (double)F[b];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[21 + a] += (double)F[a] * (double)dot;
+      acc[27] += 1.0;
     }
-#pragma unroll
-  for (int it = 0; it < kReducePerThread; ++it) {
-    if (!keep[it]) continue;
-    float p[3];
-    apply4(T, r[it].x, r[it].y, r[it].z, p);
-    const float4 n4 = nr[it];
-    float F[6];
-    F[0] = p[1] * n4.z - p[2] * n4.y;
-    F[1] = p[2] * n4.x - p[0] * n4.z;
-    F[2] = p[0] * n4.y - p[1] * n4.x;
-    F[3] = n4.x;
-    F[4] = n4.y;
-    F[5] = n4.z;
-    const float dl0 = p[0] - q[it].x, dl1 = p[1] - q[it].y, dl2 = p[2] - q[it].z;
-    float dot = dl0 * n4.x;
-    dot += dl1 * n4.y;
-    dot += dl2 * n4.z;
-    int c = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-      for (int b = a; b < 6; ++b) acc[c++] += (double)F[a] * (double)F[b];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] += (double)F[a] * (double)dot;
-    acc[27] += 1.0;
   }
   acc[28] = (double)tpts;
   acc[29] = (double)tnod;
-  __shared__ double part[kNNBlock / 64][kRedCols];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // row sums (DPP) -> one partial per row of 16 lanes in LDS -> a fixed-order sum of the
+  // block's rows (no cross-row shuffles)
+  constexpr int kRows = kNNBlock / 16;
+  __shared__ double part[kRows][kRedCols];
+  const int lane = threadIdx.x & 63;
+  const int row = threadIdx.x >> 4;
 #pragma unroll
   for (int i = 0; i < kRedCols; ++i) {
-    const double v = wave_sum_d(acc[i]);
-    if (lane == 0) part[wave][i] = v;
+    const double v = row_sum_d(acc[i]);
+    if ((lane & 15) == 0) part[row][i] = v;
   }
   __syncthreads();
   if (threadIdx.x < kRedCols) {
     double v = 0.0;
-    for (int w = 0; w < kNNBlock / 64; ++w) v += part[w][threadIdx.x];
+#pragma unroll
+    for (int w = 0; w < kRows; ++w) v += part[w][threadIdx.x];
     slab[(size_t)blockIdx.x * kRedCols + threadIdx.x] = v;
   }
 }
