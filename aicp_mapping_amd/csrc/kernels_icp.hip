@@ -1965,20 +1965,14 @@ __device__ __forceinline__ double dpp_d(double v) {
   return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
 }
 
-// Sum over the 64 lanes in a fixed order (quads, rows of 16 via rotations, then the row
-// broadcasts), valid in every lane: DPP moves instead of LDS-crossbar shuffles.
-// the sum over the lane's row of 16, valid in every lane of the row
+// the sum over the lane's row of 16 in a fixed order (quads, then rotations), valid in every
+// lane of the row: DPP moves instead of LDS-crossbar shuffles
 __device__ __forceinline__ double row_sum_d(double v) {
   v += dpp_d<0xB1>(v);  // quad_perm [1,0,3,2]
   v += dpp_d<0x4E>(v);  // quad_perm [2,3,0,1]
   v += dpp_d<0x124>(v); // row_ror:4
   v += dpp_d<0x128>(v); // row_ror:8
   return v;
-}
-__device__ __forceinline__ double wave_sum_d(double v) {
-  v = row_sum_d(v);
-  const double r0 = __shfl(v, 0, 64), r1 = __shfl(v, 16, 64), r2 = __shfl(v, 32, 64), r3 = __shfl(v, 48, 64);
-  return (r0 + r1) + (r2 + r3);
 }
 
 __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
@@ -2083,17 +2077,27 @@ __global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__
   PairState& s = st[pair];
   if (!s.active) return;
   const PairDesc& d = pd[pair];
-  __shared__ double part[4][kRedCols];
+  // the pair's slab rows: thread t sums column t % kRedCols over rows t / kRedCols + 8 k
+  // (independent loads, contiguous across the block), then a fixed-order sum of the 8 groups
+  constexpr int kGroups = 256 / kRedCols;
+  __shared__ double part[kGroups][kRedCols];
   __shared__ double tot[kRedCols];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  for (int c = 0; c < kRedCols; ++c) {
+  const int t = threadIdx.x;
+  if (t < kGroups * kRedCols) {
+    const int g = t / kRedCols, c = t - g * kRedCols;
+    const double* col = slab + (size_t)d.red_blk_off * kRedCols + c;
     double v = 0.0;
-    for (uint32_t r = t; r < d.n_red_blk; r += 256) v += slab[(size_t)(d.red_blk_off + r) * kRedCols + c];
-    v = wave_sum_d(v);
-    if (lane == 0) part[wave][c] = v;
+#pragma unroll 4
+    for (uint32_t r = g; r < d.n_red_blk; r += kGroups) v += col[(size_t)r * kRedCols];
+    part[g][c] = v;
   }
   __syncthreads();
-  if (t < kRedCols) tot[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+  if (t < kRedCols) {
+    double v = part[0][t];
+#pragma unroll
+    for (int g = 1; g < kGroups; ++g) v += part[g][t];
+    tot[t] = v;
+  }
   __syncthreads();
   if (t != 0) return;
   s.touched_pts += (uint64_t)tot[28];
