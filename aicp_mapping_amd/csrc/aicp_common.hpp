@@ -37,7 +37,7 @@ constexpr uint32_t kLeaf = 3;
 constexpr int kMaxPairs = 4096;     // pairs per batch
 constexpr int kXcdGroups = 8;       // work groups of the persistent kernels (one per XCD)
 constexpr int kCtrStride = 16;      // words between the per-group work counters (64 B)
-constexpr int kCtrWords = 2 * kXcdGroups * kCtrStride;  // ICP NN counters, then normals kNN
+constexpr int kCtrWords = 3 * kXcdGroups * kCtrStride;  // ICP NN counters, normals kNN, ICP group 1 NN
 
 // Compacted list of the pairs still iterating (k_active_list), consumed by the persistent
 // NN kernel: slot s of the work space belongs to pair[e] with off[e] <= s < off[e+1].
@@ -154,6 +154,7 @@ struct IcpParams {
   int32_t smooth;
   float min_rot, min_trans;
   int32_t knn_normals;
+  int32_t prof_slot;  // diagnostic builds (AICP_XCD_PROF): the launch's record slot
 };
 
 }  // namespace aicp

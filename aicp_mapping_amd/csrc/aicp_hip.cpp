@@ -110,6 +110,34 @@ struct Maps {  // block maps of one flat grid
   }
 };
 
+// ICP pair groups (1 or 2; AICP_ICP_GROUPS=2 selects two). Two groups measured slower on C2
+// (3480 -> 3390 clouds/s): an NN launch over half the pairs takes 62 % of a full one.
+int icp_groups(size_t P) {
+  static int g = -1;
+  if (g < 0) {
+    const char* e = std::getenv("AICP_ICP_GROUPS");
+    g = (e && std::atoi(e) == 2) ? 2 : 1;
+  }
+  return P >= 2 ? g : 1;
+}
+bool icp_serial_nn() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("AICP_ICP_SERIAL_NN");
+    v = (e && std::atoi(e) == 0) ? 0 : 1;
+  }
+  return v == 1;
+}
+struct IcpGroup {
+  int p0 = 0, np = 0;
+  uint32_t reads = 0;
+  BlockMap msel{}, mred{};
+  hipStream_t st = nullptr;
+  ActiveList* al = nullptr;
+  uint32_t* ctr = nullptr;
+  hipEvent_t nn_done = nullptr;
+};
+
 }  // namespace
 
 struct aicp_hip_batch {
@@ -601,7 +629,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     if (!e) HIPC(hipEventCreate(&e));
   const bool timeNN = (flags & AICP_RUN_TIME_NN) && doIcp;
   if (timeNN)
-    while ((int)ctx->nn_ev.size() < 2 * cfg->max_iter) {
+    while ((int)ctx->nn_ev.size() < 2 * 2 * cfg->max_iter) {  // up to two ICP groups
       hipEvent_t e;
       HIPC(hipEventCreate(&e));
       ctx->nn_ev.push_back(e);
@@ -611,7 +639,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   HIPC(ensure(ctx->desc, P * sizeof(PairDesc)));
   HIPC(ensure(ctx->state, P * sizeof(PairState)));
   if (P > (size_t)kMaxPairs) FAIL(AICP_ERR_UNSUPPORTED, "more than 4096 pairs in one batch");
-  HIPC(ensure(ctx->active, sizeof(ActiveList)));
+  HIPC(ensure(ctx->active, 2 * sizeof(ActiveList)));
   HIPC(ensure(ctx->ctrs, kCtrWords * 4));
   HIPC(ensure(ctx->pin_desc, 3 * P * sizeof(PairDesc)));
   HIPC(ensure(ctx->pin_state, P * sizeof(PairState)));
@@ -854,20 +882,79 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     prm.min_rot = cfg->min_diff_rot;
     prm.min_trans = cfg->min_diff_trans;
     prm.knn_normals = cfg->knn_normals;
-    ActiveList* dAl = ctx->active.as<ActiveList>();
+    // The ICP loop in one pair group on s, or two on s and s2: group g's NN launch waits for the
+    // other group's previous NN launch, so the NN launches never share the chip with each other,
+    // and each group's select / reduce / update (short, low-occupancy kernels) runs underneath
+    // the other group's NN launch instead of between two NN launches.
+    const int G = icp_groups(P);
+    IcpGroup grp[2];
+    {
+      const std::vector<PairDesc>& hd = B->desc;
+      uint64_t tot = 0, acc = 0;
+      for (size_t i = 0; i < P; ++i) tot += hd[i].n_read;
+      size_t p1 = P;
+      if (G == 2) {
+        p1 = 1;
+        for (size_t i = 0; i + 1 < P; ++i) {  // first pair of group 1: about half the readings before it
+          acc += hd[i].n_read;
+          p1 = i + 1;
+          if (2 * acc >= tot) break;
+        }
+      }
+      uint32_t sel_blk = 0;
+      for (size_t i = 0; i < p1; ++i) sel_blk += (hd[i].n_read + kNNBlock * kSelPerThread - 1) / (kNNBlock * kSelPerThread);
+      const uint32_t red_blk = p1 < P ? hd[p1].red_blk_off : (uint32_t)B->n_red_total;
+      for (int g = 0; g < G; ++g) {
+        IcpGroup& q = grp[g];
+        q.p0 = g ? (int)p1 : 0;
+        q.np = g ? (int)(P - p1) : (int)p1;
+        q.reads = 0;
+        for (int i = q.p0; i < q.p0 + q.np; ++i) q.reads += hd[i].n_read;
+        q.msel = B->m_sel;
+        q.mred = B->m_red;
+        if (g == 0) {
+          q.msel.n_blocks = sel_blk;
+          q.mred.n_blocks = red_blk;
+        } else {
+          q.msel.pair += sel_blk;
+          q.msel.start += sel_blk;
+          q.msel.n_blocks -= sel_blk;
+          q.mred.pair += red_blk;
+          q.mred.start += red_blk;
+          q.mred.n_blocks -= red_blk;
+        }
+        q.st = g ? s2 : s;
+        q.al = ctx->active.as<ActiveList>() + g;
+        q.ctr = g ? dCtr + 2 * kXcdGroups * kCtrStride : dCtr;
+        q.nn_done = ctx->ev[13 + g];
+      }
+    }
+    if (G == 2) HIPC(hipStreamWaitEvent(s2, ctx->ev[9], 0));
     for (int it = 0; it < cfg->max_iter; ++it) {
-      launch_active_list(s, (int)P, dDesc, dState, dAl, dCtr);
-      if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it], s));
-      launch_icp_nn(s, (int)B->total_read, dDesc, dState, dAl, readc, nodes,
-                    ctx->tl_total ? ctx->tl.as<uint4>() : nullptr, parent, bpts,
-                    ctx->tl_total ? ctx->ptl.as<uint2>() : nullptr, ctx->match.as<int32_t>(), ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm);
-      if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * it + 1], s));
-      ++nn_launches;
-      launch_icp_select(s, B->m_sel, (int)P, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
-                        ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>());
-      launch_icp_reduce(s, B->m_red, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
-                        ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>());
-      launch_icp_update(s, (int)P, dDesc, dState, ctx->slab.as<double>(), prm);
+      for (int g = 0; g < G; ++g) {
+        const IcpGroup& q = grp[g];
+        const PairDesc* gd = dDesc + q.p0;
+        PairState* gs = dState + q.p0;
+        launch_active_list(q.st, q.np, gd, gs, q.al, q.ctr);
+        if (G == 2 && icp_serial_nn()) HIPC(hipStreamWaitEvent(q.st, grp[1 - g].nn_done, 0));
+        prm.prof_slot = nn_launches;
+        if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches], q.st));
+        launch_icp_nn(q.st, (int)q.reads, gd, gs, q.al, readc, nodes, ctx->tl_total ? ctx->tl.as<uint4>() : nullptr,
+                      parent, bpts, ctx->tl_total ? ctx->ptl.as<uint2>() : nullptr, ctx->match.as<int32_t>(),
+                      ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), q.ctr, prm);
+        if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches + 1], q.st));
+        if (G == 2) HIPC(hipEventRecord(q.nn_done, q.st));
+        ++nn_launches;
+        launch_icp_select(q.st, q.msel, q.np, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
+                          ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), q.p0);
+        launch_icp_reduce(q.st, q.mred, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
+                          ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>());
+        launch_icp_update(q.st, q.np, gd, gs, ctx->slab.as<double>(), prm);
+      }
+    }
+    if (G == 2) {
+      HIPC(hipEventRecord(ctx->ev[15], s2));
+      HIPC(hipStreamWaitEvent(s, ctx->ev[15], 0));
     }
     launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
     if (std::getenv("AICP_NN_PROF_DUMP")) {

@@ -49,8 +49,9 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
 // TrimmedDist limit per active pair. m: blocks of kNNBlock * kSelPerThread readings;
 // hist1: n_pairs * kHistBins zeroed words, cand: total_read words, cand_cnt: n_pairs zeroed
 // words (both left zeroed for the next call).
+// m covers pairs p0 .. p0 + n_pairs - 1 (absolute pair indices into pd / st / hist1 / cand_cnt).
 void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* pd, PairState* st,
-                       const float* d2, uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt);
+                       const float* d2, uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, int p0 = 0);
 void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const PairState* st,
                        const float4* read_c, const int32_t* match, const float* d2,
                        const uint32_t* touched, const float4* bpts, const float4* bnrm, double* slab);

@@ -10,14 +10,15 @@
 //                  over the whole chip: digit-1 histograms per 1024 readings, then the bin's
 //                  values compacted per pair and finished by one workgroup per pair
 //   k_icp_reduce   TrimmedDist weights + getMatchedPoints gather + point-to-plane F, dot and the
-//                  27-entry normal-equation sums in double from exact float products; wave
-//                  butterfly + LDS, one deterministic partial row per workgroup (no atomics)
+//                  27-entry normal-equation sums in double from exact float products; DPP row
+//                  sums + LDS, one deterministic partial row per workgroup (no atomics)
 //   k_icp_update   fixed-order sum of the partial rows, 6x6 solve, AngleAxis update of T_iter,
 //                  Counter + Differential checkers, per-pair active flag
 // SurfaceNormal: k_knn_ids (persistent kNN, eps 0, ids only) + k_normals_from_ids (uniform
 // covariance / eigen work per point).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 
 #include <cstdlib>
@@ -1234,6 +1235,12 @@ struct SM0 {
   }
 };
 
+#ifndef AICP_XCD_PROF
+#define AICP_XCD_PROF 0  // diagnostic builds: per-XCD-group first start / last end of each NN launch
+#endif
+#if AICP_XCD_PROF
+__device__ unsigned long long g_xcd_prof[64 * kXcdGroups * 2];
+#endif
 #ifndef AICP_NN_PROF
 #define AICP_NN_PROF 0  // diagnostic builds: per-phase s_memtime cycles of the persistent waves
 #endif
@@ -1711,6 +1718,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
                                                 uint32_t* ctr, IcpParams prm) {
   const uint32_t total = al->total;
   if (total == 0) return;
+#if AICP_XCD_PROF
+  const uint64_t xt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // chunk context: wave-uniform (scalar registers)
   uint32_t c_lo = 0, c_n = 0, c_read = 0, c_node = 0, c_ref = 0;
   int c_pair = 0;
@@ -1751,6 +1761,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
         d2out[qidx] = t.res_d2();
         touched[qidx] = (min(t.tn, 65535u) << 16) | min(t.tp, 65535u);
       });
+#if AICP_XCD_PROF
+  // per launch slot and XCD group: earliest wave start, latest wave end (100 MHz clock)
+  const uint64_t xt1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && prm.prof_slot < 64) {
+    unsigned long long* r = g_xcd_prof + (prm.prof_slot * kXcdGroups + blockIdx.x % kXcdGroups) * 2;
+    atomicMin(&r[0], (unsigned long long)xt0);
+    atomicMax(&r[1], (unsigned long long)xt1);
+  }
+#endif
 }
 
 // rank k -> (bin, k - count before bin) over h[nb] with 1024 threads; result in res[0..1]
@@ -2067,7 +2086,9 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
     double v = 0.0;
 #pragma unroll
     for (int w = 0; w < kRows; ++w) v += part[w][threadIdx.x];
-    slab[(size_t)blockIdx.x * kRedCols + threadIdx.x] = v;
+    // the pair's partial rows start at red_blk_off (m may cover a subset of the pairs)
+    const uint32_t row = d.red_blk_off + m.start[blockIdx.x] / (kNNBlock * kReducePerThread * kReduceChunks);
+    slab[(size_t)row * kRedCols + threadIdx.x] = v;
   }
 }
 
@@ -2358,6 +2379,7 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
                    const float4* bpts, const uint2* ptl, int32_t* match, float* d2, uint32_t* touched,
                    uint32_t* ctr, const IcpParams& prm) {
   const int g = persistent_grid(grid_items, AICP_NN_WAVES);
+  if (g == 0) return;  // a pair group without readings
   if (nn_engine() == 4 && tl && ptl)
     k_icp_nn<Trav2S><<<g, 256, 0, s>>>(pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
   else if (nn_engine() == 3 && tl && ptl)
@@ -2369,6 +2391,28 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
     k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, nullptr, match, d2, touched, ctr, prm);
 }
 void nn_prof_dump() {
+#if AICP_XCD_PROF
+  static unsigned long long h[64 * kXcdGroups * 2];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_xcd_prof), sizeof(h)) == hipSuccess) {
+    for (int l = 0; l < 64; ++l) {
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (int g = 0; g < kXcdGroups; ++g) {
+        t0 = std::min(t0, h[(l * kXcdGroups + g) * 2]);
+        t1 = std::max(t1, h[(l * kXcdGroups + g) * 2 + 1]);
+      }
+      if (t1 == 0) continue;
+      fprintf(stderr, "xcd launch %2d: %6.1f us |", l, (t1 - t0) / 100.0);
+      for (int g = 0; g < kXcdGroups; ++g)
+        fprintf(stderr, " %6.1f", (h[(l * kXcdGroups + g) * 2 + 1] - t0) / 100.0);
+      fprintf(stderr, "\n");
+    }
+  }
+  for (int i = 0; i < 64 * kXcdGroups; ++i) {
+    h[2 * i] = ~0ull;
+    h[2 * i + 1] = 0;
+  }
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_prof), h, sizeof(h));
+#endif
 #if AICP_NN_PROF
   unsigned long long h[8];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_nn_prof), sizeof(h)) == hipSuccess) {
@@ -2383,12 +2427,12 @@ void nn_prof_dump() {
 }
 
 void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* pd, PairState* st, const float* d2,
-                       uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt) {
+                       uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, int p0) {
   if (!m.n_blocks) return;
   k_sel_hist<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, hist1);
-  k_sel_find1<<<n_pairs, 1024, 0, s>>>(st, hist1);
+  k_sel_find1<<<n_pairs, 1024, 0, s>>>(st + p0, hist1 + (size_t)p0 * kHistBins);
   k_sel_compact<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, cand, cand_cnt);
-  k_sel_final<<<n_pairs, 1024, 0, s>>>(pd, st, cand, cand_cnt);
+  k_sel_final<<<n_pairs, 1024, 0, s>>>(pd + p0, st + p0, cand, cand_cnt + p0);
 }
 void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const PairState* st, const float4* read_c,
                        const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
