@@ -562,6 +562,65 @@ int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean = false) {
   return std::min(kFarStack - 2, T.needed > 0 ? std::max(l + 1, T.needed) : l + 4);
 }
 
+// The overlap's second half on stream s (the first, the key boxes, is queued before the trees):
+// wait for the boxes, size one byte map per reading and per reference group, mark, count,
+// ratio. Runs on its own host thread while the main thread queues the trees, so the marking
+// starts as soon as the boxes are known instead of after the raw tree's host polls.
+int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairDesc* dDesc, PairState* dState,
+                 PairDesc* dG, PairState* dGst, const float4* readS, double res, bool set_ratio, std::string& err) {
+  hipStream_t s = ctx->stream;
+  TCHK(hipSetDevice(ctx->device));
+  TCHK(hipEventSynchronize(ctx->ev[1]));
+  // one map per overlap group (reference side) and one per pair (reading side), each over
+  // the padded key box of that cloud's keys and origin
+  uint64_t bm_bytes = 0;
+  TCHK(ensure(ctx->pin_ovl, (P + G) * sizeof(OvlDesc)));
+  TCHK(ensure(ctx->ovl, (P + G) * sizeof(OvlDesc)));
+  OvlDesc* ho = ctx->pin_ovl.as<OvlDesc>();
+  auto size_map = [&](const PairState& hs, OvlDesc& o) -> bool {
+    uint64_t vox = 1;
+    for (int k = 0; k < 3; ++k) {
+      int lo = hs.ovl_bbox[k], hi = hs.ovl_bbox[3 + k];
+      if (lo > hi) lo = hi = 0;  // nothing inside the key range
+      o.min[k] = lo - 2;
+      o.dim[k] = (hi - lo) + 5;
+      vox *= (uint64_t)o.dim[k];
+    }
+    o.bytes = (vox + 15) / 16 * 16;
+    o.off = bm_bytes;
+    bm_bytes += o.bytes;
+    return vox <= (1ull << 34);
+  };
+  for (size_t i = 0; i < P; ++i)
+    if (!size_map(ctx->pin_state.as<PairState>()[i], ho[i]))
+      TFAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
+  for (size_t g = 0; g < G; ++g)
+    if (!size_map(ctx->pin_gstate.as<PairState>()[g], ho[P + g]))
+      TFAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
+  // all maps of the batch at once: at most half the free device memory (beyond what the
+  // arena already holds), so a few far outlier points fail this batch with a clear error
+  // instead of an allocation failure
+  size_t free_b = 0, total_b = 0;
+  TCHK(hipMemGetInfo(&free_b, &total_b));
+  const uint64_t limit = ctx->bitmap.cap + free_b / 2;
+  if (bm_bytes > limit)
+    TFAIL(AICP_ERR_UNSUPPORTED, "overlap voxel maps need " + std::to_string(bm_bytes >> 20) + " MiB, more than " +
+                                    std::to_string(limit >> 20) +
+                                    " MiB available: far outlier points? crop the clouds or split the batch");
+  TCHK(ensure(ctx->bitmap, bm_bytes));
+  TCHK(hipMemcpyAsync(ctx->ovl.p, ho, (P + G) * sizeof(OvlDesc), hipMemcpyHostToDevice, s));
+  TCHK(hipEventRecord(ctx->ev[6], s));
+  uint8_t* bm = ctx->bitmap.as<uint8_t>();
+  const OvlDesc* dOvl = ctx->ovl.as<OvlDesc>();
+  TCHK(hipMemsetAsync(bm, 0, bm_bytes, s));
+  launch_ovl_mark(s, B->m_gref, dG, dOvl + P, dGst, B->ref_raw.as<float4>(), 0, res, bm);
+  launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm);
+  launch_ovl_count(s, (int)P, (int)G, dDesc, dOvl, dOvl + P, dState, dGst, bm);
+  launch_ovl_finish(s, (int)P, dDesc, dState, dGst, set_ratio ? 1 : 0);
+  TCHK(hipGetLastError());
+  return AICP_OK;
+}
+
 // the centred reference's matcher tree and the pairs' frames, on stream3 (worker thread)
 int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dDesc, PairDesc* dRdesc,
                   int plan, std::string& err) {
@@ -719,6 +778,22 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     }
     return r;
   };
+  // the overlap's map sizing and marking (stream s), on its own host thread when the trees are
+  // queued too
+  std::thread ovl_thread;
+  int orc = AICP_OK;
+  std::string oerr;
+  Joiner ojoiner{ovl_thread};
+  auto join_ovl = [&](int r) {
+    if (ovl_thread.joinable()) ovl_thread.join();
+    if (!r && orc) {
+      ctx->err = oerr;
+      r = orc;
+    }
+    return r;
+  };
+  if (doOvl && doIcp)
+    ovl_thread = std::thread([&] { orc = overlap_maps(ctx, B, P, G, dDesc, dState, dG, dGst, readS, res, true, oerr); });
   if (doIcp) {
     HIPC(ensure(ctx->rdesc, R * sizeof(PairDesc)));
     HIPC(ensure(ctx->rstate, R * sizeof(PairState)));
@@ -790,55 +865,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
     HIPC(hipEventRecord(ctx->ev[10], s2));
   }
-  // overlap: size the voxel maps from the key boxes, then mark
-  uint64_t bm_bytes = 0;
   if (doOvl) {
-    HIPC(hipEventSynchronize(ctx->ev[1]));
-    // one map per overlap group (reference side) and one per pair (reading side), each over
-    // the padded key box of that cloud's keys and origin
-    HIPC(ensure(ctx->pin_ovl, (P + G) * sizeof(OvlDesc)));
-    HIPC(ensure(ctx->ovl, (P + G) * sizeof(OvlDesc)));
-    OvlDesc* ho = ctx->pin_ovl.as<OvlDesc>();
-    auto size_map = [&](const PairState& hs, OvlDesc& o) -> bool {
-      uint64_t vox = 1;
-      for (int k = 0; k < 3; ++k) {
-        int lo = hs.ovl_bbox[k], hi = hs.ovl_bbox[3 + k];
-        if (lo > hi) lo = hi = 0;  // nothing inside the key range
-        o.min[k] = lo - 2;
-        o.dim[k] = (hi - lo) + 5;
-        vox *= (uint64_t)o.dim[k];
-      }
-      o.bytes = (vox + 15) / 16 * 16;
-      o.off = bm_bytes;
-      bm_bytes += o.bytes;
-      return vox <= (1ull << 34);
-    };
-    for (size_t i = 0; i < P; ++i)
-      if (!size_map(ctx->pin_state.as<PairState>()[i], ho[i]))
-        FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
-    for (size_t g = 0; g < G; ++g)
-      if (!size_map(ctx->pin_gstate.as<PairState>()[g], ho[P + g]))
-        FAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
-    // all maps of the batch at once: at most half the free device memory (beyond what the
-    // arena already holds), so a few far outlier points fail this batch with a clear error
-    // instead of an allocation failure
-    size_t free_b = 0, total_b = 0;
-    HIPC(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t limit = ctx->bitmap.cap + free_b / 2;
-    if (bm_bytes > limit)
-      FAIL(AICP_ERR_UNSUPPORTED, "overlap voxel maps need " + std::to_string(bm_bytes >> 20) + " MiB, more than " +
-                                     std::to_string(limit >> 20) +
-                                     " MiB available: far outlier points? crop the clouds or split the batch");
-    HIPC(ensure(ctx->bitmap, bm_bytes));
-    HIPC(hipMemcpyAsync(ctx->ovl.p, ho, (P + G) * sizeof(OvlDesc), hipMemcpyHostToDevice, s));
-    HIPC(hipEventRecord(ctx->ev[6], s));
-    uint8_t* bm = ctx->bitmap.as<uint8_t>();
-    const OvlDesc* dOvl = ctx->ovl.as<OvlDesc>();
-    HIPC(hipMemsetAsync(bm, 0, bm_bytes, s));
-    launch_ovl_mark(s, B->m_gref, dG, dOvl + P, dGst, B->ref_raw.as<float4>(), 0, res, bm);
-    launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm);
-    launch_ovl_count(s, (int)P, (int)G, dDesc, dOvl, dOvl + P, dState, dGst, bm);
-    launch_ovl_finish(s, (int)P, dDesc, dState, dGst, doIcp ? 1 : 0);
+    rc = join_ovl(doIcp ? AICP_OK : overlap_maps(ctx, B, P, G, dDesc, dState, dG, dGst, readS, res, false, oerr));
+    if (!doIcp && rc) ctx->err = oerr;
+    if (rc) return join_worker(rc);
   }
   HIPC(hipEventRecord(ctx->ev[2], s));
   IcpParams prm{};
