@@ -117,11 +117,20 @@ constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #define AICP_NN_PREFMIN 0  // Trav2C: per-depth running minimum of the far bounds in LDS (climb pruning; off: C2 -1 %, C4 +20 %)
 #endif
 [[maybe_unused]] constexpr int kPmDepth = 24;  // depths whose running minimum is kept (deeper levels climb unpruned)
+#ifndef AICP_NN_POPCHK
+#define AICP_NN_POPCHK 1  // Trav2C (CLIMB2): after a frame pop, skip the rest of the climb when no level above the frame's node can pass (per-depth prefix minima, one byte each, in LDS)
+#endif
+[[maybe_unused]] constexpr int kPopDepth = 16;  // depths whose prefix minimum is kept (frames deeper than this climb unchecked)
+[[maybe_unused]] constexpr int kStartBits = 26;  // LDS frames keep P's depth above the start node id
 #ifndef AICP_NN_CLIMB2
 #define AICP_NN_CLIMB2 1  // Trav2C: climb one treelet (record + parent, up to two levels) per iteration
 #endif
 #ifndef AICP_NN_CLIMB4
 #define AICP_NN_CLIMB4 0  // Trav2C (with CLIMB2): two treelets per climb round trip through the treelet links (measured 6 % slower: the extra records are mostly not needed)
+#endif
+#if AICP_NN_POPCHK && (!AICP_NN_CLIMB2 || AICP_NN_CLIMB4 || AICP_NN_PREFMIN)
+#undef AICP_NN_POPCHK
+#define AICP_NN_POPCHK 0  // the pop check belongs to the one-treelet climb
 #endif
 #ifndef AICP_NN_LDS_FRAMES
 #define AICP_NN_LDS_FRAMES 3  // Trav2C: innermost far-descent frames kept in LDS (20 B each per lane; 4 measured no faster)
@@ -307,6 +316,20 @@ __device__ __forceinline__ float min_bound(float a, float b) {
   return __int_as_float(min(__float_as_int(a), __float_as_int(b)));
 }
 
+// One-byte lower bound of a non-negative float (the prefix minima of AICP_NN_POPCHK): code 0 is
+// 0.0, code c >= 1 is the float with bits kPmBase + ((c - 1) << 21) (two mantissa bits), and a
+// value always encodes to a code that decodes to <= itself (truncation, clamping at 255 only
+// lowers it), so a failed far test on the decoded bound implies a failed test on the true one.
+constexpr uint32_t kPmBase = 0x30000000u;  // 2^-31
+__device__ __forceinline__ uint32_t pm_enc(float v) {
+  const int32_t u = __float_as_int(v);
+  const int32_t c = ((u - (int32_t)kPmBase) >> 21) + 1;
+  return (uint32_t)min(max(c, 0), 255);
+}
+__device__ __forceinline__ float pm_dec(uint32_t c) {
+  return c == 0 ? 0.f : __uint_as_float(kPmBase + ((c - 1u) << 21));
+}
+
 struct Trav2C {
   const uint4* tl;       // the pair's treelets
   const uint2* ptl;      // the pair's treelet links {parent of the root, parent of the parent treelet's root}
@@ -316,6 +339,7 @@ struct Trav2C {
   int32_t n, start, sp, pl;  // node ids; pl: parent of the node the last descent ended in
   int32_t dep;               // depth of n (descent) / of the node climbed from (climb)
   uint16_t* pm;              // this lane's prefix-minimum column in LDS (AICP_NN_PREFMIN)
+  uint8_t* pmb;              // this lane's one-byte prefix minima per depth in LDS (AICP_NN_POPCHK)
   uint32_t lb0, lcnt;        // bucket of the leaf the last descent ended in
   NnLdsFrame* lf;            // this lane's LDS frames (AICP_NN_LDS_FRAMES, stride kNNBlock)
   uint32_t tp, tn;
@@ -356,6 +380,9 @@ struct Trav2C {
     ++tn;
 #if AICP_NN_PREFMIN
     if (dep < kPmDepth) pm[dep * kNNBlock] = (uint16_t)(__float_as_uint(minFar) >> 16);
+    ++dep;
+#elif AICP_NN_POPCHK
+    if (dep < kPopDepth) pmb[dep * kNNBlock] = (uint8_t)pm_enc(minFar);
     ++dep;
 #endif
     return no > 0.f;
@@ -433,8 +460,9 @@ struct Trav2C {
 #if AICP_NN_CLIMB2
   // far test of node p (slot s of record r, parent pp); on a pass: push the frame, start the far
   // descent and return true
+  // dp: depth of p (AICP_NN_POPCHK: kept in the frame, the far descent starts at dp + 1)
   __device__ __forceinline__ bool far_push(FarStack& fs, const uint4& r, int32_t p, uint32_t s, int32_t pp,
-                                           float maxE2, float maxR2) {
+                                           float maxE2, float maxR2, int32_t dp = 0) {
     const uint32_t T = (uint32_t)p >> 2;
     const uint32_t w = slot_word(r, s), cd = (r.w >> (2 * s)) & 3u;
     const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
@@ -445,10 +473,15 @@ struct Trav2C {
     const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
     // the innermost frames live in LDS (no scratch traffic: scratch frames are written back
     // to HBM through L2), deeper nesting in the scratch stack
+#if AICP_NN_POPCHK
+    const int32_t sdp = start | (dp << kStartBits);  // node ids < 2^kStartBits (host-checked)
+#else
+    const int32_t sdp = start;
+#endif
     if (sp < AICP_NN_LDS_FRAMES)
-      lf[sp * kNNBlock] = NnLdsFrame{(int32_t)(((uint32_t)pp & 0x3fffffffu) | (cd << 30)), rd, oc, start,
+      lf[sp * kNNBlock] = NnLdsFrame{(int32_t)(((uint32_t)pp & 0x3fffffffu) | (cd << 30)), rd, oc, sdp,
                                      __int_as_float(max(__float_as_int(minFar), 0) | (p == start ? (int32_t)0x80000000 : 0))};
-    else fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, 0};
+    else fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, dp};
     ++sp;
     const float nn = -no * no;
     if (cd == 0) noc0 = nn;
@@ -458,6 +491,9 @@ struct Trav2C {
     n = far;
     start = far;
     pl = p;
+#if AICP_NN_POPCHK
+    dep = dp + 1;
+#endif
     return true;
   }
 
@@ -540,7 +576,12 @@ struct Trav2C {
   }
 #else
   // the climb one treelet per iteration: one record (and its root's parent) per round trip, the
-  // node and, for a child slot, the treelet root above it
+  // node and, for a child slot, the treelet root above it.
+  // With AICP_NN_POPCHK, dep tracks the depth of c: after a frame pop, the prefix minimum of the
+  // far bounds from the frame's start down to P's parent (written by that descent and untouched
+  // by the deeper far descents since) decides at once whether any level left to climb can pass.
+  // The far tests it skips are ones the climb would have made and failed, so the visit order,
+  // counts and result are unchanged.
   __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
     int32_t c = n, pc = pl;
     if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
@@ -553,8 +594,14 @@ struct Trav2C {
           // P only matters through P == start (the sign bit of mn); any other id != start will do
           const NnLdsFrame g = lf[sp * kNNBlock];
           const int32_t mi = __float_as_int(g.mnf);
+#if AICP_NN_POPCHK
+          const int32_t gs = g.start & ((1 << kStartBits) - 1);
+          f = FarFrame{g.PPcd, g.rd, g.old, __int_as_float(mi & 0x7fffffff), gs, mi < 0 ? gs : -2,
+                       g.PPcd & 0x3fffffff, (int32_t)((uint32_t)g.start >> kStartBits)};
+#else
           f = FarFrame{g.PPcd, g.rd, g.old, __int_as_float(mi & 0x7fffffff), g.start, mi < 0 ? g.start : -2,
                        g.PPcd & 0x3fffffff, 0};
+#endif
         } else {
           f = fs.f[sp];
         }
@@ -568,6 +615,13 @@ struct Trav2C {
         c = f.P;
         pc = f.PP;
         if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
+#if AICP_NN_POPCHK
+        dep = f.pad;  // depth of P
+        if (c != start && dep <= kPopDepth) {
+          const float b = pm_dec(pmb[(dep - 1) * kNNBlock]);
+          if (!(b <= maxR2 && b * maxE2 < best.v[0])) c = start;
+        }
+#endif
         continue;
       }
       const int32_t p = pc;
@@ -575,13 +629,19 @@ struct Trav2C {
       int32_t rootpp;
       const uint4 r = ld_rec_up(tl + T, ptl + T, rootpp);
       const int32_t root = (int32_t)(T << 2);
-      if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2)) return false;
+      if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2, dep - 1)) return false;
       c = p;
       pc = s != 0 ? root : rootpp;
+#if AICP_NN_POPCHK
+      --dep;
+#endif
       if (s == 0 || c == start) continue;
-      if (far_push(fs, r, root, 0, rootpp, maxE2, maxR2)) return false;
+      if (far_push(fs, r, root, 0, rootpp, maxE2, maxR2, dep - 1)) return false;
       c = root;
       pc = rootpp;
+#if AICP_NN_POPCHK
+      --dep;
+#endif
     }
   }
 #endif  // AICP_NN_CLIMB4
@@ -1363,6 +1423,12 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       if constexpr (is_coop<Eng>::value && !is_sm<Eng>::value) {
         __shared__ NnLdsFrame lds_frames[AICP_NN_LDS_FRAMES * kNNBlock];
         t.lf = lds_frames + threadIdx.x;
+      }
+#endif
+#if AICP_NN_POPCHK
+      if constexpr (is_coop<Eng>::value && !is_sm<Eng>::value) {
+        __shared__ uint8_t pmb_lds[kPopDepth * kNNBlock];
+        t.pmb = pmb_lds + threadIdx.x;
       }
 #endif
       if (has && t.climb(fs, maxE2, maxR2)) {
