@@ -811,7 +811,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
         rd.tl_cap = (uint32_t)(4 * (uint64_t)rd.n_ref + 4);
         ctx->tl_total += rd.tl_cap;
       }
-      if (ctx->tl_total >= (1ull << 32)) ctx->tl_total = 0;  // offsets do not fit: Trav<1>
+      if (ctx->tl_total >= (1ull << 28)) ctx->tl_total = 0;  // 32-bit byte offsets do not fit: Trav<1>
       // the NN kernel's LDS frames keep a node id (< 16 * (n_ref + 1)) in 26 bits
       for (size_t r = 0; r < R; ++r)
         if (ctx->pin_rdesc.as<PairDesc>()[r].n_ref > 4000000u) ctx->tl_total = 0;

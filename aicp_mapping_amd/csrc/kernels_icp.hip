@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 
 #include <cstdlib>
@@ -330,25 +331,44 @@ __device__ __forceinline__ float pm_dec(uint32_t c) {
   return c == 0 ? 0.f : __uint_as_float(kPmBase + ((c - 1u) << 21));
 }
 
+#if AICP_NN_POPCHK
+// the NN kernel's one-byte prefix minima, depth-major: lane t of the block at [d * kNNBlock + t]
+// (module scope, addressed from threadIdx.x at each use: the fetch, the descent and the climb
+// all reach it, from the first round on)
+__shared__ uint8_t g_pmb[kPopDepth * kNNBlock];
+__device__ __forceinline__ uint8_t& pmb_at(int d) { return g_pmb[d * kNNBlock + threadIdx.x]; }
+#endif
+
 struct Trav2C {
-  const uint4* tl;       // the pair's treelets
-  const uint2* ptl;      // the pair's treelet links {parent of the root, parent of the parent treelet's root}
+  const uint4* tlb;      // the batch's treelets (uniform: set per chunk)
+  const uint2* ptlb;     // the batch's treelet links {parent of the root, parent of the parent treelet's root}
+  uint32_t tlo;          // the pair's first treelet: one VGPR instead of two 64-bit pointers
   uint32_t pbase;        // the pair's first bucket point
   float q0, q1, q2;
   float noc0, noc1, noc2, rd, minFar;  // noc = -(off * off) per axis (libnabo's off[] enters only so)
   int32_t n, start, sp, pl;  // node ids; pl: parent of the node the last descent ended in
   int32_t dep;               // depth of n (descent) / of the node climbed from (climb)
   uint16_t* pm;              // this lane's prefix-minimum column in LDS (AICP_NN_PREFMIN)
-  uint8_t* pmb;              // this lane's one-byte prefix minima per depth in LDS (AICP_NN_POPCHK)
   uint32_t lb0, lcnt;        // bucket of the leaf the last descent ended in
   NnLdsFrame* lf;            // this lane's LDS frames (AICP_NN_LDS_FRAMES, stride kNNBlock)
   uint32_t tp, tn;
   Best<1> best;
 
-  __device__ __forceinline__ void bind(const uint4* t, const uint2* b, uint32_t tl_off, uint32_t ref_off) {
-    tl = t + tl_off;
-    ptl = b + tl_off;
+  __device__ __forceinline__ void bind(const uint4*, const uint2*, uint32_t tl_off, uint32_t ref_off) {
+    tlo = tl_off;
     pbase = ref_off;
+  }
+  __device__ __forceinline__ void bind_batch(const uint4* t, const uint2* b) {  // wave-uniform
+    tlb = t;
+    ptlb = b;
+  }
+  // treelet T of the pair / its link: 32-bit byte offsets from the uniform bases (host-checked
+  // to fit), so each address is one VGPR added to an SGPR pair
+  __device__ __forceinline__ const uint4* trec(uint32_t T) const {
+    return reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(tlb) + ((tlo + T) << 4));
+  }
+  __device__ __forceinline__ const uint2* tlink(uint32_t T) const {
+    return reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(ptlb) + ((tlo + T) << 3));
   }
   __device__ __forceinline__ float res_d2() const { return best.v[0]; }
   __device__ __forceinline__ int32_t res_id() const { return best.id[0]; }
@@ -382,7 +402,7 @@ struct Trav2C {
     if (dep < kPmDepth) pm[dep * kNNBlock] = (uint16_t)(__float_as_uint(minFar) >> 16);
     ++dep;
 #elif AICP_NN_POPCHK
-    if (dep < kPopDepth) pmb[dep * kNNBlock] = (uint8_t)pm_enc(minFar);
+    if (dep < kPopDepth) pmb_at(dep) = (uint8_t)pm_enc(minFar);
     ++dep;
 #endif
     return no > 0.f;
@@ -393,7 +413,7 @@ struct Trav2C {
   __device__ __forceinline__ void descend() {
     minFar = __builtin_inff();
     uint32_t T = (uint32_t)n >> 2, s = (uint32_t)n & 3u;
-    uint4 r = ld_rec(tl + T);
+    uint4 r = ld_rec(trec(T));
     uint32_t w = r.x, cd = r.w & 3u;
     if (s == 0 && cd != kLeaf) {
       s = decide(w, cd) ? 2u : 1u;
@@ -408,7 +428,7 @@ struct Trav2C {
       pl = n;
       T = (r.w >> 6) + 2 * (s - 1) + (right ? 1u : 0u);
       n = (int32_t)(T << 2);
-      r = ld_rec(tl + T);
+      r = ld_rec(trec(T));
       w = r.x;
       cd = r.w & 3u;
       if (cd == kLeaf) break;
@@ -552,8 +572,8 @@ struct Trav2C {
       }
       const uint32_t X = (uint32_t)pc >> 2;
       if (!have_px) {
-        uint2 lk = ptl[X];
-        uint4 r = tl[X];
+        uint2 lk = *tlink(X);
+        uint4 r = *trec(X);
         asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w), "+v"(lk.x), "+v"(lk.y));
         if (climb_treelet(fs, r, pc, (int32_t)lk.x, c, pc, maxE2, maxR2)) return false;
         px = (int32_t)lk.y;
@@ -563,9 +583,9 @@ struct Trav2C {
       // pc in treelet X, px = parent of X's root in treelet Y (px < 0: X is the root treelet)
       // three independent loads, one wait
       const uint32_t Y = (uint32_t)max(px, 0) >> 2;
-      uint2 ly = ptl[Y];
-      uint4 rx = tl[X];
-      uint4 ry = tl[Y];
+      uint2 ly = *tlink(Y);
+      uint4 rx = *trec(X);
+      uint4 ry = *trec(Y);
       asm volatile("" : "+v"(rx.x), "+v"(rx.y), "+v"(rx.z), "+v"(rx.w), "+v"(ry.x), "+v"(ry.y), "+v"(ry.z),
                    "+v"(ry.w), "+v"(ly.x), "+v"(ly.y));
       if (climb_treelet(fs, rx, pc, px, c, pc, maxE2, maxR2)) return false;
@@ -618,7 +638,7 @@ struct Trav2C {
 #if AICP_NN_POPCHK
         dep = f.pad;  // depth of P
         if (c != start && dep <= kPopDepth) {
-          const float b = pm_dec(pmb[(dep - 1) * kNNBlock]);
+          const float b = pm_dec(pmb_at(dep - 1));
           if (!(b <= maxR2 && b * maxE2 < best.v[0])) c = start;
         }
 #endif
@@ -627,7 +647,7 @@ struct Trav2C {
       const int32_t p = pc;
       const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
       int32_t rootpp;
-      const uint4 r = ld_rec_up(tl + T, ptl + T, rootpp);
+      const uint4 r = ld_rec_up(trec(T), tlink(T), rootpp);
       const int32_t root = (int32_t)(T << 2);
       if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2, dep - 1)) return false;
       c = p;
@@ -1361,7 +1381,8 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
         }
         pool = base;
         pool_end = min(base + 64u, hi);
-        on_chunk(base);
+        if constexpr (std::is_invocable_v<OnChunk, uint32_t, Eng&>) on_chunk(base, t);  // may set uniform engine state
+        else on_chunk(base);
       }
       const uint32_t rank = (uint32_t)__popcll(needm & ((1ull << lane) - 1ull));
       const uint32_t avail = pool_end - pool;
@@ -1420,15 +1441,9 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       }
       AICP_PF(pf_buck);
 #if AICP_NN_LDS_FRAMES > 0
-      if constexpr (is_coop<Eng>::value && !is_sm<Eng>::value) {
+      if constexpr (is_coop<Eng>::value && !is_sm<Eng>::value) {  // used by the climb only
         __shared__ NnLdsFrame lds_frames[AICP_NN_LDS_FRAMES * kNNBlock];
         t.lf = lds_frames + threadIdx.x;
-      }
-#endif
-#if AICP_NN_POPCHK
-      if constexpr (is_coop<Eng>::value && !is_sm<Eng>::value) {
-        __shared__ uint8_t pmb_lds[kPopDepth * kNNBlock];
-        t.pmb = pmb_lds + threadIdx.x;
       }
 #endif
       if (has && t.climb(fs, maxE2, maxR2)) {
@@ -1793,7 +1808,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
   uint32_t qidx = 0;
   persistent_xcd<Eng>(
       total, ctr, prm.maxE2, prm.maxR2, nodes, bpts,
-      [&](uint32_t base) {
+      [&](uint32_t base, Eng& t) {
+        if constexpr (std::is_same<Eng, Trav2C>::value) t.bind_batch(nodes, ptl);
         int lo = 0, hi = (int)al->n - 1;
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
@@ -2483,9 +2499,9 @@ void nn_prof_dump() {
   unsigned long long h[8];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_nn_prof), sizeof(h)) == hipSuccess) {
     const double tot = (double)(h[0] + h[1] + h[2] + h[3]);
-    fprintf(stderr, "nn_prof: fill %.1f%% descent %.1f%% bucket %.1f%% climb %.1f%% | rounds %llu, mean active lanes %.1f\n",
+    fprintf(stderr, "nn_prof: fill %.1f%% descent %.1f%% bucket %.1f%% climb %.1f%% | rounds %llu, mean active lanes %.1f | cached starts %llu, full %llu\n",
             100.0 * h[0] / tot, 100.0 * h[1] / tot, 100.0 * h[2] / tot, 100.0 * h[3] / tot, h[4],
-            h[4] ? (double)h[5] / h[4] : 0.0);
+            h[4] ? (double)h[5] / h[4] : 0.0, h[6], h[7]);
   }
   unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_nn_prof), z, sizeof(z));
