@@ -294,6 +294,41 @@ def test_batch_deterministic_and_order_independent(ctx, L):
     np.testing.assert_array_equal(Ta[1], Tc[0])
 
 
+def test_concurrent_contexts_identical(ctx, L):
+    """Two contexts on one device driven by two host threads at once (bench.py --lanes): each
+    batch's transforms and touch counts equal a lone run's (no shared device state)."""
+    import threading
+
+    prs = [sy.make_pair(20000, 20000, seed=90 + i) for i in range(4)]
+    pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
+    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+    T0, s0, rc0 = ctx.align_batch(pairs, flags=flags, resolution=RES)
+    assert rc0 == 0
+    ctxs = [L.Context(0), L.Context(0)]
+    batches = [c.upload(pairs) for c in ctxs]
+    out = [None, None]
+
+    def work(i):
+        for _ in range(3):
+            batches[i].run(L.default_config(), RES, flags)
+        out[i] = (batches[i].transforms(), batches[i].stats_dicts())
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for T, st in out:
+        np.testing.assert_array_equal(T, T0)
+        for a, b in zip(st, s0):
+            assert (a["iterations"], a["nn_points_touched"], a["nn_nodes_touched"]) == \
+                   (b["iterations"], b["nn_points_touched"], b["nn_nodes_touched"])
+    for b in batches:
+        b.free()
+    for c in ctxs:
+        c.close()
+
+
 @pytest.mark.parametrize("plan", ["1", "2", "0"])
 def test_planned_tree_build(ctx, L, monkeypatch, plan):
     """The kd-trees are built with a planned number of global levels and no host read-back.
