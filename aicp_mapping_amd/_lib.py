@@ -18,6 +18,7 @@ AICP_ERR_CONVERGENCE = 1
 AICP_ERR_INVALID = 2
 AICP_ERR_HIP = 3
 AICP_ERR_UNSUPPORTED = 4
+AICP_ERR_TRANSFORMATION = 5
 
 AICP_RUN_OVERLAP = 1
 AICP_RUN_ICP = 2
@@ -192,6 +193,11 @@ class ConvergenceError(AicpError):
     """Maps PM::ConvergenceError (uncaught in the reference, app.cpp:210)."""
 
 
+class TransformationError(AicpError):
+    """Maps PM::TransformationError: RigidTransformation::checkParameters rejected a transform
+    applied to the reading (|1 - det R| > 0.001)."""
+
+
 def default_config(**kw) -> IcpConfig:
     c = IcpConfig()
     lib.aicp_hip_default_config(C.byref(c))
@@ -290,6 +296,8 @@ class Context:
     def check(self, rc):
         if rc == AICP_ERR_CONVERGENCE:
             raise ConvergenceError(rc, self.last_error())
+        if rc == AICP_ERR_TRANSFORMATION:
+            raise TransformationError(rc, self.last_error())
         if rc != AICP_OK:
             raise AicpError(rc, self.last_error())
 

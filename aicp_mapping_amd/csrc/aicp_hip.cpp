@@ -112,21 +112,31 @@ struct Maps {  // block maps of one flat grid
 
 // ICP pair groups (1 or 2; AICP_ICP_GROUPS=2 selects two). Two groups measured slower on C2
 // (3480 -> 3390 clouds/s): an NN launch over half the pairs takes 62 % of a full one.
+// (function-local statics: initialised once, thread-safe under concurrent contexts)
 int icp_groups(size_t P) {
-  static int g = -1;
-  if (g < 0) {
+  static const int g = [] {
     const char* e = std::getenv("AICP_ICP_GROUPS");
-    g = (e && std::atoi(e) == 2) ? 2 : 1;
-  }
+    return (e && std::atoi(e) == 2) ? 2 : 1;
+  }();
   return P >= 2 ? g : 1;
 }
 bool icp_serial_nn() {
-  static int v = -1;
-  if (v < 0) {
+  static const bool v = [] {
     const char* e = std::getenv("AICP_ICP_SERIAL_NN");
-    v = (e && std::atoi(e) == 0) ? 0 : 1;
-  }
-  return v == 1;
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+// SurfaceNormalDataPointsFilter builds its own libnabo tree with the default bucket size (8),
+// whatever bucketSize the chain gives the KDTreeMatcher
+constexpr int kNormalsBucket = 8;
+
+// Test-only: AICP_FORCE_TRAV1=1 runs the ICP NN on node records (Trav<1>), the engine used when
+// treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records); read per
+// call so a test can switch it.
+bool force_trav1() {
+  const char* e = std::getenv("AICP_FORCE_TRAV1");
+  return e && e[0] == '1';
 }
 struct IcpGroup {
   int p0 = 0, np = 0;
@@ -169,6 +179,7 @@ struct aicp_hip_ctx {
   uint64_t tl_total = 0;  // matcher treelet records allotted for this batch (0: no treelets, Trav<1>)
   TreeBufs tb[2];  // [0] raw-coordinate tree (stream2), [1] centred matcher tree (stream3)
   PinBuf pin_desc, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
+  PinBuf pin_pf;  // pre-filter read-backs (PfHost): outlive any early return of pf_core
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev[16] = {};
   int last_nn_launches = 0;
@@ -815,6 +826,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       // the NN kernel's LDS frames keep a node id (< 16 * (n_ref + 1)) in 26 bits
       for (size_t r = 0; r < R; ++r)
         if (ctx->pin_rdesc.as<PairDesc>()[r].n_ref > 4000000u) ctx->tl_total = 0;
+      if (force_trav1()) ctx->tl_total = 0;
     }
     HIPC(ensure(ctx->rdesc_raw, R * sizeof(PairDesc)));
     HIPC(hipStreamWaitEvent(s2, ctx->ev[7], 0));
@@ -830,11 +842,11 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     // SurfaceNormal runs on the reference as given, before the centring (ICP::compute,
     // SURVEY A.1 steps 1-2): its own libnabo tree over the raw coordinates first
     rc = device_trees_begin(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(),
-                            B->ref_raw.as<float4>(), 0, cfg->bucket_size, ctx->bpts_raw, ctx->nodes_raw);
+                            B->ref_raw.as<float4>(), 0, kNormalsBucket, ctx->bpts_raw, ctx->nodes_raw);
     if (rc) return join_worker(rc);
     // s2: raw tree levels + subtrees, SurfaceNormal, all enqueued before the host waits for
     // the overlap's key boxes
-    rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), cfg->bucket_size,
+    rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), kNormalsBucket,
                           ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0], true));
     if (rc) return join_worker(rc);
     // the raw tree as treelet records too (the kNN's engine, TravT); errors into its control
@@ -850,7 +862,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       HIPC(ensure(ctx->tlr_rank, ((size_t)cap + 1) * 4));
       HIPC(ensure(ctx->tlr_temp, tbb));
       TreeBufs& T0 = ctx->tb[0];
-      HIPC(launch_treelets(s2, (int)R, cap, ctx->rdesc_raw.as<PairDesc>(), ctx->nodes_raw.as<uint4>(), cfg->bucket_size,
+      HIPC(launch_treelets(s2, (int)R, cap, ctx->rdesc_raw.as<PairDesc>(), ctx->nodes_raw.as<uint4>(), kNormalsBucket,
                            ctx->tlr_flag.as<uint32_t>(), ctx->tlr_rank.as<uint32_t>(), ctx->tlr_temp.p, tbb,
                            ctx->tl_raw.as<uint4>(), ctx->link_raw.as<uint2>(), T0.tw.ctl));
       HIPC(hipMemcpyAsync(T0.pin_ctl.p, T0.tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
@@ -1146,7 +1158,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   for (auto& t : ctx->tb) t.release_all();
   free_batch(ctx->oneshot);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
-                    &ctx->pin_rdesc, &ctx->pin_gdesc, &ctx->pin_gstate})
+                    &ctx->pin_rdesc, &ctx->pin_gdesc, &ctx->pin_gstate, &ctx->pin_pf})
     release(*b);
   for (auto e : ctx->nn_ev) (void)hipEventDestroy(e);
   for (auto e : ctx->ev)
@@ -1188,6 +1200,8 @@ int aicp_hip_batch_run(aicp_hip_ctx* ctx, aicp_hip_batch* batch, const aicp_icp_
   return run_batch(ctx, batch, cfg, resolution, flags, out_T, stats, nullptr);
 }
 
+constexpr size_t kOneshotKeepBytes = size_t(1) << 30;
+
 int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
                          double resolution, int flags, float* out_T, aicp_icp_stats* stats) {
   if (!ctx) return AICP_ERR_INVALID;
@@ -1195,9 +1209,15 @@ int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const ai
   // one-shot batches reuse the context's batch buffers (no device allocation per call)
   if (!ctx->oneshot) ctx->oneshot = new aicp_hip_batch();
   aicp_hip_batch* B = ctx->oneshot;
-  const int rc = upload_pairs(ctx, pairs, n_pairs, B);
-  if (rc) return rc;
-  return aicp_hip_batch_run(ctx, B, cfg, resolution, flags, out_T, stats);
+  int rc = upload_pairs(ctx, pairs, n_pairs, B);
+  if (!rc) rc = aicp_hip_batch_run(ctx, B, cfg, resolution, flags, out_T, stats);
+  // the input copies of a very large one-shot batch are not kept for the next call
+  if (B->ref_raw.cap + B->read_raw.cap > kOneshotKeepBytes) {
+    (void)hipStreamSynchronize(ctx->stream);
+    release(B->ref_raw);
+    release(B->read_raw);
+  }
+  return rc;
 }
 
 int aicp_hip_register_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
@@ -1505,6 +1525,14 @@ struct PfRun {  // device results of pf_core
   const uint32_t* inv = nullptr;     // sampled index -> bucket position
   const int32_t* cluster_of = nullptr;
 };
+// host side of pf_core's device-to-host copies, in the context's pinned memory: a copy still in
+// flight when pf_core returns early on an error writes into memory that stays valid
+struct PfHost {
+  PfCtl hc;
+  unsigned long long ht[2];
+  uint32_t tl_err;
+  uint32_t hf[2];
+};
 struct PfLayout {
   PfCtl* ctl;
   float4* pts4;  // the input, n points
@@ -1544,9 +1572,14 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   PfCtl* dctl = Lo.ctl;
   const PfWork& W = Lo.W;
   HIPC(ensure(ctx->ref1, n * 16));
-  PfCtl hc{};
+  HIPC(ensure(ctx->pin_pf, sizeof(PfHost)));
+  HIPC(hipStreamSynchronize(s));  // no copy of an earlier call is still in flight into pin_pf
+  PfHost& H = *ctx->pin_pf.as<PfHost>();
+  PfCtl& hc = H.hc;
+  hc = PfCtl{};
   for (int k = 0; k < 3; ++k) hc.lo[k] = 0xFFFFFFFFu;
   HIPC(hipMemcpyAsync(dctl, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
+  HIPC(hipStreamSynchronize(s));  // hc is reused as the destination of the read-backs below
   HIPC(hipEventRecord(E[0], s));
   HIPC(launch_pf_voxel(s, (uint32_t)n, Lo.pts4, 1.f / prm->leaf_size, dctl, W, ctx->ref1.as<float4>()));
   HIPC(hipEventRecord(E[1], s));
@@ -1629,7 +1662,7 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   // until one changes no label (labels only decrease, so this ends; V passes bound any schedule)
   launch_rg_components(s, V, NB, nbp, em, comp, label);
   constexpr int R = 2;
-  uint32_t hf[R];
+  uint32_t* hf = H.hf;
   for (uint64_t launches = 0;; launches += R) {
     if (launches > (uint64_t)V + 2 * R) FAIL(AICP_ERR_HIP, "region growing did not reach its fixed point");
     HIPC(hipMemsetAsync(flags, 0, R * 4, s));
@@ -1650,10 +1683,10 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
                          cluster_of, dctl));
   HIPC(hipEventRecord(E[5], s));
   HIPC(hipMemcpyAsync(&hc, dctl, sizeof(hc), hipMemcpyDeviceToHost, s));
-  unsigned long long ht[2] = {0, 0};
+  unsigned long long* ht = H.ht;
   HIPC(hipMemcpyAsync(ht, dtouch, 16, hipMemcpyDeviceToHost, s));
-  uint32_t tl_err = 0;
-  HIPC(hipMemcpyAsync(&tl_err, &ctx->tb[0].tw.ctl->error, 4, hipMemcpyDeviceToHost, s));
+  const uint32_t& tl_err = H.tl_err;
+  HIPC(hipMemcpyAsync(&H.tl_err, &ctx->tb[0].tw.ctl->error, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   if (tl_err & 4) FAIL(AICP_ERR_HIP, "pre-filter treelets exceed their allotment");
   aicp_prefilter_stats& ps = ctx->last_pf;
@@ -1807,8 +1840,13 @@ int aicp_hip_map_merge(aicp_hip_ctx* ctx, aicp_hip_map* map, const float* pts, s
   if (need > map->pts.cap) {  // grow with copy (ensure() would drop the content)
     DevBuf nb;
     HIPC(ensure(nb, std::max(need, 2 * map->pts.cap)));
-    if (map->n) HIPC(hipMemcpyAsync(nb.p, map->pts.p, map->n * 16, hipMemcpyDeviceToDevice, s));
-    HIPC(hipStreamSynchronize(s));
+    hipError_t e = map->n ? hipMemcpyAsync(nb.p, map->pts.p, map->n * 16, hipMemcpyDeviceToDevice, s) : hipSuccess;
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {  // the map keeps its old buffer; the new one is released
+      (void)hipStreamSynchronize(s);
+      release(nb);
+      FAIL(AICP_ERR_HIP, std::string("map merge: grow copy: ") + hipGetErrorString(e));
+    }
     release(map->pts);
     map->pts = nb;
   }

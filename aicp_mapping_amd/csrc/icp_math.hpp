@@ -50,6 +50,17 @@ AICP_HD void ident4(float* T) {
   for (int i = 0; i < 16; ++i) T[i] = (i % 5 == 0) ? 1.f : 0.f;
 }
 
+// RigidTransformation::checkParameters (libpointmatcher 1.2.x): the rotation block
+// is accepted when |1 - det R| <= 0.001 (a NaN determinant passes, as the comparison is false).
+// Eigen's 3x3 determinant: cofactor expansion along the first column, float.
+AICP_HD bool rigid_ok(const float* T) {
+  const float d0 = m4(T, 0, 0) * (m4(T, 1, 1) * m4(T, 2, 2) - m4(T, 1, 2) * m4(T, 2, 1));
+  const float d1 = m4(T, 1, 0) * (m4(T, 0, 1) * m4(T, 2, 2) - m4(T, 0, 2) * m4(T, 2, 1));
+  const float d2 = m4(T, 2, 0) * (m4(T, 0, 1) * m4(T, 1, 2) - m4(T, 0, 2) * m4(T, 1, 1));
+  const float det = (d0 - d1) + d2;
+  return !(fabsf(1.f - det) > 0.001f);
+}
+
 // ΔT from the solution x = (rotation vector, translation), Eigen::AngleAxis semantics.
 AICP_HD void delta_transform(const float* x, float* T) {
   const float sq = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];

@@ -57,7 +57,7 @@ void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const Pair
                        const uint32_t* touched, const float4* bpts, const float4* bnrm, double* slab);
 void launch_icp_update(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
                        const double* slab, const IcpParams& prm);
-void launch_finalize(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
+void launch_finalize(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st,
                      float* outT);
 
 // AICP_NN_PROF builds: print and reset the NN kernel's per-phase cycle shares (stderr)

@@ -2229,7 +2229,15 @@ __global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__
   delta_transform(x, dT);
   mul4(dT, s.T, s.T);
   s.inlier_ratio = (float)((double)(float)kept / (double)d.n_read);
-  // checkers (YAML order): Counter, then Differential
+  // checkers (YAML order): Counter, then Differential. The new T_iter is applied to the reading
+  // at the start of the next iteration (or, inside the final T, to the output reading), where
+  // RigidTransformation::checkParameters throws TransformationError on |1 - det R| > 0.001.
+  if (!rigid_ok(s.T)) {
+    s.iters += 1;
+    s.status = 5;
+    s.active = 0;
+    return;
+  }
   bool iterate = true;
   s.iters += 1;
   if (s.iters >= prm.max_iter) iterate = false;
@@ -2264,13 +2272,15 @@ __global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__
 }
 
 __global__ void k_finalize(int n_pairs, const PairDesc* __restrict__ pd,
-                           const PairState* __restrict__ st, float* __restrict__ outT) {
+                           PairState* __restrict__ st, float* __restrict__ outT) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
   float tmp[16], T[16];
   mul4(pd[p].Tmean, st[p].T, tmp);
   mul4(tmp, pd[p].Tinit, T);
   for (int i = 0; i < 16; ++i) outT[p * 16 + i] = T[i];
+  // registerClouds applies T to the output reading (pointmatcher_registration.cpp:128-129)
+  if (st[p].status == 0 && !rigid_ok(T)) st[p].status = 5;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2526,7 +2536,7 @@ void launch_icp_update(hipStream_t s, int n_pairs, const PairDesc* pd, PairState
                        const IcpParams& prm) {
   k_icp_update<<<n_pairs, 256, 0, s>>>(pd, st, slab, prm);
 }
-void launch_finalize(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st, float* outT) {
+void launch_finalize(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, float* outT) {
   k_finalize<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, outT);
 }
 bool launch_knn_generic(hipStream_t s, uint32_t nq, const float4* q, const uint4* nodes, const int32_t* parent,

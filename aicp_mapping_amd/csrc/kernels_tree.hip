@@ -882,6 +882,12 @@ __global__ void k_pairs_degenerate(int n_pairs, const PairDesc* __restrict__ pd,
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
   st[p].degenerate = rst[pd[p].ref_id].degenerate;
+  // ICP::compute applies T_refMean_dataIn to the reading first: RigidTransformation's
+  // checkParameters throws TransformationError for a non-rigid initial transform
+  if (!rigid_ok(pd[p].Tinit)) {
+    st[p].status = 5;
+    st[p].active = 0;
+  }
 }
 
 inline unsigned grid_of(size_t n) { return (unsigned)((n + 255) / 256); }

@@ -24,11 +24,14 @@ def _ctx(ctx):
 
 
 def _cluster_rgb(c: int) -> float:
-    """Colour of cluster c as PCL's packed-float rgb. The reference draws random colours
-    (srand(time(NULL)), filteringUtils.cpp:89-96); a fixed hash of the cluster index here."""
+    """Colour of cluster c as the reference stores it: ``points[idx].rgb = rgb`` with an int32
+    ``rgb = (r << 16) | (g << 8) | b`` (filteringUtils.cpp:92-100) is a numeric int -> float
+    conversion of the float field, not a bit-packed colour, and so it is here. The reference draws
+    r, g, b at random (srand(time(NULL)), :89); a fixed hash of the cluster index here, so runs
+    are repeatable."""
     h = (c * 2654435761 + 12345) & 0xFFFFFFFF
-    rgb = np.uint32(((h >> 8) & 0xFF) << 16 | ((h >> 16) & 0xFF) << 8 | ((h >> 24) & 0xFF))
-    return float(rgb.view(np.float32))
+    rgb = ((h >> 8) & 0xFF) << 16 | ((h >> 16) & 0xFF) << 8 | ((h >> 24) & 0xFF)
+    return float(np.float32(rgb))
 
 
 def regionGrowingUniformPlaneSegmentationFilter(cloud_in, *args, ctx=None, params=None):
@@ -42,7 +45,7 @@ def regionGrowingUniformPlaneSegmentationFilter(cloud_in, *args, ctx=None, param
       view_point a 4x4 pose, clusters a list to fill like ``std::vector<pcl::PointIndices>&``):
       returns the sampled cloud as (V, 12) PointXYZRGBNormal rows {x, y, z, 1, nx, ny, nz, 0,
       rgb, curvature, 0, 0}; normals face view_point.translation(); each kept cluster's points
-      carry one colour.
+      carry one colour (rgb = float(int32 colour), the reference's numeric conversion).
 
     cloud_in: (N, 3|4|8|12) float32 rows. ctx: an aicp Context (default: one on device 0)."""
     if len(args) > 2:
@@ -51,7 +54,8 @@ def regionGrowingUniformPlaneSegmentationFilter(cloud_in, *args, ctx=None, param
     if len(args) == 2:
         view_point, clusters = args
         T = np.asarray(view_point, np.float64).reshape(4, 4)
-        prm = params or _lib.default_prefilter()
+        # a copy: the caller's params keep their own viewpoint (the first overload's is (0,0,0))
+        prm = _lib.PrefilterParams.from_buffer_copy(params) if params is not None else _lib.default_prefilter()
         for i in range(3):
             prm.viewpoint[i] = float(np.float32(T[i, 3]))
         r = c.prefilter(cloud_in, prm, details=True)

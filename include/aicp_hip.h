@@ -43,6 +43,9 @@ extern "C" {
                                    pointmatcher_registration.cpp:60-64,96-100) */
 #define AICP_ERR_HIP 3          /* HIP runtime failure or extension unavailable */
 #define AICP_ERR_UNSUPPORTED 4  /* chain element or size not supported by this core */
+#define AICP_ERR_TRANSFORMATION 5 /* maps PM::TransformationError: a transform applied to the
+                                     reading has |1 - det R| > 0.001 (RigidTransformation::
+                                     checkParameters; the initial T, every T_iter, the final T) */
 
 typedef struct aicp_hip_ctx aicp_hip_ctx;
 typedef struct aicp_hip_batch aicp_hip_batch;

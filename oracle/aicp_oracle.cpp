@@ -713,6 +713,18 @@ void ident4(float* T) {
   for (int i = 0; i < 16; ++i) T[i] = (i % 5 == 0) ? 1.f : 0.f;
 }
 
+// RigidTransformation::checkParameters: false when |1 - det(R)| > 0.001, R the
+// top-left 3x3 block, det by Eigen's first-column cofactor expansion (float). Called by every
+// transformations.apply: T_refMean_dataIn, each T_iter applied at the start of an iteration,
+// and the final T applied to the output reading (pointmatcher_registration.cpp:128-129).
+bool rigid_params_ok(const float* T) {
+  const float a = M4(T, 0, 0) * (M4(T, 1, 1) * M4(T, 2, 2) - M4(T, 1, 2) * M4(T, 2, 1));
+  const float b = M4(T, 1, 0) * (M4(T, 0, 1) * M4(T, 2, 2) - M4(T, 0, 2) * M4(T, 2, 1));
+  const float c = M4(T, 2, 0) * (M4(T, 0, 1) * M4(T, 1, 2) - M4(T, 0, 2) * M4(T, 1, 1));
+  const float det = (a - b) + c;
+  return !(std::fabs(1.f - det) > 0.001f);
+}
+
 // Eigen::AngleAxis<float>(x.head(3).norm(), x.head(3).normalized()).toRotationMatrix()
 // with translation x.segment(3,3); sin/cos evaluated in double and rounded to float.
 void delta_transform(const float* x, float* T) {
@@ -1090,6 +1102,7 @@ int ao_icp(const float* ref, int64_t m, int64_t rs, const float* read, int64_t n
   else
     ident4(Tinit);
   mul4(TmeanInv, Tinit, TrmDin);
+  if (!rigid_params_ok(TrmDin)) return st->status = 5;  // TransformationError
   std::vector<float> rd((size_t)n * 3);
   for (int64_t i = 0; i < n; ++i) {
     const float p[3] = {read[i * ds + 0], read[i * ds + 1], read[i * ds + 2]};
@@ -1121,6 +1134,7 @@ int ao_icp(const float* ref, int64_t m, int64_t rs, const float* read, int64_t n
   int iter = 0;
   bool iterate = true;
   while (iterate) {
+    if (!rigid_params_ok(Titer)) return st->status = 5;  // TransformationError
     for (int64_t i = 0; i < n; ++i) apply4(Titer, &rd[3 * i], &step[3 * i]);
     for (int64_t i = 0; i < n; ++i) {
       s.q = &step[3 * i];
@@ -1211,6 +1225,8 @@ int ao_icp(const float* ref, int64_t m, int64_t rs, const float* read, int64_t n
   float tmp[16];
   mul4(Tmean, Titer, tmp);
   mul4(tmp, TrmDin, T_out);
+  // registerClouds applies the final T to the reading (pointmatcher_registration.cpp:128-129)
+  if (!rigid_params_ok(T_out)) return st->status = 5;
   return st->status = 0;
 }
 

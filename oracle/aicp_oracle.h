@@ -42,7 +42,8 @@ typedef struct {
 
 #define AO_TRACE_MAX 64
 typedef struct {
-  int32_t status;             /* 0 ok, 1 convergence error, 2 invalid               */
+  int32_t status;             /* 0 ok, 1 convergence error, 2 invalid,
+                                 5 TransformationError (|1 - det R| > 0.001)      */
   int32_t iterations;
   int32_t converged;          /* differential checker fired                          */
   int32_t degenerate_normals;

@@ -194,6 +194,49 @@ def test_icp_matches_oracle(ctx, oracle, seed, n, ratio):
     assert rg < 2e-3 and tg < 2e-2
 
 
+@pytest.mark.parametrize("bucket,force", [(16, "0"), (8, "1"), (3, "0")])
+def test_node_record_engine_matches_oracle(ctx, oracle, L, monkeypatch, bucket, force):
+    """The NN engine over node records (Trav<1>) serves chains with KDTreeMatcher bucketSize
+    above 15 (treelet leaf slots hold 4-bit counts), references above 4 M points and batches
+    past 2^28 treelet records; AICP_FORCE_TRAV1=1 selects it on a normal cloud. Both paths give
+    the oracle's transform, iteration count and libnabo touch counts; SurfaceNormal keeps its own
+    bucket-8 tree whatever the matcher's bucketSize."""
+    pr = sy.make_pair(20000, 20000, seed=61)
+    monkeypatch.setenv("AICP_FORCE_TRAV1", force)
+    cfg = L.default_config(trimmed_ratio=0.6, bucket_size=bucket)
+    T, st, rc = ctx.align_batch([dict(ref=pr.ref, read=pr.read)], cfg, flags=L.AICP_RUN_ICP)
+    monkeypatch.delenv("AICP_FORCE_TRAV1")
+    rc1, T1, st1 = oracle.icp(pr.ref, pr.read, oracle.default_config(trimmed_ratio=0.6, bucket_size=bucket))
+    assert rc == 0 and rc1 == 0
+    r, t = sy.rot_err(T1, T[0])
+    assert r < 1e-6 and t < 1e-5, (r, t)
+    assert st[0]["iterations"] == st1.iterations
+    assert (st[0]["nn_points_touched"], st[0]["nn_nodes_touched"]) == (st1.nn_points_touched, st1.nn_nodes_touched)
+    assert st[0]["degenerate_normals"] == st1.degenerate_normals
+
+
+def test_transformation_error_non_rigid_init(ctx, oracle, L):
+    """A non-rigid initial transform: ICP::compute applies T_refMean_dataIn to the reading and
+    RigidTransformation::checkParameters throws TransformationError (|1 - det R| > 0.001); the
+    device reports AICP_ERR_TRANSFORMATION like the oracle's status 5, and the context keeps
+    working."""
+    pr = sy.make_pair(5000, 5000, seed=62)
+    T0 = np.eye(4)
+    T0[:3, :3] *= 1.01  # det 1.0303
+    _, st, rc = ctx.align_batch([dict(ref=pr.ref, read=pr.read, init_T=T0)], L.default_config(trimmed_ratio=0.6),
+                                flags=L.AICP_RUN_ICP, raise_on_error=False)
+    rc1, _, _ = oracle.icp(pr.ref, pr.read, oracle.default_config(trimmed_ratio=0.6), T0=T0)
+    assert rc == L.AICP_ERR_TRANSFORMATION and st[0]["status"] == L.AICP_ERR_TRANSFORMATION and rc1 == 5
+    with pytest.raises(L.TransformationError):
+        ctx.align_batch([dict(ref=pr.ref, read=pr.read, init_T=T0)], L.default_config(trimmed_ratio=0.6),
+                        flags=L.AICP_RUN_ICP)
+    T0[:3, :3] = np.eye(3) * 0.99985  # det 0.99955: within the 0.001 tolerance, accepted
+    _, st, rc = ctx.align_batch([dict(ref=pr.ref, read=pr.read, init_T=T0)], L.default_config(trimmed_ratio=0.6),
+                                flags=L.AICP_RUN_ICP, raise_on_error=False)
+    rc1, _, _ = oracle.icp(pr.ref, pr.read, oracle.default_config(trimmed_ratio=0.6), T0=T0)
+    assert rc == 0 and rc1 == 0
+
+
 def test_icp_initial_transform(ctx, oracle):
     pr = sy.make_pair(10000, 10000, seed=11)
     T0 = sy.make_T(yaw_deg=1.5, pitch_deg=0.0, roll_deg=0.0, t=(0.1, -0.05, 0.0))
