@@ -34,6 +34,7 @@ EXPORTS = [
     "aicp_hip_dists_quantile", "aicp_hip_solve6", "aicp_hip_default_prefilter", "aicp_hip_prefilter",
     "aicp_hip_last_prefilter_stats", "aicp_hip_map_create", "aicp_hip_map_free", "aicp_hip_map_size",
     "aicp_hip_map_download", "aicp_hip_map_crop", "aicp_hip_map_merge", "aicp_hip_map_prefilter",
+    "aicp_hip_default_sequence_params", "aicp_hip_sequence_run", "aicp_hip_last_sequence_timing",
 ]
 
 
@@ -116,6 +117,50 @@ class PrefilterStats(C.Structure):
     ]
 
 
+class Cloud(C.Structure):
+    _fields_ = [
+        ("pts", C.POINTER(C.c_float)),
+        ("n", C.c_uint64),
+        ("stride", C.c_uint64),
+        ("origin", C.c_double * 3),
+    ]
+
+
+class SequenceParams(C.Structure):
+    _fields_ = [
+        ("reference_update_frequency", C.c_int32),
+        ("max_correction_magnitude", C.c_float),
+        ("resolution", C.c_double),
+        ("flags", C.c_int32),
+    ]
+
+
+class SequenceResult(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("accepted", C.c_int32),
+        ("reference", C.c_int32),
+        ("is_reference", C.c_int32),
+        ("corrected_origin", C.c_double * 3),
+        ("icp", IcpStats),
+    ]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k in ("status", "accepted", "reference", "is_reference")}
+        d["corrected_origin"] = [float(x) for x in self.corrected_origin]
+        d["icp"] = self.icp.as_dict()
+        return d
+
+
+class SequenceTiming(C.Structure):
+    _fields_ = [
+        ("windows", C.c_int32),
+        ("replans", C.c_int32),
+        ("wall_ms", C.c_double),
+        ("device_ms", C.c_double),
+    ]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
@@ -177,6 +222,11 @@ def _load():
     L.aicp_hip_map_crop.argtypes = [vp, vp, C.c_float, C.c_float, fp, fp, sz, szp]
     L.aicp_hip_map_merge.argtypes = [vp, vp, fp, sz, sz, fp]
     L.aicp_hip_map_prefilter.argtypes = [vp, vp, C.POINTER(PrefilterParams)]
+    L.aicp_hip_default_sequence_params.argtypes = [C.POINTER(SequenceParams)]
+    L.aicp_hip_default_sequence_params.restype = None
+    L.aicp_hip_sequence_run.argtypes = [vp, cfgp, C.POINTER(SequenceParams), C.POINTER(Cloud), C.POINTER(Cloud), sz,
+                                        fp, C.POINTER(SequenceResult), C.POINTER(C.c_size_t)]
+    L.aicp_hip_last_sequence_timing.argtypes = [vp, C.POINTER(SequenceTiming)]
     return L
 
 
@@ -258,6 +308,28 @@ def make_pair(ref, read, ref_origin=(0, 0, 0), read_origin=(0, 0, 0), init_T=Non
     return p, keep
 
 
+def default_sequence_params(**kw) -> SequenceParams:
+    """App's stream settings (aicp_hip_default_sequence_params): reference every 5 accepted
+    readings, max_correction_magnitude 1.0, octomap 0.2 m, per-reading overlap auto-tune."""
+    p = SequenceParams()
+    lib.aicp_hip_default_sequence_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def make_cloud(pts, origin=(0, 0, 0)):
+    """Returns (Cloud, keepalive) for (N, 3|4|8|12) float32 rows."""
+    a = as_points(pts)
+    c = Cloud()
+    c.pts = _fptr(a)
+    c.n = a.shape[0]
+    c.stride = a.shape[1] * 4
+    for k in range(3):
+        c.origin[k] = float(origin[k])
+    return c, a
+
+
 def default_prefilter(**kw) -> PrefilterParams:
     """filteringUtils.cpp:12,22,27-34 (aicp_hip_default_prefilter); keyword overrides."""
     p = PrefilterParams()
@@ -324,6 +396,36 @@ class Context:
 
     def upload(self, pairs):
         return ResidentBatch(self, pairs)
+
+    def sequence_run(self, first, first_origin, readings, origins, cfg=None, params=None, raise_on_error=True):
+        """App's frame-to-reference stream (aicp_hip_sequence_run): the first cloud is the
+        reference, readings[i] (prior-pose origin origins[i]) are registered in order with the
+        windowed reference update and the max-correction drop. Returns (T[n, 4, 4] row-major
+        corrections, list of result dicts, n_done, rc)."""
+        cfg = cfg or default_config()
+        prm = params or default_sequence_params()
+        n = len(readings)
+        fc, keep0 = make_cloud(first, first_origin)
+        arr = (Cloud * max(n, 1))()
+        keep = [keep0]
+        for i, r in enumerate(readings):
+            c, k = make_cloud(r, origins[i])
+            arr[i] = c
+            keep.append(k)
+        outT = np.zeros((max(n, 1), 16), np.float32)
+        res = (SequenceResult * max(n, 1))()
+        done = C.c_size_t(0)
+        rc = lib.aicp_hip_sequence_run(self.h, C.byref(cfg), C.byref(prm), C.byref(fc), arr, n, _fptr(outT), res,
+                                       C.byref(done))
+        if raise_on_error and rc != AICP_OK:
+            self.check(rc)
+        T = outT[:n].reshape(-1, 4, 4).transpose(0, 2, 1).copy()
+        return T, [res[i].as_dict() for i in range(done.value)], done.value, rc
+
+    def last_sequence_timing(self):
+        t = SequenceTiming()
+        self.check(lib.aicp_hip_last_sequence_timing(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in SequenceTiming._fields_}
 
     def last_nn_timing(self):
         n = C.c_int()

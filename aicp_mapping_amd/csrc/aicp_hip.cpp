@@ -28,90 +28,13 @@
 #include "aicp_common.hpp"
 #include "icp_math.hpp"
 #include "kernels.hpp"
+#include "runtime.hpp"
 
 using namespace aicp;
+using namespace aicp::rt;
 
 namespace {
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  template <class T>
-  T* as() const {
-    return reinterpret_cast<T*>(p);
-  }
-};
-
-struct PinBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  template <class T>
-  T* as() const {
-    return reinterpret_cast<T*>(p);
-  }
-};
-
-hipError_t ensure(DevBuf& b, size_t bytes) {
-  if (bytes <= b.cap && b.p) return hipSuccess;
-  if (b.p) (void)hipFree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-  const size_t nb = std::max<size_t>(256, bytes + bytes / 4);
-  const hipError_t e = hipMalloc(&b.p, nb);
-  if (e == hipSuccess) b.cap = nb;
-  return e;
-}
-hipError_t ensure(PinBuf& b, size_t bytes) {
-  if (bytes <= b.cap && b.p) return hipSuccess;
-  if (b.p) (void)hipHostFree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-  const size_t nb = std::max<size_t>(256, bytes + bytes / 4);
-  const hipError_t e = hipHostMalloc(&b.p, nb, hipHostMallocDefault);
-  if (e == hipSuccess) b.cap = nb;
-  return e;
-}
-void release(DevBuf& b) {
-  if (b.p) (void)hipFree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-}
-void release(PinBuf& b) {
-  if (b.p) (void)hipHostFree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-}
-
-// Work space of one kd-tree construction (kernels_tree.hip). Two sets: the raw-coordinate
-// tree (SurfaceNormal) and the centred matcher tree are built concurrently on two streams.
-struct TreeBufs {
-  DevBuf W0, W1, segof0, segof1, seg0, seg1, flag, X1, X2, posL, posR, ev, valid, subs, ecnt, sums, pdepth, ctl,
-      scan;
-  PinBuf pin_ctl;
-  TreeWork tw{};    // device_trees_begin -> device_trees_end
-  int planned = 0;  // global levels enqueued without host polling (0: polled build)
-  int needed = 0;   // global levels the last planned build actually used
-  void release_all() {
-    for (DevBuf* b : {&W0, &W1, &segof0, &segof1, &seg0, &seg1, &flag, &X1, &X2, &posL, &posR, &ev, &valid, &subs,
-                      &ecnt, &sums, &pdepth, &ctl, &scan})
-      release(*b);
-    release(pin_ctl);
-  }
-};
-
-struct Maps {  // block maps of one flat grid
-  std::vector<int32_t> pair;
-  std::vector<uint32_t> start;
-  void add(int p, uint32_t n, uint32_t per_block) {
-    for (uint32_t s = 0; s < n; s += per_block) {
-      pair.push_back(p);
-      start.push_back(s);
-    }
-  }
-};
-
-// ICP pair groups (1 or 2; AICP_ICP_GROUPS=2 selects two). Two groups measured slower on C2
-// (3480 -> 3390 clouds/s): an NN launch over half the pairs takes 62 % of a full one.
 // (function-local statics: initialised once, thread-safe under concurrent contexts)
 int icp_groups(size_t P) {
   static const int g = [] {
@@ -127,17 +50,6 @@ bool icp_serial_nn() {
   }();
   return v;
 }
-// SurfaceNormalDataPointsFilter builds its own libnabo tree with the default bucket size (8),
-// whatever bucketSize the chain gives the KDTreeMatcher
-constexpr int kNormalsBucket = 8;
-
-// Test-only: AICP_FORCE_TRAV1=1 runs the ICP NN on node records (Trav<1>), the engine used when
-// treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records); read per
-// call so a test can switch it.
-bool force_trav1() {
-  const char* e = std::getenv("AICP_FORCE_TRAV1");
-  return e && e[0] == '1';
-}
 struct IcpGroup {
   int p0 = 0, np = 0;
   uint32_t reads = 0;
@@ -150,63 +62,16 @@ struct IcpGroup {
 
 }  // namespace
 
-struct aicp_hip_batch {
-  size_t P = 0;
-  std::vector<PairDesc> desc;
-  std::vector<PairDesc> rdesc;  // one per distinct reference cloud (tree + normals built once)
-  std::vector<PairDesc> gdesc;  // one per overlap group: distinct (reference cloud, origin)
-  uint64_t total_ref = 0, total_read = 0;
-  uint32_t n_red_total = 0;
-  DevBuf ref_raw, read_raw, maps;
-  BlockMap m_read{}, m_gref{}, m_red{}, m_sel{};
-};
+namespace aicp {
+namespace rt {
 
-struct aicp_hip_map {  // a device-resident point cloud (float4, w = 1)
-  DevBuf pts;
-  size_t n = 0;
-};
-
-struct aicp_hip_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // raw kd-tree + normals, concurrent with the overlap on `stream`
-  hipStream_t stream3 = nullptr;  // centroid + matcher kd-tree, concurrent with both
-  std::string err;
-  DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
-      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
-      nrm_raw, inv, gdesc, gstate, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, tl, ptl, tl_flag,
-      tl_rank, tl_temp, pf_a, pf_b, tl_raw, link_raw, tlr_flag, tlr_rank, tlr_temp;
-  uint64_t tl_total = 0;  // matcher treelet records allotted for this batch (0: no treelets, Trav<1>)
-  TreeBufs tb[2];  // [0] raw-coordinate tree (stream2), [1] centred matcher tree (stream3)
-  PinBuf pin_desc, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
-  PinBuf pin_pf;  // pre-filter read-backs (PfHost): outlive any early return of pf_core
-  std::vector<hipEvent_t> nn_ev;
-  hipEvent_t ev[16] = {};
-  int last_nn_launches = 0;
-  double last_nn_ms = 0, last_nn_bytes = 0;
-  uint64_t last_queries = 0;
-  double last_phase[5] = {0, 0, 0, 0, 0};
-  aicp_prefilter_stats last_pf{};  // timing and kNN counts of the last pre-filter
-  aicp_hip_batch* oneshot = nullptr;  // buffers of aicp_hip_align_batch, kept across calls
-  hipEvent_t pf_ev[8] = {};
-};
-
-#define HIPC(x)                                                                   \
-  do {                                                                            \
-    const hipError_t e_ = (x);                                                    \
-    if (e_ != hipSuccess) {                                                       \
-      ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);                  \
-      return AICP_ERR_HIP;                                                        \
-    }                                                                             \
-  } while (0)
-
-#define FAIL(code, msg)   \
-  do {                    \
-    ctx->err = (msg);     \
-    return (code);        \
-  } while (0)
-
-namespace {
+// Test-only: AICP_FORCE_TRAV1=1 runs the ICP NN on node records (Trav<1>), the engine used when
+// treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records); read per
+// call so a test can switch it.
+bool force_trav1() {
+  const char* e = std::getenv("AICP_FORCE_TRAV1");
+  return e && e[0] == '1';
+}
 
 bool valid_pair(const aicp_pair& p) {
   if (!p.ref || !p.read || p.n_ref < 1 || p.n_read < 1) return false;
@@ -226,12 +91,6 @@ void pack_xyz(const float* src, uint64_t n, uint64_t stride_bytes, float* dst3) 
 }
 // Strided xyz -> float4 for many clouds at once, split into equal point ranges over host
 // threads (the packing, not the DMA, bounded the host-buffer path: one thread moves ~5 GB/s)
-struct PackSeg {
-  const float* src;
-  uint64_t n, stride;
-  float* dst4;
-};
-void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4);
 void pack_many(const std::vector<PackSeg>& segs) {
   uint64_t total = 0;
   for (const PackSeg& g : segs) total += g.n;
@@ -416,21 +275,6 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   return AICP_OK;
 }
 
-// Tree builders report errors into `err` (they also run on a worker thread, see run_batch).
-#define TCHK(x)                                                                   \
-  do {                                                                            \
-    const hipError_t e_ = (x);                                                    \
-    if (e_ != hipSuccess) {                                                       \
-      err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
-      return AICP_ERR_HIP;                                                        \
-    }                                                                             \
-  } while (0)
-#define TFAIL(code, msg) \
-  do {                   \
-    err = (msg);         \
-    return (code);       \
-  } while (0)
-
 // Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device: raw[ΣM] float4,
 // dDesc with ref_off / n_ref / Tin. Writes bpts_out (bucket order, w = local id), nodes_out
 // and the desc fields mean, Tmean, Tinit, node_off, n_nodes, tree_depth.
@@ -496,11 +340,11 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
 // the host polls the next level's segment count from level 4 on (fallback when a planned
 // build turned out too shallow).
 int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan) {
+                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst) {
   const size_t n = (size_t)total;
   const TreeWork& w = T.tw;
   float4* bpts = bpts_out.as<float4>();
-  TreeCtl* hctl = T.pin_ctl.as<TreeCtl>();
+  TreeCtl* hctl = ctl_dst ? ctl_dst : T.pin_ctl.as<TreeCtl>();
   T.planned = 0;
   if (plan > 0) {
     plan = std::min(plan, kFarStack - 2);
@@ -535,8 +379,10 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
 // back asynchronously at the end of the build). Segments left above kSubMax points at the last
 // planned level were finished by the subtree kernel's global path, so the tree is complete.
 int device_trees_check(TreeBufs& T, std::string& err) {
+  return device_trees_check_ctl(T, T.pin_ctl.as<TreeCtl>(), err);
+}
+int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err) {
   if (!T.planned) return AICP_OK;
-  const TreeCtl* hctl = T.pin_ctl.as<TreeCtl>();
   int used = 0;
   while (used < kFarStack + 1 && hctl->nseg[used]) ++used;
   // oversized segments at the last planned level: plan deeper next time
@@ -553,7 +399,7 @@ int device_trees_check(TreeBufs& T, std::string& err) {
 // left: C2 with 8 instead of 11 levels, +2 %).
 // AICP_TREE_PLAN=k forces k levels (tests: a too-shallow plan); AICP_TREE_PLAN=0 selects the
 // host-polled build (A/B measurements).
-int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean = false) {
+int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean) {
   if (const char* e = std::getenv("AICP_TREE_PLAN")) {
     const int v = std::atoi(e);
     return v > 0 ? std::min(kFarStack - 2, v) : 0;
@@ -1110,7 +956,8 @@ int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, Pa
   return AICP_OK;
 }
 
-}  // namespace
+}  // namespace rt
+}  // namespace aicp
 
 extern "C" {
 
@@ -1157,6 +1004,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
   free_batch(ctx->oneshot);
+  seq_state_free(ctx->seq);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
                     &ctx->pin_rdesc, &ctx->pin_gdesc, &ctx->pin_gstate, &ctx->pin_pf})
     release(*b);

@@ -469,6 +469,54 @@ AICP_HD bool normal_from_cov(const double* C, float* nrm) {
   return true;
 }
 
+// Translation of the corrected pose of an accepted reading: correction_iso * prior_pose
+// (AlignedCloud::updateCloud, aligned_cloud.cpp:61-70; removePitchRollCorrection keeps the
+// translation), with correction_iso = fromMatrix4fToIsometry3d(T) (common.cpp:4-23):
+// Eigen::Quaternionf of T's rotation block (float, Eigen's trace / largest-diagonal branches),
+// cast to double, Quaterniond::toRotationMatrix, translation = float T(0..2, 3) as double.
+// Only the prior pose's translation o enters: R_q * o + t, row sums left to right, no FMA.
+// The float square root is the correctly rounded one ((float)sqrt(double), exact for floats).
+AICP_HD void corrected_origin(const float* T, const double* o, double* out) {
+  float m[3][3];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) m[r][c] = T[c * 4 + r];
+  float q[4];  // x, y, z, w
+  float t = (m[0][0] + m[1][1]) + m[2][2];
+  if (t > 0.f) {
+    t = (float)sqrt((double)(t + 1.f));
+    q[3] = 0.5f * t;
+    t = 0.5f / t;
+    q[0] = (m[2][1] - m[1][2]) * t;
+    q[1] = (m[0][2] - m[2][0]) * t;
+    q[2] = (m[1][0] - m[0][1]) * t;
+  } else {
+    int i = 0;
+    if (m[1][1] > m[0][0]) i = 1;
+    if (m[2][2] > m[i][i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = (float)sqrt((double)(((m[i][i] - m[j][j]) - m[k][k]) + 1.f));
+    q[i] = 0.5f * t;
+    t = 0.5f / t;
+    q[3] = (m[k][j] - m[j][k]) * t;
+    q[j] = (m[j][i] + m[i][j]) * t;
+    q[k] = (m[k][i] + m[i][k]) * t;
+  }
+  const double x = q[0], y = q[1], z = q[2], w = q[3];
+  const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w;
+  const double txx = tx * x, txy = ty * x, txz = tz * x;
+  const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  const double R[3][3] = {{1.0 - (tyy + tzz), txy - twz, txz + twy},
+                          {txy + twz, 1.0 - (txx + tzz), tyz - twx},
+                          {txz - twy, tyz + twx, 1.0 - (txx + tyy)}};
+  for (int r = 0; r < 3; ++r) out[r] = ((R[r][0] * o[0] + R[r][1] * o[1]) + R[r][2] * o[2]) + (double)T[12 + r];
+}
+
+// App::processCloud's drop test (app.cpp:366-373): any |T(i,3)| > max_correction_magnitude
+AICP_HD bool correction_rejected(const float* T, float max_corr) {
+  return fabsf(T[12]) > max_corr || fabsf(T[13]) > max_corr || fabsf(T[14]) > max_corr;
+}
+
 // replaceRatioConfigFile text round trip for r in [0.1, 1): "%g" keeps 6 significant digits
 // = 1e-6 resolution; m = rint(r * 1e6) is exact in double and float(m / 1e6) is the
 // correctly rounded parse (no double-rounding hazard: m/1e6 is never within 2^-54 of a

@@ -140,8 +140,20 @@ void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDes
 // |A| per group (gst.ovl_counts[0]), |B| and |A∩B| per pair (st.ovl_counts[1], [2])
 void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
                       const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps);
+// the parts of launch_ovl_count: |S| of n maps into st[i].ovl_counts[slot]; |A∩B| per pair
+void launch_ovl_popcount(hipStream_t s, int n, const OvlDesc* od, PairState* st, int slot, const uint8_t* maps);
+void launch_ovl_intersect(hipStream_t s, int n_pairs, const PairDesc* pd, const OvlDesc* od_read, const OvlDesc* od_ref,
+                          PairState* st, const uint8_t* maps);
 void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
                        int set_ratio);
+
+// ---- frame-to-reference stream (kernels_sequence.hip) ---------------------------------------
+// gd->ref_origin = translation of fromMatrix4fToIsometry3d(T) * prior pose of src (1 thread)
+void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T);
+// od[i] (min, dim, bytes) from st[i].ovl_bbox; od[i].off preset; bytes > cap[i]: ovl_err, empty map
+void launch_ovl_size(hipStream_t s, int n, PairState* st, OvlDesc* od, const uint64_t* cap);
+// zero the n maps of od[] (device-side sizes, each at most max_bytes)
+void launch_ovl_clear(hipStream_t s, int n, const OvlDesc* od, uint8_t* maps, uint64_t max_bytes);
 
 // ---- pre-filter (kernels_prefilter.hip): regionGrowingUniformPlaneSegmentationFilter -------
 constexpr int kPfMaxNbrs = 16;  // RegionGrowing neighbours per point (edge mask bits)

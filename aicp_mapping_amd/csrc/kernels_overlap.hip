@@ -299,6 +299,13 @@ void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* 
   k_ovl_popcount<<<n_pairs * kCountBlocksPerMap, 256, 0, s>>>(od_read, st, 1, maps);
   k_ovl_intersect<<<n_pairs * kCountBlocksPerMap, 256, 0, s>>>(pd, od_read, od_ref, st, maps);
 }
+void launch_ovl_popcount(hipStream_t s, int n, const OvlDesc* od, PairState* st, int slot, const uint8_t* maps) {
+  if (n) k_ovl_popcount<<<n * kCountBlocksPerMap, 256, 0, s>>>(od, st, slot, maps);
+}
+void launch_ovl_intersect(hipStream_t s, int n_pairs, const PairDesc* pd, const OvlDesc* od_read, const OvlDesc* od_ref,
+                          PairState* st, const uint8_t* maps) {
+  if (n_pairs) k_ovl_intersect<<<n_pairs * kCountBlocksPerMap, 256, 0, s>>>(pd, od_read, od_ref, st, maps);
+}
 void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
                        int set_ratio) {
   k_ovl_finish<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, gst, set_ratio);

@@ -1,0 +1,74 @@
+// kernels_sequence.hip — the device side of App's frame-to-reference stream (sequence.cpp).
+//
+// The next reference is built from the last reading of a window without a host round trip:
+// k_seq_next_ref writes its sensor origin (the corrected pose's translation, app.cpp:375-391)
+// into the overlap group descriptor, k_transform (kernels_icp.hip) writes the corrected cloud,
+// and the voxel maps of the overlap are sized on the device (k_ovl_size) inside a slot whose
+// capacity the host bounds from the source cloud's extent (a rigid motion keeps its diameter).
+#include <hip/hip_runtime.h>
+
+#include "aicp_common.hpp"
+#include "icp_math.hpp"
+#include "kernels.hpp"
+
+namespace aicp {
+
+// gd: the new window's overlap group; src: the reading that becomes the reference; T: its
+// correction (column-major, the finalize output)
+__global__ void k_seq_next_ref(PairDesc* gd, const PairDesc* __restrict__ src, const float* __restrict__ T) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float Tl[16];
+  for (int k = 0; k < 16; ++k) Tl[k] = T[k];
+  double o[3];
+  corrected_origin(Tl, src->read_origin, o);
+  for (int k = 0; k < 3; ++k) gd->ref_origin[k] = o[k];
+}
+
+// one map per entry from the key box in st[i].ovl_bbox (k_ovl_init + k_ovl_bbox), padded by 2
+// voxels below and 2 above like the batch path's host sizing; od[i].off is preset by the host.
+// A box beyond cap[i] bytes is reported (ovl_err) and gets an empty map: every mark and lookup
+// then fails its bounds test, so nothing is stored outside the slot.
+__global__ void k_ovl_size(int n, PairState* st, OvlDesc* od, const uint64_t* __restrict__ cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  OvlDesc& o = od[i];
+  uint64_t vox = 1;
+  for (int k = 0; k < 3; ++k) {
+    int lo = st[i].ovl_bbox[k], hi = st[i].ovl_bbox[3 + k];
+    if (lo > hi) lo = hi = 0;  // nothing inside the key range
+    o.min[k] = lo - 2;
+    o.dim[k] = (hi - lo) + 5;
+    vox *= (uint64_t)o.dim[k];
+  }
+  o.bytes = (vox + 15) / 16 * 16;
+  if (o.bytes > cap[i]) {
+    for (int k = 0; k < 3; ++k) o.dim[k] = 0;
+    o.bytes = 0;
+    st[i].ovl_err = 1;
+  }
+}
+
+// zero the n maps of od[] (sizes known on the device only), 16 B per store
+__global__ __launch_bounds__(256) void k_ovl_clear(int n, const OvlDesc* __restrict__ od, uint8_t* maps) {
+  for (int m = 0; m < n; ++m) {
+    const OvlDesc& o = od[m];
+    uint4* p = (uint4*)(maps + o.off);
+    const uint64_t n16 = o.bytes / 16;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n16; w += (uint64_t)gridDim.x * blockDim.x)
+      p[w] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T) {
+  k_seq_next_ref<<<1, 64, 0, s>>>(gd, src, T);
+}
+void launch_ovl_size(hipStream_t s, int n, PairState* st, OvlDesc* od, const uint64_t* cap) {
+  if (n) k_ovl_size<<<(n + 63) / 64, 64, 0, s>>>(n, st, od, cap);
+}
+void launch_ovl_clear(hipStream_t s, int n, const OvlDesc* od, uint8_t* maps, uint64_t max_bytes) {
+  if (!n || !max_bytes) return;
+  const uint64_t blocks = (max_bytes / 16 + 255) / 256;
+  k_ovl_clear<<<(unsigned)(blocks < 2048 ? (blocks ? blocks : 1) : 2048), 256, 0, s>>>(n, od, maps);
+}
+
+}  // namespace aicp

@@ -1,0 +1,204 @@
+// runtime.hpp — host-side runtime shared by the C-ABI translation units (aicp_hip.cpp, sequence.cpp):
+// device / pinned buffers, kd-tree work space, the context and batch objects, error macros.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/aicp_hip.h"
+#include "aicp_common.hpp"
+#include "kernels.hpp"
+
+namespace aicp {
+namespace rt {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+inline hipError_t ensure(DevBuf& b, size_t bytes) {
+  if (bytes <= b.cap && b.p) return hipSuccess;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  const size_t nb = std::max<size_t>(256, bytes + bytes / 4);
+  const hipError_t e = hipMalloc(&b.p, nb);
+  if (e == hipSuccess) b.cap = nb;
+  return e;
+}
+inline hipError_t ensure(PinBuf& b, size_t bytes) {
+  if (bytes <= b.cap && b.p) return hipSuccess;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  const size_t nb = std::max<size_t>(256, bytes + bytes / 4);
+  const hipError_t e = hipHostMalloc(&b.p, nb, hipHostMallocDefault);
+  if (e == hipSuccess) b.cap = nb;
+  return e;
+}
+inline void release(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+inline void release(PinBuf& b) {
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
+// Work space of one kd-tree construction (kernels_tree.hip). Two sets: the raw-coordinate
+// tree (SurfaceNormal) and the centred matcher tree are built concurrently on two streams.
+struct TreeBufs {
+  DevBuf W0, W1, segof0, segof1, seg0, seg1, flag, X1, X2, posL, posR, ev, valid, subs, ecnt, sums, pdepth, ctl,
+      scan;
+  PinBuf pin_ctl;
+  TreeWork tw{};    // device_trees_begin -> device_trees_end
+  int planned = 0;  // global levels enqueued without host polling (0: polled build)
+  int needed = 0;   // global levels the last planned build actually used
+  void release_all() {
+    for (DevBuf* b : {&W0, &W1, &segof0, &segof1, &seg0, &seg1, &flag, &X1, &X2, &posL, &posR, &ev, &valid, &subs,
+                      &ecnt, &sums, &pdepth, &ctl, &scan})
+      release(*b);
+    release(pin_ctl);
+  }
+};
+
+struct Maps {  // block maps of one flat grid
+  std::vector<int32_t> pair;
+  std::vector<uint32_t> start;
+  void add(int p, uint32_t n, uint32_t per_block) {
+    for (uint32_t s = 0; s < n; s += per_block) {
+      pair.push_back(p);
+      start.push_back(s);
+    }
+  }
+};
+
+// ICP pair groups (1 or 2; AICP_ICP_GROUPS=2 selects two). Two groups measured slower on C2
+// (3480 -> 3390 clouds/s): an NN launch over half the pairs takes 62 % of a full one.
+
+// SurfaceNormalDataPointsFilter builds its own libnabo tree with the default bucket size (8),
+// whatever bucketSize the chain gives the KDTreeMatcher
+constexpr int kNormalsBucket = 8;
+
+struct PackSeg {
+  const float* src;
+  uint64_t n, stride;
+  float* dst4;
+};
+// Strided xyz -> float4 (w = 1) for many clouds at once, split into equal point ranges over
+// up to 16 host threads
+void pack_many(const std::vector<PackSeg>& segs);
+void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4);
+bool valid_pair(const aicp_pair& p);
+double ev_ms(hipEvent_t a, hipEvent_t b);
+bool read_order_enabled();
+bool force_trav1();
+
+// Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device (kernels_tree.hip).
+int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
+                       const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out);
+// plan > 0: `plan` global levels with no host read-back; the control block is copied to
+// ctl_dst (default T.pin_ctl) at the end of the build
+int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
+                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst = nullptr);
+// errors of a planned build whose control block is in hctl (after its stream completed)
+int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err);
+int device_trees_check(TreeBufs& T, std::string& err);
+int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean = false);
+int check_cfg(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, int flags);
+
+struct SeqState;  // sequence.cpp
+void seq_state_free(SeqState* s);
+
+}  // namespace rt
+}  // namespace aicp
+
+struct aicp_hip_batch {
+  size_t P = 0;
+  std::vector<aicp::PairDesc> desc;
+  std::vector<aicp::PairDesc> rdesc;  // one per distinct reference cloud (tree + normals built once)
+  std::vector<aicp::PairDesc> gdesc;  // one per overlap group: distinct (reference cloud, origin)
+  uint64_t total_ref = 0, total_read = 0;
+  uint32_t n_red_total = 0;
+  aicp::rt::DevBuf ref_raw, read_raw, maps;
+  aicp::BlockMap m_read{}, m_gref{}, m_red{}, m_sel{};
+};
+
+struct aicp_hip_map {  // a device-resident point cloud (float4, w = 1)
+  aicp::rt::DevBuf pts;
+  size_t n = 0;
+};
+
+struct aicp_hip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // raw kd-tree + normals, concurrent with the overlap on `stream`
+  hipStream_t stream3 = nullptr;  // centroid + matcher kd-tree, concurrent with both
+  std::string err;
+  aicp::rt::DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
+      ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
+      nrm_raw, inv, gdesc, gstate, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, tl, ptl, tl_flag,
+      tl_rank, tl_temp, pf_a, pf_b, tl_raw, link_raw, tlr_flag, tlr_rank, tlr_temp;
+  uint64_t tl_total = 0;  // matcher treelet records allotted for this batch (0: no treelets, Trav<1>)
+  aicp::rt::TreeBufs tb[2];  // [0] raw-coordinate tree (stream2), [1] centred matcher tree (stream3)
+  aicp::rt::PinBuf pin_desc, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;
+  aicp::rt::PinBuf pin_pf;  // pre-filter read-backs (PfHost): outlive any early return of pf_core
+  std::vector<hipEvent_t> nn_ev;
+  hipEvent_t ev[16] = {};
+  int last_nn_launches = 0;
+  double last_nn_ms = 0, last_nn_bytes = 0;
+  uint64_t last_queries = 0;
+  double last_phase[5] = {0, 0, 0, 0, 0};
+  aicp_prefilter_stats last_pf{};  // timing and kNN counts of the last pre-filter
+  aicp_hip_batch* oneshot = nullptr;  // buffers of aicp_hip_align_batch, kept across calls
+  hipEvent_t pf_ev[8] = {};
+  aicp::rt::SeqState* seq = nullptr;  // aicp_hip_sequence_run's buffers (sequence.cpp), kept across calls
+};
+
+#define HIPC(x)                                                                   \
+  do {                                                                            \
+    const hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess) {                                                       \
+      ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);                  \
+      return AICP_ERR_HIP;                                                        \
+    }                                                                             \
+  } while (0)
+
+#define FAIL(code, msg)   \
+  do {                    \
+    ctx->err = (msg);     \
+    return (code);        \
+  } while (0)
+
+// Tree builders report errors into `err` (they also run on a worker thread, see run_batch).
+#define TCHK(x)                                                                   \
+  do {                                                                            \
+    const hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess) {                                                       \
+      err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
+      return AICP_ERR_HIP;                                                        \
+    }                                                                             \
+  } while (0)
+#define TFAIL(code, msg) \
+  do {                   \
+    err = (msg);         \
+    return (code);       \
+  } while (0)

@@ -1,0 +1,821 @@
+// sequence.cpp — App's frame-to-reference stream on the device (aicp_hip_sequence_run).
+//
+// Reference behaviour (aicp_core/src/registration/app.cpp:282-414, robot working mode):
+//   - the first cloud is the reference (app.cpp:285-312);
+//   - every reading: overlap with the reference -> auto-tuned ratio -> ICP (runAicpPipeline,
+//     app.cpp:218-247);
+//   - |t_i| > max_correction_magnitude drops the reading (app.cpp:366-373);
+//   - an accepted reading is transformed by its correction (pcl::transformPointCloud) and added
+//     to the graph; the reference_update_frequency-th accepted reading since the last update
+//     becomes the reference, its corrected pose (correction * prior pose) the new sensor origin
+//     (app.cpp:375-391, aligned_cloud.cpp:61-70);
+//   - an exception from registerClouds ends the worker (app.cpp:210).
+//
+// Device design. Readings go in windows of F = reference_update_frequency: the readings of a
+// window are independent given its reference, so they run as one batch. Window w+1's reference
+// is the last reading of window w corrected by its own T: k_seq_next_ref + k_transform build it
+// on the device right after window w's ICP, and the whole sequence is enqueued at once with no
+// host synchronisation between windows (the host packs and uploads window w+1 while the device
+// runs window w). That schedule predicts that every reading is accepted; the host checks the
+// prediction once at the end and, at the first window with a dropped reading, keeps the results
+// up to there and enqueues the rest again from the true state (same reference, fewer readings
+// still to collect). Results therefore equal App's order of events in every case.
+//
+// Per window, five streams:
+//   up   H2D of the readings and the window's descriptors (pinned staging, ring of K slots)
+//   rd   reading side: state init, Morton order, reading voxel maps (independent of the reference)
+//   r3   next reference points (k_seq_next_ref, k_transform), centroid + matcher kd-tree
+//   r2   raw kd-tree + SurfaceNormal, normals into the matcher tree's order
+//   icp  reference voxel map, overlap counts, ratio, ICP loop, corrections
+// Device buffers live in K window slots (reused with event waits); descriptors, states and
+// corrections of all readings are kept for the final read-back.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/aicp_hip.h"
+#include "aicp_common.hpp"
+#include "icp_math.hpp"
+#include "kernels.hpp"
+#include "runtime.hpp"
+
+using namespace aicp;
+using namespace aicp::rt;
+
+namespace aicp {
+namespace rt {
+
+// A fixed pool of host threads for packing (spawning 16 threads per window costs more than the
+// packing of a window's readings).
+class WorkerPool {
+ public:
+  explicit WorkerPool(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // fn(task) for task in [0, n), on the pool and the calling thread; returns when all are done
+  // and no worker is inside the task loop any more (so the next run() may reset the counter)
+  void run(size_t n, const std::function<void(size_t)>& fn) {
+    if (n == 0) return;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(mu_);
+    done_cv_.wait(l, [&] { return done_ == n_ && active_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const size_t i = next_.fetch_add(1);
+      if (i >= n_) return;
+      (*fn_)(i);
+      std::lock_guard<std::mutex> l(mu_);
+      if (++done_ == n_) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || (gen_ != seen && fn_ != nullptr); });
+        if (stop_) return;
+        seen = gen_;
+        ++active_;
+      }
+      work();
+      std::lock_guard<std::mutex> l(mu_);
+      if (--active_ == 0 && done_ == n_) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  size_t n_ = 0, done_ = 0;
+  int active_ = 0;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+constexpr int kSlots = 3;  // window slots in flight (>= 2: a window reads the previous slot's reading)
+
+struct SeqSlot {
+  // reading side (window-local offsets)
+  DevBuf read_raw, read_s, read_c, match, d2, touch, cand, slab, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, maps, bitmap,
+      ovl, caps, sel_hist, sel_cnt, ctrs, active;
+  // reference side
+  DevBuf ref_src, ref_raw, bpts, bnrm, nodes, tl, ptl, tl_flag, tl_rank, tl_temp, bpts_raw, nodes_raw, nrm_raw, nbids,
+      inv, rd;  // rd: rdesc, rdesc_raw, gdesc (PairDesc) + rstate, gstate (PairState)
+  TreeBufs tb[2];
+  PinBuf pin_read, pin_par, pin_src;
+  hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr;
+  bool used = false;
+};
+
+struct SeqState {
+  hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr;
+  SeqSlot slot[kSlots];
+  DevBuf desc, state, outT;
+  PinBuf pin_state, pin_out, pin_ctl;
+  std::vector<hipEvent_t> nn_ev;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+  WorkerPool pool{std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1};
+  aicp_sequence_timing last{};
+  int device = 0;
+};
+
+void seq_state_free(SeqState* S) {
+  if (!S) return;
+  for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp})
+    if (q) (void)hipStreamSynchronize(q);
+  for (SeqSlot& sl : S->slot) {
+    for (DevBuf* b : {&sl.read_raw, &sl.read_s, &sl.read_c, &sl.match, &sl.d2, &sl.touch, &sl.cand, &sl.slab,
+                      &sl.ord_k0, &sl.ord_k1, &sl.ord_v0, &sl.ord_v1, &sl.ord_tmp, &sl.maps, &sl.bitmap, &sl.ovl,
+                      &sl.caps, &sl.sel_hist, &sl.sel_cnt, &sl.ctrs, &sl.active, &sl.ref_src, &sl.ref_raw, &sl.bpts,
+                      &sl.bnrm, &sl.nodes, &sl.tl, &sl.ptl, &sl.tl_flag, &sl.tl_rank, &sl.tl_temp, &sl.bpts_raw,
+                      &sl.nodes_raw, &sl.nrm_raw, &sl.nbids, &sl.inv, &sl.rd})
+      release(*b);
+    for (auto& t : sl.tb) t.release_all();
+    for (PinBuf* b : {&sl.pin_read, &sl.pin_par, &sl.pin_src}) release(*b);
+    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done})
+      if (e) (void)hipEventDestroy(e);
+  }
+  for (DevBuf* b : {&S->desc, &S->state, &S->outT}) release(*b);
+  for (PinBuf* b : {&S->pin_state, &S->pin_out, &S->pin_ctl}) release(*b);
+  for (hipEvent_t e : S->nn_ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {S->ev_begin, S->ev_end})
+    if (e) (void)hipEventDestroy(e);
+  for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp})
+    if (q) (void)hipStreamDestroy(q);
+  delete S;
+}
+
+}  // namespace rt
+}  // namespace aicp
+
+namespace {
+
+// float AABB of a cloud's points and its sensor origin (the extent bounds its voxel maps)
+struct Box {
+  float lo[3], hi[3];
+  void reset() {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = INFINITY;
+      hi[k] = -INFINITY;
+    }
+  }
+  void add(float x, float y, float z) {
+    const float v[3] = {x, y, z};
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], v[k]);
+      hi[k] = std::max(hi[k], v[k]);
+    }
+  }
+  void merge(const Box& b) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+};
+
+// xyz at a byte stride -> float4 (w = 1) and the AABB of the finite points, in chunks over the pool
+void pack_clouds(WorkerPool& pool, const std::vector<PackSeg>& segs, std::vector<Box>& boxes) {
+  constexpr uint64_t kChunk = 1 << 15;
+  struct Task {
+    size_t seg;
+    uint64_t a, b;
+  };
+  std::vector<Task> tasks;
+  for (size_t s = 0; s < segs.size(); ++s)
+    for (uint64_t a = 0; a < segs[s].n; a += kChunk) tasks.push_back({s, a, std::min(segs[s].n, a + kChunk)});
+  std::vector<Box> part(tasks.size());
+  pool.run(tasks.size(), [&](size_t t) {
+    const Task& k = tasks[t];
+    const PackSeg& g = segs[k.seg];
+    Box bx;
+    bx.reset();
+    const char* src = reinterpret_cast<const char*>(g.src);
+    for (uint64_t i = k.a; i < k.b; ++i) {
+      const float* p = reinterpret_cast<const float*>(src + i * g.stride);
+      float* d = g.dst4 + 4 * i;
+      d[0] = p[0];
+      d[1] = p[1];
+      d[2] = p[2];
+      d[3] = 1.f;
+      if (std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2])) bx.add(p[0], p[1], p[2]);
+    }
+    part[t] = bx;
+  });
+  boxes.assign(segs.size(), Box{});
+  for (Box& b : boxes) b.reset();
+  for (size_t t = 0; t < tasks.size(); ++t) boxes[tasks[t].seg].merge(part[t]);
+}
+
+// voxel-map capacity (bytes) of a cloud with AABB b plus origin o at resolution res: `rigid`
+// allows any rotation (a rigid motion keeps the diameter; the device sizes the box after the
+// transform), otherwise the axis extents. Both include the 2 + 2 voxels of padding, one more
+// for the floor of each end, and the rounding of the corrected origin.
+uint64_t map_cap(const Box& b0, const double* o, double res, bool rigid) {
+  Box b = b0;
+  b.add((float)o[0], (float)o[1], (float)o[2]);
+  double ext[3], d2 = 0;
+  for (int k = 0; k < 3; ++k) {
+    ext[k] = std::max(0.0, (double)b.hi[k] - (double)b.lo[k]);
+    d2 += ext[k] * ext[k];
+  }
+  uint64_t vox = 1;
+  for (int k = 0; k < 3; ++k) {
+    const double e = rigid ? std::sqrt(d2) : ext[k];
+    vox *= (uint64_t)std::ceil(e / res) + 8;
+  }
+  return (vox + 15) / 16 * 16;
+}
+
+struct Win {
+  size_t p0, np;
+  int src;  // -1: the first cloud; else the reading whose corrected cloud is the reference
+  int slot;
+  int index;  // window number in this pass
+};
+
+}  // namespace
+
+// Enqueue one window. The host parts: pack + upload the readings (and the reference source when
+// it is not resident), descriptors, block maps, map capacities.
+static int enqueue_window(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                          const aicp_cloud* first, const aicp_cloud* rd, const Win& w, const float4* src_resident,
+                          std::vector<Box>& rbox, bool timeNN, int& nn_launches, TreeCtl* ctl_w) {
+  SeqSlot& sl = S->slot[w.slot];
+  const bool doOvl = prm->flags & AICP_RUN_OVERLAP;
+  const double res = prm->resolution;
+  const size_t np = w.np;
+  const aicp_cloud& src = w.src < 0 ? *first : rd[w.src];
+  const uint32_t n_ref = (uint32_t)src.n;
+  uint64_t nread = 0;
+  for (size_t i = 0; i < np; ++i) nread += rd[w.p0 + i].n;
+  // slot buffers (sizes grow to the largest window seen)
+  const size_t tl_cap = 4 * (size_t)n_ref + 4;
+  const bool use_tl = cfg->bucket_size <= 15 && n_ref <= 4000000u && tl_cap < (1ull << 28) && !force_trav1();
+  constexpr uint32_t kRedBlk = kNNBlock * kReducePerThread * kReduceChunks;
+  if (sl.used) {
+    // the slot's previous window (w - K) must be done before its buffers are rewritten, and so
+    // must window w - K + 1, whose reference was built from a reading in this slot: its ICP
+    // (the event of the next slot, ordered after its k_transform) covers both
+    const SeqSlot& nx = S->slot[(w.slot + 1) % kSlots];
+    hipEvent_t e = nx.used ? nx.ev_done : sl.ev_done;
+    for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp}) HIPC(hipStreamWaitEvent(q, e, 0));
+    HIPC(hipEventSynchronize(sl.ev_up));  // pinned staging free again
+  }
+  sl.used = true;
+  HIPC(ensure(sl.read_raw, nread * 16));
+  HIPC(ensure(sl.read_s, nread * 16));
+  HIPC(ensure(sl.read_c, nread * 16));
+  HIPC(ensure(sl.match, nread * 4));
+  HIPC(ensure(sl.d2, nread * 4));
+  HIPC(ensure(sl.touch, nread * 4));
+  HIPC(ensure(sl.cand, nread * 4));
+  HIPC(ensure(sl.sel_hist, np * kHistBins * 4));
+  HIPC(ensure(sl.sel_cnt, np * 4));
+  HIPC(ensure(sl.ctrs, kCtrWords * 4));
+  HIPC(ensure(sl.active, sizeof(ActiveList)));
+  HIPC(ensure(sl.ref_raw, (size_t)n_ref * 16));
+  HIPC(ensure(sl.bpts, (size_t)n_ref * 16));
+  HIPC(ensure(sl.bnrm, (size_t)n_ref * 16));
+  HIPC(ensure(sl.nrm_raw, (size_t)n_ref * 16));
+  HIPC(ensure(sl.nbids, (size_t)n_ref * 4 * cfg->knn_normals));
+  HIPC(ensure(sl.inv, (size_t)n_ref * 4));
+  HIPC(ensure(sl.rd, 3 * sizeof(PairDesc) + 2 * sizeof(PairState)));
+  PairDesc* dRdesc = sl.rd.as<PairDesc>();
+  PairDesc* dRraw = dRdesc + 1;
+  PairDesc* dG = dRdesc + 2;
+  PairState* dRst = reinterpret_cast<PairState*>(dRdesc + 3);
+  PairState* dGst = dRst + 1;
+  PairDesc* dDesc = S->desc.as<PairDesc>() + w.p0;
+  PairState* dState = S->state.as<PairState>() + w.p0;
+  float* dOutT = S->outT.as<float>();
+
+  // ---- host: pack the readings (+ AABBs), descriptors, block maps
+  HIPC(ensure(sl.pin_read, nread * 16));
+  std::vector<PackSeg> segs;
+  std::vector<uint32_t> loff(np);
+  {
+    uint64_t o = 0;
+    for (size_t i = 0; i < np; ++i) {
+      const aicp_cloud& c = rd[w.p0 + i];
+      loff[i] = (uint32_t)o;
+      segs.push_back(PackSeg{c.pts, c.n, c.stride, sl.pin_read.as<float>() + 4 * o});
+      o += c.n;
+    }
+  }
+  const bool upload_src = src_resident == nullptr;
+  if (upload_src) {
+    HIPC(ensure(sl.pin_src, (size_t)n_ref * 16));
+    segs.push_back(PackSeg{src.pts, src.n, src.stride, sl.pin_src.as<float>()});
+  }
+  std::vector<Box> boxes;
+  pack_clouds(S->pool, segs, boxes);
+  for (size_t i = 0; i < np; ++i) rbox[w.p0 + i] = boxes[i];
+  // AABB of the reference source: packed now, or by its own window (resident)
+  const Box src_box = upload_src ? boxes.back() : rbox[w.src];
+  Maps mr, mg, md, ms;
+  std::vector<PairDesc> hd(np);
+  uint32_t red = 0;
+  for (size_t i = 0; i < np; ++i) {
+    const aicp_cloud& c = rd[w.p0 + i];
+    PairDesc& d = hd[i];
+    d = PairDesc{};
+    d.ref_off = 0;
+    d.n_ref = n_ref;
+    d.read_off = loff[i];
+    d.n_read = (uint32_t)c.n;
+    d.red_blk_off = red;
+    d.n_red_blk = (uint32_t)((c.n + kRedBlk - 1) / kRedBlk);
+    red += d.n_red_blk;
+    ident4(d.Tin);
+    d.ratio = cfg->trimmed_ratio;
+    d.ref_id = 0;
+    d.ogroup = 0;
+    for (int k = 0; k < 3; ++k) {
+      d.read_origin[k] = c.origin[k];
+      d.ref_origin[k] = w.src < 0 ? first->origin[k] : 0.0;  // device-written for corrected references
+    }
+    mr.add((int)i, d.n_read, kNNBlock);
+    md.add((int)i, d.n_read, kRedBlk);
+    ms.add((int)i, d.n_read, kNNBlock * kSelPerThread);
+  }
+  mg.add(0, n_ref, kNNBlock);
+  PairDesc r{};
+  r.n_ref = n_ref;
+  r.ratio = cfg->trimmed_ratio;
+  ident4(r.Tin);
+  r.tl_off = 0;
+  r.tl_cap = (uint32_t)tl_cap;
+  PairDesc g = r;
+  for (int k = 0; k < 3; ++k) g.ref_origin[k] = w.src < 0 ? first->origin[k] : 0.0;
+  // voxel maps: [0] the reference (capacity for any rigid motion of its source), [1 + i] readings
+  std::vector<OvlDesc> od(np + 1);
+  std::vector<uint64_t> cap(np + 1);
+  uint64_t bm = 0, cap_max = 0;
+  for (size_t i = 0; i <= np; ++i) {
+    cap[i] = i == 0 ? map_cap(src_box, src.origin, res, w.src >= 0)
+                    : map_cap(boxes[i - 1], rd[w.p0 + i - 1].origin, res, false);
+    od[i] = OvlDesc{};
+    od[i].off = bm;
+    bm += cap[i];
+    cap_max = std::max(cap_max, cap[i]);
+  }
+  if (doOvl) {
+    HIPC(ensure(sl.bitmap, bm));
+    HIPC(ensure(sl.ovl, (np + 1) * sizeof(OvlDesc)));
+    HIPC(ensure(sl.caps, (np + 1) * 8));
+  }
+  // pinned parameter block: pair descs | rdesc, rdesc_raw, gdesc | ovl descs | caps | block maps
+  const size_t nr = mr.pair.size(), nf = mg.pair.size(), nd = md.pair.size(), ns = ms.pair.size();
+  const size_t words = 2 * (nr + nf + nd + ns);
+  const size_t o_desc = 0, o_r = o_desc + np * sizeof(PairDesc), o_ovl = o_r + 3 * sizeof(PairDesc),
+               o_cap = o_ovl + (np + 1) * sizeof(OvlDesc), o_maps = o_cap + (np + 1) * 8, total = o_maps + words * 4;
+  HIPC(ensure(sl.pin_par, total));
+  HIPC(ensure(sl.maps, words * 4));
+  char* P = sl.pin_par.as<char>();
+  std::memcpy(P + o_desc, hd.data(), np * sizeof(PairDesc));
+  std::memcpy(P + o_r, &r, sizeof(PairDesc));
+  std::memcpy(P + o_r + sizeof(PairDesc), &r, sizeof(PairDesc));
+  std::memcpy(P + o_r + 2 * sizeof(PairDesc), &g, sizeof(PairDesc));
+  std::memcpy(P + o_ovl, od.data(), (np + 1) * sizeof(OvlDesc));
+  std::memcpy(P + o_cap, cap.data(), (np + 1) * 8);
+  BlockMap m_read{}, m_gref{}, m_red{}, m_sel{};
+  {
+    uint32_t* mp = reinterpret_cast<uint32_t*>(P + o_maps);
+    size_t o = 0;
+    auto put = [&](const Maps& m, BlockMap& b) {
+      const size_t cnt = m.pair.size();
+      std::memcpy(mp + o, m.pair.data(), cnt * 4);
+      std::memcpy(mp + o + cnt, m.start.data(), cnt * 4);
+      b.pair = sl.maps.as<int32_t>() + o;
+      b.start = sl.maps.as<uint32_t>() + o + cnt;
+      b.n_blocks = (uint32_t)cnt;
+      o += 2 * cnt;
+    };
+    put(mr, m_read);
+    put(mg, m_gref);
+    put(md, m_red);
+    put(ms, m_sel);
+  }
+  HIPC(ensure(sl.slab, (size_t)red * kRedCols * 8));
+
+  // ---- up: readings, descriptors, maps (and a non-resident reference source)
+  hipStream_t su = S->s_up;
+  HIPC(hipMemcpyAsync(sl.read_raw.p, sl.pin_read.p, nread * 16, hipMemcpyHostToDevice, su));
+  HIPC(hipMemcpyAsync(dDesc, P + o_desc, np * sizeof(PairDesc), hipMemcpyHostToDevice, su));
+  HIPC(hipMemcpyAsync(dRdesc, P + o_r, 3 * sizeof(PairDesc), hipMemcpyHostToDevice, su));
+  if (doOvl) {
+    HIPC(hipMemcpyAsync(sl.ovl.p, P + o_ovl, (np + 1) * sizeof(OvlDesc), hipMemcpyHostToDevice, su));
+    HIPC(hipMemcpyAsync(sl.caps.p, P + o_cap, (np + 1) * 8, hipMemcpyHostToDevice, su));
+  }
+  HIPC(hipMemcpyAsync(sl.maps.p, P + o_maps, words * 4, hipMemcpyHostToDevice, su));
+  const float4* src_pts = src_resident;
+  if (upload_src) {
+    HIPC(ensure(sl.ref_src, (size_t)n_ref * 16));
+    HIPC(hipMemcpyAsync(sl.ref_src.p, sl.pin_src.p, (size_t)n_ref * 16, hipMemcpyHostToDevice, su));
+    src_pts = sl.ref_src.as<float4>();
+  }
+  HIPC(hipEventRecord(sl.ev_up, su));
+
+  // ---- rd: reading side
+  hipStream_t sr = S->s_rd;
+  HIPC(hipStreamWaitEvent(sr, sl.ev_up, 0));
+  launch_init_state(sr, (int)np, dDesc, dState);
+  const float4* readS = sl.read_raw.as<float4>();
+  if (read_order_enabled()) {
+    const size_t tb = read_order_temp_bytes(nread, (int)np);
+    HIPC(ensure(sl.ord_k0, nread * 8));
+    HIPC(ensure(sl.ord_k1, nread * 8));
+    HIPC(ensure(sl.ord_v0, nread * 4));
+    HIPC(ensure(sl.ord_v1, nread * 4));
+    HIPC(ensure(sl.ord_tmp, tb));
+    HIPC(launch_read_order(sr, m_read, (int)np, dDesc, sl.read_raw.as<float4>(), (uint32_t)nread,
+                           sl.ord_k0.as<uint64_t>(), sl.ord_k1.as<uint64_t>(), sl.ord_v0.as<uint32_t>(),
+                           sl.ord_v1.as<uint32_t>(), sl.ord_tmp.p, tb, sl.read_s.as<float4>()));
+    readS = sl.read_s.as<float4>();
+  }
+  OvlDesc* dOvl = doOvl ? sl.ovl.as<OvlDesc>() : nullptr;
+  const uint64_t* dCap = doOvl ? sl.caps.as<uint64_t>() : nullptr;
+  uint8_t* bmp = doOvl ? sl.bitmap.as<uint8_t>() : nullptr;
+  if (doOvl) {
+    launch_ovl_init(sr, (int)np, dDesc, dState, res, 2);
+    launch_ovl_bbox(sr, m_read, dDesc, dState, readS, 1, res);
+    launch_ovl_size(sr, (int)np, dState, dOvl + 1, dCap + 1);
+    launch_ovl_clear(sr, (int)np, dOvl + 1, bmp, cap_max);
+    launch_ovl_mark(sr, m_read, dDesc, dOvl + 1, dState, readS, 1, res, bmp);
+    launch_ovl_popcount(sr, (int)np, dOvl + 1, dState, 1, bmp);
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(sl.ev_rd, sr));
+
+  // ---- r3: the reference points, centroid + matcher tree
+  hipStream_t s3 = S->s_r3;
+  HIPC(hipStreamWaitEvent(s3, sl.ev_up, 0));
+  if (w.src >= 0) {
+    // (the source's correction is final: the previous window's ICP is before this in s_icp,
+    // and s3 waits for it through the previous slot's ev_done when resident, or it is from an
+    // earlier pass)
+    const SeqSlot& prev = S->slot[(w.slot + kSlots - 1) % kSlots];
+    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, prev.ev_done, 0));
+    launch_seq_next_ref(s3, dG, S->desc.as<PairDesc>() + w.src, dOutT + 16 * (size_t)w.src);
+    launch_transform(s3, (int)n_ref, dOutT + 16 * (size_t)w.src, src_pts, sl.ref_raw.as<float4>());
+  } else {
+    HIPC(hipMemcpyAsync(sl.ref_raw.p, src_pts, (size_t)n_ref * 16, hipMemcpyDeviceToDevice, s3));
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(sl.ev_ref, s3));
+  const int bucket = cfg->bucket_size;
+  int rc = device_trees_begin(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, sl.ref_raw.as<float4>(), 1, bucket, sl.bpts,
+                              sl.nodes);
+  if (rc) return rc;
+  rc = device_trees_end(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, bucket, sl.bpts, sl.nodes,
+                        plan_levels(n_ref, sl.tb[1]), ctl_w + 1);
+  if (rc) return rc;
+  if (use_tl) {
+    const uint32_t ncap = 2 * n_ref + 2;
+    const size_t tb = tree_scan_temp_bytes((size_t)ncap + 1);
+    HIPC(ensure(sl.tl, tl_cap * 16));
+    HIPC(ensure(sl.ptl, tl_cap * 8));
+    HIPC(ensure(sl.tl_flag, ((size_t)ncap + 1) * 4));
+    HIPC(ensure(sl.tl_rank, ((size_t)ncap + 1) * 4));
+    HIPC(ensure(sl.tl_temp, tb));
+    HIPC(launch_treelets(s3, 1, ncap, dRdesc, sl.nodes.as<uint4>(), bucket, sl.tl_flag.as<uint32_t>(),
+                         sl.tl_rank.as<uint32_t>(), sl.tl_temp.p, tb, sl.tl.as<uint4>(), sl.ptl.as<uint2>(),
+                         sl.tb[1].tw.ctl));
+    HIPC(hipMemcpyAsync(ctl_w + 1, sl.tb[1].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
+  }
+  HIPC(hipEventRecord(sl.ev_s3, s3));
+
+  // ---- r2: raw-coordinate tree + SurfaceNormal (reference as given)
+  hipStream_t s2 = S->s_r2;
+  HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
+  launch_init_state(s2, 1, dRraw, dRst);
+  rc = device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
+                          sl.bpts_raw, sl.nodes_raw);
+  if (rc) return rc;
+  rc = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw,
+                        plan_levels(n_ref, sl.tb[0], true), ctl_w);
+  if (rc) return rc;
+  uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kXcdGroups * kCtrStride;
+  HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
+  if (!launch_normals(s2, 1, n_ref, dRraw, dRst, sl.nodes_raw.as<uint4>(), nullptr, sl.bpts_raw.as<float4>(),
+                      sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr))
+    FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
+  HIPC(hipStreamWaitEvent(s2, sl.ev_s3, 0));
+  launch_normals_to_matcher(s2, 1, n_ref, dRdesc, sl.bpts.as<float4>(), sl.bpts_raw.as<float4>(),
+                            sl.nrm_raw.as<float4>(), sl.inv.as<uint32_t>(), sl.bnrm.as<float4>());
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(sl.ev_s2, s2));
+
+  // ---- icp: reference voxel map, overlap, ratio, then the ICP loop
+  hipStream_t si = S->s_icp;
+  if (doOvl) {
+    HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
+    launch_ovl_init(si, 1, dG, dGst, res, 1);
+    launch_ovl_bbox(si, m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
+    launch_ovl_size(si, 1, dGst, dOvl, dCap);
+    launch_ovl_clear(si, 1, dOvl, bmp, cap[0]);
+    launch_ovl_mark(si, m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
+    launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
+  }
+  HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));
+  if (doOvl) {
+    launch_ovl_intersect(si, (int)np, dDesc, dOvl + 1, dOvl, dState, bmp);
+    launch_ovl_finish(si, (int)np, dDesc, dState, dGst, 1);
+  }
+  HIPC(hipStreamWaitEvent(si, sl.ev_s3, 0));
+  launch_pairs_from_refs(si, (int)np, dDesc, dRdesc);
+  HIPC(hipStreamWaitEvent(si, sl.ev_s2, 0));
+  launch_pairs_degenerate(si, (int)np, dDesc, dState, dRst);
+  launch_prepare_read(si, m_read, dDesc, readS, sl.read_c.as<float4>());
+  HIPC(hipMemsetAsync(sl.sel_hist.p, 0, np * kHistBins * 4, si));
+  HIPC(hipMemsetAsync(sl.sel_cnt.p, 0, np * 4, si));
+  IcpParams ip{};
+  ip.maxE2 = (1 + cfg->nn_epsilon) * (1 + cfg->nn_epsilon);
+  ip.maxR2 = cfg->nn_max_dist * cfg->nn_max_dist;
+  ip.max_iter = cfg->max_iter;
+  ip.smooth = cfg->smooth_length;
+  ip.min_rot = cfg->min_diff_rot;
+  ip.min_trans = cfg->min_diff_trans;
+  ip.knn_normals = cfg->knn_normals;
+  ActiveList* al = sl.active.as<ActiveList>();
+  uint32_t* ctr = sl.ctrs.as<uint32_t>();
+  for (int it = 0; it < cfg->max_iter; ++it) {
+    launch_active_list(si, (int)np, dDesc, dState, al, ctr);
+    ip.prof_slot = nn_launches;
+    if (timeNN) {
+      while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
+        hipEvent_t e;
+        HIPC(hipEventCreate(&e));
+        S->nn_ev.push_back(e);
+      }
+      HIPC(hipEventRecord(S->nn_ev[2 * nn_launches], si));
+    }
+    launch_icp_nn(si, (int)nread, dDesc, dState, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
+                  use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
+                  use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
+                  sl.touch.as<uint32_t>(), ctr, ip);
+    if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], si));
+    ++nn_launches;
+    launch_icp_select(si, m_sel, (int)np, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
+                      sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), 0);
+    launch_icp_reduce(si, m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
+                      sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>());
+    launch_icp_update(si, (int)np, dDesc, dState, sl.slab.as<double>(), ip);
+  }
+  launch_finalize(si, (int)np, dDesc, dState, dOutT + 16 * w.p0);
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(sl.ev_done, si));
+  return AICP_OK;
+}
+
+static int seq_init(aicp_hip_ctx* ctx, size_t n) {
+  if (!ctx->seq) {
+    SeqState* S = new SeqState();
+    ctx->seq = S;
+    S->device = ctx->device;
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+    for (hipStream_t* q : {&S->s_up, &S->s_rd, &S->s_r2, &S->s_r3, &S->s_icp})
+      HIPC(hipStreamCreateWithPriority(q, hipStreamNonBlocking, (q == &S->s_rd || q == &S->s_up) ? lo : hi));
+    for (SeqSlot& sl : S->slot)
+      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done})
+        HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    HIPC(hipEventCreate(&S->ev_begin));
+    HIPC(hipEventCreate(&S->ev_end));
+  }
+  SeqState* S = ctx->seq;
+  for (SeqSlot& sl : S->slot) sl.used = false;
+  HIPC(ensure(S->desc, n * sizeof(PairDesc)));
+  HIPC(ensure(S->state, n * sizeof(PairState)));
+  HIPC(ensure(S->outT, n * 64));
+  HIPC(ensure(S->pin_state, n * sizeof(PairState)));
+  HIPC(ensure(S->pin_out, n * 64));
+  return AICP_OK;
+}
+
+static int seq_sync(aicp_hip_ctx* ctx, SeqState* S) {
+  for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp}) HIPC(hipStreamSynchronize(q));
+  return AICP_OK;
+}
+
+extern "C" {
+
+void aicp_hip_default_sequence_params(aicp_sequence_params* p) {
+  if (!p) return;
+  *p = aicp_sequence_params{};
+  p->reference_update_frequency = 5;  // aicp.launch:61
+  p->max_correction_magnitude = 1.0f;  // aicp.launch:63
+  p->resolution = (double)0.2f;        // octomapResolution read as float (yaml_configurator.cpp:81)
+  p->flags = AICP_RUN_OVERLAP;
+}
+
+int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                          const aicp_cloud* first, const aicp_cloud* readings, size_t n, float* out_T,
+                          aicp_sequence_result* out, size_t* n_done) {
+  if (!ctx || !cfg || !prm || !first || (n && (!readings || !out_T || !out)) || !n_done) return AICP_ERR_INVALID;
+  const auto t0 = std::chrono::steady_clock::now();
+  *n_done = 0;
+  const int F = prm->reference_update_frequency;
+  if (F < 1) FAIL(AICP_ERR_INVALID, "reference_update_frequency must be >= 1");
+  const bool doOvl = prm->flags & AICP_RUN_OVERLAP;
+  if (doOvl && !(prm->resolution > 0)) FAIL(AICP_ERR_INVALID, "resolution");
+  int rc = check_cfg(ctx, cfg, AICP_RUN_ICP | (doOvl ? AICP_RUN_OVERLAP : 0));
+  if (rc) return rc;
+  auto valid = [](const aicp_cloud& c) {
+    return c.pts && c.n >= 1 && c.n < (1ull << 28) && c.stride >= 12 && c.stride % 4 == 0;
+  };
+  if (!valid(*first)) FAIL(AICP_ERR_INVALID, "invalid first cloud");
+  for (size_t i = 0; i < n; ++i)
+    if (!valid(readings[i])) FAIL(AICP_ERR_INVALID, "invalid reading " + std::to_string(i));
+  if ((size_t)F > (size_t)kMaxPairs) FAIL(AICP_ERR_UNSUPPORTED, "reference_update_frequency above 4096");
+  if (n == 0) return AICP_OK;
+  HIPC(hipSetDevice(ctx->device));
+  rc = seq_init(ctx, n);
+  if (rc) return rc;
+  SeqState* S = ctx->seq;
+  const bool timeNN = prm->flags & AICP_RUN_TIME_NN;
+  int nn_launches = 0, windows = 0, replans = 0;
+  HIPC(hipEventRecord(S->ev_begin, S->s_up));
+  // state at the start of a pass: next reading, reference source, accepted since its update
+  size_t p = 0;
+  int src = -1, acc = 0;
+  std::vector<uint8_t> accepted(n, 0);
+  std::vector<Box> rbox(n);
+  int status = AICP_OK;
+  while (p < n) {
+    // plan: every reading accepted
+    std::vector<Win> plan;
+    {
+      size_t q = p;
+      int s = src, a = acc, k = 0;
+      while (q < n) {
+        const size_t np = std::min<size_t>((size_t)(F - a), n - q);
+        plan.push_back(Win{q, np, s, k % kSlots, k});
+        q += np;
+        s = (int)(q - 1);
+        a = 0;
+        ++k;
+      }
+    }
+    HIPC(ensure(S->pin_ctl, plan.size() * 2 * sizeof(TreeCtl)));
+    TreeCtl* ctl = S->pin_ctl.as<TreeCtl>();
+    std::memset(ctl, 0, plan.size() * 2 * sizeof(TreeCtl));
+    for (size_t k = 0; k < plan.size(); ++k) {
+      const Win& w = plan[k];
+      // the reference source is resident in the previous window's slot, except for the first
+      // window of a pass (the first cloud, or a reading of an earlier pass): uploaded again
+      const float4* resident = nullptr;
+      if (k > 0) {
+        const Win& pw = plan[k - 1];
+        uint64_t off = 0;
+        for (size_t i = pw.p0; i < (size_t)w.src; ++i) off += readings[i].n;
+        resident = S->slot[pw.slot].read_raw.as<float4>() + off;
+      }
+      rc = enqueue_window(ctx, S, cfg, prm, first, readings, w, resident, rbox, timeNN, nn_launches, ctl + 2 * k);
+      if (rc) {
+        (void)seq_sync(ctx, S);
+        return rc;
+      }
+      ++windows;
+    }
+    // read back every reading of this pass
+    const size_t pe = n;
+    HIPC(hipMemcpyAsync(S->pin_state.as<PairState>() + p, S->state.as<PairState>() + p, (pe - p) * sizeof(PairState),
+                        hipMemcpyDeviceToHost, S->s_icp));
+    HIPC(hipMemcpyAsync(S->pin_out.as<float>() + 16 * p, S->outT.as<float>() + 16 * p, (pe - p) * 64,
+                        hipMemcpyDeviceToHost, S->s_icp));
+    HIPC(hipEventRecord(S->ev_end, S->s_icp));
+    rc = seq_sync(ctx, S);
+    if (rc) return rc;
+    for (size_t k = 0; k < plan.size(); ++k) {
+      for (int t = 0; t < 2; ++t) {
+        rc = device_trees_check_ctl(S->slot[plan[k].slot].tb[t], ctl + 2 * k + t, ctx->err);
+        if (rc) return rc;
+      }
+      if ((ctl[2 * k + 1].error & 4)) FAIL(AICP_ERR_HIP, "matcher treelets exceed their allotment");
+    }
+    // check the prediction window by window
+    const PairState* hs = S->pin_state.as<PairState>();
+    const float* hT = S->pin_out.as<float>();
+    bool replan = false;
+    for (const Win& w : plan) {
+      int a = (w.p0 == p) ? acc : 0;
+      for (size_t i = w.p0; i < w.p0 + w.np; ++i) {
+        int st = hs[i].status;
+        if (doOvl && hs[i].ovl_err && !st) st = AICP_ERR_HIP;
+        out[i].status = st;
+        out[i].reference = w.src;
+        out[i].is_reference = 0;
+        if (st) {  // the worker ends here (app.cpp:210): nothing after this reading happened
+          status = st;
+          *n_done = i + 1;
+          accepted[i] = 0;
+          break;
+        }
+        accepted[i] = !correction_rejected(hT + 16 * i, prm->max_correction_magnitude);
+        a += accepted[i];
+      }
+      if (status) break;
+      if (a == F) {
+        out[w.p0 + w.np - 1].is_reference = 1;
+        continue;
+      }
+      if (w.p0 + w.np < n) {  // a reading was dropped: the reference stays, the window goes on
+        p = w.p0 + w.np;
+        src = w.src;
+        acc = a;
+        replan = true;
+        ++replans;
+        break;
+      }
+    }
+    if (status || !replan) {
+      if (!status) *n_done = n;
+      break;
+    }
+  }
+  // results
+  const PairState* hs = S->pin_state.as<PairState>();
+  const float* hT = S->pin_out.as<float>();
+  for (size_t i = 0; i < *n_done; ++i) {
+    std::memcpy(out_T + 16 * i, hT + 16 * i, 64);
+    aicp_sequence_result& r = out[i];
+    r.accepted = accepted[i];
+    for (int k = 0; k < 3; ++k) r.corrected_origin[k] = 0.0;
+    if (r.accepted) corrected_origin(hT + 16 * i, readings[i].origin, r.corrected_origin);
+    const PairState& st = hs[i];
+    aicp_icp_stats& o = r.icp;
+    std::memset(&o, 0, sizeof(o));
+    o.status = r.status;
+    o.iterations = st.iters;
+    o.converged = st.converged;
+    o.degenerate_normals = st.degenerate;
+    o.inlier_ratio = st.inlier_ratio;
+    o.trimmed_ratio = st.ratio;
+    o.overlap_percent = st.overlap;
+    o.nn_points_touched = st.touched_pts;
+    o.nn_nodes_touched = st.touched_nodes;
+    for (int k = 0; k < 3; ++k) o.overlap_keys[k] = st.ovl_counts[k];
+  }
+  // timing
+  ctx->last_nn_launches = timeNN ? nn_launches : 0;
+  ctx->last_nn_ms = 0;
+  if (timeNN)
+    for (int i = 0; i < nn_launches; ++i) ctx->last_nn_ms += ev_ms(S->nn_ev[2 * i], S->nn_ev[2 * i + 1]);
+  uint64_t queries = 0, tp = 0, tn = 0;
+  for (size_t i = 0; i < *n_done; ++i) {
+    queries += (uint64_t)hs[i].iters * readings[i].n;
+    tp += hs[i].touched_pts;
+    tn += hs[i].touched_nodes;
+  }
+  ctx->last_nn_bytes = (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0;
+  ctx->last_queries = queries;
+  S->last.windows = windows;
+  S->last.replans = replans;
+  S->last.device_ms = ev_ms(S->ev_begin, S->ev_end);
+  S->last.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (status) ctx->err = "reading " + std::to_string(*n_done - 1) + ": status " + std::to_string(status);
+  return status;
+}
+
+int aicp_hip_last_sequence_timing(const aicp_hip_ctx* ctx, aicp_sequence_timing* out) {
+  if (!ctx || !out) return AICP_ERR_INVALID;
+  *out = ctx->seq ? ctx->seq->last : aicp_sequence_timing{};
+  return AICP_OK;
+}
+
+}  // extern "C"

@@ -161,6 +161,42 @@ def make_sequence(n_readings: int = 64, ref_every: int = 5, n_points: int = 1200
     return pairs
 
 
+@dataclass
+class Stream:
+    first: np.ndarray          # the first cloud (App's first reference), world frame
+    first_origin: np.ndarray   # its sensor origin
+    readings: list             # reading clouds in their drifted (odometry) frame
+    origins: list              # prior-pose translations (sensor origins) in that frame
+    T_gt: list                 # correction that re-aligns each reading (drift^-1)
+
+
+def make_stream(n_readings: int = 64, n_points: int = 120000, seed: int = 1, step: float = 0.3,
+                sensor_z: float = 0.7, half: float = 30.0, T_gt=None, jumps=None) -> Stream:
+    """The input of App's frame-to-reference stream (app.cpp:282-414) for the C2/C3 configs of
+    SURVEY.md §8(d): a first cloud at the start of the path, then readings taken `step` m apart
+    along x, each perturbed by the odometry drift T_gt^-1. Unlike make_sequence, references are
+    not sampled here: App builds them from the corrected readings. jumps: {reading index: extra
+    translation (3,)} of that reading's drift, to make App drop it (max_correction_magnitude)."""
+    T_gt = T_GT if T_gt is None else np.asarray(T_gt, np.float64)
+    scene = make_scene(seed)
+    o0 = np.array([0.0, 0.0, sensor_z])
+    rng0 = np.random.default_rng(seed * 7919 + 1000)
+    first = _subsample_raster(sample_scene(scene, rng0, o0, half=half), n_points, rng0).astype(np.float32)
+    reads, origins, gts = [], [], []
+    for i in range(n_readings):
+        Tg = T_gt.copy()
+        if jumps and i in jumps:
+            Tg[:3, 3] += np.asarray(jumps[i], np.float64)
+        Ti = np.linalg.inv(Tg)
+        o_w = np.array([(i + 1) * step, 0.0, sensor_z])
+        rng = np.random.default_rng(seed * 7919 + 5000 + i)
+        w = _subsample_raster(sample_scene(scene, rng, o_w, half=half), n_points, rng)
+        reads.append((w @ Ti[:3, :3].T + Ti[:3, 3]).astype(np.float32))
+        origins.append(Ti[:3, :3] @ o_w + Ti[:3, 3])
+        gts.append(Tg)
+    return Stream(first, o0, reads, origins, gts)
+
+
 def make_cube(min_corner=-2.0, max_corner=2.0, step=0.05):
     """The cube of aicp_core/src/tools/create_cube_cloud.cpp:13-90 (float loop counters)."""
     vals = []

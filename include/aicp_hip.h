@@ -224,6 +224,56 @@ int aicp_hip_last_nn_timing(const aicp_hip_ctx* ctx, int* n_launches, double* to
  * [3] icp loop, [4] total wall time. [0] runs concurrently with [1]-[2]. */
 int aicp_hip_last_phase_ms(const aicp_hip_ctx* ctx, double out_ms[5]);
 
+/* ---- App's frame-to-reference stream (app.cpp:282-414, robot working mode) ---------------------
+ * The first cloud becomes the reference (app.cpp:285-312). Every reading is registered against
+ * the current reference (overlap -> auto-tuned ratio -> ICP, app.cpp:218-247); a correction with
+ * |t_i| > max_correction_magnitude drops the reading (app.cpp:366-373); an accepted reading is
+ * transformed by its correction (pcl::transformPointCloud, float) and, when it is the
+ * reference_update_frequency-th accepted reading since the last reference update, it becomes the
+ * next reference with the translation of its corrected pose correction * prior pose as sensor
+ * origin (app.cpp:375-391, aligned_cloud.cpp:61-70, common.cpp:4-23). A registration error ends
+ * the stream, as the uncaught exception ends App's worker (app.cpp:210).
+ * Inputs are host buffers (pre-filtered clouds, as App passes read_prefiltered); everything
+ * from the upload to the corrections runs on the device, the next reference included. */
+typedef struct {
+  const float* pts;      /* x, y, z at `stride` bytes */
+  uint64_t n;
+  uint64_t stride;
+  double origin[3];      /* prior pose translation = sensor origin (octrees_overlap.cpp:229-230) */
+} aicp_cloud;
+
+typedef struct {
+  int32_t reference_update_frequency; /* 5 (aicp.launch:61) */
+  float max_correction_magnitude;     /* 1.0 (aicp.launch:63; aicp_ros_node.cpp:28 default 0.5) */
+  double resolution;                  /* octomapResolution (0.2, aicp_config.yaml:21) */
+  int32_t flags;                      /* AICP_RUN_OVERLAP: per-reading overlap + auto-tuned ratio
+                                         (else cfg->trimmed_ratio); AICP_RUN_TIME_NN */
+} aicp_sequence_params;
+
+typedef struct {
+  int32_t status;          /* AICP_* of this reading's registration */
+  int32_t accepted;        /* 0: dropped, some |t_i| > max_correction_magnitude */
+  int32_t reference;       /* cloud it was registered against: -1 the first cloud, else a reading */
+  int32_t is_reference;    /* 1: it became the next reference */
+  double corrected_origin[3]; /* translation of correction * prior pose (accepted readings) */
+  aicp_icp_stats icp;
+} aicp_sequence_result;
+
+typedef struct {
+  int32_t windows;         /* reference windows run (incl. re-runs after a misprediction) */
+  int32_t replans;         /* re-plans after a dropped reading or an error */
+  double wall_ms;          /* the whole call: packing, H2D, device work, D2H */
+  double device_ms;        /* first upload enqueued -> last correction (HIP events) */
+} aicp_sequence_timing;
+
+void aicp_hip_default_sequence_params(aicp_sequence_params* out);
+/* out_T: 16 floats per reading (correction, column-major); out: per reading; *n_done = readings
+ * processed (all of them unless a registration error ended the stream at reading n_done - 1). */
+int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                          const aicp_cloud* first, const aicp_cloud* readings, size_t n_readings,
+                          float* out_T /* 16*n */, aicp_sequence_result* out /* n */, size_t* n_done);
+int aicp_hip_last_sequence_timing(const aicp_hip_ctx* ctx, aicp_sequence_timing* out);
+
 /* ---- kernel-level entry points (parity tests and diagnostics) --------------------------- */
 /* kd-tree over pts (as given, no centring) + k-NN of queries: libnabo
  * KDTreeUnbalancedPtInLeavesImplicitBoundsStackOpt order, ALLOW_SELF_MATCH.

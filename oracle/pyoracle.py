@@ -298,3 +298,105 @@ def prefilter(pts, params=None):
     V = ns.value
     return dict(out=out[:no.value].copy(), sampled=sampled[:V].copy(), labels=labels[:V].copy(),
                 n_clusters=nc.value)
+
+
+# ---------------------------------------------------------------- App's stream ----------------
+def transform_cloud(T, pts):
+    """pcl::transformPointCloud (pcl 1.8 common/impl/transforms.hpp) in float: x' = ((r00 x +
+    r01 y) + r02 z) + t0 per row, each operation rounded to float. T: 4x4 row-major."""
+    T = np.asarray(T, np.float32)
+    P = np.ascontiguousarray(pts, np.float32)[:, :3]
+    out = np.empty_like(P)
+    for r in range(3):
+        s = T[r, 0] * P[:, 0]
+        s = (s + T[r, 1] * P[:, 1]).astype(np.float32)
+        s = (s + T[r, 2] * P[:, 2]).astype(np.float32)
+        out[:, r] = (s + T[r, 3]).astype(np.float32)
+    return out
+
+
+def corrected_origin(T, prior_origin):
+    """Translation of correction_iso * prior_pose (aligned_cloud.cpp:61-70) with
+    correction_iso = fromMatrix4fToIsometry3d(T) (common.cpp:4-23): Eigen's Quaternionf of the
+    float rotation block (trace branch / largest-diagonal branch), cast to double,
+    toRotationMatrix in double, R * o + t with left-to-right row sums."""
+    f = np.float32
+    m = np.asarray(T, np.float32)[:3, :3]
+    q = [f(0)] * 4  # x, y, z, w
+    t = f(f(m[0, 0] + m[1, 1]) + m[2, 2])
+    if t > f(0):
+        t = f(np.sqrt(f(t + f(1))))
+        q[3] = f(f(0.5) * t)
+        t = f(f(0.5) / t)
+        q[0] = f(f(m[2, 1] - m[1, 2]) * t)
+        q[1] = f(f(m[0, 2] - m[2, 0]) * t)
+        q[2] = f(f(m[1, 0] - m[0, 1]) * t)
+    else:
+        i = 0
+        if m[1, 1] > m[0, 0]:
+            i = 1
+        if m[2, 2] > m[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        t = f(np.sqrt(f(f(f(m[i, i] - m[j, j]) - m[k, k]) + f(1))))
+        q[i] = f(f(0.5) * t)
+        t = f(f(0.5) / t)
+        q[3] = f(f(m[k, j] - m[j, k]) * t)
+        q[j] = f(f(m[j, i] + m[i, j]) * t)
+        q[k] = f(f(m[k, i] + m[i, k]) * t)
+    x, y, z, w = (float(v) for v in q)
+    tx, ty, tz = 2.0 * x, 2.0 * y, 2.0 * z
+    twx, twy, twz = tx * w, ty * w, tz * w
+    txx, txy, txz = tx * x, ty * x, tz * x
+    tyy, tyz, tzz = ty * y, tz * y, tz * z
+    R = [[1.0 - (tyy + tzz), txy - twz, txz + twy],
+         [txy + twz, 1.0 - (txx + tzz), tyz - twx],
+         [txz - twy, tyz + twx, 1.0 - (txx + tyy)]]
+    o = [float(v) for v in prior_origin]
+    Tt = np.asarray(T, np.float32)
+    return np.array([((R[r][0] * o[0] + R[r][1] * o[1]) + R[r][2] * o[2]) + float(Tt[r, 3]) for r in range(3)])
+
+
+def sequence(first, first_origin, readings, origins, cfg=None, reference_update_frequency=5,
+             max_correction_magnitude=1.0, resolution=0.2, overlap=True, stop=None):
+    """App::processCloud over a stream (app.cpp:282-414, robot mode): the first cloud is the
+    reference; each reading: overlap -> ratio -> ICP against the current reference; dropped when
+    some |T(i,3)| > max_correction_magnitude (float compare, app.cpp:366-373); an accepted reading
+    is transformed by T and, as the reference_update_frequency-th accepted reading since the last
+    update, becomes the reference with origin corrected_origin(T, its origin); a registration
+    error ends the stream (app.cpp:210). stop: process only readings [0, stop).
+    Returns a list of dicts (status, T, stats, accepted, reference, is_reference,
+    corrected_origin, overlap, counts, ratio)."""
+    cfg = cfg or default_config()
+    ref, ref_origin, ref_id = _pts(first), np.asarray(first_origin, np.float64), -1
+    acc = 0
+    out = []
+    mc = np.float32(max_correction_magnitude)
+    for i, (r, o) in enumerate(zip(readings, origins)):
+        if stop is not None and i >= stop:
+            break
+        rec = dict(reference=ref_id, is_reference=0, accepted=0, corrected_origin=None)
+        if overlap:
+            ov, cnt = globals()["overlap"](ref, ref_origin, r, o, resolution)
+            ratio = autotune_ratio(ov)
+            rec.update(overlap=ov, counts=cnt)
+        else:
+            ratio = cfg.trimmed_ratio
+        c = IcpConfig.from_buffer_copy(cfg)
+        c.trimmed_ratio = ratio
+        rc, T, st = icp(ref, r, c)
+        rec.update(status=rc, T=T, stats=st, ratio=ratio)
+        out.append(rec)
+        if rc:
+            break
+        Tf = np.asarray(T, np.float32)
+        if any(abs(Tf[k, 3]) > mc for k in range(3)):
+            continue
+        rec["accepted"] = 1
+        rec["corrected_origin"] = corrected_origin(Tf, o)
+        acc += 1
+        if acc == reference_update_frequency:
+            ref, ref_origin, ref_id = transform_cloud(Tf, r), rec["corrected_origin"], i
+            rec["is_reference"] = 1
+            acc = 0
+    return out
