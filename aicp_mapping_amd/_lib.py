@@ -35,6 +35,7 @@ EXPORTS = [
     "aicp_hip_last_prefilter_stats", "aicp_hip_map_create", "aicp_hip_map_free", "aicp_hip_map_size",
     "aicp_hip_map_download", "aicp_hip_map_crop", "aicp_hip_map_merge", "aicp_hip_map_prefilter",
     "aicp_hip_default_sequence_params", "aicp_hip_sequence_run", "aicp_hip_last_sequence_timing",
+    "aicp_hip_map_register_batch",
 ]
 
 
@@ -227,6 +228,8 @@ def _load():
     L.aicp_hip_sequence_run.argtypes = [vp, cfgp, C.POINTER(SequenceParams), C.POINTER(Cloud), C.POINTER(Cloud), sz,
                                         fp, C.POINTER(SequenceResult), C.POINTER(C.c_size_t)]
     L.aicp_hip_last_sequence_timing.argtypes = [vp, C.POINTER(SequenceTiming)]
+    L.aicp_hip_map_register_batch.argtypes = [vp, cfgp, vp, C.c_float, C.c_float, C.POINTER(Cloud), fp, sz, C.c_int,
+                                              fp, stp]
     return L
 
 

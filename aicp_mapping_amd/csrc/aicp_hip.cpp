@@ -145,7 +145,10 @@ int check_cfg(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, int flags) {
   return AICP_OK;
 }
 
-int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_batch* B) {
+// refs_on_device: every pair has a reference of its own (n_ref points) that the caller writes
+// into B->ref_raw at rdesc[i].ref_off afterwards (the localization batch's map crops); the
+// pairs' ref pointers are then not read.
+int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_batch* B, bool refs_on_device) {
   if (!pairs || n == 0) FAIL(AICP_ERR_INVALID, "no pairs");
   B->P = n;
   B->desc.assign(n, PairDesc{});
@@ -162,7 +165,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     if (!valid_pair(p)) FAIL(AICP_ERR_INVALID, "invalid pair " + std::to_string(i));
     PairDesc& d = B->desc[i];
     int32_t rid = -1;
-    for (size_t r = 0; r < rep.size(); ++r) {
+    for (size_t r = 0; r < rep.size() && !refs_on_device; ++r) {
       const aicp_pair& q = pairs[rep[r]];
       if (q.ref == p.ref && q.n_ref == p.n_ref && q.ref_stride == p.ref_stride) {
         rid = (int32_t)r;
@@ -231,16 +234,18 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   // raw clouds as float4
   HIPC(ensure(B->ref_raw, ro * 16));
   HIPC(ensure(B->read_raw, wo * 16));
-  HIPC(ensure(ctx->pin_io, (ro + wo) * 16));  // references, then readings: the readings are
+  HIPC(ensure(ctx->pin_io, ((refs_on_device ? 0 : ro) + wo) * 16));  // references, then readings: the readings are
   float* st = ctx->pin_io.as<float>();          // packed while the references' DMA runs
   std::vector<PackSeg> segs;
-  for (size_t r = 0; r < rep.size(); ++r) {
-    const PairDesc& d = B->rdesc[r];
-    segs.push_back(PackSeg{pairs[rep[r]].ref, d.n_ref, pairs[rep[r]].ref_stride, st + 4ull * d.ref_off});
+  if (!refs_on_device) {
+    for (size_t r = 0; r < rep.size(); ++r) {
+      const PairDesc& d = B->rdesc[r];
+      segs.push_back(PackSeg{pairs[rep[r]].ref, d.n_ref, pairs[rep[r]].ref_stride, st + 4ull * d.ref_off});
+    }
+    pack_many(segs);
+    HIPC(hipMemcpyAsync(B->ref_raw.p, st, ro * 16, hipMemcpyHostToDevice, ctx->stream));
   }
-  pack_many(segs);
-  HIPC(hipMemcpyAsync(B->ref_raw.p, st, ro * 16, hipMemcpyHostToDevice, ctx->stream));
-  float* sw = st + 4ull * ro;
+  float* sw = refs_on_device ? st : st + 4ull * ro;
   segs.clear();
   for (size_t i = 0; i < n; ++i) {
     const PairDesc& d = B->desc[i];
@@ -1004,6 +1009,9 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
   free_batch(ctx->oneshot);
+  free_batch(ctx->mapbatch);
+  release(ctx->crop_ws);
+  release(ctx->pin_crop);
   seq_state_free(ctx->seq);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
                     &ctx->pin_rdesc, &ctx->pin_gdesc, &ctx->pin_gstate, &ctx->pin_pf})
@@ -1025,7 +1033,7 @@ int aicp_hip_batch_upload(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pa
   if (!ctx || !out) return AICP_ERR_INVALID;
   HIPC(hipSetDevice(ctx->device));
   aicp_hip_batch* B = new aicp_hip_batch();
-  const int rc = upload_pairs(ctx, pairs, n_pairs, B);
+  const int rc = upload_pairs(ctx, pairs, n_pairs, B, false);
   if (rc) {
     free_batch(B);
     *out = nullptr;
@@ -1057,7 +1065,7 @@ int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const ai
   // one-shot batches reuse the context's batch buffers (no device allocation per call)
   if (!ctx->oneshot) ctx->oneshot = new aicp_hip_batch();
   aicp_hip_batch* B = ctx->oneshot;
-  int rc = upload_pairs(ctx, pairs, n_pairs, B);
+  int rc = upload_pairs(ctx, pairs, n_pairs, B, false);
   if (!rc) rc = aicp_hip_batch_run(ctx, B, cfg, resolution, flags, out_T, stats);
   // the input copies of a very large one-shot batch are not kept for the next call
   if (B->ref_raw.cap + B->read_raw.cap > kOneshotKeepBytes) {
@@ -1675,6 +1683,70 @@ int aicp_hip_map_crop(aicp_hip_ctx* ctx, const aicp_hip_map* map, float mn, floa
   if (!map->n) return AICP_OK;
   HIPC(hipSetDevice(ctx->device));
   return crop_device(ctx, map->pts.as<float4>(), map->n, inv, t, mn, mx, out, cap, out_n);
+}
+
+// Localization-only batch (localize_against_prior_map): every reading's reference is the map
+// cropped around its prior pose on the device (setReference, app.cpp:41-51), written straight
+// into the batch's reference array; the overlap is bypassed at 50 % (app.cpp:123-127), so the
+// ratio is the auto-tune of 50 (0.5).
+int aicp_hip_map_register_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_hip_map* map, float mn,
+                                float mx, const aicp_cloud* readings, const float* poses, size_t n, int flags,
+                                float* out_T, aicp_icp_stats* stats) {
+  if (!ctx || !cfg || !map || !readings || !poses || !out_T || n == 0) return AICP_ERR_INVALID;
+  if (!map->n) FAIL(AICP_ERR_INVALID, "empty map");
+  if (n > (size_t)kMaxPairs) FAIL(AICP_ERR_UNSUPPORTED, "more than 4096 readings in one batch");
+  HIPC(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const size_t ab = crop_args_bytes(), tiles = crop_tiles(map->n);
+  const size_t o_args = 0, o_cnt = (n * ab + 255) & ~size_t(255), o_off = o_cnt + n * tiles * 4,
+               o_tot = o_off + n * tiles * 4, o_base = o_tot + n * 4, total_b = o_base + n * 4;
+  HIPC(ensure(ctx->crop_ws, total_b));
+  HIPC(ensure(ctx->pin_crop, n * ab + 2 * n * 4));
+  char* ws = ctx->crop_ws.as<char>();
+  char* h = ctx->pin_crop.as<char>();
+  for (size_t i = 0; i < n; ++i) {
+    float inv[9], t[3], rpy[3];
+    crop_box_frame(poses + 16 * i, inv, t, rpy);
+    pack_crop_args(inv, t, mn, mx, h + i * ab);
+  }
+  HIPC(hipMemcpyAsync(ws + o_args, h, n * ab, hipMemcpyHostToDevice, s));
+  launch_crop_count_multi(s, (int)map->n, (int)n, ws + o_args, map->pts.as<float4>(), (uint32_t*)(ws + o_cnt),
+                          (uint32_t*)(ws + o_off), (uint32_t*)(ws + o_tot));
+  HIPC(hipGetLastError());
+  uint32_t* htot = reinterpret_cast<uint32_t*>(h + n * ab);
+  HIPC(hipMemcpyAsync(htot, ws + o_tot, n * 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  // a batch whose references are the crops (pair i: reference i), readings from the host
+  std::vector<aicp_pair> pairs(n);
+  for (size_t i = 0; i < n; ++i) {
+    const aicp_cloud& c = readings[i];
+    if (htot[i] == 0) FAIL(AICP_ERR_INVALID, "reading " + std::to_string(i) + ": empty map crop");
+    aicp_pair& p = pairs[i];
+    p = aicp_pair{};
+    p.ref = c.pts;  // not read (references on the device)
+    p.n_ref = htot[i];
+    p.ref_stride = 16;
+    p.read = c.pts;
+    p.n_read = c.n;
+    p.read_stride = c.stride;
+    for (int k = 0; k < 3; ++k) {
+      p.ref_origin[k] = poses[16 * i + 12 + k];
+      p.read_origin[k] = c.origin[k];
+    }
+  }
+  if (!ctx->mapbatch) ctx->mapbatch = new aicp_hip_batch();
+  aicp_hip_batch* B = ctx->mapbatch;
+  int rc = upload_pairs(ctx, pairs.data(), n, B, true);
+  if (rc) return rc;
+  uint32_t* hbase = htot + n;
+  for (size_t i = 0; i < n; ++i) hbase[i] = B->rdesc[i].ref_off;
+  HIPC(hipMemcpyAsync(ws + o_base, hbase, n * 4, hipMemcpyHostToDevice, s));
+  launch_crop_scatter_multi(s, (int)map->n, (int)n, ws + o_args, map->pts.as<float4>(), (const uint32_t*)(ws + o_off),
+                            (const uint32_t*)(ws + o_base), B->ref_raw.as<float4>());
+  HIPC(hipGetLastError());
+  aicp_icp_config c = *cfg;
+  c.trimmed_ratio = aicp_hip_autotune_ratio(50.0f);  // octree_overlap_ = 50.0 (app.cpp:123-127)
+  return run_batch(ctx, B, &c, 0.0, AICP_RUN_ICP | (flags & AICP_RUN_TIME_NN), out_T, stats, nullptr);
 }
 
 int aicp_hip_map_merge(aicp_hip_ctx* ctx, aicp_hip_map* map, const float* pts, size_t n, size_t stride,

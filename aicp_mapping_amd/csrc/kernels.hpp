@@ -74,6 +74,15 @@ size_t crop_tiles(size_t n);
 void launch_crop_box(hipStream_t s, int n, const float inv[9], const float t[3], float mn, float mx,
                      const float4* pts, uint32_t* tile_cnt, uint32_t* tile_off, uint32_t* total,
                      float4* out);
+// many crops of one map (one per localization reading): args = n_crops packed CropBoxArgs
+// (pack_crop_args, crop_args_bytes each); tile_cnt / tile_off: n_crops * crop_tiles(n) words;
+// totals: n_crops words. The scatter writes crop c at out + base_of[c], in input order.
+size_t crop_args_bytes();
+void pack_crop_args(const float inv[9], const float t[3], float mn, float mx, void* dst);
+void launch_crop_count_multi(hipStream_t s, int n, int n_crops, const void* args, const float4* pts,
+                             uint32_t* tile_cnt, uint32_t* tile_off, uint32_t* totals);
+void launch_crop_scatter_multi(hipStream_t s, int n, int n_crops, const void* args, const float4* pts,
+                               const uint32_t* tile_off, const uint32_t* base_of, float4* out);
 void launch_solve6(hipStream_t s, const double* A, const double* b, double* x, int32_t* path);
 
 // ---- kd-tree construction (kernels_tree.hip) ---------------------------------------------

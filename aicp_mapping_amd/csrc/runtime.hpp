@@ -171,6 +171,9 @@ struct aicp_hip_ctx {
   aicp_hip_batch* oneshot = nullptr;  // buffers of aicp_hip_align_batch, kept across calls
   hipEvent_t pf_ev[8] = {};
   aicp::rt::SeqState* seq = nullptr;  // aicp_hip_sequence_run's buffers (sequence.cpp), kept across calls
+  aicp_hip_batch* mapbatch = nullptr;  // aicp_hip_map_register_batch's batch buffers
+  aicp::rt::DevBuf crop_ws;            // its crop work space
+  aicp::rt::PinBuf pin_crop;
 };
 
 #define HIPC(x)                                                                   \

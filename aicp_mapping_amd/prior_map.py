@@ -58,6 +58,29 @@ class PriorMap:
                                                n, C.byref(m)))
         return out[:m.value].copy()
 
+    def register_batch(self, readings, poses, mn: float = -15.0, mx: float = 15.0, cfg=None, flags: int = 0):
+        """Localization-only registration of a batch (aicp_hip_map_register_batch): reading i
+        against this map cropped on the device around poses[i] (4x4 row-major prior pose), overlap
+        fixed at 50 % (app.cpp:41-51,123-127). readings: list of (N, 3|4|8|12) float32 rows.
+        Returns (T[n, 4, 4] row-major, list of stats dicts, rc)."""
+        cfg = cfg or L.default_config()
+        n = len(readings)
+        arr = (L.Cloud * n)()
+        keep = []
+        for i, r in enumerate(readings):
+            P = np.asarray(poses[i], np.float64).reshape(4, 4)
+            c, k = L.make_cloud(r, P[:3, 3])
+            arr[i] = c
+            keep.append(k)
+        pz = np.ascontiguousarray(np.stack([np.asarray(p, np.float32).reshape(4, 4).T.reshape(16) for p in poses]))
+        outT = np.zeros((n, 16), np.float32)
+        st = (L.IcpStats * n)()
+        rc = L.lib.aicp_hip_map_register_batch(self.ctx.h, C.byref(cfg), self.h, float(mn), float(mx), arr, L._fptr(pz),
+                                               n, int(flags), L._fptr(outT), st)
+        if rc != L.AICP_OK:
+            self.ctx.check(rc)
+        return outT.reshape(-1, 4, 4).transpose(0, 2, 1).copy(), [x.as_dict() for x in st], rc
+
     def merge(self, points, correction) -> None:
         """*map = *map + transformPointCloud(points, correction); correction a 4x4 (row-major)."""
         pts = L.as_points(points)

@@ -91,6 +91,14 @@ typedef struct {
   double read_origin[3]; /* sensor origin of the reading                          */
 } aicp_pair;
 
+/* One cloud with its sensor origin (the sequence and localization entry points). */
+typedef struct {
+  const float* pts;      /* x, y, z at `stride` bytes */
+  uint64_t n;
+  uint64_t stride;
+  double origin[3];      /* prior pose translation = sensor origin (octrees_overlap.cpp:229-230) */
+} aicp_cloud;
+
 /* flags for aicp_hip_align_batch / aicp_hip_batch_run */
 #define AICP_RUN_OVERLAP 1      /* compute overlap and auto-tune the trimmed ratio */
 #define AICP_RUN_ICP 2          /* run the ICP registration                        */
@@ -202,6 +210,15 @@ int aicp_hip_map_download(aicp_hip_ctx* ctx, const aicp_hip_map* map, float* out
 /* getPointsInOrientedBox on the map (aicp_hip_crop_box semantics), kept points to out */
 int aicp_hip_map_crop(aicp_hip_ctx* ctx, const aicp_hip_map* map, float min, float max, const float origin[16],
                       float* out /* 3*cap */, size_t cap, size_t* out_n);
+/* Localization-only batch (localize_against_prior_map, app.cpp:41-51,123-127): reading i is
+ * registered against the map cropped on the device to [min, max]^3 around its prior pose
+ * poses[16 i .. 16 i + 15] (getPointsInOrientedBox, Matrix4f column-major); the crop goes straight
+ * into the batch's reference array (no host round trip). The overlap is fixed at 50 %, so the
+ * trimmed ratio is aicp_hip_autotune_ratio(50) = 0.5 whatever cfg->trimmed_ratio says.
+ * flags: AICP_RUN_TIME_NN only. An empty crop is AICP_ERR_INVALID. */
+int aicp_hip_map_register_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_hip_map* map, float min,
+                                float max, const aicp_cloud* readings, const float* poses /* 16*n */, size_t n,
+                                int flags, float* out_T /* 16*n */, aicp_icp_stats* stats /* n, nullable */);
 /* map += T * pts (pcl::transformPointCloud, T column-major float[16]) */
 int aicp_hip_map_merge(aicp_hip_ctx* ctx, aicp_hip_map* map, const float* pts, size_t n, size_t stride,
                        const float T[16]);
@@ -235,12 +252,6 @@ int aicp_hip_last_phase_ms(const aicp_hip_ctx* ctx, double out_ms[5]);
  * the stream, as the uncaught exception ends App's worker (app.cpp:210).
  * Inputs are host buffers (pre-filtered clouds, as App passes read_prefiltered); everything
  * from the upload to the corrections runs on the device, the next reference included. */
-typedef struct {
-  const float* pts;      /* x, y, z at `stride` bytes */
-  uint64_t n;
-  uint64_t stride;
-  double origin[3];      /* prior pose translation = sensor origin (octrees_overlap.cpp:229-230) */
-} aicp_cloud;
 
 typedef struct {
   int32_t reference_update_frequency; /* 5 (aicp.launch:61) */

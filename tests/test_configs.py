@@ -1,0 +1,138 @@
+"""The BASELINE.json configurations at their full sizes, through the C-ABI.
+
+C2 runs in tests/test_sequence.py (the frame-to-reference stream). Here:
+  C3  one KITTI HDL-64-sized pair, N = M = 600 000: overlap + auto-tuned ratio + ICP against the
+      oracle (T within 1e-6 rad / 1e-5 m, iterations, touch and key counts equal);
+  C4  localization-only: a 1 M-point map resident on the device, each reading's reference cropped
+      on the device around its prior pose (getPointsInOrientedBox) and fed straight into the
+      batch (aicp_hip_map_register_batch), r = 0.5; against the oracle's crop + ICP;
+  C5  1024 independent pairs of 60 000 points in one batch: property checks over the whole batch
+      (drift recovered, repeatable, copies of a pair give its result bit for bit) and 8 sampled
+      pairs against the oracle.
+Match: app.cpp:41-51,123-127,187-216.
+"""
+import os
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+import pytest
+
+from aicp_mapping_amd import synthetic as sy
+
+pytestmark = pytest.mark.gpu
+RES = float(np.float32(0.2))
+
+
+@pytest.fixture(scope="module")
+def L():
+    import aicp_mapping_amd._lib as L
+
+    return L
+
+
+@pytest.fixture(scope="module")
+def ctx(L):
+    c = L.Context(0)
+    yield c
+    c.close()
+
+
+def test_c3_full_size_pair(ctx, oracle, L):
+    pr = sy.make_pair(600000, 600000, seed=3)
+    assert len(pr.ref) == len(pr.read) == 600000
+    T, st, rc = ctx.align_batch([dict(ref=pr.ref, read=pr.read, ref_origin=pr.ref_origin, read_origin=pr.read_origin)],
+                                flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP, resolution=RES)
+    assert rc == 0
+    ov, cnt = oracle.overlap(pr.ref, pr.ref_origin, pr.read, pr.read_origin, RES)
+    assert st[0]["overlap_keys"] == [int(c) for c in cnt]
+    ratio = oracle.autotune_ratio(ov)
+    assert st[0]["trimmed_ratio"] == np.float32(ratio)
+    rc1, T1, st1 = oracle.icp(pr.ref, pr.read, oracle.default_config(trimmed_ratio=ratio))
+    assert rc1 == 0
+    r, t = sy.rot_err(T1, T[0])
+    assert r < 1e-6 and t < 1e-5, (r, t)
+    assert st[0]["iterations"] == st1.iterations
+    assert (st[0]["nn_points_touched"], st[0]["nn_nodes_touched"]) == (st1.nn_points_touched, st1.nn_nodes_touched)
+
+
+def _c4_map(seed, n_map):
+    scene = sy.make_scene(seed)
+    rng = np.random.default_rng(seed * 7919 + 77)
+    mp = sy.sample_scene(scene, rng, np.array([0.0, 0.0, 0.7]), half=40.0)
+    assert len(mp) >= n_map
+    return mp[rng.choice(len(mp), size=n_map, replace=False)].astype(np.float32)
+
+
+def _c4_reading(seed, i, n_points, yaw_deg):
+    """Reading i of a VLP-16 stream along x in the drifted odometry frame, and its prior pose
+    (the sensor pose in that frame: drift^-1 * [R_z(yaw) | o])."""
+    scene = sy.make_scene(seed)
+    Tg = sy.T_GT
+    Ti = np.linalg.inv(Tg)
+    o_w = np.array([(i + 1) * 0.3, 0.0, 0.7])
+    rng = np.random.default_rng(seed * 7919 + 5000 + i)
+    w = sy._subsample_raster(sy.sample_scene(scene, rng, o_w, half=30.0), n_points, rng)
+    read = (w @ Ti[:3, :3].T + Ti[:3, 3]).astype(np.float32)
+    pose_w = sy.make_T(yaw_deg=yaw_deg, pitch_deg=0.0, roll_deg=0.0, t=o_w)
+    return read, Ti @ pose_w, Tg
+
+
+def test_c4_map_crop_feeds_registration(ctx, oracle, L):
+    from aicp_mapping_amd.prior_map import PriorMap
+
+    mp = _c4_map(1, 1000000)
+    pm = PriorMap(ctx, mp)
+    reads, poses, gts = zip(*[_c4_reading(1, i, 120000, yaw) for i, yaw in ((3, 0.0), (10, 25.0))])
+    T, st, rc = pm.register_batch(list(reads), list(poses), -15.0, 15.0)
+    assert rc == 0
+    for i in range(2):
+        crop, rpy = oracle.crop_box(mp, -15.0, 15.0, poses[i])
+        dev_crop = pm.crop(-15.0, 15.0, poses[i])
+        np.testing.assert_array_equal(dev_crop, crop)  # the crop the batch registered against
+        assert 150000 < len(crop) < 400000
+        rc1, T1, st1 = oracle.icp(crop, reads[i], oracle.default_config(trimmed_ratio=0.5))
+        assert rc1 == 0 and st[i]["trimmed_ratio"] == np.float32(0.5)
+        r, t = sy.rot_err(T1, T[i])
+        assert r < 1e-6 and t < 1e-5, (i, r, t)
+        assert st[i]["iterations"] == st1.iterations
+        assert (st[i]["nn_points_touched"], st[i]["nn_nodes_touched"]) == (st1.nn_points_touched,
+                                                                           st1.nn_nodes_touched)
+    pm.free()
+
+
+def _c5_pair(seed):
+    pr = sy.make_pair(60000, 60000, seed=seed)
+    return pr.ref, pr.read, pr.ref_origin, pr.read_origin, pr.T_gt
+
+
+def test_c5_1024_pairs(ctx, oracle, L):
+    """64 distinct pairs (seeds 1000..1063), each present 16 times as separate arrays (no shared
+    reference), so the batch holds 1024 pairs of 60 000 points like C5."""
+    with ProcessPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        base = list(ex.map(_c5_pair, range(1000, 1064)))
+    pairs = []
+    for k in range(16):
+        for ref, read, ro, do, _ in base:
+            pairs.append(dict(ref=ref.copy(), read=read.copy(), ref_origin=ro, read_origin=do))
+    assert len(pairs) == 1024
+    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+    b = ctx.upload(pairs)
+    b.run(L.default_config(), RES, flags)
+    T1 = b.transforms()
+    st = b.stats_dicts()
+    b.run(L.default_config(), RES, flags)
+    np.testing.assert_array_equal(T1, b.transforms())  # repeatable
+    b.free()
+    for k in range(1, 16):  # copies give the same result wherever they sit in the batch
+        np.testing.assert_array_equal(T1[64 * k:64 * (k + 1)], T1[:64])
+    assert all(s["status"] == 0 and 1 <= s["iterations"] <= 20 for s in st)
+    errs = np.array([sy.rot_err(base[i % 64][4], T1[i]) for i in range(64)])
+    assert np.median(errs[:, 0]) < 5e-3 and np.median(errs[:, 1]) < 5e-2, np.median(errs, 0)
+    for i in (0, 9, 18, 27, 36, 45, 54, 63):  # 8 sampled pairs against the oracle
+        ref, read, ro, do, _ = base[i]
+        ov, cnt = oracle.overlap(ref, ro, read, do, RES)
+        assert st[i]["overlap_keys"] == [int(c) for c in cnt]
+        rc1, To, sto = oracle.icp(ref, read, oracle.default_config(trimmed_ratio=oracle.autotune_ratio(ov)))
+        r, t = sy.rot_err(To, T1[i])
+        assert rc1 == 0 and r < 1e-6 and t < 1e-5, (i, r, t)
+        assert st[i]["iterations"] == sto.iterations
