@@ -397,6 +397,16 @@ class Context:
         T = outT.reshape(-1, 4, 4).transpose(0, 2, 1).copy()
         return T, [s.as_dict() for s in st], rc
 
+    def register(self, ref, read, cfg=None):
+        """aicp_hip_register (registerClouds: one pair, identity initial T, the chain's ratio):
+        returns (T 4x4 row-major, stats dict)."""
+        cfg = cfg or default_config()
+        p, keep = make_pair(ref, read)
+        outT = np.zeros(16, np.float32)
+        st = IcpStats()
+        self.check(lib.aicp_hip_register(self.h, C.byref(cfg), C.byref(p), _fptr(outT), C.byref(st)))
+        return outT.reshape(4, 4).T.copy(), st.as_dict()
+
     def upload(self, pairs):
         return ResidentBatch(self, pairs)
 

@@ -369,3 +369,25 @@ def recorded_sequence_pairs(directory: str, ref_every: int = 5, max_readings: in
         if n_read % ref_every == 0:
             ref, ref_pose = xyz, p.pose
     return pairs
+
+
+def recorded_stream(directory: str, max_readings: int | None = None):
+    """The input of App's stream from a recorded directory (processFromFile, app.cpp:250-279): the
+    first cloud (first reference), then the readings with their recorded pose translations as
+    sensor origins. Returns synthetic.Stream (T_gt entries None: recordings carry no ground
+    truth); aicp_hip_sequence_run then builds the references from the corrected readings."""
+    from .synthetic import Stream
+
+    first = first_origin = None
+    reads, origins = [], []
+    for p, xyz in process_from_file(directory):
+        if first is None:
+            first, first_origin = xyz, p.pose[:3, 3].copy()
+            continue
+        reads.append(xyz)
+        origins.append(p.pose[:3, 3].copy())
+        if max_readings is not None and len(reads) >= max_readings:
+            break
+    if first is None:
+        return None
+    return Stream(first, first_origin, reads, origins, [None] * len(reads))

@@ -177,24 +177,32 @@ def make_stream(n_readings: int = 64, n_points: int = 120000, seed: int = 1, ste
     along x, each perturbed by the odometry drift T_gt^-1. Unlike make_sequence, references are
     not sampled here: App builds them from the corrected readings. jumps: {reading index: extra
     translation (3,)} of that reading's drift, to make App drop it (max_correction_magnitude)."""
-    T_gt = T_GT if T_gt is None else np.asarray(T_gt, np.float64)
-    scene = make_scene(seed)
+    first, o0 = stream_first(seed, n_points, sensor_z, half)
+    out = [stream_reading(seed, i, n_points, step, sensor_z, half, T_gt, (jumps or {}).get(i))
+           for i in range(n_readings)]
+    return Stream(first, o0, [r[0] for r in out], [r[1] for r in out], [r[2] for r in out])
+
+
+def stream_first(seed: int, n_points: int, sensor_z: float = 0.7, half: float = 30.0):
+    """make_stream's first cloud and its origin."""
     o0 = np.array([0.0, 0.0, sensor_z])
     rng0 = np.random.default_rng(seed * 7919 + 1000)
-    first = _subsample_raster(sample_scene(scene, rng0, o0, half=half), n_points, rng0).astype(np.float32)
-    reads, origins, gts = [], [], []
-    for i in range(n_readings):
-        Tg = T_gt.copy()
-        if jumps and i in jumps:
-            Tg[:3, 3] += np.asarray(jumps[i], np.float64)
-        Ti = np.linalg.inv(Tg)
-        o_w = np.array([(i + 1) * step, 0.0, sensor_z])
-        rng = np.random.default_rng(seed * 7919 + 5000 + i)
-        w = _subsample_raster(sample_scene(scene, rng, o_w, half=half), n_points, rng)
-        reads.append((w @ Ti[:3, :3].T + Ti[:3, 3]).astype(np.float32))
-        origins.append(Ti[:3, :3] @ o_w + Ti[:3, 3])
-        gts.append(Tg)
-    return Stream(first, o0, reads, origins, gts)
+    first = _subsample_raster(sample_scene(make_scene(seed), rng0, o0, half=half), n_points, rng0)
+    return first.astype(np.float32), o0
+
+
+def stream_reading(seed: int, i: int, n_points: int, step: float = 0.3, sensor_z: float = 0.7, half: float = 30.0,
+                   T_gt=None, jump=None):
+    """make_stream's reading i: (points, origin, T_gt) (independent of the others, so a process
+    pool can build a stream)."""
+    Tg = (T_GT if T_gt is None else np.asarray(T_gt, np.float64)).copy()
+    if jump is not None:
+        Tg[:3, 3] += np.asarray(jump, np.float64)
+    Ti = np.linalg.inv(Tg)
+    o_w = np.array([(i + 1) * step, 0.0, sensor_z])
+    rng = np.random.default_rng(seed * 7919 + 5000 + i)
+    w = _subsample_raster(sample_scene(make_scene(seed), rng, o_w, half=half), n_points, rng)
+    return (w @ Ti[:3, :3].T + Ti[:3, 3]).astype(np.float32), Ti[:3, :3] @ o_w + Ti[:3, 3], Tg
 
 
 def make_cube(min_corner=-2.0, max_corner=2.0, step=0.05):

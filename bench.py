@@ -1,17 +1,22 @@
 #!/usr/bin/env python3
-"""Benchmark: aligned clouds/s (+ ICP iterations/s) on the C2 workload.
+"""Benchmark: aligned clouds/s (+ ICP iterations/s) on the BASELINE.json workloads.
 
-C2 = ANYmal VLP-16 clouds of the batch_size = 80 accumulation (aicp_ros_node.cpp:40),
-N = M = 120 000 points, registered frame-to-reference in a streamed sequence of 64 readings
-with the reference replaced every 5 readings (aicp.launch reference_update_frequency). A step
-= one such sequence run end to end on the GPU: per pair octree overlap -> auto-tuned trimmed
-ratio -> ICP; per reference window centroid + kd-tree + SurfaceNormal built once (§8(f)
-rank 1). Inputs are resident in HBM before timing (aicp_hip_batch_upload); each rank
-registers its own sequence (weak scaling) and RCCL all-gathers the per-pair {T, iterations,
-inlier ratio}.
+Default (C2): App's frame-to-reference stream (app.cpp:282-414) of an ANYmal VLP-16 batch_size=80
+accumulation: a first cloud, then 64 readings of N = 120 000 points, each registered against the
+current reference (octree overlap -> auto-tuned trimmed ratio -> ICP), the reference rebuilt from
+every 5th accepted reading corrected by its own T (the dependency chain of the reference). A
+step = one aicp_hip_sequence_run over the 64 host clouds: H2D, every device phase and the read-back
+of T are inside the timed region (§8(d): host xyz in -> T out). Each rank runs its own stream
+(weak scaling); RCCL all-gathers the per-reading {T, iterations, inlier ratio}.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs 64] [--ref-every 5] [--points N]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|single|prefilter]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+Other configs: c3 (KITTI HDL-64 stream, N = 600 000), c4 (localization against a resident
+1 M-point map, device crops as references, r = 0.5), c5 (1024 independent pairs of 60 000 points
+sharded i mod G), single (one C2 pair through aicp_hip_register, latency), prefilter (§8(f)
+rank 2). The line carries the NN kernel's roofline (HIP events on its stream), the oracle as
+cpu_baseline (median of 5 bounded samples on this host) and parity against it.
 """
 from __future__ import annotations
 
@@ -38,99 +43,6 @@ def cpu_model():
     except OSError:
         pass
     return platform.processor()
-
-
-def make_pairs(n_readings, ref_every, n_points, seed):
-    from aicp_mapping_amd import synthetic as sy
-
-    return [dict(ref=pr.ref, read=pr.read, ref_origin=pr.ref_origin, read_origin=pr.read_origin, T_gt=pr.T_gt)
-            for pr in sy.make_sequence(n_readings, ref_every, n_points, seed=seed)]
-
-
-def _c5_pair(seed_points):
-    from aicp_mapping_amd import synthetic as sy
-
-    seed, n = seed_points
-    pr = sy.make_pair(n, n, seed=seed)
-    return dict(ref=pr.ref, read=pr.read, ref_origin=pr.ref_origin, read_origin=pr.read_origin, T_gt=pr.T_gt)
-
-
-def make_c5_pairs(n_total, n_points, rank, world):
-    """C5: independent pairs, seeds 1000..; rank g takes pairs i = g mod G
-    (sharding.shard_pairs). Generated in a process pool (16 workers: the box's CPU share)."""
-    from concurrent.futures import ProcessPoolExecutor
-
-    from aicp_mapping_amd import sharding as sh
-
-    mine = sh.shard_pairs(n_total, world, rank)
-    with ProcessPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
-        return list(ex.map(_c5_pair, [(1000 + i, n_points) for i in mine], chunksize=4))
-
-
-def make_c4_pairs(n_readings, n_points, map_points, crop, seed):
-    """C4 localization-only: a resident map of map_points points over the whole
-    scene; reading i (N points, sensor moving along x) registers against the map points within
-    +-crop m of its prior position (the cropped map, M ~ 250k); overlap fixed at 50 % => r = 0.5.
-    The crop is input preparation here (an axis-aligned box around the prior position)."""
-    from aicp_mapping_amd import synthetic as sy
-
-    seq = sy.make_sequence(n_readings, n_readings, n_points, seed=seed)
-    scene = sy.make_scene(seed)
-    rng = np.random.default_rng(seed * 7919 + 77)
-    mp = sy.sample_scene(scene, rng, np.array([0.0, 0.0, 0.7]), half=40.0)
-    if len(mp) > map_points:
-        mp = mp[rng.choice(len(mp), size=map_points, replace=False)]
-    mp = mp.astype(np.float32)
-    out = []
-    for i, pr in enumerate(seq):
-        o = np.array([(i + 1) * 0.3, 0.0, 0.7])  # prior position of reading i (make_sequence's path)
-        m = np.all(np.abs(mp - o.astype(np.float32)) <= crop, axis=1)
-        ref = np.ascontiguousarray(mp[m])
-        out.append(dict(ref=ref, read=pr.read, ref_origin=o, read_origin=pr.read_origin, T_gt=pr.T_gt))
-    return out, len(mp)
-
-
-def cpu_baseline(pairs, res, budget_s, cfg_ratio, run_overlap, workload):
-    """The oracle (single-thread C++ restatement of the libpointmatcher chain) on a bounded sample
-    of the same workload as the GPU run: whole pairs, as many as fit the budget. With the overlap
-    (C2, C3, C5) each pair runs overlap -> auto-tuned ratio -> ICP like the device; without it
-    (C4: localization against the map, overlap fixed) ICP runs at the configured ratio."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle as po
-
-    po.lib()
-    done = 0
-    iters = 0
-    Ts = []
-    t0 = time.perf_counter()
-    for p in pairs:
-        ratio = cfg_ratio
-        if run_overlap:
-            ov, _ = po.overlap(p["ref"], p["ref_origin"], p["read"], p["read_origin"], res)
-            ratio = po.autotune_ratio(ov)
-        rc, T, st = po.icp(p["ref"], p["read"], po.default_config(trimmed_ratio=ratio))
-        Ts.append(T)
-        done += 1
-        iters += st.iterations
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    steps = "overlap + ratio + ICP" if run_overlap else "ICP at r = %.2f" % cfg_ratio
-    return dict(value=done / dt, unit="aligned_clouds/s", cores=1, kind="port",
-                sample=f"first {done} pair(s) of [{workload}] ({steps}, N={pairs[0]['read'].shape[0]}, "
-                       f"M={pairs[0]['ref'].shape[0]}) on 1 host core ({cpu_model()}, nproc {os.cpu_count()}); "
-                       f"{iters} ICP iterations in {dt:.1f} s",
-                icp_iters_per_s=iters / dt), Ts
-
-
-def load_traffic():
-    path = os.path.join(ROOT, "profiles", "nn_traffic.json")
-    if os.path.exists(path):
-        try:
-            return json.load(open(path))
-        except (OSError, ValueError):
-            return None
-    return None
 
 
 def make_raw_clouds(n_clouds, half, spacing, seed):
@@ -262,29 +174,72 @@ def bench_prefilter(args):
         dist.destroy_process_group()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "prefilter"], default="c2",
-                    help="BASELINE.json workload (default c2: the metric's configuration); prefilter: the "
-                         "SURVEY §8(f) rank 2 pre-filter on C2's raw clouds")
-    ap.add_argument("--pairs", type=int, default=None, help="readings (pairs) per step per GPU")
-    ap.add_argument("--ref-every", type=int, default=5, help="readings per reference window")
-    ap.add_argument("--data", default=None,
-                    help="recorded directory (aicp_input_poses.csv + cloud_*.pcd) replayed instead of "
-                         "synthetic C2 clouds; the workload then names the directory")
-    ap.add_argument("--points", type=int, default=None)
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--lanes", type=int, default=1,
-                    help="independent copies of the step in flight on the GPU (each its own context, streams "
-                         "and resident batch, driven by its own host thread); the K timed steps are shared out")
-    args = ap.parse_args()
-    if args.config == "prefilter":
-        return bench_prefilter(args)
+def _stream_reading(a):
+    from aicp_mapping_amd import synthetic as sy
 
+    seed, i, n = a
+    return sy.stream_reading(seed, i, n)
+
+
+def make_stream(n_readings, n_points, seed):
+    """synthetic.make_stream built in a process pool (16 workers: the box's CPU share)."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    from aicp_mapping_amd import synthetic as sy
+
+    first, o0 = sy.stream_first(seed, n_points)
+    with ProcessPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        out = list(ex.map(_stream_reading, [(seed, i, n_points) for i in range(n_readings)]))
+    return sy.Stream(first, o0, [r[0] for r in out], [r[1] for r in out], [r[2] for r in out])
+
+
+def _c5_pair(seed_points):
+    from aicp_mapping_amd import synthetic as sy
+
+    seed, n = seed_points
+    pr = sy.make_pair(n, n, seed=seed)
+    return dict(ref=pr.ref, read=pr.read, ref_origin=pr.ref_origin, read_origin=pr.read_origin, T_gt=pr.T_gt)
+
+
+def make_c5_pairs(n_total, n_points, rank, world):
+    """C5: independent pairs, seeds 1000..; rank g takes pairs i = g mod G."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    from aicp_mapping_amd import sharding as sh
+
+    mine = sh.shard_pairs(n_total, world, rank)
+    with ProcessPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        return list(ex.map(_c5_pair, [(1000 + i, n_points) for i in mine], chunksize=4))
+
+
+def _c4_reading(a):
+    from aicp_mapping_amd import synthetic as sy
+
+    seed, i, n = a
+    read, origin, Tg = sy.stream_reading(seed, i, n)
+    Ti = np.linalg.inv(Tg)
+    pose = Ti @ sy.make_T(yaw_deg=0.0, pitch_deg=0.0, roll_deg=0.0, t=((i + 1) * 0.3, 0.0, 0.7))
+    return read, pose, Tg
+
+
+def make_c4(n_readings, n_points, map_points, seed):
+    """C4 localization-only: a resident map of map_points over the whole scene and
+    a stream of VLP-16 readings with their prior poses (drifted odometry)."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    from aicp_mapping_amd import synthetic as sy
+
+    scene = sy.make_scene(seed)
+    rng = np.random.default_rng(seed * 7919 + 77)
+    mp = sy.sample_scene(scene, rng, np.array([0.0, 0.0, 0.7]), half=40.0)
+    if len(mp) > map_points:
+        mp = mp[rng.choice(len(mp), size=map_points, replace=False)]
+    with ProcessPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        out = list(ex.map(_c4_reading, [(seed, i, n_points) for i in range(n_readings)]))
+    return mp.astype(np.float32), [o[0] for o in out], [o[1] for o in out], [o[2] for o in out]
+
+
+def init_dist():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -295,245 +250,512 @@ def main():
 
         torch.cuda.set_device(local_rank)
         dist.init_process_group(backend="nccl")
+    return rank, world, local_rank, dist
 
+
+def sync(dist):
+    if dist is not None:
+        import torch
+
+        torch.cuda.synchronize()
+        dist.barrier()
+
+
+def median_rate(fn, reps):
+    """fn() -> (units, seconds) per repetition; the median rate and the per-rep rates."""
+    rates = []
+    for _ in range(reps):
+        u, dt = fn()
+        rates.append(u / dt)
+    return float(np.median(rates)), rates
+
+
+def roofline_nn(t, kernel):
+    """roofline object of the NN kernel from aicp_hip_last_nn_timing sums (HIP events recorded
+    on the stream the NN kernel runs on)."""
+    n = max(1, t["launches"])
+    avg_ms = t["total_ms"] / n
+    achieved = (t["bytes"] / n) / (avg_ms * 1e-3) / 1e9 if t["launches"] else 0.0
+    return {
+        "kernel": kernel,
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "avg_launch_us": round(1e3 * avg_ms, 2),
+        "launches": t["launches"],
+        "algorithmic_bytes_per_launch": round(t["bytes"] / n),
+        "bytes_model": "N*(12+8) + V*16 + W*8 (SURVEY §8(d)); V, W = touched points / inner nodes",
+    }
+
+
+def load_traffic(name):
+    """PMC traffic (HBM bytes per NN launch) committed under profiles/ from a separate rocprofv3
+    --pmc pass of the same workload (tools/profile.sh); None when absent."""
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
+
+
+def base_line(args, world, metric, value, unit, ms_per_step, dtype, data, config, scaling="weak", hib=True):
+    return {
+        "metric": metric,
+        "value": round(value, 3),
+        "unit": unit,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": hib,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": data,
+        "config": config,
+    }
+
+
+METRIC = "aligned_clouds_per_s (ICP iterations/sec + aligned clouds/sec, 80-scan VLP-16 batch)"
+DTYPE = "f32 (point arithmetic; 6x6/3x3 reductions and solves in f64)"
+DATA = "synthetic (seeded planar scene per SURVEY §8(d); no recordings in the reference)"
+CHAIN = ("icp_autotuned_default.yaml (SurfaceNormal knn20, KDTree knn1 eps3.16, TrimmedDist auto-tuned, "
+         "PointToPlane, Counter20 + Differential)")
+
+
+def bench_stream(args):
+    """C2 / C3: App's frame-to-reference stream, host clouds in -> corrections out."""
     import aicp_mapping_amd._lib as L
     from aicp_mapping_amd import sharding as sh
+    from aicp_mapping_amd import synthetic as sy
 
-    res = float(np.float32(0.2))  # octomapResolution read as<float> (yaml_configurator.cpp:81)
-    cfg = L.default_config()
-    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
-    extra = {}
-    if args.data:
+    rank, world, local_rank, dist = init_dist()
+    if args.data:  # a recording in the reference's offline layout (§8(f) rank 3)
         from aicp_mapping_amd import cloud_io
 
-        pairs = cloud_io.recorded_sequence_pairs(args.data, args.ref_every, args.pairs)
-        if not pairs:
+        st = cloud_io.recorded_stream(args.data, args.pairs)
+        if st is None or not st.readings:
             raise SystemExit(f"--data {args.data}: no readable pose/cloud pairs")
-        args.pairs = len(pairs)
-        args.points = int(np.mean([len(p["read"]) for p in pairs]))
-        workload = "recorded sequence %s: %d readings (mean N=%d), reference updated every %d" % (
-            os.path.basename(os.path.abspath(args.data)), args.pairs, args.points, args.ref_every)
-    elif args.config in ("c2", "c3"):
-        args.pairs = args.pairs or 64
-        args.points = args.points or (120000 if args.config == "c2" else 600000)
-        # each rank streams its own sequence (seed 1 + rank): weak scaling over independent pairs
-        pairs = make_pairs(args.pairs, args.ref_every, args.points, seed=1 + rank)
-        workload = ("%s: %s batch_size=80 clouds, N=M=%d, frame-to-reference sequence of %d readings, "
-                    "reference updated every %d" % (args.config.upper(), "ANYmal VLP-16" if args.config == "c2"
-                                                    else "KITTI HDL-64", args.points, args.pairs, args.ref_every))
-    elif args.config == "c4":
-        args.pairs = args.pairs or 64
-        args.points = args.points or 120000
-        pairs, n_map = make_c4_pairs(args.pairs, args.points, 1000000, 15.0, seed=1 + rank)
-        cfg = L.default_config(trimmed_ratio=0.5)  # overlap fixed at 50 % (app.cpp:123-127)
-        flags = L.AICP_RUN_ICP
-        extra = {"map_points": n_map, "mean_ref_points": int(np.mean([len(p["ref"]) for p in pairs]))}
-        workload = ("C4: localization-only, %d-pt map cropped to +-15 m per reading, %d VLP-16 readings of "
-                    "N=%d, r=0.5" % (n_map, args.pairs, args.points))
+        n_read = len(st.readings)
+        n_pts = int(np.mean([len(r) for r in st.readings]))
     else:
-        args.points = args.points or 60000
-        n_total = args.pairs or 1024
-        pairs = make_c5_pairs(n_total, args.points, rank, world)
-        args.pairs = len(pairs)
-        extra = {"pairs_total": n_total}
-        workload = "C5: %d independent KITTI-like pairs, N=M=%d, seeds 1000.., sharded i mod G" % (
-            n_total, args.points)
-    order = os.environ.get("AICP_BENCH_READ_ORDER")  # experiment: host-side reading order
-    if order:
-        rng = np.random.default_rng(0)
-        for p in pairs:
-            r = p["read"]
-            if order == "shuffle":
-                idx = rng.permutation(len(r))
-            else:  # morton on 0.25 m cells
-                q = (np.floor(r / 0.25).astype(np.int64) & 1023)
-                key = np.zeros(len(r), np.int64)
-                for b in range(10):
-                    for a in range(3):
-                        key |= ((q[:, a] >> b) & 1) << (3 * b + a)
-                idx = np.argsort(key, kind="stable")
-            p["read"] = np.ascontiguousarray(r[idx])
-    n_refs = len({id(p["ref"]) for p in pairs})
+        n_read = args.pairs or 64
+        n_pts = args.points or (120000 if args.config == "c2" else 600000)
+        st = make_stream(n_read, n_pts, seed=1 + rank)
     ctx = L.Context(local_rank)
-    batch = ctx.upload(pairs)
+    cfg = L.default_config()
+    prm = L.default_sequence_params(reference_update_frequency=args.ref_every,
+                                    flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_TIME_NN)
 
-    # global index of each local pair for the result gather (C5: the i mod G shard; the other
-    # configs: every rank its own sequence, rank-major)
-    pair_index = (sh.shard_pairs(extra["pairs_total"], world, rank) if args.config == "c5" and not args.data
-                  else None)
-
-    def gather():
-        if dist is None:
-            return None
-        st = batch.stats
-        rec = sh.pack_records(batch.outT, [s.iterations for s in st], [s.inlier_ratio for s in st])
-        return sh.gather_records(rec, dist, device="cuda", pair_index=pair_index)
-
-    def sync():
+    def step():
+        T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, cfg, prm)
         if dist is not None:
-            import torch
-
-            torch.cuda.synchronize()
-            dist.barrier()
+            sh.gather_records(sh.pack_records(T.transpose(0, 2, 1).reshape(-1, 16),
+                                              [o["icp"]["iterations"] for o in out],
+                                              [o["icp"]["inlier_ratio"] for o in out]), dist, device="cuda")
+        return T, out
 
     for _ in range(args.warmup):
-        batch.run(cfg, res, flags)
-        gather()
-    sync()
-    nn_ms = nn_bytes = 0.0
-    nn_launches = 0
-    iters_total = 0
-    phases = np.zeros(5)
-    lanes = max(1, args.lanes)
-    if lanes > 1:
-        # further copies of the same step, each on its own context (streams, buffers, resident
-        # batch) and host thread, so one copy's tree builds and small ICP kernels fill the chip
-        # while another's NN launches run; the K timed steps are shared out lane by lane
-        import queue
-        import threading
-
-        lane_ctx = [(ctx, batch)]
-        for _ in range(lanes - 1):
-            c2 = L.Context(local_rank)
-            b2 = c2.upload(pairs)
-            for _ in range(max(1, args.warmup)):
-                b2.run(cfg, res, flags)
-            lane_ctx.append((c2, b2))
-        sync()
-        per_lane = [args.steps // lanes + (1 if i < args.steps % lanes else 0) for i in range(lanes)]
-        done_q = [queue.Queue() for _ in range(lanes)]
-
-        def lane_main(i):
-            c, b = lane_ctx[i]
-            for _ in range(per_lane[i]):
-                b.run(cfg, res, flags | L.AICP_RUN_TIME_NN)
-                done_q[i].put((c.last_nn_timing(), sum(s.iterations for s in b.stats), c.last_phase_ms(),
-                               b.outT.copy(), [s.iterations for s in b.stats], [s.inlier_ratio for s in b.stats]))
-
-        t0 = time.perf_counter()
-        th = [threading.Thread(target=lane_main, args=(i,)) for i in range(lanes)]
-        for x in th:
-            x.start()
-        for k in range(max(per_lane)):  # results gathered in a fixed (step, lane) order on every rank
-            for i in range(lanes):
-                if k >= per_lane[i]:
-                    continue
-                t, it, ph, outT, its, inl = done_q[i].get()
-                if dist is not None:
-                    sh.gather_records(sh.pack_records(outT, its, inl), dist, device="cuda", pair_index=pair_index)
-                nn_ms += t["total_ms"]
-                nn_bytes += t["bytes"]
-                nn_launches += t["launches"]
-                iters_total += it
-                phases += np.array([ph["overlap"], ph["normals"], ph["matcher_tree"], ph["icp_loop"], ph["total"]])
-        for x in th:
-            x.join()
-    else:
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            batch.run(cfg, res, flags | L.AICP_RUN_TIME_NN)
-            gather()
-            t = ctx.last_nn_timing()
-            nn_ms += t["total_ms"]
-            nn_bytes += t["bytes"]
-            nn_launches += t["launches"]
-            iters_total += sum(s.iterations for s in batch.stats)
-            ph = ctx.last_phase_ms()
-            phases += np.array([ph["overlap"], ph["normals"], ph["matcher_tree"], ph["icp_loop"], ph["total"]])
-    sync()
+        step()
+    sync(dist)
+    nn = dict(launches=0, total_ms=0.0, bytes=0.0)
+    iters = 0
+    dev_ms = wall_ms = 0.0
+    windows = replans = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        T, out = step()
+        t = ctx.last_nn_timing()
+        for k in ("launches", "total_ms", "bytes"):
+            nn[k] += t[k]
+        iters += sum(o["icp"]["iterations"] for o in out)
+        tm = ctx.last_sequence_timing()
+        dev_ms += tm["device_ms"]
+        wall_ms += tm["wall_ms"]
+        windows, replans = tm["windows"], tm["replans"]
+    sync(dist)
     elapsed = time.perf_counter() - t0
     if dist is not None:
         elapsed = sh.max_over_ranks(elapsed, dist, device="cuda")
-        iters_total = int(sh.sum_over_ranks(float(iters_total), dist, device="cuda"))
-
-    # PCIe-inclusive rate (not `value`): the same step from host buffers, upload + run + free
-    # (aicp_hip_align_batch); rank 0 alone, after the timed loop
-    pcie = None
-    if rank == 0 and not args.data:
-        tp = time.perf_counter()
-        reps = max(1, min(3, args.steps))
+        iters = int(sh.sum_over_ranks(float(iters), dist, device="cuda"))
+    # the same readings as a batch of independent pairs (r02's workload shape): reading i against
+    # the first cloud (i < 5) or the UNcorrected reading 5*(i//5)-1, uploaded once, run resident
+    batched = None
+    if rank == 0 and not args.no_batched:
+        refs = [(st.first, st.first_origin)] + [(st.readings[j], st.origins[j]) for j in range(4, n_read, 5)]
+        pairs = [dict(ref=refs[i // 5][0], read=st.readings[i], ref_origin=refs[i // 5][1],
+                      read_origin=st.origins[i]) for i in range(n_read)]
+        b = ctx.upload(pairs)
+        flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+        b.run(cfg, prm.resolution, flags)
+        nb = dict(launches=0, total_ms=0.0, bytes=0.0)
+        reps = max(3, args.steps)
+        tb = time.perf_counter()
         for _ in range(reps):
-            ctx.align_batch(pairs, cfg, res, flags)
-        pcie = {"clouds_per_s": round(reps * args.pairs / (time.perf_counter() - tp), 3),
-                "note": "host xyz in -> T out per step: H2D of all clouds, run, D2H (aicp_hip_align_batch)"}
-
-    # accuracy of the last step (synthetic ground truth)
-    from aicp_mapping_amd import synthetic as sy
-
-    errs = [sy.rot_err(p["T_gt"], T) for p, T in zip(pairs, batch.transforms()) if p["T_gt"] is not None]
-    st = batch.stats_dicts()
-
+            b.run(cfg, prm.resolution, flags | L.AICP_RUN_TIME_NN)
+            t = ctx.last_nn_timing()
+            for k in ("launches", "total_ms", "bytes"):
+                nb[k] += t[k]
+        dtb = time.perf_counter() - tb
+        b.free()
+        batched = {"clouds_per_s": round(reps * n_read / dtb, 3), "ms_per_step": round(1e3 * dtb / reps, 3),
+                   "roofline_nn": roofline_nn(nb, "k_icp_nn"),
+                   "note": "the same 64 readings as independent pairs against uncorrected references, all "
+                           "windows at once, inputs resident in HBM (aicp_hip_batch_run); not the stream's "
+                           "dependency chain, so not the headline"}
     if rank == 0:
-        total_pairs = (extra.get("pairs_total") or args.pairs * world) * args.steps
-        value = total_pairs / elapsed
-        avg_launch_ms = nn_ms / max(1, nn_launches)
-        achieved = (nn_bytes / max(1, nn_launches)) / (avg_launch_ms * 1e-3) / 1e9 if nn_launches else 0.0
-        # the committed PMC figure is per launch of the default C2 workload only
-        traffic = load_traffic() if (args.config == "c2" and not args.data) else None
-        out = {
-            "metric": "aligned_clouds_per_s (ICP iterations/sec + aligned clouds/sec, 80-scan VLP-16 batch)",
-            "value": round(value, 3),
-            "unit": "aligned clouds/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "strong" if args.config == "c5" else "weak",
-            "vs_baseline": None,
-            "dtype": "f32 (point arithmetic; 6x6/3x3 reductions and solves in f64)",
-            "data": ("recorded (%s)" % args.data) if args.data else
-                    "synthetic (seeded planar scene per SURVEY §8(d); no recordings in the reference)",
-            "config": {
-                "workload": workload,
-                "pairs_per_step_per_gpu": args.pairs,
-                "references_per_step_per_gpu": n_refs,
-                "chain": "icp_autotuned_default.yaml (SurfaceNormal knn20, KDTree knn1 eps3.16, "
-                         "TrimmedDist auto-tuned, PointToPlane, Counter20 + Differential)",
-                "overlap": "octree-equivalent voxel sets at 0.2 m" if flags & L.AICP_RUN_OVERLAP
-                           else "fixed 50 %% (r = %.2f)" % cfg.trimmed_ratio,
-                **extra,
-                "parallelism": "independent pairs sharded over ranks, RCCL all_gather of T",
-                "lanes": lanes,
-            },
-            "pcie_inclusive": pcie,
-            "icp_iters_per_s": round(iters_total / elapsed, 1),
-            "mean_iterations": float(np.mean([s["iterations"] for s in st])),
-            "phase_ms_per_step": dict(zip(["overlap_gpu (stream 1)", "normal_tree_and_normals_gpu (stream 2)",
-                                           "centroid_matcher_tree_gpu (stream 2)", "icp_loop_gpu", "total"],
-                                          [round(x / args.steps, 3) for x in phases])),
-            "accuracy_vs_ground_truth": {
-                "median_rot_rad": float(np.median([e[0] for e in errs])),
-                "median_trans_m": float(np.median([e[1] for e in errs])),
-                "note": "the reference chain (eps 3.16 approximate NN) stalls in local minima on some "
-                        "synthetic pairs; the oracle reproduces the same transforms (parity_vs_oracle)"}
-            if errs else None,
-            "roofline": {
-                "kernel": "k_icp_nn (transform + libnabo-order 1-NN over treelets + bucket scan)",
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic.get("bytes_per_launch") if traffic else None,
-                "avg_launch_us": round(1e3 * avg_launch_ms, 2),
-                "algorithmic_bytes_per_launch": round(nn_bytes / max(1, nn_launches)),
-                "bytes_model": "N*(12+8) + V*16 + W*8 (SURVEY §8(d)); V, W = touched points / inner nodes",
-            },
-        }
+        value = world * n_read * args.steps / elapsed
+        config = {"workload": "%s: App frame-to-reference stream, %s batch_size=80 clouds, N=M=%d, first cloud + "
+                              "%d readings, reference = every %dth accepted reading corrected on the device, "
+                              "max_correction_magnitude %.1f" % (
+                                  args.config.upper(), "ANYmal VLP-16" if args.config == "c2" else "KITTI HDL-64",
+                                  n_pts, n_read, args.ref_every, prm.max_correction_magnitude),
+                  "readings_per_step_per_gpu": n_read, "windows_per_step": windows, "replans": replans,
+                  "chain": CHAIN, "overlap": "octree-equivalent voxel sets at 0.2 m",
+                  "timed_region": "host clouds -> packing -> H2D -> device -> corrections (aicp_hip_sequence_run)",
+                  "parallelism": "one stream per rank (replicas), RCCL all_gather of T"}
+        out_line = base_line(args, world, METRIC, value, "aligned clouds/s", 1e3 * elapsed / args.steps, DTYPE, DATA,
+                             config)
+        if args.data:
+            config["workload"] = "recorded stream %s: first cloud + %d readings (mean N=%d), reference every %d" % (
+                os.path.basename(os.path.abspath(args.data)), n_read, n_pts, args.ref_every)
+            out_line["data"] = "recorded (%s)" % args.data
+        errs = [sy.rot_err(Tg, Tx) for Tg, Tx in zip(st.T_gt, T) if Tg is not None] or [(float("nan"),) * 2]
+        out_line.update({
+            "icp_iters_per_s": round(iters / elapsed, 1),
+            "mean_iterations": float(np.mean([o["icp"]["iterations"] for o in out])),
+            "device_ms_per_step": round(dev_ms / args.steps, 3),
+            "call_wall_ms_per_step": round(wall_ms / args.steps, 3),
+            "accuracy_vs_ground_truth": {"median_rot_rad": float(np.median([e[0] for e in errs])),
+                                         "median_trans_m": float(np.median([e[1] for e in errs])),
+                                         "note": "the reference chain (eps 3.16 approximate NN) stalls on this "
+                                                 "scene; the oracle gives the same transforms (parity_vs_oracle)"},
+            "roofline": roofline_nn(nn, "k_icp_nn (transform + libnabo-order 1-NN over treelets + bucket scan), "
+                                        "one launch per ICP iteration of a reference window (5 readings)"),
+            "batched_independent": batched,
+        })
+        tr = load_traffic("r03_nn_traffic_%s.json" % args.config)
+        if tr:
+            out_line["roofline"]["traffic"] = tr.get("bytes_per_launch")
+            out_line["roofline"]["traffic_source"] = tr.get("source")
         if world == 1 and not args.no_cpu_baseline:
-            cb, Ts = cpu_baseline(pairs, res, args.cpu_budget, float(cfg.trimmed_ratio),
-                                  bool(flags & L.AICP_RUN_OVERLAP), workload)
-            out["cpu_baseline"] = cb
-            # parity of this run's transforms against the oracle's (reference normal semantics)
-            pe = [sy.rot_err(To, Tg) for To, Tg in zip(Ts, batch.transforms())]
-            out["parity_vs_oracle"] = {"pairs": len(pe), "max_rot_rad": max(e[0] for e in pe),
-                                       "max_trans_m": max(e[1] for e in pe), "tol": [1e-4, 1e-3]}
-        print(json.dumps(out))
-    batch.free()
+            out_line["cpu_baseline"], out_line["parity_vs_oracle"] = cpu_stream(st, T, out, args)
+        print(json.dumps(out_line))
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def cpu_stream(st, T, out, args):
+    """The oracle's replay of App::processCloud on the first 6 readings of the same stream (one
+    reference window + the first reading registered against a corrected reading), 5 times:
+    median rate, and parity of those readings' corrections with the device's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    from aicp_mapping_amd import synthetic as sy
+
+    po.lib()
+    k = min(6, len(st.readings))
+    res = float(np.float32(0.2))
+    last = {}
+
+    def rep():
+        t = time.perf_counter()
+        last["r"] = po.sequence(st.first, st.first_origin, st.readings[:k], st.origins[:k],
+                                reference_update_frequency=args.ref_every, resolution=res)
+        return k, time.perf_counter() - t
+
+    med, rates = median_rate(rep, args.cpu_reps)
+    pe = [sy.rot_err(r["T"], T[i]) for i, r in enumerate(last["r"])]
+    same = all(r["is_reference"] == out[i]["is_reference"] and r["accepted"] == out[i]["accepted"] and
+               r["stats"].iterations == out[i]["icp"]["iterations"] for i, r in enumerate(last["r"]))
+    cb = {"value": med, "unit": "aligned_clouds/s", "cores": 1, "kind": "port",
+          "sample": "oracle replay of App's stream on readings 0..%d of the same workload (overlap + ratio + ICP, "
+                    "reference update after reading %d), N=%d, on 1 host core (%s, nproc %d); median of %d runs: %s "
+                    "clouds/s" % (k - 1, args.ref_every - 1, len(st.readings[0]), cpu_model(), os.cpu_count(),
+                                  len(rates), ", ".join("%.3f" % r for r in rates))}
+    par = {"readings": k, "max_rot_rad": max(e[0] for e in pe), "max_trans_m": max(e[1] for e in pe),
+           "same_decisions_and_iterations": bool(same), "tol": [1e-4, 1e-3]}
+    return cb, par
+
+
+def bench_c4(args):
+    """C4: localization against a resident 1 M-point map; per step the 64 host readings go in, the
+    device crops each reference out of the map (aicp_hip_map_register_batch), T comes out."""
+    import aicp_mapping_amd._lib as L
+    from aicp_mapping_amd import sharding as sh
+    from aicp_mapping_amd import synthetic as sy
+    from aicp_mapping_amd.prior_map import PriorMap
+
+    rank, world, local_rank, dist = init_dist()
+    n_read = args.pairs or 64
+    n_pts = args.points or 120000
+    mp, reads, poses, gts = make_c4(n_read, n_pts, 1000000, seed=1 + rank)
+    ctx = L.Context(local_rank)
+    pm = PriorMap(ctx, mp)  # the prior map is loaded once (App: loadMapFromFile)
+    cfg = L.default_config()
+
+    def step():
+        return pm.register_batch(reads, poses, -15.0, 15.0, cfg, flags=L.AICP_RUN_TIME_NN)
+
+    for _ in range(args.warmup):
+        step()
+    sync(dist)
+    nn = dict(launches=0, total_ms=0.0, bytes=0.0)
+    iters = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        T, st, rc = step()
+        t = ctx.last_nn_timing()
+        for k in ("launches", "total_ms", "bytes"):
+            nn[k] += t[k]
+        iters += sum(s["iterations"] for s in st)
+    sync(dist)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        elapsed = sh.max_over_ranks(elapsed, dist, device="cuda")
+    if rank == 0:
+        value = world * n_read * args.steps / elapsed
+        crops = [len(pm.crop(-15.0, 15.0, poses[i])) for i in (0, n_read - 1)]
+        config = {"workload": "C4: localization-only, %d-pt map resident on the device, %d VLP-16 readings of N=%d, "
+                              "reference = map cropped to +-15 m around each prior pose on the device "
+                              "(getPointsInOrientedBox), overlap fixed 50%% (r = 0.5)" % (len(mp), n_read, n_pts),
+                  "map_points": len(mp), "crop_points_first_last": crops, "chain": CHAIN,
+                  "timed_region": "host readings -> H2D -> device crops + registration -> T "
+                                  "(aicp_hip_map_register_batch)",
+                  "parallelism": "one stream per rank (replicas)"}
+        line = base_line(args, world, METRIC, value, "aligned clouds/s", 1e3 * elapsed / args.steps, DTYPE, DATA,
+                         config)
+        errs = [sy.rot_err(g, Tx) for g, Tx in zip(gts, T)]
+        line.update({"icp_iters_per_s": round(iters / elapsed, 1),
+                     "mean_iterations": float(np.mean([s["iterations"] for s in st])),
+                     "accuracy_vs_ground_truth": {"median_rot_rad": float(np.median([e[0] for e in errs])),
+                                                  "median_trans_m": float(np.median([e[1] for e in errs]))},
+                     "roofline": roofline_nn(nn, "k_icp_nn, one launch per ICP iteration of the 64-reading batch")})
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle as po
+
+            po.lib()
+            k = 2
+            last = {}
+
+            def rep():
+                t = time.perf_counter()
+                last["T"] = []
+                for i in range(k):
+                    crop, _ = po.crop_box(mp, -15.0, 15.0, poses[i])
+                    last["T"].append(po.icp(crop, reads[i], po.default_config(trimmed_ratio=0.5))[1])
+                return k, time.perf_counter() - t
+
+            med, rates = median_rate(rep, args.cpu_reps)
+            pe = [sy.rot_err(To, T[i]) for i, To in enumerate(last["T"])]
+            line["cpu_baseline"] = {"value": med, "unit": "aligned_clouds/s", "cores": 1, "kind": "port",
+                                    "sample": "oracle crop + ICP of readings 0..%d of the same workload on 1 host core "
+                                              "(%s, nproc %d); median of %d runs: %s" % (
+                                                  k - 1, cpu_model(), os.cpu_count(), len(rates),
+                                                  ", ".join("%.3f" % r for r in rates))}
+            line["parity_vs_oracle"] = {"pairs": k, "max_rot_rad": max(e[0] for e in pe),
+                                        "max_trans_m": max(e[1] for e in pe), "tol": [1e-4, 1e-3]}
+        print(json.dumps(line))
+    pm.free()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_c5(args):
+    """C5: 1024 independent pairs sharded i mod G; per step a rank's pairs go in from host buffers
+    and the transforms come out (aicp_hip_align_batch), RCCL all-gathers the records."""
+    import aicp_mapping_amd._lib as L
+    from aicp_mapping_amd import sharding as sh
+    from aicp_mapping_amd import synthetic as sy
+
+    rank, world, local_rank, dist = init_dist()
+    n_total = args.pairs or 1024
+    n_pts = args.points or 60000
+    pairs = make_c5_pairs(n_total, n_pts, rank, world)
+    mine = sh.shard_pairs(n_total, world, rank)
+    ctx = L.Context(local_rank)
+    cfg = L.default_config()
+    res = float(np.float32(0.2))
+    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+
+    def step():
+        T, st, rc = ctx.align_batch(pairs, cfg, res, flags | L.AICP_RUN_TIME_NN)
+        if dist is not None:
+            rec = sh.pack_records(T.transpose(0, 2, 1).reshape(-1, 16), [s["iterations"] for s in st],
+                                  [s["inlier_ratio"] for s in st])
+            sh.gather_records(rec, dist, device="cuda", pair_index=mine)
+        return T, st
+
+    for _ in range(args.warmup):
+        step()
+    sync(dist)
+    nn = dict(launches=0, total_ms=0.0, bytes=0.0)
+    iters = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        T, st = step()
+        t = ctx.last_nn_timing()
+        for k in ("launches", "total_ms", "bytes"):
+            nn[k] += t[k]
+        iters += sum(s["iterations"] for s in st)
+    sync(dist)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        elapsed = sh.max_over_ranks(elapsed, dist, device="cuda")
+        iters = int(sh.sum_over_ranks(float(iters), dist, device="cuda"))
+    if rank == 0:
+        value = n_total * args.steps / elapsed
+        config = {"workload": "C5: %d independent KITTI-like pairs, N=M=%d, seeds 1000.., sharded i mod G" % (
+                  n_total, n_pts), "pairs_total": n_total, "pairs_per_gpu": len(pairs), "chain": CHAIN,
+                  "timed_region": "host pairs -> H2D -> overlap + ratio + ICP -> T (aicp_hip_align_batch)",
+                  "parallelism": "pairs sharded i mod G, RCCL all_gather of T"}
+        line = base_line(args, world, METRIC, value, "aligned clouds/s", 1e3 * elapsed / args.steps, DTYPE, DATA,
+                         config, scaling="strong")
+        errs = [sy.rot_err(p["T_gt"], Tx) for p, Tx in zip(pairs, T)]
+        line.update({"icp_iters_per_s": round(iters / elapsed, 1),
+                     "mean_iterations": float(np.mean([s["iterations"] for s in st])),
+                     "accuracy_vs_ground_truth": {"median_rot_rad": float(np.median([e[0] for e in errs])),
+                                                  "median_trans_m": float(np.median([e[1] for e in errs]))},
+                     "roofline": roofline_nn(nn, "k_icp_nn, one launch per ICP iteration of the 1024-pair batch")})
+        tr = load_traffic("r03_nn_traffic_c5.json")
+        if tr:
+            line["roofline"]["traffic"] = tr.get("bytes_per_launch")
+            line["roofline"]["traffic_source"] = tr.get("source")
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"], line["cpu_baseline_all_cores"], line["parity_vs_oracle"] = cpu_c5(pairs, T, args)
+        print(json.dumps(line))
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_c5(pairs, T, args):
+    """The oracle on C5 pairs: 1 core (median of 5 samples of 4 pairs) and all of this rank's
+    host-core share (16 threads, one pair per thread at a time, ctypes releases the GIL; median of
+    5 samples of 64 pairs)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    from aicp_mapping_amd import synthetic as sy
+
+    po.lib()
+    res = float(np.float32(0.2))
+
+    def one(p):
+        ov, _ = po.overlap(p["ref"], p["ref_origin"], p["read"], p["read_origin"], res)
+        return po.icp(p["ref"], p["read"], po.default_config(trimmed_ratio=po.autotune_ratio(ov)))[1]
+
+    last = {}
+
+    def rep1():
+        t = time.perf_counter()
+        last["T"] = [one(p) for p in pairs[:4]]
+        return 4, time.perf_counter() - t
+
+    med1, r1 = median_rate(rep1, args.cpu_reps)
+    threads = min(16, os.cpu_count() or 1)
+    sub = pairs[:64]
+
+    def repn():
+        t = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            list(ex.map(one, sub))
+        return len(sub), time.perf_counter() - t
+
+    medn, rn = median_rate(repn, args.cpu_reps)
+    pe = [sy.rot_err(To, T[i]) for i, To in enumerate(last["T"])]
+    cb1 = {"value": med1, "unit": "aligned_clouds/s", "cores": 1, "kind": "port",
+           "sample": "oracle overlap + ratio + ICP of the first 4 pairs on 1 host core (%s, nproc %d); median of %d "
+                     "runs: %s" % (cpu_model(), os.cpu_count(), len(r1), ", ".join("%.3f" % r for r in r1))}
+    cbn = {"value": medn, "unit": "aligned_clouds/s", "cores": threads, "kind": "port",
+           "sample": "the same on the first 64 pairs, one pair per thread on %d threads (the box's host-core share "
+                     "per GPU; nproc %d); median of %d runs: %s" % (threads, os.cpu_count(), len(rn),
+                                                                   ", ".join("%.3f" % r for r in rn))}
+    par = {"pairs": len(pe), "max_rot_rad": max(e[0] for e in pe), "max_trans_m": max(e[1] for e in pe),
+           "tol": [1e-4, 1e-3]}
+    return cb1, cbn, par
+
+
+def bench_single(args):
+    """The call App actually makes: one pair per registerClouds (app.cpp:210, 528-550), host
+    buffers -> T through aicp_hip_register; latency median over the timed steps, next to the
+    oracle's on the same pair."""
+    import aicp_mapping_amd._lib as L
+    from aicp_mapping_amd import synthetic as sy
+
+    n_pts = args.points or 120000
+    first, o0 = sy.stream_first(1, n_pts)
+    read, origin, Tg = sy.stream_reading(1, 0, n_pts)
+    ctx = L.Context(0)
+    cfg = L.default_config()
+    for _ in range(max(1, args.warmup)):
+        ctx.register(first, read, cfg)
+    lat = []
+    for _ in range(max(5, args.steps)):
+        t = time.perf_counter()
+        T1, s1 = ctx.register(first, read, cfg)  # aicp_hip_register: host xyz -> T
+        lat.append(time.perf_counter() - t)
+    T, st = T1[None], [s1]
+    med = float(np.median(lat))
+    line = base_line(args, 1, "single-pair registration latency (aicp_hip_register, host xyz -> T)", 1e3 * med, "ms",
+                     1e3 * med, DTYPE, DATA,
+                     {"workload": "one C2 pair (first cloud vs reading 0 of the C2 stream), N=M=%d, ratio 0.70 "
+                                  "(registerClouds re-reads the chain; no overlap in this call)" % n_pts,
+                      "chain": CHAIN}, scaling="strong", hib=False)
+    line.update({"latency_ms_samples": [round(1e3 * x, 3) for x in lat], "iterations": st[0]["iterations"]})
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as po
+
+        po.lib()
+        lo = []
+        for _ in range(args.cpu_reps):
+            t = time.perf_counter()
+            rc1, To, sto = po.icp(first, read, po.default_config(trimmed_ratio=0.7))
+            lo.append(time.perf_counter() - t)
+        r, tt = sy.rot_err(To, T[0])
+        line["cpu_baseline"] = {"value": 1e3 * float(np.median(lo)), "unit": "ms", "cores": 1, "kind": "port",
+                                "sample": "the oracle's ICP of the same pair on 1 host core (%s), median of %d: %s ms"
+                                          % (cpu_model(), len(lo), ", ".join("%.1f" % (1e3 * x) for x in lo))}
+        line["parity_vs_oracle"] = {"rot_rad": r, "trans_m": tt, "iterations_equal": sto.iterations ==
+                                    st[0]["iterations"], "tol": [1e-4, 1e-3]}
+    print(json.dumps(line))
+    ctx.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "single", "prefilter"], default="c2",
+                    help="BASELINE.json workload (default c2: the metric's configuration)")
+    ap.add_argument("--pairs", type=int, default=None, help="readings (pairs) per step per GPU")
+    ap.add_argument("--ref-every", type=int, default=5, help="reference_update_frequency")
+    ap.add_argument("--points", type=int, default=None)
+    ap.add_argument("--data", default=None,
+                    help="recorded directory (aicp_input_poses.csv + cloud_*.pcd) replayed as the stream")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-reps", type=int, default=5, help="repetitions of the bounded CPU sample (median)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-batched", action="store_true", help="skip the batched-independent extra figure")
+    args = ap.parse_args()
+    if args.config == "prefilter":
+        return bench_prefilter(args)
+    if args.config in ("c2", "c3"):
+        return bench_stream(args)
+    if args.config == "c4":
+        return bench_c4(args)
+    if args.config == "c5":
+        return bench_c5(args)
+    return bench_single(args)
 
 
 if __name__ == "__main__":
