@@ -75,6 +75,15 @@ struct OvlDesc {
   uint64_t bytes;   // map bytes (multiple of 16)
 };
 
+// One cloud of the sparse overlap path (kernels_overlap_sparse.hip): an overlap group's reference
+// (side 0, points in ref_raw) or a pair's reading (side 1, points in the sorted readings).
+struct OvlCloud {
+  uint32_t pts_off, n;
+  uint32_t side, pad;
+  double origin[3];
+  uint64_t slot;  // first per-point key-count slot
+};
+
 struct PairState {
   float T[16];          // T_iter, column-major
   float limit;          // trimmed distance limit of the current iteration

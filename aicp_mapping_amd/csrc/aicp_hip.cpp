@@ -428,11 +428,91 @@ int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean) {
 // wait for the boxes, size one byte map per reading and per reference group, mark, count,
 // ratio. Runs on its own host thread while the main thread queues the trees, so the marking
 // starts as soon as the boxes are known instead of after the raw tree's host polls.
+// The overlap from sorted key words (kernels_overlap_sparse.hip) when the dense voxel maps of a
+// batch do not fit: counts per point -> offsets (one host read of the total) -> words -> sort ->
+// distinct counts and intersections. Same sets, same counts as the maps.
+int overlap_sparse(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairDesc* dDesc, PairState* dState,
+                   PairState* dGst, const float4* readS, double res, bool set_ratio, std::string& err) {
+  hipStream_t s = ctx->stream;
+  std::vector<OvlCloud> cl(G + P);
+  std::vector<uint32_t> bc, bs;
+  uint64_t slots = 0;
+  for (size_t c = 0; c < G + P; ++c) {
+    OvlCloud& o = cl[c];
+    o = OvlCloud{};
+    const PairDesc& d = c < G ? B->gdesc[c] : B->desc[c - G];
+    o.side = c < G ? 0 : 1;
+    o.pts_off = c < G ? d.ref_off : d.read_off;
+    o.n = c < G ? d.n_ref : d.n_read;
+    for (int k = 0; k < 3; ++k) o.origin[k] = c < G ? d.ref_origin[k] : d.read_origin[k];
+    o.slot = slots;
+    slots += o.n;
+    for (uint32_t j = 0; j < o.n; j += 256) {
+      bc.push_back((uint32_t)c);
+      bs.push_back(j);
+    }
+  }
+  if (slots >= (1ull << 32)) TFAIL(AICP_ERR_UNSUPPORTED, "sparse overlap: more than 2^32 points");
+  const size_t nb = bc.size();
+  const size_t scan_b = ovl_sparse_scan_bytes(slots);
+  const size_t o_cl = 0, o_bc = o_cl + (G + P) * sizeof(OvlCloud), o_bs = o_bc + nb * 4,
+               o_cnt = (o_bs + nb * 4 + 255) & ~size_t(255), o_off = (o_cnt + slots * 4 + 255) & ~size_t(255),
+               o_pc = o_off + slots * 8, o_pp = o_pc + (G + P) * 8, o_tmp = (o_pp + P * 8 + 255) & ~size_t(255);
+  TCHK(ensure(ctx->ovl_sp, o_tmp + scan_b));
+  const size_t o_tail = (o_bs + nb * 4 + 7) & ~size_t(7);  // read-back of the key total
+  TCHK(ensure(ctx->pin_ovl, o_tail + 16));
+  char* h = ctx->pin_ovl.as<char>();
+  std::memcpy(h + o_cl, cl.data(), (G + P) * sizeof(OvlCloud));
+  std::memcpy(h + o_bc, bc.data(), nb * 4);
+  std::memcpy(h + o_bs, bs.data(), nb * 4);
+  char* d = ctx->ovl_sp.as<char>();
+  TCHK(hipMemcpyAsync(d, h, o_bs + nb * 4, hipMemcpyHostToDevice, s));
+  TCHK(hipEventRecord(ctx->ev[6], s));
+  const OvlCloud* dcl = (const OvlCloud*)(d + o_cl);
+  const uint32_t* dbc = (const uint32_t*)(d + o_bc);
+  const uint32_t* dbs = (const uint32_t*)(d + o_bs);
+  uint32_t* cnt = (uint32_t*)(d + o_cnt);
+  uint64_t* off = (uint64_t*)(d + o_off);
+  TCHK(launch_ovl_sparse_count(s, (uint32_t)nb, dbc, dbs, dcl, B->ref_raw.as<float4>(), readS, res, (uint32_t)slots,
+                               cnt, off, d + o_tmp, scan_b));
+  uint64_t* tail = (uint64_t*)(h + o_tail);
+  TCHK(hipMemcpyAsync(tail, off + (slots - 1), 8, hipMemcpyDeviceToHost, s));
+  uint32_t* tailc = (uint32_t*)(tail + 1);
+  TCHK(hipMemcpyAsync(tailc, cnt + (slots - 1), 4, hipMemcpyDeviceToHost, s));
+  TCHK(hipStreamSynchronize(s));
+  const uint64_t n_keys = slots ? tail[0] + tailc[0] : 0;
+  const size_t sort_b = ovl_sparse_sort_bytes(n_keys);
+  size_t free_b = 0, total_b = 0;
+  TCHK(hipMemGetInfo(&free_b, &total_b));
+  if (n_keys * 16 + sort_b > ctx->ovl_keys.cap + free_b / 2)
+    TFAIL(AICP_ERR_UNSUPPORTED, "sparse overlap: " + std::to_string(n_keys) + " ray keys do not fit");
+  TCHK(ensure(ctx->ovl_keys, n_keys * 16 + sort_b + 256));
+  uint64_t* k0 = ctx->ovl_keys.as<uint64_t>();
+  uint64_t* k1 = k0 + n_keys;
+  void* tmp = (void*)(((uintptr_t)(k1 + n_keys) + 255) & ~uintptr_t(255));
+  TCHK(launch_ovl_sparse_sets(s, (uint32_t)nb, dbc, dbs, dcl, B->ref_raw.as<float4>(), readS, res, off, n_keys, k0, k1,
+                              tmp, sort_b, (int)G, (int)P, dDesc, (unsigned long long*)(d + o_pc),
+                              (unsigned long long*)(d + o_pp), dGst, dState));
+  launch_ovl_finish(s, (int)P, dDesc, dState, dGst, set_ratio ? 1 : 0);
+  TCHK(hipGetLastError());
+  return AICP_OK;
+}
+
+// dense voxel maps of one batch beyond this size take the sorted-key path instead (a 60 x 60 x 6 m
+// scene at 0.2 m is ~2.7 MB per map; 8 GiB covers thousands of such clouds)
+constexpr uint64_t kDenseMapBudget = uint64_t(8) << 30;
+
+bool force_sparse_overlap() {  // AICP_OVL_SPARSE=1: the sorted-key path for every batch (tests)
+  const char* e = std::getenv("AICP_OVL_SPARSE");
+  return e && e[0] == '1';
+}
+
 int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairDesc* dDesc, PairState* dState,
                  PairDesc* dG, PairState* dGst, const float4* readS, double res, bool set_ratio, std::string& err) {
   hipStream_t s = ctx->stream;
   TCHK(hipSetDevice(ctx->device));
   TCHK(hipEventSynchronize(ctx->ev[1]));
+  if (force_sparse_overlap()) return overlap_sparse(ctx, B, P, G, dDesc, dState, dGst, readS, res, set_ratio, err);
   // one map per overlap group (reference side) and one per pair (reading side), each over
   // the padded key box of that cloud's keys and origin
   uint64_t bm_bytes = 0;
@@ -453,22 +533,15 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
     bm_bytes += o.bytes;
     return vox <= (1ull << 34);
   };
-  for (size_t i = 0; i < P; ++i)
-    if (!size_map(ctx->pin_state.as<PairState>()[i], ho[i]))
-      TFAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
-  for (size_t g = 0; g < G; ++g)
-    if (!size_map(ctx->pin_gstate.as<PairState>()[g], ho[P + g]))
-      TFAIL(AICP_ERR_UNSUPPORTED, "overlap key box too large for the voxel maps");
-  // all maps of the batch at once: at most half the free device memory (beyond what the
-  // arena already holds), so a few far outlier points fail this batch with a clear error
-  // instead of an allocation failure
+  bool fits = true;
+  for (size_t i = 0; i < P; ++i) fits &= size_map(ctx->pin_state.as<PairState>()[i], ho[i]);
+  for (size_t g = 0; g < G; ++g) fits &= size_map(ctx->pin_gstate.as<PairState>()[g], ho[P + g]);
+  // all maps of the batch at once within half the free device memory (beyond what the arena
+  // already holds); otherwise (far outlier points: key boxes of 10^9+ voxels) the sorted-key path
   size_t free_b = 0, total_b = 0;
   TCHK(hipMemGetInfo(&free_b, &total_b));
-  const uint64_t limit = ctx->bitmap.cap + free_b / 2;
-  if (bm_bytes > limit)
-    TFAIL(AICP_ERR_UNSUPPORTED, "overlap voxel maps need " + std::to_string(bm_bytes >> 20) + " MiB, more than " +
-                                    std::to_string(limit >> 20) +
-                                    " MiB available: far outlier points? crop the clouds or split the batch");
+  const uint64_t limit = std::min<uint64_t>(ctx->bitmap.cap + free_b / 2, kDenseMapBudget);
+  if (!fits || bm_bytes > limit) return overlap_sparse(ctx, B, P, G, dDesc, dState, dGst, readS, res, set_ratio, err);
   TCHK(ensure(ctx->bitmap, bm_bytes));
   TCHK(hipMemcpyAsync(ctx->ovl.p, ho, (P + G) * sizeof(OvlDesc), hipMemcpyHostToDevice, s));
   TCHK(hipEventRecord(ctx->ev[6], s));
@@ -1011,6 +1084,8 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   free_batch(ctx->oneshot);
   free_batch(ctx->mapbatch);
   release(ctx->crop_ws);
+  release(ctx->ovl_sp);
+  release(ctx->ovl_keys);
   release(ctx->pin_crop);
   seq_state_free(ctx->seq);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,

@@ -156,6 +156,23 @@ void launch_ovl_intersect(hipStream_t s, int n_pairs, const PairDesc* pd, const 
 void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
                        int set_ratio);
 
+// ---- sparse overlap (kernels_overlap_sparse.hip): sorted key words instead of voxel maps -------
+size_t ovl_sparse_scan_bytes(size_t n_points);
+size_t ovl_sparse_sort_bytes(size_t n_keys);
+// per point key counts (cnt, n_points slots) and their exclusive prefix (off)
+hipError_t launch_ovl_sparse_count(hipStream_t s, uint32_t n_blocks, const uint32_t* blk_cloud,
+                                   const uint32_t* blk_start, const OvlCloud* clouds, const float4* ref,
+                                   const float4* read, double res, uint32_t n_points, uint32_t* cnt, uint64_t* off,
+                                   void* temp, size_t temp_bytes);
+// keys -> sorted words -> |S| of every cloud (gst[g].ovl_counts[0], st[p].ovl_counts[1]) and
+// |A ∩ B| per pair (st[p].ovl_counts[2]); clouds: n_groups groups then n_pairs readings
+hipError_t launch_ovl_sparse_sets(hipStream_t s, uint32_t n_blocks, const uint32_t* blk_cloud,
+                                  const uint32_t* blk_start, const OvlCloud* clouds, const float4* ref,
+                                  const float4* read, double res, const uint64_t* off, uint64_t n_keys,
+                                  uint64_t* keys0, uint64_t* keys1, void* temp, size_t temp_bytes, int n_groups,
+                                  int n_pairs, const PairDesc* pd, unsigned long long* per_cloud,
+                                  unsigned long long* per_pair, PairState* gst, PairState* st);
+
 // ---- frame-to-reference stream (kernels_sequence.hip) ---------------------------------------
 // gd->ref_origin = translation of fromMatrix4fToIsometry3d(T) * prior pose of src (1 thread)
 void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T);

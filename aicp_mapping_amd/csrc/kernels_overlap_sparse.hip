@@ -1,0 +1,218 @@
+// kernels_overlap_sparse.hip — the overlap's key sets as sorted key lists, for batches whose
+// dense voxel maps do not fit (a return kilometres away makes a key box of 10^12 voxels).
+//
+// Same sets as the dense path and as octomap (kernels_overlap.hip): every key of
+// computeRayKeys(origin, p) plus p's own key, per cloud. Here each key is written out as a 64-bit
+// word  cloud << 48 | k0 << 32 | k1 << 16 | k2  (cloud = overlap group, or G + pair for a reading),
+// the words of all clouds are sorted together (rocprim radix sort), and:
+//   |S_c|      = the distinct words of cloud c (a word differs from its predecessor);
+//   |A ∩ B|    = the distinct words of reading p whose key is present under p's group
+//                (binary search of group << 48 | key in the sorted array).
+// Cost: 8 B per ray key written and sorted, where the dense path stores 1 byte per ray key into
+// an L2-resident map; it is the fallback, not the default.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "aicp_common.hpp"
+#include "kernels.hpp"
+
+namespace aicp {
+
+namespace {
+
+constexpr int kKeyMax = 32768;
+
+__device__ __forceinline__ bool key_ok(double rf, float c, int& key) {
+  const int sc = (int)floor(rf * (double)c) + kKeyMax;
+  if (sc >= 0 && sc < 2 * kKeyMax) {
+    key = sc;
+    return true;
+  }
+  return false;
+}
+
+// computeRayKeys(origin, end) + the endpoint key, in k_ovl_mark's order and arithmetic
+template <class Visit>
+__device__ void ray_keys(double res, const double* org, float4 p4, Visit&& visit) {
+  const float o[3] = {(float)org[0], (float)org[1], (float)org[2]};
+  const float e[3] = {p4.x, p4.y, p4.z};
+  const double rf = 1.0 / res;
+  int ko[3], ke[3];
+  const bool okO = key_ok(rf, o[0], ko[0]) && key_ok(rf, o[1], ko[1]) && key_ok(rf, o[2], ko[2]);
+  const bool okE = key_ok(rf, e[0], ke[0]) && key_ok(rf, e[1], ke[1]) && key_ok(rf, e[2], ke[2]);
+  if (okO && okE && !(ko[0] == ke[0] && ko[1] == ke[1] && ko[2] == ke[2])) {
+    visit(ko[0], ko[1], ko[2]);
+    float dir[3] = {e[0] - o[0], e[1] - o[1], e[2] - o[2]};
+    const float nsq = dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2];
+    const float length = (float)sqrt((double)nsq);
+    for (int i = 0; i < 3; ++i) dir[i] /= length;
+    int step[3];
+    double tMax[3], tDelta[3];
+    int cur[3] = {ko[0], ko[1], ko[2]};
+    for (int i = 0; i < 3; ++i) {
+      step[i] = dir[i] > 0.0f ? 1 : (dir[i] < 0.0f ? -1 : 0);
+      if (step[i] != 0) {
+        double vb = (double(cur[i] - kKeyMax) + 0.5) * res;
+        vb += (float)(step[i] * res * 0.5);
+        tMax[i] = (vb - (double)o[i]) / (double)dir[i];
+        tDelta[i] = res / (double)fabsf(dir[i]);
+      } else {
+        tMax[i] = 1.7976931348623157e308;
+        tDelta[i] = 1.7976931348623157e308;
+      }
+    }
+    const double len = (double)length;
+    for (;;) {
+      int dim;
+      if (tMax[0] < tMax[1])
+        dim = (tMax[0] < tMax[2]) ? 0 : 2;
+      else
+        dim = (tMax[1] < tMax[2]) ? 1 : 2;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (i == dim) {
+          cur[i] = (cur[i] + step[i]) & 0xFFFF;
+          tMax[i] += tDelta[i];
+        }
+      if (cur[0] == ke[0] && cur[1] == ke[1] && cur[2] == ke[2]) break;
+      const double dfo = fmin(fmin(tMax[0], tMax[1]), tMax[2]);
+      if (dfo > len) break;
+      visit(cur[0], cur[1], cur[2]);
+    }
+  }
+  if (okE) visit(ke[0], ke[1], ke[2]);
+}
+
+__device__ __forceinline__ const float4* cloud_pts(const OvlCloud& c, const float4* ref, const float4* read) {
+  return (c.side ? read : ref) + c.pts_off;
+}
+
+__global__ __launch_bounds__(256) void k_spo_count(const uint32_t* __restrict__ blk_cloud,
+                                                   const uint32_t* __restrict__ blk_start,
+                                                   const OvlCloud* __restrict__ clouds, const float4* __restrict__ ref,
+                                                   const float4* __restrict__ read, double res,
+                                                   uint32_t* __restrict__ cnt) {
+  const OvlCloud& c = clouds[blk_cloud[blockIdx.x]];
+  const uint32_t j = blk_start[blockIdx.x] + threadIdx.x;
+  if (j >= c.n) return;
+  uint32_t k = 0;
+  ray_keys(res, c.origin, cloud_pts(c, ref, read)[j], [&](int, int, int) { ++k; });
+  cnt[c.slot + j] = k;
+}
+
+__global__ __launch_bounds__(256) void k_spo_emit(const uint32_t* __restrict__ blk_cloud,
+                                                  const uint32_t* __restrict__ blk_start,
+                                                  const OvlCloud* __restrict__ clouds, const float4* __restrict__ ref,
+                                                  const float4* __restrict__ read, double res,
+                                                  const uint64_t* __restrict__ off, uint64_t* __restrict__ keys) {
+  const uint32_t ci = blk_cloud[blockIdx.x];
+  const OvlCloud& c = clouds[ci];
+  const uint32_t j = blk_start[blockIdx.x] + threadIdx.x;
+  if (j >= c.n) return;
+  uint64_t o = off[c.slot + j];
+  const uint64_t hi = (uint64_t)ci << 48;
+  ray_keys(res, c.origin, cloud_pts(c, ref, read)[j], [&](int a, int b, int d) {
+    keys[o++] = hi | ((uint64_t)a << 32) | ((uint64_t)b << 16) | (uint64_t)d;
+  });
+}
+
+// distinct words per cloud (wave-aggregated atomics: sorted runs share their cloud)
+__global__ __launch_bounds__(256) void k_spo_unique(const uint64_t* __restrict__ keys, uint64_t total,
+                                                    unsigned long long* __restrict__ per_cloud) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < total;
+  const uint64_t k = in ? keys[i] : 0;
+  const bool uniq = in && (i == 0 || keys[i - 1] != k);
+  const uint32_t cloud = (uint32_t)(k >> 48);
+  const uint32_t c0 = __shfl(cloud, 0, 64);
+  const bool same = __all(!in || cloud == c0);
+  if (same) {
+    const uint64_t m = __ballot(uniq);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&per_cloud[c0], (unsigned long long)__popcll(m));
+  } else if (uniq) {
+    atomicAdd(&per_cloud[cloud], 1ull);
+  }
+}
+
+// |A ∩ B|: distinct words of reading clouds (>= n_groups) whose key is under the pair's group
+__global__ __launch_bounds__(256) void k_spo_intersect(const uint64_t* __restrict__ keys, uint64_t total,
+                                                       int n_groups, const PairDesc* __restrict__ pd,
+                                                       unsigned long long* __restrict__ per_pair) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const uint64_t k = keys[i];
+  if (i > 0 && keys[i - 1] == k) return;
+  const uint32_t cloud = (uint32_t)(k >> 48);
+  if ((int)cloud < n_groups) return;
+  const int p = (int)cloud - n_groups;
+  const uint64_t want = ((uint64_t)pd[p].ogroup << 48) | (k & 0xFFFFFFFFFFFFull);
+  uint64_t lo = 0, hi = total;  // first position with keys[pos] >= want
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < want)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  if (lo < total && keys[lo] == want) atomicAdd(&per_pair[p], 1ull);
+}
+
+__global__ void k_spo_counts(int n_groups, int n_pairs, const unsigned long long* __restrict__ per_cloud,
+                             const unsigned long long* __restrict__ per_pair, PairState* gst, PairState* st) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_groups) gst[i].ovl_counts[0] = per_cloud[i];
+  if (i < n_pairs) {
+    st[i].ovl_counts[1] = per_cloud[n_groups + i];
+    st[i].ovl_counts[2] = per_pair[i];
+  }
+}
+
+}  // namespace
+
+size_t ovl_sparse_scan_bytes(size_t n_points) {
+  size_t b = 0;
+  (void)rocprim::exclusive_scan(nullptr, b, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, n_points,
+                                rocprim::plus<uint64_t>());
+  return b;
+}
+size_t ovl_sparse_sort_bytes(size_t n_keys) {
+  size_t b = 0;
+  (void)rocprim::radix_sort_keys(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr, n_keys, 0, 64);
+  return b;
+}
+
+hipError_t launch_ovl_sparse_count(hipStream_t s, uint32_t n_blocks, const uint32_t* blk_cloud,
+                                   const uint32_t* blk_start, const OvlCloud* clouds, const float4* ref,
+                                   const float4* read, double res, uint32_t n_points, uint32_t* cnt, uint64_t* off,
+                                   void* temp, size_t temp_bytes) {
+  if (!n_blocks) return hipSuccess;
+  k_spo_count<<<n_blocks, 256, 0, s>>>(blk_cloud, blk_start, clouds, ref, read, res, cnt);
+  size_t b = temp_bytes;
+  return rocprim::exclusive_scan(temp, b, cnt, off, (uint64_t)0, n_points, rocprim::plus<uint64_t>(), s);
+}
+
+hipError_t launch_ovl_sparse_sets(hipStream_t s, uint32_t n_blocks, const uint32_t* blk_cloud,
+                                  const uint32_t* blk_start, const OvlCloud* clouds, const float4* ref,
+                                  const float4* read, double res, const uint64_t* off, uint64_t n_keys,
+                                  uint64_t* keys0, uint64_t* keys1, void* temp, size_t temp_bytes, int n_groups,
+                                  int n_pairs, const PairDesc* pd, unsigned long long* per_cloud,
+                                  unsigned long long* per_pair, PairState* gst, PairState* st) {
+  (void)hipMemsetAsync(per_cloud, 0, (size_t)(n_groups + n_pairs) * 8, s);
+  (void)hipMemsetAsync(per_pair, 0, (size_t)n_pairs * 8, s);
+  if (n_keys) {
+    k_spo_emit<<<n_blocks, 256, 0, s>>>(blk_cloud, blk_start, clouds, ref, read, res, off, keys0);
+    size_t b = temp_bytes;
+    const hipError_t e = rocprim::radix_sort_keys(temp, b, keys0, keys1, n_keys, 0, 64, s);
+    if (e != hipSuccess) return e;
+    const unsigned g = (unsigned)((n_keys + 255) / 256);
+    k_spo_unique<<<g, 256, 0, s>>>(keys1, n_keys, per_cloud);
+    k_spo_intersect<<<g, 256, 0, s>>>(keys1, n_keys, n_groups, pd, per_pair);
+  }
+  const int m = n_groups > n_pairs ? n_groups : n_pairs;
+  k_spo_counts<<<(m + 63) / 64, 64, 0, s>>>(n_groups, n_pairs, per_cloud, per_pair, gst, st);
+  return hipGetLastError();
+}
+
+}  // namespace aicp

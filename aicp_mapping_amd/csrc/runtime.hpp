@@ -173,6 +173,7 @@ struct aicp_hip_ctx {
   aicp::rt::SeqState* seq = nullptr;  // aicp_hip_sequence_run's buffers (sequence.cpp), kept across calls
   aicp_hip_batch* mapbatch = nullptr;  // aicp_hip_map_register_batch's batch buffers
   aicp::rt::DevBuf crop_ws;            // its crop work space
+  aicp::rt::DevBuf ovl_sp, ovl_keys;   // sparse overlap: clouds, counts, offsets / key words
   aicp::rt::PinBuf pin_crop;
 };
 

@@ -152,19 +152,36 @@ def test_overlap_far_outlier(ctx, oracle, L):
     assert st[0]["overlap_keys"] == [int(c) for c in cnt]
 
 
-def test_overlap_extreme_outlier_refused_cleanly(ctx, L):
-    """A return kilometres away in every axis would need a voxel map beyond the device's memory:
-    the batch fails with AICP_ERR_UNSUPPORTED and a message, and the context keeps working."""
+def test_overlap_extreme_outlier_sparse_path(ctx, oracle, L):
+    """A return kilometres away in every axis makes a key box of ~10^13 voxels: the batch takes the
+    sorted-key path (kernels_overlap_sparse.hip) and the key counts still equal the oracle's, like
+    octomap, whose sparse tree accepts any in-range key (octrees_overlap.cpp:184)."""
     pr = sy.make_pair(3000, 3000, seed=32)
     read = np.vstack([pr.read, [[5000.0, 5000.0, 5000.0]]]).astype(np.float32)
-    _, _, rc = ctx.align_batch([dict(ref=pr.ref, read=read, ref_origin=pr.ref_origin,
-                                     read_origin=pr.read_origin)], flags=L.AICP_RUN_OVERLAP,
-                               resolution=RES, raise_on_error=False)
-    assert rc == L.AICP_ERR_UNSUPPORTED
-    assert "voxel map" in ctx.last_error()
-    _, st, rc = ctx.align_batch([dict(ref=pr.ref, read=pr.read, ref_origin=pr.ref_origin,
+    _, st, rc = ctx.align_batch([dict(ref=pr.ref, read=read, ref_origin=pr.ref_origin,
                                       read_origin=pr.read_origin)], flags=L.AICP_RUN_OVERLAP, resolution=RES)
-    assert rc == 0 and st[0]["overlap_percent"] > 0
+    ov, cnt = oracle.overlap(pr.ref, pr.ref_origin, read, pr.read_origin, RES)
+    assert rc == 0
+    assert st[0]["overlap_keys"] == [int(c) for c in cnt]
+    assert st[0]["overlap_percent"] == np.float32(ov)
+
+
+def test_overlap_sparse_path_equals_dense(ctx, oracle, L, monkeypatch):
+    """AICP_OVL_SPARSE=1 forces the sorted-key path on an ordinary ragged batch with a shared
+    reference: every pair's three counts and ratio equal the voxel-map path's and the oracle's."""
+    seq = sy.make_sequence(n_readings=4, ref_every=2, n_points=6000, seed=5, half=20.0)
+    pairs = [dict(ref=p.ref, read=p.read[: 4000 + 500 * i], ref_origin=p.ref_origin, read_origin=p.read_origin)
+             for i, p in enumerate(seq)]
+    T0, s0, rc0 = ctx.align_batch(pairs, flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP, resolution=RES)
+    monkeypatch.setenv("AICP_OVL_SPARSE", "1")
+    T1, s1, rc1 = ctx.align_batch(pairs, flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP, resolution=RES)
+    monkeypatch.delenv("AICP_OVL_SPARSE")
+    assert rc0 == rc1 == 0
+    np.testing.assert_array_equal(T0, T1)
+    for a, b, p in zip(s0, s1, pairs):
+        assert a["overlap_keys"] == b["overlap_keys"] and a["trimmed_ratio"] == b["trimmed_ratio"]
+        ov, cnt = oracle.overlap(p["ref"], p["ref_origin"], p["read"], p["read_origin"], RES)
+        assert b["overlap_keys"] == [int(c) for c in cnt]
 
 
 # ---------------------------------------------------------------- whole ICP ---------------
