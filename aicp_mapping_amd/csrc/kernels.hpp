@@ -40,8 +40,9 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
                     const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
                     const uint4* tl = nullptr, const uint2* link = nullptr);
+// host_n (nullable): device pointer of mapped host memory that receives the active count
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
-                        ActiveList* al, uint32_t* ctr);
+                        ActiveList* al, uint32_t* ctr, uint32_t* host_n = nullptr);
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st,
                    const ActiveList* al, const float4* read_c, const uint4* nodes, const uint4* tl,
                    const int32_t* parent, const float4* bpts, const uint2* ptl, int32_t* match, float* d2,

@@ -126,6 +126,12 @@ class WorkerPool {
 };
 
 constexpr int kSlots = 3;  // window slots in flight (>= 2: a window reads the previous slot's reading)
+constexpr int kMaxPolls = 64;  // ICP iterations that can end a window's loop early
+
+bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches
+  const char* e = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
+  return e && e[0] == '1';
+}
 
 struct SeqSlot {
   // reading side (window-local offsets)
@@ -137,6 +143,10 @@ struct SeqSlot {
   TreeBufs tb[2];
   PinBuf pin_read, pin_par, pin_src;
   hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr;
+  // early exit of the ICP loop: active counts written by k_active_list into mapped host memory
+  uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), kMaxPolls words
+  uint32_t* poll_dev = nullptr;   // its device address
+  hipEvent_t ev_poll[kMaxPolls] = {};
   bool used = false;
 };
 
@@ -167,6 +177,9 @@ void seq_state_free(SeqState* S) {
     for (PinBuf* b : {&sl.pin_read, &sl.pin_par, &sl.pin_src}) release(*b);
     for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done})
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : sl.ev_poll)
+      if (e) (void)hipEventDestroy(e);
+    if (sl.poll_host) (void)hipHostFree(sl.poll_host);
   }
   for (DevBuf* b : {&S->desc, &S->state, &S->outT}) release(*b);
   for (PinBuf* b : {&S->pin_state, &S->pin_out, &S->pin_ctl}) release(*b);
@@ -269,11 +282,33 @@ struct Win {
 
 }  // namespace
 
-// Enqueue one window. The host parts: pack + upload the readings (and the reference source when
-// it is not resident), descriptors, block maps, map capacities.
-static int enqueue_window(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
-                          const aicp_cloud* first, const aicp_cloud* rd, const Win& w, const float4* src_resident,
-                          std::vector<Box>& rbox, bool timeNN, int& nn_launches, TreeCtl* ctl_w) {
+// One window's device work in three parts, enqueued in this order across windows:
+//   upload(w+1)  H2D + reading side of the next window (independent of the reference)
+//   icp(w)       the ICP loop, with early exit: the host polls the active count
+//   reference(w+1) next reference (it waits for icp(w)'s corrections) + trees + normals + overlap
+// so the reading side of w+1 overlaps window w, and window w's loop stops once its readings have
+// all converged instead of running maxIterationCount launches.
+struct WinRun {
+  Win w;
+  size_t np = 0;
+  uint64_t nread = 0;
+  uint32_t n_ref = 0;
+  size_t tl_cap = 0;
+  bool use_tl = false;
+  BlockMap m_read{}, m_gref{}, m_red{}, m_sel{};
+  std::vector<uint64_t> cap;
+  uint64_t cap_max = 0;
+  const float4* src_pts = nullptr;
+  const float4* readS = nullptr;
+  TreeCtl* ctl_w = nullptr;
+};
+
+// The host parts: pack + upload the readings (and the reference source when it is not
+// resident), descriptors, block maps, map capacities; then the reading side (stream rd).
+static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                      const aicp_cloud* first, const aicp_cloud* rd, const float4* src_resident,
+                      std::vector<Box>& rbox, WinRun& R) {
+  const Win& w = R.w;
   SeqSlot& sl = S->slot[w.slot];
   const bool doOvl = prm->flags & AICP_RUN_OVERLAP;
   const double res = prm->resolution;
@@ -315,13 +350,8 @@ static int enqueue_window(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   HIPC(ensure(sl.inv, (size_t)n_ref * 4));
   HIPC(ensure(sl.rd, 3 * sizeof(PairDesc) + 2 * sizeof(PairState)));
   PairDesc* dRdesc = sl.rd.as<PairDesc>();
-  PairDesc* dRraw = dRdesc + 1;
-  PairDesc* dG = dRdesc + 2;
-  PairState* dRst = reinterpret_cast<PairState*>(dRdesc + 3);
-  PairState* dGst = dRst + 1;
   PairDesc* dDesc = S->desc.as<PairDesc>() + w.p0;
   PairState* dState = S->state.as<PairState>() + w.p0;
-  float* dOutT = S->outT.as<float>();
 
   // ---- host: pack the readings (+ AABBs), descriptors, block maps
   HIPC(ensure(sl.pin_read, nread * 16));
@@ -481,6 +511,60 @@ static int enqueue_window(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_rd, sr));
 
+  R.np = np;
+  R.nread = nread;
+  R.n_ref = n_ref;
+  R.tl_cap = tl_cap;
+  R.use_tl = use_tl;
+  R.m_read = m_read;
+  R.m_gref = m_gref;
+  R.m_red = m_red;
+  R.m_sel = m_sel;
+  R.cap = cap;
+  R.cap_max = cap_max;
+  R.src_pts = src_pts;
+  R.readS = readS;
+  return AICP_OK;
+}
+
+#define WIN_REFS                                                   \
+  const Win& w = R.w;                                              \
+  SeqSlot& sl = S->slot[w.slot];                                   \
+  const bool doOvl = prm->flags & AICP_RUN_OVERLAP;                \
+  const double res = prm->resolution;                              \
+  const size_t np = R.np;                                          \
+  const uint32_t n_ref = R.n_ref;                                  \
+  PairDesc* dRdesc = sl.rd.as<PairDesc>();                         \
+  PairDesc* dRraw = dRdesc + 1;                                    \
+  PairDesc* dG = dRdesc + 2;                                       \
+  PairState* dRst = reinterpret_cast<PairState*>(dRdesc + 3);      \
+  PairState* dGst = dRst + 1;                                      \
+  PairDesc* dDesc = S->desc.as<PairDesc>() + w.p0;                 \
+  PairState* dState = S->state.as<PairState>() + w.p0;             \
+  float* dOutT = S->outT.as<float>();                              \
+  OvlDesc* dOvl = doOvl ? sl.ovl.as<OvlDesc>() : nullptr;          \
+  const uint64_t* dCap = doOvl ? sl.caps.as<uint64_t>() : nullptr; \
+  uint8_t* bmp = doOvl ? sl.bitmap.as<uint8_t>() : nullptr;        \
+  (void)dRraw;                                                     \
+  (void)dG;                                                        \
+  (void)dOvl;                                                      \
+  (void)n_ref;                                                     \
+  (void)dRst;                                                      \
+  (void)dGst;                                                      \
+  (void)dOutT;                                                     \
+  (void)dCap;                                                      \
+  (void)bmp;                                                       \
+  (void)res
+
+// The reference of the window (streams r3, r2) and the overlap + ICP set-up on stream icp.
+static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
+                         const aicp_sequence_params* prm, WinRun& R) {
+  WIN_REFS;
+  const float4* src_pts = R.src_pts;
+  const float4* readS = R.readS;
+  const bool use_tl = R.use_tl;
+  const size_t tl_cap = R.tl_cap;
+  TreeCtl* ctl_w = R.ctl_w;
   // ---- r3: the reference points, centroid + matcher tree
   hipStream_t s3 = S->s_r3;
   HIPC(hipStreamWaitEvent(s3, sl.ev_up, 0));
@@ -545,10 +629,10 @@ static int enqueue_window(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   if (doOvl) {
     HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
     launch_ovl_init(si, 1, dG, dGst, res, 1);
-    launch_ovl_bbox(si, m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
+    launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
     launch_ovl_size(si, 1, dGst, dOvl, dCap);
-    launch_ovl_clear(si, 1, dOvl, bmp, cap[0]);
-    launch_ovl_mark(si, m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
+    launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
+    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
     launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
   }
   HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));
@@ -560,9 +644,24 @@ static int enqueue_window(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   launch_pairs_from_refs(si, (int)np, dDesc, dRdesc);
   HIPC(hipStreamWaitEvent(si, sl.ev_s2, 0));
   launch_pairs_degenerate(si, (int)np, dDesc, dState, dRst);
-  launch_prepare_read(si, m_read, dDesc, readS, sl.read_c.as<float4>());
+  launch_prepare_read(si, R.m_read, dDesc, readS, sl.read_c.as<float4>());
   HIPC(hipMemsetAsync(sl.sel_hist.p, 0, np * kHistBins * 4, si));
   HIPC(hipMemsetAsync(sl.sel_cnt.p, 0, np * 4, si));
+  HIPC(hipGetLastError());
+  return AICP_OK;
+}
+
+// The ICP loop of the window on stream icp. From iteration smoothLength on (no pair can stop
+// earlier except on an error) k_active_list also writes the active count into mapped host
+// memory; the host, kLookahead iterations behind, stops enqueueing once it reads 0 (the
+// iterations already enqueued past that point find no active pair and return at once).
+constexpr int kLookahead = 2;
+static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                   WinRun& R, bool timeNN, int& nn_launches) {
+  WIN_REFS;
+  hipStream_t si = S->s_icp;
+  const bool use_tl = R.use_tl;
+  const uint64_t nread = R.nread;
   IcpParams ip{};
   ip.maxE2 = (1 + cfg->nn_epsilon) * (1 + cfg->nn_epsilon);
   ip.maxR2 = cfg->nn_max_dist * cfg->nn_max_dist;
@@ -573,8 +672,17 @@ static int enqueue_window(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   ip.knn_normals = cfg->knn_normals;
   ActiveList* al = sl.active.as<ActiveList>();
   uint32_t* ctr = sl.ctrs.as<uint32_t>();
-  for (int it = 0; it < cfg->max_iter; ++it) {
-    launch_active_list(si, (int)np, dDesc, dState, al, ctr);
+  int pending[kLookahead + 1];
+  int n_pending = 0;
+  bool stop = false;
+  for (int it = 0; it < cfg->max_iter && !stop; ++it) {
+    const bool poll = !early_exit_disabled() && it >= cfg->smooth_length && it < kMaxPolls;
+    if (poll) sl.poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
+    launch_active_list(si, (int)np, dDesc, dState, al, ctr, poll ? sl.poll_dev + it : nullptr);
+    if (poll) {
+      HIPC(hipEventRecord(sl.ev_poll[it], si));
+      pending[n_pending++] = it;
+    }
     ip.prof_slot = nn_launches;
     if (timeNN) {
       while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
@@ -590,11 +698,22 @@ static int enqueue_window(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
                   sl.touch.as<uint32_t>(), ctr, ip);
     if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], si));
     ++nn_launches;
-    launch_icp_select(si, m_sel, (int)np, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
+    launch_icp_select(si, R.m_sel, (int)np, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
                       sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), 0);
-    launch_icp_reduce(si, m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
+    launch_icp_reduce(si, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
                       sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>());
     launch_icp_update(si, (int)np, dDesc, dState, sl.slab.as<double>(), ip);
+    // the poll kLookahead iterations back: the device is still busy with the ones since
+    while (n_pending > 0 && it + 1 - pending[0] >= kLookahead) {
+      const int q = pending[0];
+      for (int k = 1; k < n_pending; ++k) pending[k - 1] = pending[k];
+      --n_pending;
+      HIPC(hipEventSynchronize(sl.ev_poll[q]));
+      if (sl.poll_host[q] == 0) {
+        stop = true;
+        break;
+      }
+    }
   }
   launch_finalize(si, (int)np, dDesc, dState, dOutT + 16 * w.p0);
   HIPC(hipGetLastError());
@@ -611,9 +730,13 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
     for (hipStream_t* q : {&S->s_up, &S->s_rd, &S->s_r2, &S->s_r3, &S->s_icp})
       HIPC(hipStreamCreateWithPriority(q, hipStreamNonBlocking, (q == &S->s_rd || q == &S->s_up) ? lo : hi));
-    for (SeqSlot& sl : S->slot)
+    for (SeqSlot& sl : S->slot) {
       for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+      for (hipEvent_t& e : sl.ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIPC(hipHostMalloc((void**)&sl.poll_host, kMaxPolls * 4, hipHostMallocMapped));
+      HIPC(hipHostGetDevicePointer((void**)&sl.poll_dev, sl.poll_host, 0));
+    }
     HIPC(hipEventCreate(&S->ev_begin));
     HIPC(hipEventCreate(&S->ev_end));
   }
@@ -694,8 +817,11 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     HIPC(ensure(S->pin_ctl, plan.size() * 2 * sizeof(TreeCtl)));
     TreeCtl* ctl = S->pin_ctl.as<TreeCtl>();
     std::memset(ctl, 0, plan.size() * 2 * sizeof(TreeCtl));
-    for (size_t k = 0; k < plan.size(); ++k) {
+    std::vector<WinRun> runs(plan.size());
+    auto upload = [&](size_t k) {
       const Win& w = plan[k];
+      runs[k].w = w;
+      runs[k].ctl_w = ctl + 2 * k;
       // the reference source is resident in the previous window's slot, except for the first
       // window of a pass (the first cloud, or a reading of an earlier pass): uploaded again
       const float4* resident = nullptr;
@@ -705,12 +831,19 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         for (size_t i = pw.p0; i < (size_t)w.src; ++i) off += readings[i].n;
         resident = S->slot[pw.slot].read_raw.as<float4>() + off;
       }
-      rc = enqueue_window(ctx, S, cfg, prm, first, readings, w, resident, rbox, timeNN, nn_launches, ctl + 2 * k);
-      if (rc) {
-        (void)seq_sync(ctx, S);
-        return rc;
-      }
+      return win_upload(ctx, S, cfg, prm, first, readings, resident, rbox, runs[k]);
+    };
+    rc = upload(0);
+    if (!rc) rc = win_reference(ctx, S, cfg, prm, runs[0]);
+    for (size_t k = 0; k < plan.size() && !rc; ++k) {
+      if (k + 1 < plan.size()) rc = upload(k + 1);
+      if (!rc) rc = win_icp(ctx, S, cfg, prm, runs[k], timeNN, nn_launches);
+      if (!rc && k + 1 < plan.size()) rc = win_reference(ctx, S, cfg, prm, runs[k + 1]);
       ++windows;
+    }
+    if (rc) {
+      (void)seq_sync(ctx, S);
+      return rc;
     }
     // read back every reading of this pass
     const size_t pe = n;
