@@ -30,6 +30,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "aicp_common.hpp"
 #include "icp_math.hpp"
@@ -766,6 +767,166 @@ __device__ void subtree_build(const SubSeg& g, uint32_t total, float4* pts, PosT
   if (lane == 0 && pair_depth[g.pair] < maxd) atomicMax(&pair_depth[g.pair], maxd);
 }
 
+// ---- block subtree builder: the same nodes, level by level, one node per wave -----------------
+// A segment's subtree has ~(count / bucket) nodes but only ~log2(count / bucket) levels: the
+// waves of a block take the nodes of one level each (a node is still split by one wave with the
+// same Hoare passes, so the swaps and the resulting order are the wave builder's), and a block
+// barrier separates the levels. Far fewer dependent steps per segment than depth-first by one wave.
+constexpr int kSubWaves = 8;
+constexpr int kSubLevelCap = 256;  // nodes above bucket per level (<= kSubMax / (bucket + 1))
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// wave_hoare with wave-local synchronisation (the other waves of the block work on other nodes)
+__device__ __forceinline__ void wave_hoare_w(float4* pts, uint16_t* posA, uint16_t* posB, uint32_t lo_b, uint32_t br,
+                                             uint32_t end, int cd, float cut, bool eq) {
+  const int lane = threadIdx.x & 63;
+  uint32_t ra = 0, rb = 0;
+  for (uint32_t jb = lo_b; jb < end; jb += 64) {
+    const uint32_t j = jb + lane;
+    const bool ok = j < end;
+    bool pr = false;
+    if (ok) {
+      const float v = coord(pts[j], cd);
+      pr = eq ? (v == cut) : (v < cut);
+    }
+    const bool ml = ok && j < br && !pr, mr = ok && j >= br && pr;
+    const uint64_t ma = __ballot(ml), mb = __ballot(mr);
+    if (ml) posA[ra + popc_lt(ma)] = (uint16_t)j;
+    if (mr) posB[rb + popc_lt(mb)] = (uint16_t)j;
+    ra += (uint32_t)__popcll(ma);
+    rb += (uint32_t)__popcll(mb);
+  }
+  wave_sync_lds();
+  for (uint32_t k = lane; k < ra; k += 64) {
+    const uint32_t a = posA[k], b = posB[rb - 1 - k];
+    const float4 t = pts[a];
+    pts[a] = pts[b];
+    pts[b] = t;
+  }
+  wave_sync_lds();
+}
+
+__global__ __launch_bounds__(64 * kSubWaves) void k_tr_subtree_blk(uint32_t total, const TreeCtl* __restrict__ ctl,
+                                                                   const SubSeg* __restrict__ subs,
+                                                                   const float4* __restrict__ W,
+                                                                   float4* __restrict__ bpts, NodeEvent* ev,
+                                                                   uint8_t* valid, uint32_t* ecnt,
+                                                                   int32_t* pair_depth, int bucket) {
+  __shared__ float4 pts[kSubMax];
+  __shared__ uint16_t posA[kSubWaves][kSubMax / 2], posB[kSubWaves][kSubMax / 2];
+  __shared__ SubNode lvl[2][kSubLevelCap];
+  __shared__ uint32_t n_lvl[2];
+  __shared__ int32_t maxd;
+  const uint32_t n_small = ctl->n_small;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t si = blockIdx.x; si < n_small; si += gridDim.x) {
+    __syncthreads();  // the previous segment's last LDS reads precede this one's loads
+    const SubSeg g = subs[si];
+    if (g.c > (uint32_t)kSubMax) continue;  // oversized: k_tr_subtree's global path
+    const uint32_t gf = g.f;
+    for (uint32_t j = threadIdx.x; j < g.c; j += blockDim.x) pts[j] = W[gf + j];
+    if (threadIdx.x == 0) {
+      SubNode& r = lvl[0][0];
+      r.lf = 0;
+      r.lc = g.c;
+      r.depth = g.depth;
+      for (int k = 0; k < 3; ++k) {
+        r.mn[k] = g.mn[k];
+        r.mx[k] = g.mx[k];
+      }
+      r.pf = g.parent_f;
+      r.pdepth = g.parent_depth;
+      n_lvl[0] = 1;
+      n_lvl[1] = 0;
+      maxd = g.depth;
+    }
+    __syncthreads();
+    int cur = 0;
+    for (;;) {
+      const uint32_t n = n_lvl[cur];
+      if (n == 0) break;
+      for (uint32_t i = wv; i < n; i += kSubWaves) {
+        const SubNode nd = lvl[cur][i];  // count > bucket (leaves are emitted when created)
+        int cd;
+        float ideal;
+        split_dim(nd.mn, nd.mx, cd, ideal);
+        const uint32_t a0 = nd.lf, end = nd.lf + nd.lc;
+        float mn = __builtin_inff(), mx = -__builtin_inff();
+        for (uint32_t j = a0 + lane; j < end; j += 64) {
+          const float v = coord(pts[j], cd);
+          mn = fminf(mn, v);
+          mx = fmaxf(mx, v);
+        }
+        const float lo = wave_min(mn), hi = wave_max(mx);
+        const float cut = ideal < lo ? lo : (ideal > hi ? hi : ideal);
+        uint32_t nl = 0, ne = 0;
+        for (uint32_t j = a0 + lane; j < end; j += 64) {
+          const float v = coord(pts[j], cd);
+          nl += v < cut ? 1u : 0u;
+          ne += v == cut ? 1u : 0u;
+        }
+        nl = wave_sum_u(nl);
+        ne = wave_sum_u(ne);
+        const uint32_t br1 = nl, br2 = nl + ne, count = nd.lc;
+        wave_hoare_w(pts, posA[wv], posB[wv], a0, a0 + br1, end, cd, cut, false);
+        if (ne) wave_hoare_w(pts, posA[wv], posB[wv], a0 + br1, a0 + br2, end, cd, cut, true);
+        uint32_t left;
+        if (ideal < lo) left = 1;
+        else if (ideal > hi) left = count - 1;
+        else if (br1 > count / 2) left = br1;
+        else if (br2 < count / 2) left = br2;
+        else left = count / 2;
+        if (lane == 0) {
+          NodeEvent e{};
+          e.f = gf + nd.lf;
+          e.c = count;
+          e.depth = nd.depth;
+          e.pair = g.pair;
+          e.cut_bits = __float_as_uint(cut);
+          e.cd = cd;
+          e.left = left;
+          e.parent_f = nd.pf;
+          e.parent_depth = nd.pdepth;
+          emit_event(ev, valid, ecnt, total, e);
+          atomicMax(&maxd, nd.depth + 1);
+          for (int side = 0; side < 2; ++side) {
+            SubNode c;
+            c.lf = side ? nd.lf + left : nd.lf;
+            c.lc = side ? count - left : left;
+            c.depth = nd.depth + 1;
+            c.pf = gf + nd.lf;
+            c.pdepth = nd.depth;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              c.mn[k] = (side && k == cd) ? cut : nd.mn[k];
+              c.mx[k] = (!side && k == cd) ? cut : nd.mx[k];
+            }
+            if (c.lc <= (uint32_t)bucket) {
+              emit_event(ev, valid, ecnt, total, leaf_event(gf + c.lf, c.lc, c.depth, g.pair, c.pf, c.pdepth));
+            } else {
+              const uint32_t q = atomicAdd(&n_lvl[cur ^ 1], 1u);
+              if (q < (uint32_t)kSubLevelCap) lvl[cur ^ 1][q] = c;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        n_lvl[cur] = 0;
+        if (n_lvl[cur ^ 1] > (uint32_t)kSubLevelCap) n_lvl[cur ^ 1] = kSubLevelCap;  // (bucket >= 4: never)
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+    for (uint32_t j = threadIdx.x; j < g.c; j += blockDim.x) bpts[gf + j] = pts[j];
+    if (threadIdx.x == 0 && pair_depth[g.pair] < maxd) atomicMax(&pair_depth[g.pair], maxd);
+  }
+}
+
 // Grid-stride over the small segments (the grid does not depend on their count, which only
 // the device knows). A segment above kSubMax points -- left over when the planned number of
 // global levels was too small for the data -- is finished in place in global memory with the
@@ -774,7 +935,7 @@ __global__ __launch_bounds__(64) void k_tr_subtree(uint32_t total, const TreeCtl
                                                    const SubSeg* __restrict__ subs, const float4* __restrict__ W,
                                                    float4* __restrict__ bpts, uint32_t* __restrict__ posL,
                                                    uint32_t* __restrict__ posR, NodeEvent* ev, uint8_t* valid,
-                                                   uint32_t* ecnt, int32_t* pair_depth, int bucket) {
+                                                   uint32_t* ecnt, int32_t* pair_depth, int bucket, int blk_done) {
   __shared__ float4 pts[kSubMax];
   __shared__ uint16_t posA[kSubMax / 2], posB[kSubMax / 2];
   __shared__ SubNode stk[kFarStack];
@@ -785,6 +946,7 @@ __global__ __launch_bounds__(64) void k_tr_subtree(uint32_t total, const TreeCtl
     const SubSeg g = subs[si];
     const uint32_t gf = g.f;
     if (g.c <= (uint32_t)kSubMax) {
+      if (blk_done) continue;  // built by k_tr_subtree_blk
       for (uint32_t j = lane; j < g.c; j += 64) pts[j] = W[gf + j];
       __syncthreads();
       subtree_build<uint16_t>(g, total, pts, posA, posB, stk, ev, valid, ecnt, pair_depth, bucket);
@@ -1071,11 +1233,26 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
 
 // grid: an upper bound of the small-segment count (<= total / (bucket + 1) + pairs), capped;
 // the kernel strides over the device-side count
+bool subtree_blk_enabled() {  // AICP_SUBTREE_BLK=0: the depth-first wave builder for every segment
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_SUBTREE_BLK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts, int bucket) {
   const size_t bound = std::min<size_t>(w.max_seg, (size_t)total / (size_t)(bucket + 1) + (size_t)w.n_pairs + 1);
-  const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, 16384));
+  const bool blk = subtree_blk_enabled() && bucket >= 4;  // level widths fit kSubLevelCap
+  if (blk) {
+    const unsigned gb = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, 2048));
+    k_tr_subtree_blk<<<gb, 64 * kSubWaves, 0, s>>>(total, w.ctl, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt,
+                                                   w.pair_depth, bucket);
+  }
+  // oversized segments (a planned build that was too shallow), or every segment without blk
+  const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, blk ? 256 : 16384));
   k_tr_subtree<<<g, 64, 0, s>>>(total, w.ctl, w.subs, w.W[0], bpts, w.posL, w.posR, w.ev, w.valid, w.ecnt,
-                                w.pair_depth, bucket);
+                                w.pair_depth, bucket, blk ? 1 : 0);
   return hipGetLastError();
 }
 

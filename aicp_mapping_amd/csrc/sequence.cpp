@@ -36,6 +36,8 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -581,8 +583,36 @@ static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_ref, s3));
+  // (order of enqueueing: the longest chain first -- the raw tree + SurfaceNormal on r2 -- so
+  // the device starts it while the host still enqueues the matcher tree)
+  // ---- icp: reference voxel map, overlap, ratio, then the ICP loop
+  hipStream_t si = S->s_icp;
+  if (doOvl) {
+    HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
+    launch_ovl_init(si, 1, dG, dGst, res, 1);
+    launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
+    launch_ovl_size(si, 1, dGst, dOvl, dCap);
+    launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
+    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
+    launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
+  }
+  // ---- r2: raw-coordinate tree + SurfaceNormal (reference as given, SURVEY A.1 step 1)
+  hipStream_t s2 = S->s_r2;
+  HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
+  launch_init_state(s2, 1, dRraw, dRst);
+  int rc = device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
+                          sl.bpts_raw, sl.nodes_raw);
+  if (rc) return rc;
+  rc = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw,
+                        plan_levels(n_ref, sl.tb[0], true), ctl_w);
+  if (rc) return rc;
+  uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kXcdGroups * kCtrStride;
+  HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
+  if (!launch_normals(s2, 1, n_ref, dRraw, dRst, sl.nodes_raw.as<uint4>(), nullptr, sl.bpts_raw.as<float4>(),
+                      sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr))
+    FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
   const int bucket = cfg->bucket_size;
-  int rc = device_trees_begin(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, sl.ref_raw.as<float4>(), 1, bucket, sl.bpts,
+  rc = device_trees_begin(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, sl.ref_raw.as<float4>(), 1, bucket, sl.bpts,
                               sl.nodes);
   if (rc) return rc;
   rc = device_trees_end(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, bucket, sl.bpts, sl.nodes,
@@ -603,38 +633,12 @@ static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   }
   HIPC(hipEventRecord(sl.ev_s3, s3));
 
-  // ---- r2: raw-coordinate tree + SurfaceNormal (reference as given, SURVEY A.1 step 1)
-  hipStream_t s2 = S->s_r2;
-  HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
-  launch_init_state(s2, 1, dRraw, dRst);
-  rc = device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
-                          sl.bpts_raw, sl.nodes_raw);
-  if (rc) return rc;
-  rc = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw,
-                        plan_levels(n_ref, sl.tb[0], true), ctl_w);
-  if (rc) return rc;
-  uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kXcdGroups * kCtrStride;
-  HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
-  if (!launch_normals(s2, 1, n_ref, dRraw, dRst, sl.nodes_raw.as<uint4>(), nullptr, sl.bpts_raw.as<float4>(),
-                      sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr))
-    FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
   HIPC(hipStreamWaitEvent(s2, sl.ev_s3, 0));
   launch_normals_to_matcher(s2, 1, n_ref, dRdesc, sl.bpts.as<float4>(), sl.bpts_raw.as<float4>(),
                             sl.nrm_raw.as<float4>(), sl.inv.as<uint32_t>(), sl.bnrm.as<float4>());
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_s2, s2));
 
-  // ---- icp: reference voxel map, overlap, ratio, then the ICP loop
-  hipStream_t si = S->s_icp;
-  if (doOvl) {
-    HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
-    launch_ovl_init(si, 1, dG, dGst, res, 1);
-    launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
-    launch_ovl_size(si, 1, dGst, dOvl, dCap);
-    launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
-    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
-    launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
-  }
   HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));
   if (doOvl) {
     launch_ovl_intersect(si, (int)np, dDesc, dOvl + 1, dOvl, dState, bmp);
@@ -833,14 +837,29 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       }
       return win_upload(ctx, S, cfg, prm, first, readings, resident, rbox, runs[k]);
     };
-    rc = upload(0);
-    if (!rc) rc = win_reference(ctx, S, cfg, prm, runs[0]);
+    // AICP_SEQ_PROF=1: host time per part (diagnostic, stderr)
+    static const bool prof = [] {
+      const char* e = std::getenv("AICP_SEQ_PROF");
+      return e && e[0] == '1';
+    }();
+    double hp[3] = {0, 0, 0};
+    auto timed = [&](int slot, const std::function<int()>& f) {
+      const auto a = std::chrono::steady_clock::now();
+      const int r = f();
+      hp[slot] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+      return r;
+    };
+    rc = timed(0, [&] { return upload(0); });
+    if (!rc) rc = timed(1, [&] { return win_reference(ctx, S, cfg, prm, runs[0]); });
     for (size_t k = 0; k < plan.size() && !rc; ++k) {
-      if (k + 1 < plan.size()) rc = upload(k + 1);
-      if (!rc) rc = win_icp(ctx, S, cfg, prm, runs[k], timeNN, nn_launches);
-      if (!rc && k + 1 < plan.size()) rc = win_reference(ctx, S, cfg, prm, runs[k + 1]);
+      if (k + 1 < plan.size()) rc = timed(0, [&] { return upload(k + 1); });
+      if (!rc) rc = timed(2, [&] { return win_icp(ctx, S, cfg, prm, runs[k], timeNN, nn_launches); });
+      if (!rc && k + 1 < plan.size()) rc = timed(1, [&] { return win_reference(ctx, S, cfg, prm, runs[k + 1]); });
       ++windows;
     }
+    if (prof)
+      std::fprintf(stderr, "[aicp seq] host ms: upload %.2f reference %.2f icp(incl. polls) %.2f over %zu windows\n",
+                   hp[0], hp[1], hp[2], plan.size());
     if (rc) {
       (void)seq_sync(ctx, S);
       return rc;

@@ -409,6 +409,22 @@ def test_planned_tree_build(ctx, L, monkeypatch, plan):
                (b["iterations"], b["tree_depth"], b["nn_points_touched"], b["nn_nodes_touched"])
 
 
+def test_block_subtree_builder_matches_oracle_trees(ctx, oracle, L):
+    """k_tr_subtree_blk (the waves of a block take the nodes of a level) builds libnabo's trees:
+    the touch counts depend on every node of the matcher tree and the normals on the raw tree."""
+    prs = [sy.make_pair(25000, 25000, seed=80 + i) for i in range(2)]
+    pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
+    T, st, rc = ctx.align_batch(pairs, flags=L.AICP_RUN_ICP, cfg=L.default_config(trimmed_ratio=0.65))
+    assert rc == 0
+    for i, p in enumerate(prs):
+        rc1, T1, st1 = oracle.icp(p.ref, p.read, oracle.default_config(trimmed_ratio=0.65))
+        assert (st[i]["nn_points_touched"], st[i]["nn_nodes_touched"], st[i]["tree_depth"]) == \
+               (st1.nn_points_touched, st1.nn_nodes_touched, st1.tree_depth)
+        assert st[i]["degenerate_normals"] == st1.degenerate_normals
+        r, t = sy.rot_err(T1, T[i])
+        assert r < 1e-6 and t < 1e-5
+
+
 def test_resident_batch_full_size_round_trip(ctx, L):
     """C2 size (N = M = 120k): properties at full size (recovers T_gt, repeatable)."""
     prs = [sy.make_pair(120000, 120000, seed=100 + i) for i in range(2)]

@@ -7,4 +7,3 @@ OUT=gpurun_out/prof_$R
 rm -rf $OUT && mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 tools/seqtime.py > $OUT/seq_trace.log 2>&1 || { tail -20 $OUT/seq_trace.log; exit 1; }
 tail -2 $OUT/seq_trace.log
-find $OUT -name "*kernel_stats.csv" | head -1 | xargs cat | cut -c1-160 | head -40
