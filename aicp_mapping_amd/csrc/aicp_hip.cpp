@@ -284,7 +284,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
 // dDesc with ref_off / n_ref / Tin. Writes bpts_out (bucket order, w = local id), nodes_out
 // and the desc fields mean, Tmean, Tinit, node_off, n_nodes, tree_depth.
 int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                       const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out) {
+                       const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out, bool launch) {
   const size_t n = (size_t)total;
   const size_t max_seg = n / 2 + P + 1;
   TCHK(ensure(bpts_out, n * 16));
@@ -310,7 +310,8 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
   const size_t tb = tree_scan_temp_bytes(n + 2);
   TCHK(ensure(T.scan, tb));
   TCHK(ensure(T.pin_ctl, sizeof(TreeCtl)));
-  TreeWork w{};
+  TreeWork w;
+  std::memset(&w, 0, sizeof(w));  // (a graph key in sequence.cpp compares its bytes)
   w.W[0] = T.W0.as<float4>();
   w.W[1] = T.W1.as<float4>();
   w.segof[0] = T.segof0.as<int32_t>();
@@ -333,9 +334,9 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
   w.scan_temp = T.scan.p;
   w.scan_temp_bytes = T.scan.cap;
   w.max_seg = max_seg;
-  float4* bpts = bpts_out.as<float4>();
-  TCHK(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts, bucket));
   T.tw = w;
+  if (!launch) return AICP_OK;  // work space only (before a stream capture)
+  TCHK(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts_out.as<float4>(), bucket));
   return AICP_OK;
 }
 
@@ -345,7 +346,7 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
 // the host polls the next level's segment count from level 4 on (fallback when a planned
 // build turned out too shallow).
 int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst) {
+                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst, bool copy_ctl) {
   const size_t n = (size_t)total;
   const TreeWork& w = T.tw;
   float4* bpts = bpts_out.as<float4>();
@@ -357,7 +358,7 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
       TCHK(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket, level == plan - 1));
     TCHK(launch_tree_subtrees(s, (uint32_t)n, w, bpts, bucket));
     TCHK(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
-    TCHK(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
+    if (copy_ctl) TCHK(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
     T.planned = plan;
     return AICP_OK;
   }

@@ -40,9 +40,12 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
                     const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
                     const uint4* tl = nullptr, const uint2* link = nullptr);
-// host_n (nullable): device pointer of mapped host memory that receives the active count
+// host_n (nullable): device pointer of mapped host memory that receives the active count;
+// done_sig (nullable, signal memory): once no pair is active, the final corrections go to outT
+// and *ticket is stored to done_sig (the sequence's next reference waits on it)
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
-                        ActiveList* al, uint32_t* ctr, uint32_t* host_n = nullptr);
+                        ActiveList* al, uint32_t* ctr, uint32_t* host_n = nullptr, uint64_t* done_sig = nullptr,
+                        const uint64_t* ticket = nullptr, float* outT = nullptr);
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st,
                    const ActiveList* al, const float4* read_c, const uint4* nodes, const uint4* tl,
                    const int32_t* parent, const float4* bpts, const uint2* ptl, int32_t* match, float* d2,
@@ -175,8 +178,13 @@ hipError_t launch_ovl_sparse_sets(hipStream_t s, uint32_t n_blocks, const uint32
                                   unsigned long long* per_pair, PairState* gst, PairState* st);
 
 // ---- frame-to-reference stream (kernels_sequence.hip) ---------------------------------------
-// gd->ref_origin = translation of fromMatrix4fToIsometry3d(T) * prior pose of src (1 thread)
-void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T);
+// gd->ref_origin = translation of fromMatrix4fToIsometry3d(T) * prior pose of src (1 thread);
+// T is read at system scope (written by another stream's kernel, released through a signal)
+// and copied to Tcopy for the transform that follows on the same stream
+void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy);
+// the window's descriptors, states and corrections into the sequence's arrays (np readings)
+void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState* st, const float* T, PairDesc* gd,
+                       PairState* gst, float* gT);
 // od[i] (min, dim, bytes) from st[i].ovl_bbox; od[i].off preset; bytes > cap[i]: ovl_err, empty map
 void launch_ovl_size(hipStream_t s, int n, PairState* st, OvlDesc* od, const uint64_t* cap);
 // zero the n maps of od[] (device-side sizes, each at most max_bytes)

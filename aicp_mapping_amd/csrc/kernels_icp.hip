@@ -1535,7 +1535,8 @@ __global__ void k_init_state(int n_pairs, const PairDesc* __restrict__ pd, PairS
 // one workgroup: prefix of n_read over the pairs still active + zero the work counter
 __global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDesc* __restrict__ pd,
                                                       const PairState* __restrict__ st,
-                                                      ActiveList* al, uint32_t* ctr, uint32_t* host_n) {
+                                                      ActiveList* al, uint32_t* ctr, uint32_t* host_n,
+                                                      uint64_t* done_sig, const uint64_t* ticket, float* outT) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t wcnt[16];
   __shared__ uint32_t carry_off, carry_cnt;
@@ -1585,6 +1586,18 @@ __global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDes
     al->total = carry_off;
     al->off[carry_cnt] = carry_off;
     if (host_n) *host_n = carry_cnt;  // mapped host memory: the sequence's early-exit poll
+  }
+  // every pair has stopped: their corrections are final (k_finalize's arithmetic), and the
+  // sequence's next reference, waiting on done_sig on another stream, may start now
+  if (done_sig && carry_cnt == 0) {
+    for (int p = t; p < n_pairs; p += 1024) {
+      float tmp[16];
+      mul4(pd[p].Tmean, st[p].T, tmp);
+      mul4(tmp, pd[p].Tinit, outT + 16 * (size_t)p);
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(done_sig, *ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -2452,8 +2465,8 @@ bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   return true;
 }
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st, ActiveList* al,
-                        uint32_t* ctr, uint32_t* host_n) {
-  k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr, host_n);
+                        uint32_t* ctr, uint32_t* host_n, uint64_t* done_sig, const uint64_t* ticket, float* outT) {
+  k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT);
 }
 // NN engine of the ICP matcher: 4 = Trav2S, 3 = Trav2C (default), 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
 // (design experiments, tools/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:

@@ -15,10 +15,13 @@ namespace aicp {
 
 // gd: the new window's overlap group; src: the reading that becomes the reference; T: its
 // correction (column-major, the finalize output)
-__global__ void k_seq_next_ref(PairDesc* gd, const PairDesc* __restrict__ src, const float* __restrict__ T) {
+__global__ void k_seq_next_ref(PairDesc* gd, const PairDesc* __restrict__ src, const float* T, float* Tcopy) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   float Tl[16];
-  for (int k = 0; k < 16; ++k) Tl[k] = T[k];
+  for (int k = 0; k < 16; ++k) {
+    Tl[k] = __hip_atomic_load(T + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    Tcopy[k] = Tl[k];
+  }
   double o[3];
   corrected_origin(Tl, src->read_origin, o);
   for (int k = 0; k < 3; ++k) gd->ref_origin[k] = o[k];
@@ -59,8 +62,26 @@ __global__ __launch_bounds__(256) void k_ovl_clear(int n, const OvlDesc* __restr
   }
 }
 
-void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T) {
-  k_seq_next_ref<<<1, 64, 0, s>>>(gd, src, T);
+// word copies of the three arrays (one block; a window holds at most kMaxPairs readings)
+__global__ __launch_bounds__(256) void k_seq_commit(int np, const uint32_t* __restrict__ d, const uint32_t* __restrict__ st,
+                                                    const uint32_t* __restrict__ T, uint32_t* gd, uint32_t* gst,
+                                                    uint32_t* gT) {
+  const uint32_t nd = (uint32_t)np * (sizeof(PairDesc) / 4), ns = (uint32_t)np * (sizeof(PairState) / 4),
+                 nt = (uint32_t)np * 16;
+  for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) gd[i] = d[i];
+  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) gst[i] = st[i];
+  for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) gT[i] = T[i];
+}
+
+void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState* st, const float* T, PairDesc* gd,
+                       PairState* gst, float* gT) {
+  static_assert(sizeof(PairDesc) % 4 == 0 && sizeof(PairState) % 4 == 0, "word copies");
+  if (np > 0)
+    k_seq_commit<<<1, 256, 0, s>>>(np, (const uint32_t*)d, (const uint32_t*)st, (const uint32_t*)T, (uint32_t*)gd,
+                                   (uint32_t*)gst, (uint32_t*)gT);
+}
+void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy) {
+  k_seq_next_ref<<<1, 64, 0, s>>>(gd, src, T, Tcopy);
 }
 void launch_ovl_size(hipStream_t s, int n, PairState* st, OvlDesc* od, const uint64_t* cap) {
   if (n) k_ovl_size<<<(n + 63) / 64, 64, 0, s>>>(n, st, od, cap);

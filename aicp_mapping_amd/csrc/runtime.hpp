@@ -113,12 +113,15 @@ bool read_order_enabled();
 bool force_trav1();
 
 // Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device (kernels_tree.hip).
+// launch = false: allocate the work space only (nothing enqueued; before a stream capture)
 int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                       const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out);
+                       const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out,
+                       bool launch = true);
 // plan > 0: `plan` global levels with no host read-back; the control block is copied to
-// ctl_dst (default T.pin_ctl) at the end of the build
+// ctl_dst (default T.pin_ctl) at the end of the build unless copy_ctl is false
 int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst = nullptr);
+                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst = nullptr,
+                     bool copy_ctl = true);
 // errors of a planned build whose control block is in hctl (after its stream completed)
 int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err);
 int device_trees_check(TreeBufs& T, std::string& err);

@@ -21,14 +21,20 @@
 // up to there and enqueues the rest again from the true state (same reference, fewer readings
 // still to collect). Results therefore equal App's order of events in every case.
 //
-// Per window, five streams:
-//   up   H2D of the readings and the window's descriptors (pinned staging, ring of K slots)
-//   rd   reading side: state init, Morton order, reading voxel maps (independent of the reference)
+// Per window, four streams (HIP shares GPU_MAX_HW_QUEUES hardware queues per priority level;
+// streams beyond that run in submission order, so the sequence keeps to few):
+//   rd   H2D of the readings and descriptors (pinned staging, ring of K slots), then the
+//        reading side: state init, Morton order, reading voxel maps (independent of the reference)
 //   r3   next reference points (k_seq_next_ref, k_transform), centroid + matcher kd-tree
 //   r2   raw kd-tree + SurfaceNormal, normals into the matcher tree's order
 //   icp  reference voxel map, overlap counts, ratio, ICP loop, corrections
-// Device buffers live in K window slots (reused with event waits); descriptors, states and
-// corrections of all readings are kept for the final read-back.
+// Window w+1's reference waits for window w's corrections on the device: the ICP stream stores
+// w's ticket into signal memory as soon as no reading of w is active (k_active_list), and r3
+// waits for it (hipStreamWaitValue64); the host never blocks between windows and enqueues ahead
+// (where the runtime lacks stream wait-values, it polls each window's convergence instead).
+// The kd-tree builds and the ICP loop -- ~100 and ~160 short kernels -- are replayed from
+// hipGraphs captured per slot. Device buffers live in K window slots (reused with event waits);
+// states and corrections of all readings are committed to sequence-wide arrays for the read-back.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,6 +49,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/aicp_hip.h"
@@ -127,6 +134,49 @@ class WorkerPool {
   bool stop_ = false;
 };
 
+// A captured launch sequence (hipGraph) replayed while its key -- every argument and buffer
+// address it was captured with -- stays the same: one graph launch instead of ~100 kernel
+// launches per kd-tree build, ~160 per ICP loop (the host cost of those launches, ~5 us each,
+// was the stream's bottleneck).
+struct GraphCache {
+  std::vector<uint64_t> key;
+  hipGraphExec_t exec = nullptr;
+  bool broken = false;  // a capture failed: direct launches from then on
+  void reset() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    exec = nullptr;
+    key.clear();
+  }
+};
+
+bool seq_prof() {  // AICP_SEQ_PROF=1: host time per part and device phase times (stderr)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_SEQ_PROF");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+bool graphs_enabled() {  // AICP_SEQ_GRAPHS=0: direct launches (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_SEQ_GRAPHS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+struct Key {
+  std::vector<uint64_t> v;
+  template <class T>
+  Key& operator<<(const T& x) {
+    static_assert(std::is_trivially_copyable<T>::value, "plain values");
+    uint64_t w[(sizeof(T) + 7) / 8] = {};
+    std::memcpy(w, &x, sizeof(T));
+    v.insert(v.end(), w, w + (sizeof(T) + 7) / 8);
+    return *this;
+  }
+};
+
 constexpr int kSlots = 3;  // window slots in flight (>= 2: a window reads the previous slot's reading)
 constexpr int kMaxPolls = 64;  // ICP iterations that can end a window's loop early
 
@@ -141,7 +191,8 @@ struct SeqSlot {
       ovl, caps, sel_hist, sel_cnt, ctrs, active;
   // reference side
   DevBuf ref_src, ref_raw, bpts, bnrm, nodes, tl, ptl, tl_flag, tl_rank, tl_temp, bpts_raw, nodes_raw, nrm_raw, nbids,
-      inv, rd;  // rd: rdesc, rdesc_raw, gdesc (PairDesc) + rstate, gstate (PairState)
+      inv, rd, tsrc,  // rd: rdesc, rdesc_raw, gdesc (PairDesc) + rstate, gstate (PairState); tsrc: source T
+      wdesc, wstate, woutT, wticket;  // the window's readings (committed to the sequence's arrays at its end)
   TreeBufs tb[2];
   PinBuf pin_read, pin_par, pin_src;
   hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr;
@@ -149,6 +200,7 @@ struct SeqSlot {
   uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), kMaxPolls words
   uint32_t* poll_dev = nullptr;   // its device address
   hipEvent_t ev_poll[kMaxPolls] = {};
+  GraphCache g_raw, g_match, g_icp;
   bool used = false;
 };
 
@@ -159,6 +211,12 @@ struct SeqState {
   PinBuf pin_state, pin_out, pin_ctl;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+  // device-side window dependency: window k's ICP stores ticket k to `sig` (signal memory) once
+  // its corrections are final; the next reference's stream waits for it (hipStreamWaitValue64)
+  uint64_t* sig = nullptr;
+  uint64_t ticket = 0;
+  std::vector<hipEvent_t> tev;  // seq_prof(): 5 timing events per window
+  bool use_wait = false;
   WorkerPool pool{std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1};
   aicp_sequence_timing last{};
   int device = 0;
@@ -173,9 +231,11 @@ void seq_state_free(SeqState* S) {
                       &sl.ord_k0, &sl.ord_k1, &sl.ord_v0, &sl.ord_v1, &sl.ord_tmp, &sl.maps, &sl.bitmap, &sl.ovl,
                       &sl.caps, &sl.sel_hist, &sl.sel_cnt, &sl.ctrs, &sl.active, &sl.ref_src, &sl.ref_raw, &sl.bpts,
                       &sl.bnrm, &sl.nodes, &sl.tl, &sl.ptl, &sl.tl_flag, &sl.tl_rank, &sl.tl_temp, &sl.bpts_raw,
-                      &sl.nodes_raw, &sl.nrm_raw, &sl.nbids, &sl.inv, &sl.rd})
+                      &sl.nodes_raw, &sl.nrm_raw, &sl.nbids, &sl.inv, &sl.rd, &sl.tsrc, &sl.wdesc, &sl.wstate,
+                      &sl.woutT, &sl.wticket})
       release(*b);
     for (auto& t : sl.tb) t.release_all();
+    for (GraphCache* g : {&sl.g_raw, &sl.g_match, &sl.g_icp}) g->reset();
     for (PinBuf* b : {&sl.pin_read, &sl.pin_par, &sl.pin_src}) release(*b);
     for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done})
       if (e) (void)hipEventDestroy(e);
@@ -184,11 +244,13 @@ void seq_state_free(SeqState* S) {
     if (sl.poll_host) (void)hipHostFree(sl.poll_host);
   }
   for (DevBuf* b : {&S->desc, &S->state, &S->outT}) release(*b);
+  if (S->sig) (void)hipFree(S->sig);
   for (PinBuf* b : {&S->pin_state, &S->pin_out, &S->pin_ctl}) release(*b);
   for (hipEvent_t e : S->nn_ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : S->tev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {S->ev_begin, S->ev_end})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp})
+  for (hipStream_t q : {S->s_rd, S->s_icp})  // (s_up = s_rd; s_r2, s_r3 are the context's)
     if (q) (void)hipStreamDestroy(q);
   delete S;
 }
@@ -303,7 +365,43 @@ struct WinRun {
   const float4* src_pts = nullptr;
   const float4* readS = nullptr;
   TreeCtl* ctl_w = nullptr;
+  uint64_t ticket = 0, src_ticket = 0;  // this window's ICP ticket; the previous window's
+  const PairDesc* src_desc = nullptr;   // the reference source's descriptor and correction
+  const float* src_T = nullptr;
+  hipEvent_t* tev = nullptr;            // seq_prof(): ref start, matcher done, normals done, ICP start, ICP done
 };
+
+// Run `enqueue` on stream s through the cache: replay the graph if the key matches, otherwise
+// capture it (the enqueue must not allocate or synchronise) and replay; direct launches when
+// graphs are off or a capture failed.
+static int graph_run(aicp_hip_ctx* ctx, GraphCache& gc, hipStream_t s, const Key& key,
+                     const std::function<int()>& enqueue) {
+  if (!graphs_enabled() || gc.broken) return enqueue();
+  if (!gc.exec || gc.key != key.v) {
+    gc.reset();
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) != hipSuccess) {
+      (void)hipGetLastError();
+      gc.broken = true;
+      return enqueue();
+    }
+    const int rc = enqueue();
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    hipGraphExec_t ex = nullptr;
+    const bool ok = rc == AICP_OK && e == hipSuccess && g && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;
+    if (g) (void)hipGraphDestroy(g);
+    if (!ok) {
+      (void)hipGetLastError();
+      gc.broken = true;
+      if (rc) return rc;
+      return enqueue();
+    }
+    gc.exec = ex;
+    gc.key = key.v;
+  }
+  HIPC(hipGraphLaunch(gc.exec, s));
+  return AICP_OK;
+}
 
 // The host parts: pack + upload the readings (and the reference source when it is not
 // resident), descriptors, block maps, map capacities; then the reading side (stream rd).
@@ -351,9 +449,14 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   HIPC(ensure(sl.nbids, (size_t)n_ref * 4 * cfg->knn_normals));
   HIPC(ensure(sl.inv, (size_t)n_ref * 4));
   HIPC(ensure(sl.rd, 3 * sizeof(PairDesc) + 2 * sizeof(PairState)));
+  HIPC(ensure(sl.tsrc, 64));
+  HIPC(ensure(sl.wdesc, np * sizeof(PairDesc)));
+  HIPC(ensure(sl.wstate, np * sizeof(PairState)));
+  HIPC(ensure(sl.woutT, np * 64));
+  HIPC(ensure(sl.wticket, 8));
   PairDesc* dRdesc = sl.rd.as<PairDesc>();
-  PairDesc* dDesc = S->desc.as<PairDesc>() + w.p0;
-  PairState* dState = S->state.as<PairState>() + w.p0;
+  PairDesc* dDesc = sl.wdesc.as<PairDesc>();
+  PairState* dState = sl.wstate.as<PairState>();
 
   // ---- host: pack the readings (+ AABBs), descriptors, block maps
   HIPC(ensure(sl.pin_read, nread * 16));
@@ -541,9 +644,9 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   PairDesc* dG = dRdesc + 2;                                       \
   PairState* dRst = reinterpret_cast<PairState*>(dRdesc + 3);      \
   PairState* dGst = dRst + 1;                                      \
-  PairDesc* dDesc = S->desc.as<PairDesc>() + w.p0;                 \
-  PairState* dState = S->state.as<PairState>() + w.p0;             \
-  float* dOutT = S->outT.as<float>();                              \
+  PairDesc* dDesc = sl.wdesc.as<PairDesc>();                       \
+  PairState* dState = sl.wstate.as<PairState>();                   \
+  float* dOutT = sl.woutT.as<float>();                             \
   OvlDesc* dOvl = doOvl ? sl.ovl.as<OvlDesc>() : nullptr;          \
   const uint64_t* dCap = doOvl ? sl.caps.as<uint64_t>() : nullptr; \
   uint8_t* bmp = doOvl ? sl.bitmap.as<uint8_t>() : nullptr;        \
@@ -559,6 +662,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   (void)res
 
 // The reference of the window (streams r3, r2) and the overlap + ICP set-up on stream icp.
+// The two kd-tree builds (+ SurfaceNormal) are replayed from graphs (graph_run).
 static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
                          const aicp_sequence_params* prm, WinRun& R) {
   WIN_REFS;
@@ -567,25 +671,29 @@ static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   const bool use_tl = R.use_tl;
   const size_t tl_cap = R.tl_cap;
   TreeCtl* ctl_w = R.ctl_w;
-  // ---- r3: the reference points, centroid + matcher tree
+  // ---- r3: the reference points
   hipStream_t s3 = S->s_r3;
   HIPC(hipStreamWaitEvent(s3, sl.ev_up, 0));
   if (w.src >= 0) {
-    // (the source's correction is final: the previous window's ICP is before this in s_icp,
-    // and s3 waits for it through the previous slot's ev_done when resident, or it is from an
-    // earlier pass)
-    const SeqSlot& prev = S->slot[(w.slot + kSlots - 1) % kSlots];
-    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, prev.ev_done, 0));
-    launch_seq_next_ref(s3, dG, S->desc.as<PairDesc>() + w.src, dOutT + 16 * (size_t)w.src);
-    launch_transform(s3, (int)n_ref, dOutT + 16 * (size_t)w.src, src_pts, sl.ref_raw.as<float4>());
+    // the source's correction must be final: from the previous window of this pass (its ICP
+    // signals the ticket as soon as every reading has stopped, before the loop's remaining no-op
+    // launches; or, polled mode, its ev_done), or from an earlier pass (synchronised)
+    if (w.index > 0) {
+      if (S->use_wait)
+        HIPC(hipStreamWaitValue64(s3, S->sig, R.src_ticket, hipStreamWaitValueGte, ~0ull));
+      else
+        HIPC(hipStreamWaitEvent(s3, S->slot[(w.slot + kSlots - 1) % kSlots].ev_done, 0));
+    }
+    if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
+    launch_seq_next_ref(s3, dG, R.src_desc, R.src_T, sl.tsrc.as<float>());
+    launch_transform(s3, (int)n_ref, sl.tsrc.as<float>(), src_pts, sl.ref_raw.as<float4>());
   } else {
+    if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
     HIPC(hipMemcpyAsync(sl.ref_raw.p, src_pts, (size_t)n_ref * 16, hipMemcpyDeviceToDevice, s3));
   }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_ref, s3));
-  // (order of enqueueing: the longest chain first -- the raw tree + SurfaceNormal on r2 -- so
-  // the device starts it while the host still enqueues the matcher tree)
-  // ---- icp: reference voxel map, overlap, ratio, then the ICP loop
+  // ---- icp: reference voxel map
   hipStream_t si = S->s_icp;
   if (doOvl) {
     HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
@@ -596,48 +704,91 @@ static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
     launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
   }
-  // ---- r2: raw-coordinate tree + SurfaceNormal (reference as given, SURVEY A.1 step 1)
-  hipStream_t s2 = S->s_r2;
-  HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
-  launch_init_state(s2, 1, dRraw, dRst);
-  int rc = device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
-                          sl.bpts_raw, sl.nodes_raw);
-  if (rc) return rc;
-  rc = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw,
-                        plan_levels(n_ref, sl.tb[0], true), ctl_w);
-  if (rc) return rc;
-  uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kXcdGroups * kCtrStride;
-  HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
-  if (!launch_normals(s2, 1, n_ref, dRraw, dRst, sl.nodes_raw.as<uint4>(), nullptr, sl.bpts_raw.as<float4>(),
-                      sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr))
-    FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
+  // work spaces first: nothing may be allocated inside a capture
   const int bucket = cfg->bucket_size;
+  int rc = device_trees_begin(sl.tb[0], ctx->err, S->s_r2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0,
+                              kNormalsBucket, sl.bpts_raw, sl.nodes_raw, false);
+  if (rc) return rc;
   rc = device_trees_begin(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, sl.ref_raw.as<float4>(), 1, bucket, sl.bpts,
-                              sl.nodes);
+                          sl.nodes, false);
   if (rc) return rc;
-  rc = device_trees_end(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, bucket, sl.bpts, sl.nodes,
-                        plan_levels(n_ref, sl.tb[1]), ctl_w + 1);
-  if (rc) return rc;
+  const uint32_t ncap = 2 * n_ref + 2;
+  const size_t tlb = tree_scan_temp_bytes((size_t)ncap + 1);
   if (use_tl) {
-    const uint32_t ncap = 2 * n_ref + 2;
-    const size_t tb = tree_scan_temp_bytes((size_t)ncap + 1);
     HIPC(ensure(sl.tl, tl_cap * 16));
     HIPC(ensure(sl.ptl, tl_cap * 8));
     HIPC(ensure(sl.tl_flag, ((size_t)ncap + 1) * 4));
     HIPC(ensure(sl.tl_rank, ((size_t)ncap + 1) * 4));
-    HIPC(ensure(sl.tl_temp, tb));
-    HIPC(launch_treelets(s3, 1, ncap, dRdesc, sl.nodes.as<uint4>(), bucket, sl.tl_flag.as<uint32_t>(),
-                         sl.tl_rank.as<uint32_t>(), sl.tl_temp.p, tb, sl.tl.as<uint4>(), sl.ptl.as<uint2>(),
-                         sl.tb[1].tw.ctl));
-    HIPC(hipMemcpyAsync(ctl_w + 1, sl.tb[1].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
+    HIPC(ensure(sl.tl_temp, tlb));
   }
+  const int plan0 = plan_levels(n_ref, sl.tb[0]), plan1 = plan_levels(n_ref, sl.tb[1]);
+  const bool capturable = plan0 > 0 && plan1 > 0;  // (a host-polled build cannot be captured)
+  // ---- r2: raw-coordinate tree + SurfaceNormal (reference as given, SURVEY A.1 step 1)
+  hipStream_t s2 = S->s_r2;
+  HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
+  uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kXcdGroups * kCtrStride;
+  auto raw_build = [&]() -> int {
+    launch_init_state(s2, 1, dRraw, dRst);
+    int r = device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
+                               sl.bpts_raw, sl.nodes_raw);
+    if (r) return r;
+    r = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw, plan0,
+                         ctl_w, !capturable);
+    if (r) return r;
+    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
+    if (!launch_normals(s2, 1, n_ref, dRraw, dRst, sl.nodes_raw.as<uint4>(), nullptr, sl.bpts_raw.as<float4>(),
+                        sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr))
+      FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
+    HIPC(hipGetLastError());
+    return AICP_OK;
+  };
+  if (capturable) {
+    Key k;
+    k << n_ref << plan0 << cfg->knn_normals << dRraw << sl.ref_raw.p << sl.bpts_raw.p << sl.nodes_raw.p
+      << sl.nrm_raw.p << sl.nbids.p << sl.ctrs.p << sl.tb[0].tw;
+    rc = graph_run(ctx, sl.g_raw, s2, k, raw_build);
+    if (rc) return rc;
+    HIPC(hipMemcpyAsync(ctl_w, sl.tb[0].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
+  } else {
+    rc = raw_build();
+    if (rc) return rc;
+  }
+  // ---- r3: centroid + matcher tree + treelets
+  auto match_build = [&]() -> int {
+    int r = device_trees_begin(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, sl.ref_raw.as<float4>(), 1, bucket, sl.bpts,
+                               sl.nodes);
+    if (r) return r;
+    r = device_trees_end(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, bucket, sl.bpts, sl.nodes, plan1, ctl_w + 1,
+                         !capturable);
+    if (r) return r;
+    if (use_tl)
+      HIPC(launch_treelets(s3, 1, ncap, dRdesc, sl.nodes.as<uint4>(), bucket, sl.tl_flag.as<uint32_t>(),
+                           sl.tl_rank.as<uint32_t>(), sl.tl_temp.p, tlb, sl.tl.as<uint4>(), sl.ptl.as<uint2>(),
+                           sl.tb[1].tw.ctl));
+    HIPC(hipGetLastError());
+    return AICP_OK;
+  };
+  if (capturable) {
+    Key k;
+    k << n_ref << plan1 << bucket << use_tl << tl_cap << dRdesc << sl.ref_raw.p << sl.bpts.p << sl.nodes.p
+      << sl.tb[1].tw;
+    if (use_tl) k << sl.tl.p << sl.ptl.p << sl.tl_flag.p << sl.tl_rank.p << sl.tl_temp.p << tlb;
+    rc = graph_run(ctx, sl.g_match, s3, k, match_build);
+  } else {
+    rc = match_build();
+  }
+  if (rc) return rc;
+  if (capturable || use_tl)
+    HIPC(hipMemcpyAsync(ctl_w + 1, sl.tb[1].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
   HIPC(hipEventRecord(sl.ev_s3, s3));
+  if (R.tev) HIPC(hipEventRecord(R.tev[1], s3));
 
   HIPC(hipStreamWaitEvent(s2, sl.ev_s3, 0));
   launch_normals_to_matcher(s2, 1, n_ref, dRdesc, sl.bpts.as<float4>(), sl.bpts_raw.as<float4>(),
                             sl.nrm_raw.as<float4>(), sl.inv.as<uint32_t>(), sl.bnrm.as<float4>());
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_s2, s2));
+  if (R.tev) HIPC(hipEventRecord(R.tev[2], s2));
 
   HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));
   if (doOvl) {
@@ -655,10 +806,14 @@ static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   return AICP_OK;
 }
 
-// The ICP loop of the window on stream icp. From iteration smoothLength on (no pair can stop
-// earlier except on an error) k_active_list also writes the active count into mapped host
-// memory; the host, kLookahead iterations behind, stops enqueueing once it reads 0 (the
-// iterations already enqueued past that point find no active pair and return at once).
+// The ICP loop of the window on stream icp.
+//   signal mode (hipStreamWaitValue available): every maxIterationCount launch is enqueued, as one
+//     graph; k_active_list publishes the corrections and the window's ticket as soon as no pair is
+//     active, and the iterations after that find no active pair and return at once;
+//   polled mode: from iteration smoothLength on (no pair can stop earlier except on an error)
+//     k_active_list also writes the active count into mapped host memory; the host, kLookahead
+//     iterations behind, stops enqueueing once it reads 0.
+// The window's states and corrections are then committed to the sequence's arrays.
 constexpr int kLookahead = 2;
 static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
                    WinRun& R, bool timeNN, int& nn_launches) {
@@ -666,7 +821,8 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
   hipStream_t si = S->s_icp;
   const bool use_tl = R.use_tl;
   const uint64_t nread = R.nread;
-  IcpParams ip{};
+  IcpParams ip;
+  std::memset(&ip, 0, sizeof(ip));  // (compared bytewise in the graph key)
   ip.maxE2 = (1 + cfg->nn_epsilon) * (1 + cfg->nn_epsilon);
   ip.maxR2 = cfg->nn_max_dist * cfg->nn_max_dist;
   ip.max_iter = cfg->max_iter;
@@ -676,52 +832,97 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
   ip.knn_normals = cfg->knn_normals;
   ActiveList* al = sl.active.as<ActiveList>();
   uint32_t* ctr = sl.ctrs.as<uint32_t>();
-  int pending[kLookahead + 1];
-  int n_pending = 0;
-  bool stop = false;
-  for (int it = 0; it < cfg->max_iter && !stop; ++it) {
-    const bool poll = !early_exit_disabled() && it >= cfg->smooth_length && it < kMaxPolls;
-    if (poll) sl.poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
-    launch_active_list(si, (int)np, dDesc, dState, al, ctr, poll ? sl.poll_dev + it : nullptr);
-    if (poll) {
-      HIPC(hipEventRecord(sl.ev_poll[it], si));
-      pending[n_pending++] = it;
-    }
-    ip.prof_slot = nn_launches;
-    if (timeNN) {
-      while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
-        hipEvent_t e;
-        HIPC(hipEventCreate(&e));
-        S->nn_ev.push_back(e);
-      }
-      HIPC(hipEventRecord(S->nn_ev[2 * nn_launches], si));
-    }
+  const bool wait_mode = S->use_wait;
+  uint64_t* tk = sl.wticket.as<uint64_t>();
+  auto iteration = [&](int it, bool poll) {
+    launch_active_list(si, (int)np, dDesc, dState, al, ctr, poll ? sl.poll_dev + it : nullptr,
+                       wait_mode ? S->sig : nullptr, tk, dOutT);
     launch_icp_nn(si, (int)nread, dDesc, dState, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
                   use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
                   use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
                   sl.touch.as<uint32_t>(), ctr, ip);
-    if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], si));
-    ++nn_launches;
     launch_icp_select(si, R.m_sel, (int)np, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
                       sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), 0);
     launch_icp_reduce(si, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
                       sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>());
     launch_icp_update(si, (int)np, dDesc, dState, sl.slab.as<double>(), ip);
-    // the poll kLookahead iterations back: the device is still busy with the ones since
-    while (n_pending > 0 && it + 1 - pending[0] >= kLookahead) {
-      const int q = pending[0];
-      for (int k = 1; k < n_pending; ++k) pending[k - 1] = pending[k];
-      --n_pending;
-      HIPC(hipEventSynchronize(sl.ev_poll[q]));
-      if (sl.poll_host[q] == 0) {
-        stop = true;
-        break;
+  };
+  if (wait_mode) HIPC(hipStreamWriteValue64(si, tk, R.ticket, 0));
+  if (R.tev) HIPC(hipEventRecord(R.tev[3], si));
+  if (wait_mode && !timeNN) {
+    ip.prof_slot = 0;
+    Key k;
+    k << np << nread << use_tl << ip << R.m_sel.pair << R.m_sel.start << R.m_sel.n_blocks << R.m_red.pair
+      << R.m_red.start << R.m_red.n_blocks << sl.wdesc.p << sl.wstate.p << sl.woutT.p << tk
+      << S->sig << sl.active.p << sl.ctrs.p << sl.read_c.p << sl.nodes.p << sl.tl.p << sl.bpts.p << sl.ptl.p
+      << sl.match.p << sl.d2.p << sl.touch.p << sl.sel_hist.p << sl.cand.p << sl.sel_cnt.p << sl.bnrm.p
+      << sl.slab.p;
+    const int rc = graph_run(ctx, sl.g_icp, si, k, [&]() -> int {
+      for (int it = 0; it < cfg->max_iter; ++it) iteration(it, false);
+      launch_finalize(si, (int)np, dDesc, dState, dOutT);
+      HIPC(hipGetLastError());
+      return AICP_OK;
+    });
+    if (rc) return rc;
+    nn_launches += cfg->max_iter;
+  } else {
+    int pending[kLookahead + 1];
+    int n_pending = 0;
+    bool stop = false;
+    for (int it = 0; it < cfg->max_iter && !stop; ++it) {
+      const bool poll = !wait_mode && !early_exit_disabled() && it >= cfg->smooth_length && it < kMaxPolls;
+      if (poll) sl.poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
+      ip.prof_slot = nn_launches;
+      if (timeNN) {
+        while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
+          hipEvent_t e;
+          HIPC(hipEventCreate(&e));
+          S->nn_ev.push_back(e);
+        }
+      }
+      // (the NN launch is bracketed by its events: active list before, select after)
+      launch_active_list(si, (int)np, dDesc, dState, al, ctr, poll ? sl.poll_dev + it : nullptr,
+                         wait_mode ? S->sig : nullptr, tk, dOutT);
+      if (poll) {
+        HIPC(hipEventRecord(sl.ev_poll[it], si));
+        pending[n_pending++] = it;
+      }
+      if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches], si));
+      launch_icp_nn(si, (int)nread, dDesc, dState, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
+                    use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
+                    use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
+                    sl.touch.as<uint32_t>(), ctr, ip);
+      if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], si));
+      ++nn_launches;
+      launch_icp_select(si, R.m_sel, (int)np, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
+                        sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), 0);
+      launch_icp_reduce(si, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(),
+                        sl.d2.as<float>(), sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(),
+                        sl.slab.as<double>());
+      launch_icp_update(si, (int)np, dDesc, dState, sl.slab.as<double>(), ip);
+      if (wait_mode) continue;  // all maxIterationCount launches
+      // the poll kLookahead iterations back: the device is still busy with the ones since
+      while (n_pending > 0 && it + 1 - pending[0] >= kLookahead) {
+        const int q = pending[0];
+        for (int j = 1; j < n_pending; ++j) pending[j - 1] = pending[j];
+        --n_pending;
+        HIPC(hipEventSynchronize(sl.ev_poll[q]));
+        if (sl.poll_host[q] == 0) {
+          stop = true;
+          break;
+        }
       }
     }
+    launch_finalize(si, (int)np, dDesc, dState, dOutT);
   }
-  launch_finalize(si, (int)np, dDesc, dState, dOutT + 16 * w.p0);
+  HIPC(hipGetLastError());
+  // (a window whose loop ran all maxIterationCount launches never saw an empty active list)
+  if (wait_mode) HIPC(hipStreamWriteValue64(si, S->sig, R.ticket, 0));
+  launch_seq_commit(si, (int)np, dDesc, dState, dOutT, S->desc.as<PairDesc>() + w.p0,
+                    S->state.as<PairState>() + w.p0, S->outT.as<float>() + 16 * w.p0);
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_done, si));
+  if (R.tev) HIPC(hipEventRecord(R.tev[4], si));
   return AICP_OK;
 }
 
@@ -732,8 +933,15 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     S->device = ctx->device;
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-    for (hipStream_t* q : {&S->s_up, &S->s_rd, &S->s_r2, &S->s_r3, &S->s_icp})
-      HIPC(hipStreamCreateWithPriority(q, hipStreamNonBlocking, (q == &S->s_rd || q == &S->s_up) ? lo : hi));
+    // Few streams: HIP gives each priority level a pool of GPU_MAX_HW_QUEUES (4) hardware
+    // queues and shares them beyond that, and streams sharing a queue run in submission order.
+    // The tree streams are the context's (stream2, stream3: high priority); the ICP stream is
+    // the third high-priority one; uploads and the reading side share one low-priority stream.
+    HIPC(hipStreamCreateWithPriority(&S->s_rd, hipStreamNonBlocking, lo));
+    HIPC(hipStreamCreateWithPriority(&S->s_icp, hipStreamNonBlocking, hi));
+    S->s_up = S->s_rd;
+    S->s_r2 = ctx->stream2;
+    S->s_r3 = ctx->stream3;
     for (SeqSlot& sl : S->slot) {
       for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -743,6 +951,17 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     }
     HIPC(hipEventCreate(&S->ev_begin));
     HIPC(hipEventCreate(&S->ev_end));
+    // AICP_SEQ_SYNC=poll: the host polls each window's convergence instead (A/B, fallback)
+    const char* e = std::getenv("AICP_SEQ_SYNC");
+    int can = 0;
+    if (!(e && std::strcmp(e, "poll") == 0) &&
+        hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, ctx->device) == hipSuccess && can &&
+        hipExtMallocWithFlags((void**)&S->sig, 8, hipMallocSignalMemory) == hipSuccess) {
+      HIPC(hipStreamWriteValue64(S->s_icp, S->sig, 0, 0));
+      HIPC(hipStreamSynchronize(S->s_icp));
+      S->use_wait = true;
+    }
+    (void)hipGetLastError();
   }
   SeqState* S = ctx->seq;
   for (SeqSlot& sl : S->slot) sl.used = false;
@@ -822,10 +1041,29 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     TreeCtl* ctl = S->pin_ctl.as<TreeCtl>();
     std::memset(ctl, 0, plan.size() * 2 * sizeof(TreeCtl));
     std::vector<WinRun> runs(plan.size());
+    if (seq_prof()) {
+      while (S->tev.size() < 5 * plan.size()) {
+        hipEvent_t e;
+        HIPC(hipEventCreate(&e));
+        S->tev.push_back(e);
+      }
+      for (size_t k = 0; k < plan.size(); ++k) runs[k].tev = S->tev.data() + 5 * k;
+    }
     auto upload = [&](size_t k) {
       const Win& w = plan[k];
       runs[k].w = w;
       runs[k].ctl_w = ctl + 2 * k;
+      runs[k].ticket = ++S->ticket;
+      runs[k].src_ticket = k > 0 ? runs[k - 1].ticket : 0;
+      if (k > 0) {  // the source is the previous window's last reading, still in its slot
+        const Win& pw = plan[k - 1];
+        const size_t off = (size_t)w.src - pw.p0;
+        runs[k].src_desc = S->slot[pw.slot].wdesc.as<PairDesc>() + off;
+        runs[k].src_T = S->slot[pw.slot].woutT.as<float>() + 16 * off;
+      } else if (w.src >= 0) {  // a reading of an earlier pass: committed
+        runs[k].src_desc = S->desc.as<PairDesc>() + w.src;
+        runs[k].src_T = S->outT.as<float>() + 16 * (size_t)w.src;
+      }
       // the reference source is resident in the previous window's slot, except for the first
       // window of a pass (the first cloud, or a reading of an earlier pass): uploaded again
       const float4* resident = nullptr;
@@ -837,11 +1075,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       }
       return win_upload(ctx, S, cfg, prm, first, readings, resident, rbox, runs[k]);
     };
-    // AICP_SEQ_PROF=1: host time per part (diagnostic, stderr)
-    static const bool prof = [] {
-      const char* e = std::getenv("AICP_SEQ_PROF");
-      return e && e[0] == '1';
-    }();
+    const bool prof = seq_prof();
     double hp[3] = {0, 0, 0};
     auto timed = [&](int slot, const std::function<int()>& f) {
       const auto a = std::chrono::steady_clock::now();
@@ -873,6 +1107,22 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     HIPC(hipEventRecord(S->ev_end, S->s_icp));
     rc = seq_sync(ctx, S);
     if (rc) return rc;
+    if (prof && plan.size() > 2) {  // device phase times, averaged over the windows after the first
+      double a[5] = {0, 0, 0, 0, 0};
+      const size_t m = plan.size() - 1;
+      for (size_t k = 1; k < plan.size(); ++k) {
+        const hipEvent_t* t = runs[k].tev;
+        a[0] += ev_ms(t[0], t[1]);
+        a[1] += ev_ms(t[0], t[2]);
+        a[2] += ev_ms(t[0], t[3]);
+        a[3] += ev_ms(t[3], t[4]);
+        a[4] += ev_ms(runs[k - 1].tev[0], t[0]);
+      }
+      std::fprintf(stderr,
+                   "[aicp seq] device ms/window: ref->matcher %.3f ref->normals %.3f ref->icp start %.3f icp %.3f "
+                   "period %.3f\n",
+                   a[0] / m, a[1] / m, a[2] / m, a[3] / m, a[4] / m);
+    }
     for (size_t k = 0; k < plan.size(); ++k) {
       for (int t = 0; t < 2; ++t) {
         rc = device_trees_check_ctl(S->slot[plan[k].slot].tb[t], ctl + 2 * k + t, ctx->err);

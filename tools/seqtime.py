@@ -5,7 +5,8 @@ import aicp_mapping_amd._lib as L
 from aicp_mapping_amd import synthetic as sy
 st = sy.make_stream(n_readings=64, n_points=120000, seed=1)
 ctx = L.Context(0)
-prm = L.default_sequence_params(flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_TIME_NN)
+tn = os.environ.get('SEQ_TIMENN', '0') == '1'
+prm = L.default_sequence_params(flags=L.AICP_RUN_OVERLAP | (L.AICP_RUN_TIME_NN if tn else 0))
 for k in range(6):
     t = time.perf_counter()
     T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)

@@ -9,7 +9,12 @@ win = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 for r in rows:
     r["s"] = int(r["Start_Timestamp"])
     r["e"] = int(r["End_Timestamp"])
-    r["n"] = r["Kernel_Name"].split("(")[0].replace("aicp::", "").replace("(anonymous namespace)::", "")[-40:]
+    nm = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+    base = nm.split("(")[0]
+    if "rocprim" in base:
+        base = "rocprim::" + ("init_lookback" if "init_lookback" in nm else "scan" if "scan" in nm else
+                              "sort" if "sort" in nm else "other")
+    r["n"] = base.replace("aicp::", "").replace("void ", "")[-40:]
 rows.sort(key=lambda r: r["s"])
 fin = [r for r in rows if "k_finalize" in r["n"]]
 # 13 windows per run; run boundaries: finalize index
