@@ -149,9 +149,17 @@ struct SubSeg {
   int32_t parent_depth;
 };
 
+// A segment of at most kMidMax points is split in one workgroup's LDS (k_tr_mid) down to
+// segments of <= kSubMax points; larger ones by the global levels.
+#ifndef AICP_MIDMAX
+#define AICP_MIDMAX 8192
+#endif
+constexpr int kMidMax = AICP_MIDMAX;
+
 struct TreeCtl {
   uint32_t nseg[kFarStack + 2];  // segments per global level
   uint32_t n_small;              // SubSeg entries
+  uint32_t n_mid;                // mid-size segments (k_tr_mid)
   uint32_t n_big;                // of which above kSubMax points (planned build too shallow)
   int32_t error;
 };

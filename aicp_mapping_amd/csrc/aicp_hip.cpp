@@ -303,6 +303,8 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
   TCHK(ensure(T.ev, (2 * n + 2) * sizeof(NodeEvent)));
   TCHK(ensure(T.valid, 2 * n + 2));
   TCHK(ensure(T.subs, max_seg * sizeof(SubSeg)));
+  TCHK(ensure(T.mids, max_seg * sizeof(SubSeg)));
+  TCHK(ensure(T.lb, lb_bytes((uint32_t)n)));
   TCHK(ensure(T.ecnt, (n + 2) * 4));
   TCHK(ensure(T.sums, P * 6 * 8));
   TCHK(ensure(T.pdepth, P * 4));
@@ -326,6 +328,10 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
   w.ev = T.ev.as<NodeEvent>();
   w.valid = T.valid.as<uint8_t>();
   w.subs = T.subs.as<SubSeg>();
+  w.mids = T.mids.as<SubSeg>();
+  w.lb = T.lb.as<uint64_t>();
+  w.lb_stride = lb_stride_words((uint32_t)n);
+  w.mid_max = tree_mid_max();
   w.n_pairs = (int)P;
   w.ecnt = T.ecnt.as<uint32_t>();
   w.sums = T.sums.as<uint64_t>();
@@ -356,6 +362,7 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
     plan = std::min(plan, kFarStack - 2);
     for (int level = 0; level < plan; ++level)
       TCHK(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket, level == plan - 1));
+    TCHK(launch_tree_mid(s, (uint32_t)n, w, bpts, bucket));
     TCHK(launch_tree_subtrees(s, (uint32_t)n, w, bpts, bucket));
     TCHK(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
     if (copy_ctl) TCHK(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
@@ -372,6 +379,7 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
     }
   }
   if (!done) TFAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
+  TCHK(launch_tree_mid(s, (uint32_t)n, w, bpts, bucket));
   TCHK(launch_tree_subtrees(s, (uint32_t)n, w, bpts, bucket));
   TCHK(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
   TCHK(hipMemcpyAsync(&hctl->error, &w.ctl->error, 4, hipMemcpyDeviceToHost, s));
@@ -382,7 +390,7 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
 }
 
 // After the stream of a planned build has completed: its errors (the control block was copied
-// back asynchronously at the end of the build). Segments left above kSubMax points at the last
+// back asynchronously at the end of the build). Segments left above kMidMax points at the last
 // planned level were finished by the subtree kernel's global path, so the tree is complete.
 int device_trees_check(TreeBufs& T, std::string& err) {
   return device_trees_check_ctl(T, T.pin_ctl.as<TreeCtl>(), err);
@@ -411,7 +419,7 @@ int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean) {
     return v > 0 ? std::min(kFarStack - 2, v) : 0;
   }
   int l = 0;
-  while (((uint64_t)kSubMax << l) < n_max) ++l;
+  while (((uint64_t)tree_mid_max() << l) < n_max) ++l;
   // lean: the balanced estimate + 1, whatever the previous build used; the few segments still
   // above kSubMax go to the subtree kernel's global path (used for the raw-coordinate tree on
   // the critical stream: C2 +2 %, the leftovers cost less than the full-length levels)

@@ -102,6 +102,7 @@ struct TreeWork {
   NodeEvent* ev;         // 2 * total slots (leaf: first position; inner: total + split position)
   uint8_t* valid;        // 2 * total
   SubSeg* subs;          // wave-subtree segments, max_seg
+  SubSeg* mids;          // mid-size segments (kSubMax < count <= kMidMax), max_seg
   uint32_t* ecnt;        // nodes ending at each position, total + 2
   uint64_t* sums;        // 6 per pair (128-bit fixed-point coordinate sums)
   int32_t* pair_depth;   // per pair
@@ -110,8 +111,15 @@ struct TreeWork {
   size_t scan_temp_bytes;
   size_t max_seg;
   int n_pairs;
+  uint64_t* lb;          // look-back words of the build's scans (lb_bytes), zeroed by launch_tree_prepare
+  size_t lb_stride;      // words per scan
+  uint32_t mid_max;      // segments up to this size leave the global levels (kMidMax; kSubMax: no mid builder)
 };
+bool tree_lookback_enabled();
+uint32_t tree_mid_max();
 size_t tree_scan_temp_bytes(size_t n);
+size_t lb_bytes(uint32_t total);
+size_t lb_stride_words(uint32_t total);
 // centroid (center = 1) + frames in pd, centred points, root segments
 // matcher treelets of n_refs trees (rd[r].tl_off / tl_cap set by the host): flag, rank: cap + 1
 // words each; temp: tree_scan_temp_bytes(cap + 1); errors into ctl->error (bit 4)
@@ -125,6 +133,8 @@ hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairD
 // kernel (its global-memory path) instead of a next level
 hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const TreeWork& w, float4* bpts,
                              int bucket, bool last);
+// mid-size segments, one workgroup each: nodes split in LDS until the pieces fit the subtree builders
+hipError_t launch_tree_mid(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts, int bucket);
 // subtrees of the segments with <= kSubMax points, one wave each (grid-stride over the device count)
 hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts,
                                 int bucket);

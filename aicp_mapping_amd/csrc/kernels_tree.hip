@@ -186,6 +186,99 @@ __device__ __forceinline__ float seg_cut(const TreeSeg& s) {
   return s.ideal < lo ? lo : (s.ideal > hi ? hi : s.ideal);
 }
 
+// ---- single-pass scan (decoupled look-back) ---------------------------------------------------
+// Exclusive scan of per-position counts over [0, n), written to X, in ONE launch: a tile of
+// kLbTile positions per workgroup (tile order from an atomic ticket, so every tile's predecessors
+// have started), its aggregate published at once, its inclusive prefix once the look-back over
+// the predecessors' words (flag << 32 | value, one 64-bit word each) reaches an inclusive one.
+// The counts are computed inside (a predicate: no flag array, no separate flag kernel). `st` holds the
+// ticket and one word per tile, zeroed before the launch; a stalled look-back (impossible while
+// tiles only wait on earlier tickets) gives up after a bounded spin and reports ctl->error 16.
+constexpr int kLbThreads = 256;
+constexpr int kLbItems = 8;
+constexpr uint32_t kLbTile = kLbThreads * kLbItems;
+constexpr uint64_t kLbAgg = 1ull << 32, kLbIncl = 2ull << 32;
+
+__host__ __device__ constexpr uint32_t lb_words(uint32_t n) { return (n + kLbTile - 1) / kLbTile + 1; }
+
+template <class Val>
+__device__ __forceinline__ void lookback_scan(uint32_t n, Val val, uint32_t* __restrict__ X, uint64_t* st,
+                                              TreeCtl* ctl) {
+  __shared__ uint32_t s_tile, s_excl, s_wsum[kLbThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) s_tile = atomicAdd(reinterpret_cast<unsigned int*>(st), 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  uint64_t* tw = st + 1;  // tile words
+  const uint32_t i0 = tile * kLbTile + (uint32_t)t * kLbItems;
+  uint32_t v[kLbItems];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kLbItems; ++j) {
+    v[j] = i0 + j < n ? val(i0 + j) : 0u;
+    sum += v[j];
+  }
+  // block exclusive prefix of the thread sums
+  uint32_t x = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
+  __syncthreads();
+  uint32_t wbase = 0, agg = 0;
+#pragma unroll
+  for (int w = 0; w < kLbThreads / 64; ++w) {
+    const uint32_t a = s_wsum[w];
+    if (w < wv) wbase += a;
+    agg += a;
+  }
+  const uint32_t texcl = wbase + x - sum;
+  if (wv == 0) {
+    uint32_t excl = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(&tw[0], kLbIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&tw[tile], kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t top = (int64_t)tile - 1;  // the nearest predecessor not summed yet
+      uint32_t spins = 0;
+      for (;;) {
+        const int64_t idx = top - lane;
+        const uint64_t w = idx >= 0 ? __hip_atomic_load(&tw[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : kLbIncl;
+        const uint32_t flag = (uint32_t)(w >> 32);
+        const uint64_t incl = __ballot(flag == 2), zero = __ballot(flag == 0);
+        const int first = incl ? __ffsll((long long)incl) - 1 : 64;  // nearest inclusive word
+        const uint64_t need = first == 64 ? ~0ull : ((2ull << first) - 1ull);
+        if (zero & need) {  // a predecessor up to there has not published yet
+          if (++spins > (1u << 22)) {
+            if (lane == 0) atomicOr(&ctl->error, 16);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint32_t part = lane <= first ? (uint32_t)w : 0u;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+        excl += part;
+        if (first < 64) break;
+        top -= 64;
+      }
+      if (lane == 0) __hip_atomic_store(&tw[tile], kLbIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  uint32_t run = s_excl + texcl;
+#pragma unroll
+  for (int j = 0; j < kLbItems; ++j) {
+    if (i0 + j < n) X[i0 + j] = run;
+    run += v[j];
+  }
+}
+
 // ---- centroid --------------------------------------------------------------------------------
 // Exact order-independent sum: every coordinate as round(x * 2^40) in 128-bit two's complement
 // (64-bit atomics with carry), so the result does not depend on the reduction order.
@@ -289,7 +382,7 @@ __global__ void k_tr_init_boxes(int n_pairs, TreeSeg* seg) {
 __global__ __launch_bounds__(256) void k_tr_center(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
                                                    const float4* __restrict__ raw, float4* __restrict__ W,
                                                    int32_t* __restrict__ segof, TreeSeg* seg,
-                                                   float4* __restrict__ bpts, int bucket) {
+                                                   float4* __restrict__ bpts, int bucket, uint32_t mid_max) {
   const uint32_t base = blockIdx.x * blockDim.x;
   const uint32_t i = base + threadIdx.x;
   const bool ok = i < total;
@@ -303,7 +396,7 @@ __global__ __launch_bounds__(256) void k_tr_center(int n_pairs, uint32_t total, 
     const float4 p = raw[i];
     c = make_float4(p.x - d.mean[0], p.y - d.mean[1], p.z - d.mean[2], __int_as_float((int32_t)(i - d.ref_off)));
     W[i] = c;
-    segof[i] = d.n_ref <= (uint32_t)kSubMax ? -1 : pair;
+    segof[i] = d.n_ref <= mid_max ? -1 : pair;
     if (d.n_ref <= (uint32_t)bucket) bpts[i] = c;
   }
   const float v[3] = {c.x, c.y, c.z};
@@ -331,10 +424,11 @@ __global__ __launch_bounds__(256) void k_tr_center(int n_pairs, uint32_t total, 
 }
 
 // Level-0 segments from the boxes. A pair with n_ref <= bucket is one leaf (its points are
-// final); one with n_ref <= kSubMax goes straight to the wave subtree builder.
+// final); one with n_ref <= kSubMax goes straight to the subtree builders, one with
+// n_ref <= kMidMax to the mid-size builder.
 __global__ void k_tr_roots(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd, TreeSeg* seg,
-                           SubSeg* subs, TreeCtl* ctl, NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
-                           int bucket) {
+                           SubSeg* subs, SubSeg* mids, TreeCtl* ctl, NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
+                           int bucket, uint32_t mid_max) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
   TreeSeg& s = seg[p];
@@ -352,12 +446,12 @@ __global__ void k_tr_roots(int n_pairs, uint32_t total, const PairDesc* __restri
   split_dim(s.mn, s.mx, s.cd, s.ideal);
   s.lo = 0xffffffffu;
   s.hi = 0u;
-  if (d.n_ref <= (uint32_t)kSubMax) {
+  if (d.n_ref <= mid_max) {
     if (d.n_ref <= (uint32_t)bucket) {
       emit_event(ev, valid, ecnt, total, leaf_event(d.ref_off, d.n_ref, 0, p, 0, -1));
     } else {
-      const uint32_t si = atomicAdd(&ctl->n_small, 1u);
-      SubSeg& g = subs[si];
+      const uint32_t si = atomicAdd(d.n_ref <= (uint32_t)kSubMax ? &ctl->n_small : &ctl->n_mid, 1u);
+      SubSeg& g = (d.n_ref <= (uint32_t)kSubMax ? subs : mids)[si];
       g.f = d.ref_off;
       g.c = d.n_ref;
       g.pair = p;
@@ -414,6 +508,26 @@ __global__ __launch_bounds__(256) void k_tr_flag1(uint32_t total, const int32_t*
     if (s >= 0) f = coord(W[i], seg[s].cd) < seg_cut(seg[s]) ? 1u : 0u;
   }
   flag[i] = f;
+}
+
+// X1 = exclusive scan of the pass-1 predicate (k_tr_flag1's) over positions [0, total]
+__global__ __launch_bounds__(kLbThreads) void k_tr_scan1(uint32_t total, const int32_t* __restrict__ segof,
+                                                        const float4* __restrict__ W, const TreeSeg* __restrict__ seg,
+                                                        uint32_t* __restrict__ X, uint64_t* st, TreeCtl* ctl) {
+  lookback_scan(
+      total + 1,
+      [&](uint32_t i) -> uint32_t {
+        if (i >= total) return 0u;
+        const int s = segof[i];
+        return (s >= 0 && coord(W[i], seg[s].cd) < seg_cut(seg[s])) ? 1u : 0u;
+      },
+      X, st, ctl);
+}
+
+// X = exclusive scan of c[0, n)
+__global__ __launch_bounds__(kLbThreads) void k_tr_scan_counts(uint32_t n, const uint32_t* __restrict__ c,
+                                                              uint32_t* __restrict__ X, uint64_t* st, TreeCtl* ctl) {
+  lookback_scan(n, [&](uint32_t i) -> uint32_t { return c[i]; }, X, st, ctl);
 }
 
 // Destination of the element at local position li in a Hoare pass over [lo_b, count) with
@@ -497,12 +611,13 @@ __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t*
   if (li == 0) seg[s].br1 = br1;
 }
 
-// split: left-count rule, node event of this segment, children: leaf events, wave-subtree
-// segments (count <= kSubMax) or next-level segments
+// split: left-count rule, node event of this segment, children: leaf events, subtree segments
+// (count <= kSubMax), mid-size segments (<= kMidMax) or next-level segments
 __global__ __launch_bounds__(256) void k_tr_split(int level, int last, uint32_t total, TreeSeg* seg, TreeSeg* next,
-                                                  SubSeg* subs, TreeCtl* ctl, const uint32_t* __restrict__ X2,
+                                                  SubSeg* subs, SubSeg* mids, TreeCtl* ctl, const uint32_t* __restrict__ X2,
                                                   NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
-                                                  int32_t* pair_depth, int bucket, uint32_t max_seg) {
+                                                  int32_t* pair_depth, int bucket, uint32_t max_seg,
+                                                  uint32_t mid_max) {
   const uint32_t si = blockIdx.x * blockDim.x + threadIdx.x;
   if (si >= ctl->nseg[level]) return;
   TreeSeg& g = seg[si];
@@ -546,15 +661,16 @@ __global__ __launch_bounds__(256) void k_tr_split(int level, int last, uint32_t 
       g.child[side] = -1;
       continue;
     }
-    if (cc <= (uint32_t)kSubMax || last) {  // last planned level: oversized ones too (global path)
-      if (cc > (uint32_t)kSubMax) atomicAdd(&ctl->n_big, 1u);
-      const uint32_t ni = atomicAdd(&ctl->n_small, 1u);
+    if (cc <= mid_max || last) {  // last planned level: oversized ones too (global path)
+      const bool mid = cc > (uint32_t)kSubMax && cc <= mid_max;
+      if (cc > mid_max) atomicAdd(&ctl->n_big, 1u);
+      const uint32_t ni = atomicAdd(mid ? &ctl->n_mid : &ctl->n_small, 1u);
       if (ni >= max_seg) {
         atomicOr(&ctl->error, 4);
         g.child[side] = -1;
         continue;
       }
-      SubSeg& c = subs[ni];
+      SubSeg& c = (mid ? mids : subs)[ni];
       c.f = cf;
       c.c = cc;
       c.pair = g.pair;
@@ -927,6 +1043,208 @@ __global__ __launch_bounds__(64 * kSubWaves) void k_tr_subtree_blk(uint32_t tota
   }
 }
 
+// ---- mid-size builder: one workgroup splits a segment of <= kMidMax points in LDS ----------------
+// The global levels stop at kMidMax points (instead of kSubMax): a workgroup of 16 waves loads the
+// segment into LDS and splits its nodes above kSubMax points one after another with block-wide
+// reductions and Hoare passes (the same node rule and the same swaps as the sequential loop: the
+// k-th misplaced element from the left swaps with the k-th from the right), depth first; the
+// pieces of <= kSubMax points go to the subtree builders, leaves are emitted at once.
+constexpr int kMidThreads = 1024;
+constexpr int kMidWaves = kMidThreads / 64;
+constexpr int kMidStack = 32;
+
+template <class T, class Op>
+__device__ __forceinline__ T mid_allreduce(T v, Op op, T* scratch) {
+  v = wave_reduce_dpp(v, op);
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
+  __syncthreads();
+  T r = scratch[0];
+#pragma unroll
+  for (int i = 1; i < kMidWaves; ++i) r = op(r, scratch[i]);
+  __syncthreads();
+  return r;
+}
+
+// one Hoare pass over local [lo_b, end) with boundary br, the whole workgroup
+__device__ void mid_hoare(float4* pts, uint16_t* posA, uint16_t* posB, uint32_t* sA, uint32_t* sB, uint32_t lo_b,
+                          uint32_t br, uint32_t end, int cd, float cut, bool eq) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint32_t ra = 0, rb = 0;
+  for (uint32_t jb = lo_b; jb < end; jb += kMidThreads) {
+    const uint32_t j = jb + t;
+    const bool ok = j < end;
+    bool pr = false;
+    if (ok) {
+      const float v = coord(pts[j], cd);
+      pr = eq ? (v == cut) : (v < cut);
+    }
+    const bool ml = ok && j < br && !pr, mr = ok && j >= br && pr;
+    const uint64_t ma = __ballot(ml), mb = __ballot(mr);
+    if (lane == 0) {
+      sA[wv] = (uint32_t)__popcll(ma);
+      sB[wv] = (uint32_t)__popcll(mb);
+    }
+    __syncthreads();
+    uint32_t oa = ra, ob = rb, ta = 0, tb = 0;
+#pragma unroll
+    for (int w = 0; w < kMidWaves; ++w) {
+      const uint32_t a = sA[w], b = sB[w];
+      if (w < wv) {
+        oa += a;
+        ob += b;
+      }
+      ta += a;
+      tb += b;
+    }
+    if (ml) posA[oa + popc_lt(ma)] = (uint16_t)j;
+    if (mr) posB[ob + popc_lt(mb)] = (uint16_t)j;
+    ra += ta;
+    rb += tb;
+    __syncthreads();
+  }
+  for (uint32_t k = t; k < ra; k += kMidThreads) {
+    const uint32_t a = posA[k], b = posB[rb - 1 - k];
+    const float4 x = pts[a];
+    pts[a] = pts[b];
+    pts[b] = x;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kMidThreads) void k_tr_mid(uint32_t total, TreeCtl* ctl, const SubSeg* __restrict__ mids,
+                                                        SubSeg* subs, float4* W, float4* __restrict__ bpts,
+                                                        NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
+                                                        int32_t* pair_depth, int bucket, uint32_t max_seg) {
+  __shared__ float4 pts[kMidMax];
+  __shared__ uint16_t posA[kMidMax / 2], posB[kMidMax / 2];
+  __shared__ uint32_t sA[kMidWaves], sB[kMidWaves];
+  __shared__ float sF[kMidWaves];
+  __shared__ uint32_t sU[kMidWaves];
+  __shared__ SubNode stk[kMidStack];
+  __shared__ int sp_s;
+  __shared__ int32_t maxd_s;
+  const int t = threadIdx.x;
+  const uint32_t n_mid = ctl->n_mid;
+  for (uint32_t mi = blockIdx.x; mi < n_mid; mi += gridDim.x) {
+    __syncthreads();  // the previous segment's last LDS reads precede this one's loads
+    const SubSeg g = mids[mi];
+    const uint32_t gf = g.f;
+    for (uint32_t j = t; j < g.c; j += kMidThreads) pts[j] = W[gf + j];
+    if (t == 0) {
+      SubNode& r = stk[0];
+      r.lf = 0;
+      r.lc = g.c;
+      r.depth = g.depth;
+      for (int k = 0; k < 3; ++k) {
+        r.mn[k] = g.mn[k];
+        r.mx[k] = g.mx[k];
+      }
+      r.pf = g.parent_f;
+      r.pdepth = g.parent_depth;
+      sp_s = 1;
+      maxd_s = g.depth;
+    }
+    __syncthreads();
+    for (;;) {
+      const int sp = sp_s;
+      if (sp == 0) break;
+      const SubNode nd = stk[sp - 1];  // count > kSubMax: split here
+      __syncthreads();
+      int cd;
+      float ideal;
+      split_dim(nd.mn, nd.mx, cd, ideal);
+      const uint32_t a0 = nd.lf, end = nd.lf + nd.lc, count = nd.lc;
+      float mn = __builtin_inff(), mx = -__builtin_inff();
+      for (uint32_t j = a0 + t; j < end; j += kMidThreads) {
+        const float v = coord(pts[j], cd);
+        mn = fminf(mn, v);
+        mx = fmaxf(mx, v);
+      }
+      const float lo = mid_allreduce(mn, [](float a, float b) { return fminf(a, b); }, sF);
+      const float hi = mid_allreduce(mx, [](float a, float b) { return fmaxf(a, b); }, sF);
+      const float cut = ideal < lo ? lo : (ideal > hi ? hi : ideal);
+      uint32_t nl = 0, ne = 0;
+      for (uint32_t j = a0 + t; j < end; j += kMidThreads) {
+        const float v = coord(pts[j], cd);
+        nl += v < cut ? 1u : 0u;
+        ne += v == cut ? 1u : 0u;
+      }
+      nl = mid_allreduce(nl, [](uint32_t a, uint32_t b) { return a + b; }, sU);
+      ne = mid_allreduce(ne, [](uint32_t a, uint32_t b) { return a + b; }, sU);
+      const uint32_t br1 = nl, br2 = nl + ne;
+      mid_hoare(pts, posA, posB, sA, sB, a0, a0 + br1, end, cd, cut, false);
+      if (ne) mid_hoare(pts, posA, posB, sA, sB, a0 + br1, a0 + br2, end, cd, cut, true);
+      uint32_t left;
+      if (ideal < lo) left = 1;
+      else if (ideal > hi) left = count - 1;
+      else if (br1 > count / 2) left = br1;
+      else if (br2 < count / 2) left = br2;
+      else left = count / 2;
+      if (t == 0) {
+        NodeEvent e{};
+        e.f = gf + nd.lf;
+        e.c = count;
+        e.depth = nd.depth;
+        e.pair = g.pair;
+        e.cut_bits = __float_as_uint(cut);
+        e.cd = cd;
+        e.left = left;
+        e.parent_f = nd.pf;
+        e.parent_depth = nd.pdepth;
+        emit_event(ev, valid, ecnt, total, e);
+        if (nd.depth + 1 > maxd_s) maxd_s = nd.depth + 1;
+        int spn = sp - 1;
+        for (int side = 0; side < 2; ++side) {
+          SubNode c;
+          c.lf = side ? nd.lf + left : nd.lf;
+          c.lc = side ? count - left : left;
+          c.depth = nd.depth + 1;
+          c.pf = gf + nd.lf;
+          c.pdepth = nd.depth;
+          for (int k = 0; k < 3; ++k) {
+            c.mn[k] = (side && k == cd) ? cut : nd.mn[k];
+            c.mx[k] = (!side && k == cd) ? cut : nd.mx[k];
+          }
+          if (c.lc <= (uint32_t)bucket) {
+            emit_event(ev, valid, ecnt, total, leaf_event(gf + c.lf, c.lc, c.depth, g.pair, c.pf, c.pdepth));
+          } else if (c.lc <= (uint32_t)kSubMax) {
+            const uint32_t ni = atomicAdd(&ctl->n_small, 1u);
+            if (ni >= max_seg) {
+              atomicOr(&ctl->error, 4);
+              continue;
+            }
+            SubSeg& o = subs[ni];
+            o.f = gf + c.lf;
+            o.c = c.lc;
+            o.pair = g.pair;
+            o.depth = c.depth;
+            for (int k = 0; k < 3; ++k) {
+              o.mn[k] = c.mn[k];
+              o.mx[k] = c.mx[k];
+            }
+            o.parent_f = c.pf;
+            o.parent_depth = c.pdepth;
+          } else if (spn < kMidStack) {
+            stk[spn++] = c;
+          } else {
+            atomicOr(&ctl->error, 8);
+          }
+        }
+        sp_s = spn;
+      }
+      __syncthreads();
+    }
+    // points back: W for the subtree builders, bpts for the leaves emitted here (the subtree
+    // builders overwrite their ranges of bpts)
+    for (uint32_t j = t; j < g.c; j += kMidThreads) {
+      const float4 p = pts[j];
+      W[gf + j] = p;
+      bpts[gf + j] = p;
+    }
+    if (t == 0 && pair_depth[g.pair] < maxd_s) atomicMax(&pair_depth[g.pair], maxd_s);
+  }
+}
+
 // Grid-stride over the small segments (the grid does not depend on their count, which only
 // the device knows). A segment above kSubMax points -- left over when the planned number of
 // global levels was too small for the data -- is finished in place in global memory with the
@@ -1192,6 +1510,24 @@ void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, Pai
   k_pairs_degenerate<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, rst);
 }
 
+// look-back words of every scan of a build: two per global level and the node count scan
+size_t lb_stride_words(uint32_t total) { return lb_words(total + 2); }
+bool tree_lookback_enabled() {  // AICP_TREE_LB=0: rocprim scans and a flag kernel (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_TREE_LB");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+uint32_t tree_mid_max() {  // AICP_TREE_MID=0: no mid-size builder, global levels down to kSubMax (A/B)
+  static const uint32_t v = [] {
+    const char* e = std::getenv("AICP_TREE_MID");
+    return (e && e[0] == '0') ? (uint32_t)kSubMax : (uint32_t)kMidMax;
+  }();
+  return v;
+}
+size_t lb_bytes(uint32_t total) { return (size_t)(2 * kFarStack + 1) * lb_stride_words(total) * 8; }
+
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
                                int center, const TreeWork& w, float4* bpts, int bucket) {
   (void)hipMemsetAsync(w.sums, 0, (size_t)n_pairs * 6 * sizeof(uint64_t), s);
@@ -1199,12 +1535,14 @@ hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairD
   (void)hipMemsetAsync(w.ecnt, 0, ((size_t)total + 2) * 4, s);
   (void)hipMemsetAsync(w.valid, 0, 2 * (size_t)total, s);
   (void)hipMemsetAsync(w.pair_depth, 0, (size_t)n_pairs * 4, s);
+  (void)hipMemsetAsync(w.lb, 0, lb_bytes(total), s);
   if (center) k_tr_sum<<<grid_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.sums);
   k_tr_frames<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.sums, center);
   k_tr_init_boxes<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, w.seg[0]);
-  k_tr_center<<<grid_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.W[0], w.segof[0], w.seg[0], bpts, bucket);
-  k_tr_roots<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, total, pd, w.seg[0], w.subs, w.ctl, w.ev, w.valid, w.ecnt,
-                                                  bucket);
+  k_tr_center<<<grid_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.W[0], w.segof[0], w.seg[0], bpts, bucket,
+                                             w.mid_max);
+  k_tr_roots<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, total, pd, w.seg[0], w.subs, w.mids, w.ctl, w.ev, w.valid, w.ecnt,
+                                                  bucket, w.mid_max);
   return hipGetLastError();
 }
 
@@ -1216,16 +1554,28 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   const unsigned gp = grid_of(total), gp1 = grid_of((size_t)total + 1);
   // segments at this level: at most n_pairs << level and at most total / kSubMax
   const unsigned gs = grid_of(std::min<size_t>(w.max_seg, (size_t)w.n_pairs << std::min(level, 20)));
+  const uint32_t nt1 = lb_words(total + 1) - 1;  // tiles of a scan over [0, total]
+  uint64_t* st1 = w.lb + (size_t)(2 * level) * w.lb_stride;
+  uint64_t* st2 = st1 + w.lb_stride;
+  const bool lb = tree_lookback_enabled();
   k_tr_minmax<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[0], seg);
-  k_tr_flag1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.flag);
-  hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X1, (size_t)total + 1);
-  if (e != hipSuccess) return e;
+  if (lb) {
+    k_tr_scan1<<<nt1, kLbThreads, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, st1, w.ctl);
+  } else {
+    k_tr_flag1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.flag);
+    const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X1, (size_t)total + 1);
+    if (e != hipSuccess) return e;
+  }
   k_tr_pos<<<gp, 256, 0, s>>>(total, 1, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR);
   k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR, w.W[1], w.flag);
-  e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X2, (size_t)total + 1);
-  if (e != hipSuccess) return e;
-  k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.ctl, w.X2, w.ev, w.valid, w.ecnt, w.pair_depth,
-                                bucket, (uint32_t)w.max_seg);
+  if (lb) {
+    k_tr_scan_counts<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, w.ctl);
+  } else {
+    const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X2, (size_t)total + 1);
+    if (e != hipSuccess) return e;
+  }
+  k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.mids, w.ctl, w.X2, w.ev, w.valid, w.ecnt, w.pair_depth,
+                                bucket, (uint32_t)w.max_seg, w.mid_max);
   k_tr_pos<<<gp, 256, 0, s>>>(total, 2, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR);
   k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR, w.W[0], w.segof[b], bpts);
   return hipGetLastError();
@@ -1256,11 +1606,26 @@ hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, const TreeWork& w
   return hipGetLastError();
 }
 
+hipError_t launch_tree_mid(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts, int bucket) {
+  // grid: an upper bound of the mid-size segment count, capped (the kernel strides over the
+  // device-side count)
+  const size_t bound = std::min<size_t>(w.max_seg, (size_t)total / (size_t)(kSubMax + 1) + (size_t)w.n_pairs + 1);
+  const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, 1024));
+  k_tr_mid<<<g, kMidThreads, 0, s>>>(total, w.ctl, w.mids, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt, w.pair_depth,
+                                     bucket, (uint32_t)w.max_seg);
+  return hipGetLastError();
+}
+
 hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const TreeWork& w,
                               uint4* nodes) {
   // S[p] = #nodes with end < p  (exclusive scan over end positions 0..total+1)
-  hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.ecnt, w.X1, (size_t)total + 2);
-  if (e != hipSuccess) return e;
+  if (tree_lookback_enabled()) {
+    k_tr_scan_counts<<<lb_words(total + 2) - 1, kLbThreads, 0, s>>>(total + 2, w.ecnt, w.X1,
+                                                                      w.lb + (size_t)(2 * kFarStack) * w.lb_stride, w.ctl);
+  } else {
+    const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.ecnt, w.X1, (size_t)total + 2);
+    if (e != hipSuccess) return e;
+  }
   k_tr_emit<<<grid_of(2 * (size_t)total), 256, 0, s>>>(total, w.ev, w.valid, w.X1, pd, nodes, w.ctl);
   k_tr_desc<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.X1, w.pair_depth, w.ctl);
   return hipGetLastError();

@@ -66,15 +66,15 @@ inline void release(PinBuf& b) {
 // Work space of one kd-tree construction (kernels_tree.hip). Two sets: the raw-coordinate
 // tree (SurfaceNormal) and the centred matcher tree are built concurrently on two streams.
 struct TreeBufs {
-  DevBuf W0, W1, segof0, segof1, seg0, seg1, flag, X1, X2, posL, posR, ev, valid, subs, ecnt, sums, pdepth, ctl,
-      scan;
+  DevBuf W0, W1, segof0, segof1, seg0, seg1, flag, X1, X2, posL, posR, ev, valid, subs, mids, ecnt, sums, pdepth,
+      ctl, scan, lb;
   PinBuf pin_ctl;
   TreeWork tw{};    // device_trees_begin -> device_trees_end
   int planned = 0;  // global levels enqueued without host polling (0: polled build)
   int needed = 0;   // global levels the last planned build actually used
   void release_all() {
     for (DevBuf* b : {&W0, &W1, &segof0, &segof1, &seg0, &seg1, &flag, &X1, &X2, &posL, &posR, &ev, &valid, &subs,
-                      &ecnt, &sums, &pdepth, &ctl, &scan})
+                      &mids, &ecnt, &lb, &sums, &pdepth, &ctl, &scan})
       release(*b);
     release(pin_ctl);
   }
