@@ -838,6 +838,11 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(ensure(ctx->sel_cnt, P * 4));
     HIPC(hipMemsetAsync(ctx->sel_hist.p, 0, P * kHistBins * 4, s));
     HIPC(hipMemsetAsync(ctx->sel_cnt.p, 0, P * 4, s));
+    const bool fuse = icp_fuse_enabled();
+    if (fuse) {
+      HIPC(ensure(ctx->isync, icp_sync_words(P) * 4));
+      HIPC(hipMemsetAsync(ctx->isync.p, 0, icp_sync_words(P) * 4, s));
+    }
     float4* bpts = ctx->bpts.as<float4>();
     float4* bnrm = ctx->bnrm.as<float4>();
     float4* readc = ctx->read_c.as<float4>();
@@ -913,7 +918,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
         const IcpGroup& q = grp[g];
         const PairDesc* gd = dDesc + q.p0;
         PairState* gs = dState + q.p0;
-        launch_active_list(q.st, q.np, gd, gs, q.al, q.ctr);
+        if (!fuse || it == 0) launch_active_list(q.st, q.np, gd, gs, q.al, q.ctr);
         if (G == 2 && icp_serial_nn()) HIPC(hipStreamWaitEvent(q.st, grp[1 - g].nn_done, 0));
         prm.prof_slot = nn_launches;
         if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches], q.st));
@@ -923,6 +928,19 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
         if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches + 1], q.st));
         if (G == 2) HIPC(hipEventRecord(q.nn_done, q.st));
         ++nn_launches;
+        if (fuse) {  // select + reduce with the per-pair steps and the next active list inside
+          IcpIterSync y = icp_sync_layout(ctx->isync.as<uint32_t>(), P, g);
+          y.np = q.np;
+          y.pd = gd;
+          y.st = gs;
+          y.al = q.al;
+          y.ctr = q.ctr;
+          launch_icp_select_f(q.st, q.msel, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
+                              ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), y);
+          launch_icp_reduce_f(q.st, q.mred, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
+                              ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>(), prm, y);
+          continue;
+        }
         launch_icp_select(q.st, q.msel, q.np, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
                           ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), q.p0);
         launch_icp_reduce(q.st, q.mred, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
@@ -1095,6 +1113,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   release(ctx->crop_ws);
   release(ctx->ovl_sp);
   release(ctx->ovl_keys);
+  release(ctx->isync);
   release(ctx->pin_crop);
   seq_state_free(ctx->seq);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,

@@ -46,6 +46,36 @@ bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
                         ActiveList* al, uint32_t* ctr, uint32_t* host_n = nullptr, uint64_t* done_sig = nullptr,
                         const uint64_t* ticket = nullptr, float* outT = nullptr);
+// Fused ICP iteration (AICP_ICP_FUSE=0 restores one launch per step): the last workgroup of a
+// pair to finish the histogram / compaction / reduction runs that pair's find1 / final select /
+// update, and the last pair of the group rebuilds the active list for the next iteration (and,
+// when none is left, publishes the corrections and the sequence ticket). Four launches per
+// iteration (NN, select x2, reduce) instead of eight. Counters start at zero (icp_sync_words per
+// pair group) and reset themselves.
+struct IcpIterSync {
+  uint32_t* sel1;   // per pair (absolute index): histogram workgroups arrived
+  uint32_t* sel2;   // per pair: compaction workgroups arrived
+  uint32_t* red;    // per pair: reduction workgroups arrived
+  uint32_t* pairs;  // pairs of the group done with this iteration
+  int np;           // the group's pairs (pd, st point at its first)
+  const PairDesc* pd;
+  PairState* st;
+  ActiveList* al;
+  uint32_t* ctr;
+  uint32_t* host_n;    // nullable: the active count for the next iteration (mapped host memory)
+  uint64_t* done_sig;  // nullable: see launch_active_list
+  const uint64_t* ticket;
+  float* outT;
+};
+bool icp_fuse_enabled();
+inline size_t icp_sync_words(size_t n_pairs) { return 3 * n_pairs + 2; }
+// sync words laid out for pairs [0, n_pairs): sel1 | sel2 | red | pairs (2: one per group)
+IcpIterSync icp_sync_layout(uint32_t* words, size_t n_pairs, int group);
+void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
+                         uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y);
+void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float4* read_c,
+                         const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
+                         const float4* bnrm, double* slab, const IcpParams& prm, const IcpIterSync& y);
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st,
                    const ActiveList* al, const float4* read_c, const uint4* nodes, const uint4* tl,
                    const int32_t* parent, const float4* bpts, const uint2* ptl, int32_t* match, float* d2,
@@ -116,6 +146,7 @@ struct TreeWork {
   uint32_t mid_max;      // segments up to this size leave the global levels (kMidMax; kSubMax: no mid builder)
 };
 bool tree_lookback_enabled();
+bool tree_bsearch_enabled();
 uint32_t tree_mid_max();
 size_t tree_scan_temp_bytes(size_t n);
 size_t lb_bytes(uint32_t total);

@@ -1532,19 +1532,19 @@ __global__ void k_init_state(int n_pairs, const PairDesc* __restrict__ pd, PairS
   s.th[0][0] = s.th[0][1] = s.th[0][2] = 0.0;
 }
 
-// one workgroup: prefix of n_read over the pairs still active + zero the work counter
-__global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDesc* __restrict__ pd,
-                                                      const PairState* __restrict__ st,
-                                                      ActiveList* al, uint32_t* ctr, uint32_t* host_n,
-                                                      uint64_t* done_sig, const uint64_t* ticket, float* outT) {
+// one workgroup (any size, whole waves): prefix of n_read over the pairs still active + zero the
+// work counter
+__device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
+                                 ActiveList* al, uint32_t* ctr, uint32_t* host_n, uint64_t* done_sig,
+                                 const uint64_t* ticket, float* outT) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t wcnt[16];
   __shared__ uint32_t carry_off, carry_cnt;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = (int)blockDim.x;
   if (t == 0) carry_off = carry_cnt = 0;
   if (t < kXcdGroups) ctr[t * kCtrStride] = 0;
   __syncthreads();
-  for (int base = 0; base < n_pairs; base += 1024) {
+  for (int base = 0; base < n_pairs; base += nt) {
     const int p = base + t;
     const bool a = p < n_pairs && st[p].active;
     // each pair's slot range is padded to a multiple of 64: a 64-slot chunk of the NN work space
@@ -1575,7 +1575,7 @@ __global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDes
       al->off[e] = bo + x - v;
     }
     __syncthreads();
-    if (t == 1023) {
+    if (t == nt - 1) {
       carry_off = bo + x;
       carry_cnt = bc + c;
     }
@@ -1590,7 +1590,7 @@ __global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDes
   // every pair has stopped: their corrections are final (k_finalize's arithmetic), and the
   // sequence's next reference, waiting on done_sig on another stream, may start now
   if (done_sig && carry_cnt == 0) {
-    for (int p = t; p < n_pairs; p += 1024) {
+    for (int p = t; p < n_pairs; p += nt) {
       float tmp[16];
       mul4(pd[p].Tmean, st[p].T, tmp);
       mul4(tmp, pd[p].Tinit, outT + 16 * (size_t)p);
@@ -1599,6 +1599,38 @@ __global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDes
     __syncthreads();
     if (t == 0) __hip_atomic_store(done_sig, *ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+__global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDesc* __restrict__ pd,
+                                                      const PairState* __restrict__ st,
+                                                      ActiveList* al, uint32_t* ctr, uint32_t* host_n,
+                                                      uint64_t* done_sig, const uint64_t* ticket, float* outT) {
+  active_list_body(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT);
+}
+
+// The last workgroup to arrive at a per-pair (or per-group) counter runs the serial step that
+// follows (fused ICP iteration, AICP_ICP_FUSE): every wave's stores complete, one lane releases
+// them at agent scope and adds; the last one acquires before reading what the others wrote
+// (cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md: release fence, vmcnt wait, then
+// the counter; acquire on the reading side). The counter is reset for the next launch.
+__device__ __forceinline__ bool last_arrival(uint32_t* cnt, uint32_t n_expected) {
+  __shared__ uint32_t s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = atomicAdd(cnt, 1u);
+    const bool last = old + 1 == n_expected;
+    if (last) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last ? 1u : 0u;
+  }
+  __syncthreads();
+  return s_last != 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1868,10 +1900,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
 #endif
 }
 
-// rank k -> (bin, k - count before bin) over h[nb] with 1024 threads; result in res[0..1]
+// rank k -> (bin, k - count before bin) over h[nb] (nb a multiple of the block size, whole
+// waves); result in res[0..1]
 __device__ void block_find_rank(const uint32_t* h, int nb, uint32_t k, uint32_t* res, uint32_t* wsum) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int per = nb / 1024;
+  const int per = nb / (int)blockDim.x;
   uint32_t local = 0;
   for (int i = 0; i < per; ++i) local += h[t * per + i];
   uint32_t x = local;
@@ -1942,28 +1975,28 @@ __global__ __launch_bounds__(256) void k_sel_hist(BlockMap m, const PairDesc* __
   }
 }
 
-__global__ __launch_bounds__(1024) void k_sel_find1(PairState* st, uint32_t* __restrict__ hist1) {
-  const int pair = blockIdx.x;
-  PairState& s = st[pair];
-  if (!s.active) return;
+// per pair (one workgroup, any size): n = #finite, k, bin b1 holding rank k, rank r1 inside it;
+// the global histogram is read (atomics wrote it; agent-scope loads) and zeroed for the next
+// iteration. Returns false when the pair stopped (no finite distance).
+__device__ bool sel_find1_body(PairState& s, uint32_t* __restrict__ g) {
   __shared__ uint32_t h[kHistBins];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t res[2];
-  const int t = threadIdx.x, lane = t & 63;
-  uint32_t* g = hist1 + (size_t)pair * kHistBins;
-  const uint32_t a = g[2 * t], b = g[2 * t + 1];
-  h[2 * t] = a;
-  h[2 * t + 1] = b;
-  g[2 * t] = 0;  // ready for the next iteration
-  g[2 * t + 1] = 0;
-  uint32_t v = a + b;
+  const int t = threadIdx.x, lane = t & 63, nt = (int)blockDim.x;
+  uint32_t v = 0;
+  for (int i = t; i < kHistBins; i += nt) {
+    const uint32_t c = __hip_atomic_load(&g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h[i] = c;
+    g[i] = 0;  // ready for the next iteration
+    v += c;
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   if (lane == 0) wsum[t >> 6] = v;
   __syncthreads();
   if (t == 0) {
     uint32_t n = 0;
-    for (int w = 0; w < 16; ++w) n += wsum[w];
+    for (int w = 0; w < nt / 64; ++w) n += wsum[w];
     res[0] = n;
   }
   __syncthreads();
@@ -1974,7 +2007,7 @@ __global__ __launch_bounds__(1024) void k_sel_find1(PairState* st, uint32_t* __r
       s.status = 1;
       s.active = 0;
     }
-    return;
+    return false;
   }
   const float ratio = s.ratio;
   uint32_t k;
@@ -1991,6 +2024,58 @@ __global__ __launch_bounds__(1024) void k_sel_find1(PairState* st, uint32_t* __r
     s.sel_r1 = res[1];
     s.n_finite = (int32_t)n;
   }
+  return true;
+}
+
+__global__ __launch_bounds__(1024) void k_sel_find1(PairState* st, uint32_t* __restrict__ hist1) {
+  const int pair = blockIdx.x;
+  PairState& s = st[pair];
+  if (!s.active) return;
+  (void)sel_find1_body(s, hist1 + (size_t)pair * kHistBins);
+}
+
+// a pair is done with this iteration; the group's last one builds the next active list
+__device__ void pair_done(const IcpIterSync& y) {
+  if (!last_arrival(y.pairs, y.al->n)) return;
+  active_list_body(y.np, y.pd, y.st, y.al, y.ctr, y.host_n, y.done_sig, y.ticket, y.outT);
+}
+
+// k_sel_hist + (last workgroup of the pair) k_sel_find1; a pair that stops here is done with
+// the iteration
+__global__ __launch_bounds__(256) void k_sel_hist_f(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
+                                                    const float* __restrict__ d2, uint32_t* __restrict__ hist1,
+                                                    IcpIterSync y) {
+  const int pair = m.pair[blockIdx.x];
+  if (!st[pair].active) return;
+  __shared__ uint32_t h[2][kHistBins];  // one sub-histogram per wave pair (LDS atomic conflicts)
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2 * kHistBins / 256; ++i) (&h[0][0])[t + 256 * i] = 0;
+  const PairDesc& d = pd[pair];
+  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
+  const uint32_t j0 = m.start[blockIdx.x];
+  uint32_t v[kSelPerThread];
+#pragma unroll
+  for (int u = 0; u < kSelPerThread; ++u) {
+    const uint32_t j = j0 + t + 256u * u;
+    v[u] = j < d.n_read ? bits[j] : kInfBits;
+  }
+  __syncthreads();
+  uint32_t* mine = h[t >> 7];
+#pragma unroll
+  for (int u = 0; u < kSelPerThread; ++u)
+    if (v[u] != kInfBits) atomicAdd(&mine[v[u] >> 21], 1u);
+  __syncthreads();
+  uint32_t* g = hist1 + (size_t)pair * kHistBins;
+#pragma unroll
+  for (int i = 0; i < kHistBins / 256; ++i) {
+    const int b = t + 256 * i;
+    const uint32_t c = h[0][b] + h[1][b];
+    if (c) atomicAdd(&g[b], c);
+  }
+  const uint32_t nblk = (d.n_read + 256u * kSelPerThread - 1) / (256u * kSelPerThread);
+  if (!last_arrival(&y.sel1[pair], nblk)) return;
+  if (!sel_find1_body(st[pair], g)) pair_done(y);
 }
 
 __global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc* __restrict__ pd,
@@ -2037,28 +2122,24 @@ __global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc*
   }
 }
 
-__global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__ pd, PairState* st,
-                                                    const uint32_t* __restrict__ cand, uint32_t* __restrict__ cand_cnt) {
-  const int pair = blockIdx.x;
-  PairState& s = st[pair];
-  if (!s.active) return;
+// per pair (one workgroup, any size): digits 2 (bits 20..10) and 3 (bits 9..0) over the candidates
+__device__ void sel_final_body(PairState& s, const uint32_t* __restrict__ cv, uint32_t* cand_cnt) {
   __shared__ uint32_t h[kHistBins];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t res[2];
-  const int t = threadIdx.x;
-  const uint32_t c = cand_cnt[pair];
-  const uint32_t* cv = cand + pd[pair].read_off;
-  for (int i = t; i < kHistBins; i += 1024) h[i] = 0;
+  const int t = threadIdx.x, nt = (int)blockDim.x;
+  const uint32_t c = __hip_atomic_load(cand_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = t; i < kHistBins; i += nt) h[i] = 0;
   __syncthreads();
-  for (uint32_t i = t; i < c; i += 1024) atomicAdd(&h[(cv[i] >> 10) & 2047u], 1u);
+  for (uint32_t i = t; i < c; i += nt) atomicAdd(&h[(cv[i] >> 10) & 2047u], 1u);
   __syncthreads();
   block_find_rank(h, kHistBins, s.sel_r1, res, wsum);
   const uint32_t b2 = res[0], r2 = res[1];
   __syncthreads();
-  for (int i = t; i < kHistBins; i += 1024) h[i] = 0;
+  for (int i = t; i < kHistBins; i += nt) h[i] = 0;
   __syncthreads();
   const uint32_t hi21 = (s.sel_b1 << 11) | b2;
-  for (uint32_t i = t; i < c; i += 1024) {
+  for (uint32_t i = t; i < c; i += nt) {
     const uint32_t v = cv[i];
     if ((v >> 10) == hi21) atomicAdd(&h[v & 1023u], 1u);
   }
@@ -2066,8 +2147,64 @@ __global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__
   block_find_rank(h, kHist3Bins, r2, res, wsum);
   if (t == 0) {
     s.limit = __uint_as_float((hi21 << 10) | res[0]);
-    cand_cnt[pair] = 0;  // ready for the next iteration
+    *cand_cnt = 0;  // ready for the next iteration
   }
+}
+
+__global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__ pd, PairState* st,
+                                                    const uint32_t* __restrict__ cand, uint32_t* __restrict__ cand_cnt) {
+  const int pair = blockIdx.x;
+  PairState& s = st[pair];
+  if (!s.active) return;
+  sel_final_body(s, cand + pd[pair].read_off, cand_cnt + pair);
+}
+
+// k_sel_compact + (last workgroup of the pair) k_sel_final
+__global__ __launch_bounds__(256) void k_sel_compact_f(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
+                                                       const float* __restrict__ d2, uint32_t* __restrict__ cand,
+                                                       uint32_t* __restrict__ cand_cnt, IcpIterSync y) {
+  const int pair = m.pair[blockIdx.x];
+  PairState& s = st[pair];
+  if (!s.active) return;
+  __shared__ uint32_t wcount[4];
+  __shared__ uint32_t base;
+  const PairDesc& d = pd[pair];
+  const uint32_t b1 = s.sel_b1;
+  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t j0 = m.start[blockIdx.x];
+  uint32_t v[kSelPerThread];
+#pragma unroll
+  for (int u = 0; u < kSelPerThread; ++u) {
+    const uint32_t j = j0 + t + 256u * u;
+    v[u] = j < d.n_read ? bits[j] : kInfBits;
+  }
+  uint32_t mine = 0;  // this wave's hits
+#pragma unroll
+  for (int u = 0; u < kSelPerThread; ++u)
+    mine += (uint32_t)__popcll(__ballot(v[u] != kInfBits && (v[u] >> 21) == b1));
+  if (lane == 0) wcount[w] = mine;
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    base = tot ? atomicAdd(&cand_cnt[pair], tot) : 0u;
+  }
+  __syncthreads();
+  if (wcount[w]) {
+    uint32_t o = base;
+    for (int k = 0; k < w; ++k) o += wcount[k];
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int u = 0; u < kSelPerThread; ++u) {
+      const bool hit = v[u] != kInfBits && (v[u] >> 21) == b1;
+      const uint64_t mk = __ballot(hit);
+      if (hit) cand[d.read_off + o + (uint32_t)__popcll(mk & below)] = v[u];
+      o += (uint32_t)__popcll(mk);
+    }
+  }
+  const uint32_t nblk = (d.n_read + 256u * kSelPerThread - 1) / (256u * kSelPerThread);
+  if (!last_arrival(&y.sel2[pair], nblk)) return;
+  sel_final_body(s, cand + d.read_off, cand_cnt + pair);
 }
 
 // DPP lane moves of a double (both halves with the same control); lanes outside the
@@ -2090,15 +2227,12 @@ __device__ __forceinline__ double row_sum_d(double v) {
   return v;
 }
 
-__global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
-    BlockMap m, const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
-    const float4* __restrict__ read_c, const int32_t* __restrict__ match,
-    const float* __restrict__ d2, const uint32_t* __restrict__ touched, const float4* __restrict__ bpts,
-    const float4* __restrict__ bnrm, double* __restrict__ slab) {
-  const int pair = m.pair[blockIdx.x];
-  const PairState& s = st[pair];
-  if (!s.active) return;
-  const PairDesc& d = pd[pair];
+// one reduce workgroup's partial sums (kRedCols) into its slab row
+__device__ __forceinline__ void icp_reduce_body(BlockMap m, const PairDesc& d, const PairState& s,
+                                                const float4* __restrict__ read_c, const int32_t* __restrict__ match,
+                                                const float* __restrict__ d2, const uint32_t* __restrict__ touched,
+                                                const float4* __restrict__ bpts, const float4* __restrict__ bnrm,
+                                                double* __restrict__ slab) {
   float T[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) T[i] = s.T[i];
@@ -2188,35 +2322,19 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
   }
 }
 
-__global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__ pd, PairState* st,
-                                                    const double* __restrict__ slab, IcpParams prm) {
-  const int pair = blockIdx.x;
-  PairState& s = st[pair];
+__global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
+    BlockMap m, const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
+    const float4* __restrict__ read_c, const int32_t* __restrict__ match,
+    const float* __restrict__ d2, const uint32_t* __restrict__ touched, const float4* __restrict__ bpts,
+    const float4* __restrict__ bnrm, double* __restrict__ slab) {
+  const int pair = m.pair[blockIdx.x];
+  const PairState& s = st[pair];
   if (!s.active) return;
-  const PairDesc& d = pd[pair];
-  // the pair's slab rows: thread t sums column t % kRedCols over rows t / kRedCols + 8 k
-  // (independent loads, contiguous across the block), then a fixed-order sum of the 8 groups
-  constexpr int kGroups = 256 / kRedCols;
-  __shared__ double part[kGroups][kRedCols];
-  __shared__ double tot[kRedCols];
-  const int t = threadIdx.x;
-  if (t < kGroups * kRedCols) {
-    const int g = t / kRedCols, c = t - g * kRedCols;
-    const double* col = slab + (size_t)d.red_blk_off * kRedCols + c;
-    double v = 0.0;
-#pragma unroll 4
-    for (uint32_t r = g; r < d.n_red_blk; r += kGroups) v += col[(size_t)r * kRedCols];
-    part[g][c] = v;
-  }
-  __syncthreads();
-  if (t < kRedCols) {
-    double v = part[0][t];
-#pragma unroll
-    for (int g = 1; g < kGroups; ++g) v += part[g][t];
-    tot[t] = v;
-  }
-  __syncthreads();
-  if (t != 0) return;
+  icp_reduce_body(m, pd[pair], s, read_c, match, d2, touched, bpts, bnrm, slab);
+}
+
+// the serial part of an ICP update (one lane): solve, compose, checkers
+__device__ void update_serial(const PairDesc& d, PairState& s, const double* tot, const IcpParams& prm) {
   s.touched_pts += (uint64_t)tot[28];
   s.touched_nodes += (uint64_t)tot[29];
   const int32_t kept = (int32_t)tot[27];
@@ -2283,6 +2401,60 @@ __global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__
     }
   }
   s.active = iterate ? 1 : 0;
+}
+
+// one pair's update by a 256-thread workgroup: its slab rows summed (thread t sums column
+// t % kRedCols over rows t / kRedCols + 8 k -- independent loads, contiguous across the block --
+// then a fixed-order sum of the 8 groups), then update_serial on lane 0
+__device__ void icp_update_body(const PairDesc& d, PairState& s, const double* __restrict__ slab,
+                                const IcpParams& prm) {
+  constexpr int kGroups = 256 / kRedCols;
+  __shared__ double part[kGroups][kRedCols];
+  __shared__ double tot[kRedCols];
+  const int t = threadIdx.x;
+  if (t < kGroups * kRedCols) {
+    const int g = t / kRedCols, c = t - g * kRedCols;
+    const double* col = slab + (size_t)d.red_blk_off * kRedCols + c;
+    double v = 0.0;
+#pragma unroll 4
+    for (uint32_t r = g; r < d.n_red_blk; r += kGroups) v += col[(size_t)r * kRedCols];
+    part[g][c] = v;
+  }
+  __syncthreads();
+  if (t < kRedCols) {
+    double v = part[0][t];
+#pragma unroll
+    for (int g = 1; g < kGroups; ++g) v += part[g][t];
+    tot[t] = v;
+  }
+  __syncthreads();
+  if (t == 0) update_serial(d, s, tot, prm);
+}
+
+__global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__ pd, PairState* st,
+                                                    const double* __restrict__ slab, IcpParams prm) {
+  const int pair = blockIdx.x;
+  PairState& s = st[pair];
+  if (!s.active) return;
+  icp_update_body(pd[pair], s, slab, prm);
+}
+
+// k_icp_reduce + (last workgroup of the pair) k_icp_update + (last pair of the group) the next
+// active list
+__global__ __launch_bounds__(kNNBlock) void k_icp_reduce_f(
+    BlockMap m, const PairDesc* __restrict__ pd, PairState* st, const float4* __restrict__ read_c,
+    const int32_t* __restrict__ match, const float* __restrict__ d2, const uint32_t* __restrict__ touched,
+    const float4* __restrict__ bpts, const float4* __restrict__ bnrm, double* __restrict__ slab, IcpParams prm,
+    IcpIterSync y) {
+  static_assert(kNNBlock == 256, "icp_update_body: 256 threads");
+  const int pair = m.pair[blockIdx.x];
+  PairState& s = st[pair];
+  if (!s.active) return;
+  const PairDesc& d = pd[pair];
+  icp_reduce_body(m, d, s, read_c, match, d2, touched, bpts, bnrm, slab);
+  if (!last_arrival(&y.red[pair], d.n_red_blk)) return;
+  icp_update_body(d, s, slab, prm);
+  pair_done(y);
 }
 
 __global__ void k_finalize(int n_pairs, const PairDesc* __restrict__ pd,
@@ -2539,6 +2711,33 @@ void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* p
   k_sel_find1<<<n_pairs, 1024, 0, s>>>(st + p0, hist1 + (size_t)p0 * kHistBins);
   k_sel_compact<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, cand, cand_cnt);
   k_sel_final<<<n_pairs, 1024, 0, s>>>(pd + p0, st + p0, cand, cand_cnt + p0);
+}
+bool icp_fuse_enabled() {  // AICP_ICP_FUSE=0: one launch per step (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_ICP_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+IcpIterSync icp_sync_layout(uint32_t* words, size_t n_pairs, int group) {
+  IcpIterSync y{};
+  y.sel1 = words;
+  y.sel2 = words + n_pairs;
+  y.red = words + 2 * n_pairs;
+  y.pairs = words + 3 * n_pairs + group;
+  return y;
+}
+void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
+                         uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y) {
+  if (!m.n_blocks) return;
+  k_sel_hist_f<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, hist1, y);
+  k_sel_compact_f<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, cand, cand_cnt, y);
+}
+void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float4* read_c,
+                         const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
+                         const float4* bnrm, double* slab, const IcpParams& prm, const IcpIterSync& y) {
+  if (m.n_blocks)
+    k_icp_reduce_f<<<m.n_blocks, kNNBlock, 0, s>>>(m, pd, st, read_c, match, d2, touched, bpts, bnrm, slab, prm, y);
 }
 void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const PairState* st, const float4* read_c,
                        const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,

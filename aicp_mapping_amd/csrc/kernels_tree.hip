@@ -294,38 +294,40 @@ __device__ __forceinline__ void atomic_add128(uint64_t* w, uint64_t lo, int64_t 
   atomicAdd((unsigned long long*)(w + 1), (unsigned long long)((uint64_t)hi + carry));
 }
 
+// Per-pair reductions over the points use tiles of kTile positions per 256-thread block (8 per
+// thread): a tile inside one pair (the common case) reduces in registers + LDS and issues one
+// atomic per word, so a 120k-point cloud makes ~60 atomics per word instead of ~470.
+constexpr int kTileItems = 8;
+constexpr uint32_t kTile = 256 * kTileItems;
+inline unsigned tiles_of(size_t n) { return (unsigned)std::max<size_t>(1, (n + kTile - 1) / kTile); }
+
 __global__ __launch_bounds__(256) void k_tr_sum(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
                                                 const float4* __restrict__ raw, uint64_t* sums) {
   __shared__ uint64_t slo[3][4];
   __shared__ int64_t shi[3][4];
-  const uint32_t base = blockIdx.x * blockDim.x;
-  const uint32_t i = base + threadIdx.x;
-  const bool ok = i < total;
-  const uint32_t last = min(base + 255u, total - 1);
-  // a block inside one pair (the common case) reduces in LDS and issues 2 atomics per axis
+  const uint32_t base = blockIdx.x * kTile;
+  const uint32_t last = min(base + kTile - 1, total - 1);
   const int p_first = pair_of_pos(pd, n_pairs, base), p_last = pair_of_pos(pd, n_pairs, last);
   const bool uniform = p_first == p_last;
-  const int pair = ok ? (uniform ? p_first : pair_of_pos(pd, n_pairs, i)) : -1;
-  const float4 p = ok ? raw[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float c[3] = {p.x, p.y, p.z};
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t alo[3] = {0, 0, 0};
+  int64_t ahi[3] = {0, 0, 0};
+  for (int j = 0; j < kTileItems; ++j) {
+    const uint32_t i = base + (uint32_t)j * 256 + threadIdx.x;
+    const bool ok = i < total;
+    const int pair = ok ? (uniform ? p_first : pair_of_pos(pd, n_pairs, i)) : -1;
+    const float4 p = ok ? raw[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float c[3] = {p.x, p.y, p.z};
 #pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const int64_t q = ok ? fixed40(c[d]) : 0;
-    uint64_t lo = (uint64_t)q;
-    int64_t hi = q < 0 ? -1 : 0;
-    if (uniform) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t lo_o = __shfl_xor(lo, off, 64);
-        const int64_t hi_o = __shfl_xor(hi, off, 64);
-        add128(lo, hi, lo_o, hi_o);
+    for (int d = 0; d < 3; ++d) {
+      const int64_t q = ok ? fixed40(c[d]) : 0;
+      uint64_t lo = (uint64_t)q;
+      int64_t hi = q < 0 ? -1 : 0;
+      if (uniform) {
+        add128(alo[d], ahi[d], lo, hi);
+        continue;
       }
-      if (lane == 0) {
-        slo[d][w] = lo;
-        shi[d][w] = hi;
-      }
-    } else {  // pair boundary inside the block: segmented wave scan, one atomic pair per run
+      // pair boundary inside the tile: segmented wave scan, one atomic pair per run
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
         const int ko = __shfl_up(pair, off, 64);
@@ -338,6 +340,21 @@ __global__ __launch_bounds__(256) void k_tr_sum(int n_pairs, uint32_t total, con
     }
   }
   if (!uniform) return;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    uint64_t lo = alo[d];
+    int64_t hi = ahi[d];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t lo_o = __shfl_xor(lo, off, 64);
+      const int64_t hi_o = __shfl_xor(hi, off, 64);
+      add128(lo, hi, lo_o, hi_o);
+    }
+    if (lane == 0) {
+      slo[d][w] = lo;
+      shi[d][w] = hi;
+    }
+  }
   __syncthreads();
   if (threadIdx.x < 3) {
     const int d = threadIdx.x;
@@ -366,6 +383,25 @@ __global__ void k_tr_frames(int n_pairs, PairDesc* pd, const uint64_t* sums, int
   mul4(Tmi, d.Tin, d.Tinit);
 }
 
+// The build's zeroed work space in one launch (instead of a memset per buffer): up to 6 regions,
+// 16-byte words (every region is 16-byte aligned and has room up to its next multiple of 16), and
+// the root segment boxes set empty (min at the largest encoding, max at the smallest).
+struct ZeroJob {
+  uint4* p[6];
+  uint64_t n16[6];
+};
+__global__ __launch_bounds__(256) void k_tr_zero(ZeroJob job, int n_pairs, TreeSeg* seg) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+    for (uint64_t i = g; i < job.n16[r]; i += stride) job.p[r][i] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint64_t p = g; p < (uint64_t)n_pairs; p += stride)
+    for (int k = 0; k < 3; ++k) {
+      seg[p].bmn[k] = 0xffffffffu;
+      seg[p].bmx[k] = 0u;
+    }
+}
+
 // root segment boxes start empty: min at the largest encoding, max at the smallest
 __global__ void k_tr_init_boxes(int n_pairs, TreeSeg* seg) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -383,42 +419,51 @@ __global__ __launch_bounds__(256) void k_tr_center(int n_pairs, uint32_t total, 
                                                    const float4* __restrict__ raw, float4* __restrict__ W,
                                                    int32_t* __restrict__ segof, TreeSeg* seg,
                                                    float4* __restrict__ bpts, int bucket, uint32_t mid_max) {
-  const uint32_t base = blockIdx.x * blockDim.x;
-  const uint32_t i = base + threadIdx.x;
-  const bool ok = i < total;
-  const uint32_t last = min(base + 255u, total - 1);
+  const uint32_t base = blockIdx.x * kTile;
+  const uint32_t last = min(base + kTile - 1, total - 1);
   const int p_first = pair_of_pos(pd, n_pairs, base), p_last = pair_of_pos(pd, n_pairs, last);
   const bool uniform = p_first == p_last;
-  const int pair = ok ? (uniform ? p_first : pair_of_pos(pd, n_pairs, i)) : -1;
-  float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (ok) {
-    const PairDesc& d = pd[pair];
-    const float4 p = raw[i];
-    c = make_float4(p.x - d.mean[0], p.y - d.mean[1], p.z - d.mean[2], __int_as_float((int32_t)(i - d.ref_off)));
-    W[i] = c;
-    segof[i] = d.n_ref <= mid_max ? -1 : pair;
-    if (d.n_ref <= (uint32_t)bucket) bpts[i] = c;
-  }
-  const float v[3] = {c.x, c.y, c.z};
+  float amn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float amx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int j = 0; j < kTileItems; ++j) {
+    const uint32_t i = base + (uint32_t)j * 256 + threadIdx.x;
+    const bool ok = i < total;
+    const int pair = ok ? (uniform ? p_first : pair_of_pos(pd, n_pairs, i)) : -1;
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) {
+      const PairDesc& d = pd[pair];
+      const float4 p = raw[i];
+      c = make_float4(p.x - d.mean[0], p.y - d.mean[1], p.z - d.mean[2], __int_as_float((int32_t)(i - d.ref_off)));
+      W[i] = c;
+      segof[i] = d.n_ref <= mid_max ? -1 : pair;
+      if (d.n_ref <= (uint32_t)bucket) bpts[i] = c;
+    }
+    const float v[3] = {c.x, c.y, c.z};
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    float mn = ok ? v[k] : __builtin_inff(), mx = ok ? v[k] : -__builtin_inff();
-    if (uniform) {
-      block_minmax(mn, mx);
-      // one cloud spans thousands of blocks: skip the atomic when the box already holds the
-      // bound (a read costs no serialisation on the six shared words; a stale read only
-      // lets an unnecessary atomic through)
-      if (threadIdx.x == 0) {
-        const uint32_t emn = ord_enc(mn), emx = ord_enc(mx);
-        if (emn < seg[p_first].bmn[k]) atomicMin(&seg[p_first].bmn[k], emn);
-        if (emx > seg[p_first].bmx[k]) atomicMax(&seg[p_first].bmx[k], emx);
+    for (int k = 0; k < 3; ++k) {
+      float mn = ok ? v[k] : __builtin_inff(), mx = ok ? v[k] : -__builtin_inff();
+      if (uniform) {
+        amn[k] = fminf(amn[k], mn);
+        amx[k] = fmaxf(amx[k], mx);
+        continue;
       }
-    } else {
       const bool lastl = wave_seg_minmax(pair, mn, mx);
       if (ok && lastl) {
         atomicMin(&seg[pair].bmn[k], ord_enc(mn));
         atomicMax(&seg[pair].bmx[k], ord_enc(mx));
       }
+    }
+  }
+  if (!uniform) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    block_minmax(amn[k], amx[k]);
+    // a cloud spans many tiles: skip the atomic when the box already holds the bound (a stale
+    // read only lets an unnecessary atomic through)
+    if (threadIdx.x == 0) {
+      const uint32_t emn = ord_enc(amn[k]), emx = ord_enc(amx[k]);
+      if (emn < seg[p_first].bmn[k]) atomicMin(&seg[p_first].bmn[k], emn);
+      if (emx > seg[p_first].bmx[k]) atomicMax(&seg[p_first].bmx[k], emx);
     }
   }
 }
@@ -444,8 +489,10 @@ __global__ void k_tr_roots(int n_pairs, uint32_t total, const PairDesc* __restri
     s.mx[k] = ord_dec(s.bmx[k]);
   }
   split_dim(s.mn, s.mx, s.cd, s.ideal);
-  s.lo = 0xffffffffu;
-  s.hi = 0u;
+  // the points' extent along cd: the box is the points' own at the root (level 0 needs no
+  // k_tr_minmax)
+  s.lo = s.bmn[s.cd];
+  s.hi = s.bmx[s.cd];
   if (d.n_ref <= mid_max) {
     if (d.n_ref <= (uint32_t)bucket) {
       emit_event(ev, valid, ecnt, total, leaf_event(d.ref_off, d.n_ref, 0, p, 0, -1));
@@ -471,28 +518,40 @@ __global__ void k_tr_roots(int n_pairs, uint32_t total, const PairDesc* __restri
 // ---- one global level ------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_tr_minmax(uint32_t total, const int32_t* __restrict__ segof,
                                                    const float4* __restrict__ W, TreeSeg* seg) {
-  const uint32_t base = blockIdx.x * blockDim.x;
-  const uint32_t i = base + threadIdx.x;
-  const int s = i < total ? segof[i] : -1;
-  // block inside one segment (contiguous ranges: first and last position suffice)
-  const int s_first = segof[base], s_last = segof[min(base + 255u, total - 1)];
+  const uint32_t base = blockIdx.x * kTile;
+  // tile inside one segment (contiguous ranges: first and last position suffice)
+  const int s_first = segof[base], s_last = segof[min(base + kTile - 1, total - 1)];
   const bool uniform = s_first >= 0 && s_first == s_last;
-  float v = 0.f;
-  if (s >= 0) v = coord(W[i], seg[s].cd);
-  float mn = s >= 0 ? v : __builtin_inff(), mx = s >= 0 ? v : -__builtin_inff();
   if (uniform) {
+    const int cd = seg[s_first].cd;
+    float mn = __builtin_inff(), mx = -__builtin_inff();
+    for (int j = 0; j < kTileItems; ++j) {
+      const uint32_t i = base + (uint32_t)j * 256 + threadIdx.x;
+      if (i < total) {
+        const float v = coord(W[i], cd);
+        mn = fminf(mn, v);
+        mx = fmaxf(mx, v);
+      }
+    }
     block_minmax(mn, mx);
-    if (threadIdx.x == 0) {  // top levels: thousands of blocks per segment; see k_tr_center
+    if (threadIdx.x == 0) {  // top levels: many tiles per segment; see k_tr_center
       const uint32_t emn = ord_enc(mn), emx = ord_enc(mx);
       if (emn < seg[s_first].lo) atomicMin(&seg[s_first].lo, emn);
       if (emx > seg[s_first].hi) atomicMax(&seg[s_first].hi, emx);
     }
     return;
   }
-  const bool last = wave_seg_minmax(s, mn, mx);
-  if (s >= 0 && last) {
-    atomicMin(&seg[s].lo, ord_enc(mn));
-    atomicMax(&seg[s].hi, ord_enc(mx));
+  for (int j = 0; j < kTileItems; ++j) {
+    const uint32_t i = base + (uint32_t)j * 256 + threadIdx.x;
+    const int s = i < total ? segof[i] : -1;
+    float v = 0.f;
+    if (s >= 0) v = coord(W[i], seg[s].cd);
+    float mn = s >= 0 ? v : __builtin_inff(), mx = s >= 0 ? v : -__builtin_inff();
+    const bool last = wave_seg_minmax(s, mn, mx);
+    if (s >= 0 && last) {
+      atomicMin(&seg[s].lo, ord_enc(mn));
+      atomicMax(&seg[s].hi, ord_enc(mx));
+    }
   }
 }
 
@@ -550,6 +609,40 @@ struct HoareRanks {
   }
 };
 
+// The partner of the element at local position li directly, without the position arrays: the
+// k-th misplaced element from the left pairs with the k-th from the right, so the partner of a
+// misplaced-left element is the (nmr - 1 - k)-th predicate element of [br, count) and the partner
+// of a misplaced-right one the k-th non-predicate element of [lo_b, br); both are found by binary
+// search over the monotone counts X (L2-resident) instead of a scatter kernel (k_tr_pos) and a
+// kernel boundary.
+__device__ __forceinline__ uint32_t hoare_partner(uint32_t li, bool pred, uint32_t f, uint32_t lo_b, uint32_t br,
+                                                  uint32_t count, const uint32_t* __restrict__ X) {
+  if (li < br) {
+    if (pred) return li;
+    const uint32_t k = (li - lo_b) - (X[f + li] - X[f + lo_b]);
+    const uint32_t xb = X[f + br], nmr = X[f + count] - xb;
+    const uint32_t target = xb + (nmr - 1 - k);  // smallest q in (br, count] with X[f + q] > target
+    uint32_t lo = br + 1, hi = count;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (X[f + mid] > target) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo - 1;
+  }
+  if (!pred) return li;
+  const uint32_t xb = X[f + br];
+  const uint32_t k = (X[f + count] - xb) - 1 - (X[f + li] - xb);
+  const uint32_t x0 = X[f + lo_b];  // smallest q in (lo_b, br] with #non-predicate in [lo_b, q) > k
+  uint32_t lo = lo_b + 1, hi = br;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((mid - lo_b) - (X[f + mid] - x0) > k) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo - 1;
+}
+
 // partner positions of the misplaced elements of a pass
 __global__ __launch_bounds__(256) void k_tr_pos(uint32_t total, int pass, const int32_t* __restrict__ segof,
                                                 const float4* __restrict__ W, const TreeSeg* __restrict__ seg,
@@ -585,7 +678,7 @@ __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t*
                                                   const float4* __restrict__ W, TreeSeg* seg,
                                                   const uint32_t* __restrict__ X, const uint32_t* __restrict__ posL,
                                                   const uint32_t* __restrict__ posR, float4* __restrict__ W1,
-                                                  uint32_t* __restrict__ flag2) {
+                                                  uint32_t* __restrict__ flag2, int bsearch) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > total) return;
   if (i == total) {
@@ -602,9 +695,14 @@ __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t*
   const float v = coord(p, g.cd), cut = seg_cut(g);
   const uint32_t f = g.first, li = i - f;
   const uint32_t br1 = X[f + g.count] - X[f];
-  bool left;
-  const int32_t k = HoareRanks::rank(li, v < cut, f, 0, br1, g.count, X, left);
-  uint32_t p1 = k < 0 ? li : (left ? posR[f + k] : posL[f + k]);
+  uint32_t p1;
+  if (bsearch) {
+    p1 = hoare_partner(li, v < cut, f, 0, br1, g.count, X);
+  } else {
+    bool left;
+    const int32_t k = HoareRanks::rank(li, v < cut, f, 0, br1, g.count, X, left);
+    p1 = k < 0 ? li : (left ? posR[f + k] : posL[f + k]);
+  }
   if (p1 >= g.count) p1 = li;  // unreachable for a consistent scan; keeps stores in range
   W1[f + p1] = p;
   flag2[f + p1] = (p1 >= br1 && v == cut) ? 1u : 0u;
@@ -713,7 +811,8 @@ __global__ __launch_bounds__(256) void k_tr_move2(uint32_t total, const int32_t*
                                                   const float4* __restrict__ W1, const TreeSeg* __restrict__ seg,
                                                   const uint32_t* __restrict__ X2, const uint32_t* __restrict__ posL,
                                                   const uint32_t* __restrict__ posR, float4* __restrict__ W2,
-                                                  int32_t* __restrict__ segof_next, float4* __restrict__ bpts) {
+                                                  int32_t* __restrict__ segof_next, float4* __restrict__ bpts,
+                                                  int bsearch) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int s = segof[i];
@@ -727,9 +826,13 @@ __global__ __launch_bounds__(256) void k_tr_move2(uint32_t total, const int32_t*
   const uint32_t f = g.first, li = i - f;
   uint32_t p2 = li;
   if (li >= g.br1) {
-    bool left;
-    const int32_t k = HoareRanks::rank(li, v == cut, f, g.br1, g.br2, g.count, X2, left);
-    if (k >= 0) p2 = left ? posR[f + k] : posL[f + k];
+    if (bsearch) {
+      p2 = hoare_partner(li, v == cut, f, g.br1, g.br2, g.count, X2);
+    } else {
+      bool left;
+      const int32_t k = HoareRanks::rank(li, v == cut, f, g.br1, g.br2, g.count, X2, left);
+      if (k >= 0) p2 = left ? posR[f + k] : posL[f + k];
+    }
     if (p2 >= g.count) p2 = li;  // unreachable for a consistent scan; keeps stores in range
   }
   const uint32_t q = f + p2;
@@ -1519,6 +1622,13 @@ bool tree_lookback_enabled() {  // AICP_TREE_LB=0: rocprim scans and a flag kern
   }();
   return on;
 }
+bool tree_bsearch_enabled() {  // AICP_TREE_BSEARCH=0: partner positions by k_tr_pos (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_TREE_BSEARCH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 uint32_t tree_mid_max() {  // AICP_TREE_MID=0: no mid-size builder, global levels down to kSubMax (A/B)
   static const uint32_t v = [] {
     const char* e = std::getenv("AICP_TREE_MID");
@@ -1530,16 +1640,21 @@ size_t lb_bytes(uint32_t total) { return (size_t)(2 * kFarStack + 1) * lb_stride
 
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
                                int center, const TreeWork& w, float4* bpts, int bucket) {
-  (void)hipMemsetAsync(w.sums, 0, (size_t)n_pairs * 6 * sizeof(uint64_t), s);
-  (void)hipMemsetAsync(w.ctl, 0, sizeof(TreeCtl), s);
-  (void)hipMemsetAsync(w.ecnt, 0, ((size_t)total + 2) * 4, s);
-  (void)hipMemsetAsync(w.valid, 0, 2 * (size_t)total, s);
-  (void)hipMemsetAsync(w.pair_depth, 0, (size_t)n_pairs * 4, s);
-  (void)hipMemsetAsync(w.lb, 0, lb_bytes(total), s);
-  if (center) k_tr_sum<<<grid_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.sums);
+  ZeroJob z{};
+  const size_t bytes[6] = {(size_t)n_pairs * 6 * sizeof(uint64_t), sizeof(TreeCtl), ((size_t)total + 2) * 4,
+                           2 * (size_t)total, (size_t)n_pairs * 4, lb_bytes(total)};
+  void* ptr[6] = {w.sums, w.ctl, w.ecnt, w.valid, w.pair_depth, w.lb};
+  uint64_t most = 0;
+  for (int r = 0; r < 6; ++r) {
+    z.p[r] = reinterpret_cast<uint4*>(ptr[r]);
+    z.n16[r] = (bytes[r] + 15) / 16;
+    most = std::max<uint64_t>(most, z.n16[r]);
+  }
+  k_tr_zero<<<(unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (most + 255) / 256)), 256, 0, s>>>(
+      z, n_pairs, w.seg[0]);
+  if (center) k_tr_sum<<<tiles_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.sums);
   k_tr_frames<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.sums, center);
-  k_tr_init_boxes<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, w.seg[0]);
-  k_tr_center<<<grid_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.W[0], w.segof[0], w.seg[0], bpts, bucket,
+  k_tr_center<<<tiles_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.W[0], w.segof[0], w.seg[0], bpts, bucket,
                                              w.mid_max);
   k_tr_roots<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, total, pd, w.seg[0], w.subs, w.mids, w.ctl, w.ev, w.valid, w.ecnt,
                                                   bucket, w.mid_max);
@@ -1558,7 +1673,7 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   uint64_t* st1 = w.lb + (size_t)(2 * level) * w.lb_stride;
   uint64_t* st2 = st1 + w.lb_stride;
   const bool lb = tree_lookback_enabled();
-  k_tr_minmax<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[0], seg);
+  if (level > 0) k_tr_minmax<<<tiles_of(total), 256, 0, s>>>(total, w.segof[a], w.W[0], seg);  // (level 0: roots)
   if (lb) {
     k_tr_scan1<<<nt1, kLbThreads, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, st1, w.ctl);
   } else {
@@ -1566,8 +1681,9 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
     const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X1, (size_t)total + 1);
     if (e != hipSuccess) return e;
   }
-  k_tr_pos<<<gp, 256, 0, s>>>(total, 1, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR);
-  k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR, w.W[1], w.flag);
+  const bool bs = tree_bsearch_enabled();
+  if (!bs) k_tr_pos<<<gp, 256, 0, s>>>(total, 1, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR);
+  k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR, w.W[1], w.flag, bs ? 1 : 0);
   if (lb) {
     k_tr_scan_counts<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, w.ctl);
   } else {
@@ -1576,8 +1692,9 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   }
   k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.mids, w.ctl, w.X2, w.ev, w.valid, w.ecnt, w.pair_depth,
                                 bucket, (uint32_t)w.max_seg, w.mid_max);
-  k_tr_pos<<<gp, 256, 0, s>>>(total, 2, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR);
-  k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR, w.W[0], w.segof[b], bpts);
+  if (!bs) k_tr_pos<<<gp, 256, 0, s>>>(total, 2, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR);
+  k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR, w.W[0], w.segof[b], bpts,
+                                bs ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -177,6 +177,7 @@ struct aicp_hip_ctx {
   aicp_hip_batch* mapbatch = nullptr;  // aicp_hip_map_register_batch's batch buffers
   aicp::rt::DevBuf crop_ws;            // its crop work space
   aicp::rt::DevBuf ovl_sp, ovl_keys;   // sparse overlap: clouds, counts, offsets / key words
+  aicp::rt::DevBuf isync;              // fused ICP iteration: arrival counters (icp_sync_words)
   aicp::rt::PinBuf pin_crop;
 };
 

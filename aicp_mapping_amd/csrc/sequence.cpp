@@ -192,7 +192,7 @@ struct SeqSlot {
   // reference side
   DevBuf ref_src, ref_raw, bpts, bnrm, nodes, tl, ptl, tl_flag, tl_rank, tl_temp, bpts_raw, nodes_raw, nrm_raw, nbids,
       inv, rd, tsrc,  // rd: rdesc, rdesc_raw, gdesc (PairDesc) + rstate, gstate (PairState); tsrc: source T
-      wdesc, wstate, woutT, wticket;  // the window's readings (committed to the sequence's arrays at its end)
+      wdesc, wstate, woutT, wticket, isync;  // the window's readings (committed to the sequence's arrays at its end)
   TreeBufs tb[2];
   PinBuf pin_read, pin_par, pin_src;
   hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr;
@@ -232,7 +232,7 @@ void seq_state_free(SeqState* S) {
                       &sl.caps, &sl.sel_hist, &sl.sel_cnt, &sl.ctrs, &sl.active, &sl.ref_src, &sl.ref_raw, &sl.bpts,
                       &sl.bnrm, &sl.nodes, &sl.tl, &sl.ptl, &sl.tl_flag, &sl.tl_rank, &sl.tl_temp, &sl.bpts_raw,
                       &sl.nodes_raw, &sl.nrm_raw, &sl.nbids, &sl.inv, &sl.rd, &sl.tsrc, &sl.wdesc, &sl.wstate,
-                      &sl.woutT, &sl.wticket})
+                      &sl.woutT, &sl.wticket, &sl.isync})
       release(*b);
     for (auto& t : sl.tb) t.release_all();
     for (GraphCache* g : {&sl.g_raw, &sl.g_match, &sl.g_icp}) g->reset();
@@ -454,6 +454,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   HIPC(ensure(sl.wstate, np * sizeof(PairState)));
   HIPC(ensure(sl.woutT, np * 64));
   HIPC(ensure(sl.wticket, 8));
+  HIPC(ensure(sl.isync, icp_sync_words(np) * 4));
   PairDesc* dRdesc = sl.rd.as<PairDesc>();
   PairDesc* dDesc = sl.wdesc.as<PairDesc>();
   PairState* dState = sl.wstate.as<PairState>();
@@ -834,13 +835,38 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
   uint32_t* ctr = sl.ctrs.as<uint32_t>();
   const bool wait_mode = S->use_wait;
   uint64_t* tk = sl.wticket.as<uint64_t>();
-  auto iteration = [&](int it, bool poll) {
-    launch_active_list(si, (int)np, dDesc, dState, al, ctr, poll ? sl.poll_dev + it : nullptr,
-                       wait_mode ? S->sig : nullptr, tk, dOutT);
+  const bool fuse = icp_fuse_enabled();
+  IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, 0);
+  y.np = (int)np;
+  y.pd = dDesc;
+  y.st = dState;
+  y.al = al;
+  y.ctr = ctr;
+  y.done_sig = wait_mode ? S->sig : nullptr;
+  y.ticket = tk;
+  y.outT = dOutT;
+  if (fuse) HIPC(hipMemsetAsync(sl.isync.p, 0, icp_sync_words(np) * 4, si));
+  // one iteration; fused: the active list of iteration it + 1 is built at the end of iteration it
+  // (host_n: the poll slot of it + 1)
+  auto iteration = [&](int it, uint32_t* host_n_this, uint32_t* host_n_next, hipEvent_t ev_a, hipEvent_t ev_b) {
+    if (!fuse || it == 0)
+      launch_active_list(si, (int)np, dDesc, dState, al, ctr, host_n_this, wait_mode ? S->sig : nullptr, tk, dOutT);
+    if (ev_a) (void)hipEventRecord(ev_a, si);
     launch_icp_nn(si, (int)nread, dDesc, dState, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
                   use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
                   use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
                   sl.touch.as<uint32_t>(), ctr, ip);
+    if (ev_b) (void)hipEventRecord(ev_b, si);
+    if (fuse) {
+      IcpIterSync yi = y;
+      yi.host_n = host_n_next;
+      launch_icp_select_f(si, R.m_sel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
+                          sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), yi);
+      launch_icp_reduce_f(si, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(),
+                          sl.d2.as<float>(), sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(),
+                          sl.slab.as<double>(), ip, yi);
+      return;
+    }
     launch_icp_select(si, R.m_sel, (int)np, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
                       sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), 0);
     launch_icp_reduce(si, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
@@ -856,9 +882,9 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
       << R.m_red.start << R.m_red.n_blocks << sl.wdesc.p << sl.wstate.p << sl.woutT.p << tk
       << S->sig << sl.active.p << sl.ctrs.p << sl.read_c.p << sl.nodes.p << sl.tl.p << sl.bpts.p << sl.ptl.p
       << sl.match.p << sl.d2.p << sl.touch.p << sl.sel_hist.p << sl.cand.p << sl.sel_cnt.p << sl.bnrm.p
-      << sl.slab.p;
+      << sl.slab.p << fuse << sl.isync.p;
     const int rc = graph_run(ctx, sl.g_icp, si, k, [&]() -> int {
-      for (int it = 0; it < cfg->max_iter; ++it) iteration(it, false);
+      for (int it = 0; it < cfg->max_iter; ++it) iteration(it, nullptr, nullptr, nullptr, nullptr);
       launch_finalize(si, (int)np, dDesc, dState, dOutT);
       HIPC(hipGetLastError());
       return AICP_OK;
@@ -866,12 +892,13 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
     if (rc) return rc;
     nn_launches += cfg->max_iter;
   } else {
-    int pending[kLookahead + 1];
+    int pending[kMaxPolls];
     int n_pending = 0;
     bool stop = false;
+    auto polled = [&](int q) {
+      return !wait_mode && !early_exit_disabled() && q >= cfg->smooth_length && q < kMaxPolls && q < cfg->max_iter;
+    };
     for (int it = 0; it < cfg->max_iter && !stop; ++it) {
-      const bool poll = !wait_mode && !early_exit_disabled() && it >= cfg->smooth_length && it < kMaxPolls;
-      if (poll) sl.poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
       ip.prof_slot = nn_launches;
       if (timeNN) {
         while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
@@ -880,26 +907,26 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
           S->nn_ev.push_back(e);
         }
       }
-      // (the NN launch is bracketed by its events: active list before, select after)
-      launch_active_list(si, (int)np, dDesc, dState, al, ctr, poll ? sl.poll_dev + it : nullptr,
-                         wait_mode ? S->sig : nullptr, tk, dOutT);
-      if (poll) {
-        HIPC(hipEventRecord(sl.ev_poll[it], si));
-        pending[n_pending++] = it;
+      // poll slot q holds the active count at the start of iteration q, written by the launch
+      // that builds that iteration's active list (k_active_list; fused: the previous reduce)
+      uint32_t* hn_this = nullptr;
+      uint32_t* hn_next = nullptr;
+      if ((!fuse || it == 0) && polled(it)) {
+        sl.poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
+        hn_this = sl.poll_dev + it;
       }
-      if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches], si));
-      launch_icp_nn(si, (int)nread, dDesc, dState, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
-                    use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
-                    use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
-                    sl.touch.as<uint32_t>(), ctr, ip);
-      if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], si));
+      if (fuse && polled(it + 1)) {
+        sl.poll_host[it + 1] = 0xffffffffu;
+        hn_next = sl.poll_dev + it + 1;
+      }
+      iteration(it, hn_this, hn_next, timeNN ? S->nn_ev[2 * nn_launches] : nullptr,
+                timeNN ? S->nn_ev[2 * nn_launches + 1] : nullptr);
       ++nn_launches;
-      launch_icp_select(si, R.m_sel, (int)np, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
-                        sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), 0);
-      launch_icp_reduce(si, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(),
-                        sl.d2.as<float>(), sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(),
-                        sl.slab.as<double>());
-      launch_icp_update(si, (int)np, dDesc, dState, sl.slab.as<double>(), ip);
+      for (int q : {hn_this ? it : -1, hn_next ? it + 1 : -1})
+        if (q >= 0) {
+          HIPC(hipEventRecord(sl.ev_poll[q], si));
+          pending[n_pending++] = q;
+        }
       if (wait_mode) continue;  // all maxIterationCount launches
       // the poll kLookahead iterations back: the device is still busy with the ones since
       while (n_pending > 0 && it + 1 - pending[0] >= kLookahead) {
