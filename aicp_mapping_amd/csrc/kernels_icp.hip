@@ -926,7 +926,7 @@ struct TravT {
 // one record load instruction shared by both phases. Lanes that reach a leaf wait until enough of
 // the wave is at a leaf (or nothing else can step) and then scan their buckets in one
 // cooperative pass. While-while loops make a wave wait for its slowest lane at every phase; here
-// a lane's dependent chain advances every round trip (tools/wavesim.cpp: 23 instead of 41 round
+// a lane's dependent chain advances every round trip (tools/experiments/wavesim.cpp: 23 instead of 41 round
 // trips per 64 queries). Visit order, far tests, counts and results are Trav2C's.
 enum : int32_t { kPhDesc = 0, kPhLeaf = 1, kPhClimb = 2 };
 
@@ -2641,7 +2641,7 @@ void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const Pa
   k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT);
 }
 // NN engine of the ICP matcher: 4 = Trav2S, 3 = Trav2C (default), 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
-// (design experiments, tools/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:
+// (design experiments, tools/experiments/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:
 // Trav<1> 230 us per NN launch, SM0 436 us (profiles/README.md).
 static int nn_engine() {
   static int e = -1;

@@ -12,7 +12,7 @@
 // group and shared by the pairs of a reference window; |A| is counted once per group, |B|
 // per reading, and |A∩B| by looking every voxel of a reading's map up in its group's map.
 // A 60 x 60 x 6 m scene at 0.2 m is ~2.7 M voxels = 2.7 MB per map (L2/MALL resident).
-// (tools/microbench.hip: with 16 distinct pairs, check+atomicOr bitmaps ran 11x slower.)
+// (tools/experiments/microbench.hip: with 16 distinct pairs, check+atomicOr bitmaps ran 11x slower.)
 #include <hip/hip_runtime.h>
 
 #include "aicp_common.hpp"

@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void k_pf_inv(uint32_t V, const float4* __rest
 }
 
 // Correctly rounded float square root, as sqrtf on the host: measured on gfx950, __fsqrt_rn
-// differs by one ulp on some inputs (tools/pf_eig_check.hip). The double square root rounded to
+// differs by one ulp on some inputs (tools/experiments/pf_eig_check.hip). The double square root rounded to
 // float is the correctly rounded float result (53 >= 2 * 24 + 2 bits).
 __device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x); }
 

@@ -1,7 +1,7 @@
 // pf_eig_check.hip — prints the device's PCL eigen33 intermediates for covariance matrices given
 // on stdin (9 floats per line, hex bits), to compare with the oracle. Not part of the product.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math
-//        -I aicp_mapping_amd/csrc tools/pf_eig_check.hip -o tools/pf_eig_check
+//        -I aicp_mapping_amd/csrc tools/experiments/pf_eig_check.hip -o tools/experiments/pf_eig_check
 #include "../aicp_mapping_amd/csrc/kernels_prefilter.hip"
 #include <cstdio>
 #include <vector>
