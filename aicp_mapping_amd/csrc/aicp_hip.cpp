@@ -68,6 +68,14 @@ namespace rt {
 // Test-only: AICP_FORCE_TRAV1=1 runs the ICP NN on node records (Trav<1>), the engine used when
 // treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records); read per
 // call so a test can switch it.
+int nn_interleave(int dflt) {
+  static const int v = [] {
+    const char* e = std::getenv("AICP_NN_INTERLEAVE");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  return v < 0 ? dflt : v;
+}
+
 bool force_trav1() {
   const char* e = std::getenv("AICP_FORCE_TRAV1");
   return e && e[0] == '1';
@@ -865,6 +873,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     prm.min_rot = cfg->min_diff_rot;
     prm.min_trans = cfg->min_diff_trans;
     prm.knn_normals = cfg->knn_normals;
+    prm.interleave = nn_interleave(0);  // contiguous: each XCD's L2 keeps ~1/8 of the references
     // The ICP loop in one pair group on s, or two on s and s2: group g's NN launch waits for the
     // other group's previous NN launch, so the NN launches never share the chip with each other,
     // and each group's select / reduce / update (short, low-occupancy kernels) runs underneath

@@ -1342,11 +1342,16 @@ __device__ unsigned long long g_nn_prof[8];
 template <class Eng, class OnChunk, class Fetch, class Done>
 __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, float maxE2, float maxR2,
                                                const uint4* __restrict__ nodes, const float4* __restrict__ pts,
-                                               OnChunk&& on_chunk, Fetch&& fetch, Done&& done) {
+                                               OnChunk&& on_chunk, Fetch&& fetch, Done&& done,
+                                               bool interleave = false) {
   const int lane = threadIdx.x & 63;
   const uint32_t g = blockIdx.x % kXcdGroups;
-  const uint32_t lo = (uint32_t)(((uint64_t)total * g) / kXcdGroups) & ~63u;
-  const uint32_t hi = g + 1 == kXcdGroups ? total : (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups) & ~63u;
+  // contiguous: group g serves slots [lo, hi) (its references stay in its XCD's L2); interleaved:
+  // group g serves the 64-slot chunks c with c % kXcdGroups == g (a spatially clustered run of
+  // expensive queries is spread over all XCDs instead of making one group the straggler)
+  const uint32_t lo = interleave ? 0u : (uint32_t)(((uint64_t)total * g) / kXcdGroups) & ~63u;
+  const uint32_t hi =
+      interleave || g + 1 == kXcdGroups ? total : (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups) & ~63u;
   uint32_t* gctr = ctr + g * kCtrStride;
   Eng t;
   FarStack fs;
@@ -1373,7 +1378,8 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       if (needm == 0 || exhausted) break;
       if (pool >= pool_end) {
         uint32_t base = 0;
-        if (lane == 0) base = lo + atomicAdd(gctr, 64u);
+        if (lane == 0)
+          base = interleave ? (g + kXcdGroups * atomicAdd(gctr, 1u)) * 64u : lo + atomicAdd(gctr, 64u);
         base = __builtin_amdgcn_readfirstlane(base);
         if (base >= hi) {
           exhausted = true;
@@ -1888,7 +1894,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
         match[qidx] = t.res_id();
         d2out[qidx] = t.res_d2();
         touched[qidx] = (min(t.tn, 65535u) << 16) | min(t.tp, 65535u);
-      });
+      },
+      prm.interleave != 0);
 #if AICP_XCD_PROF
   // per launch slot and XCD group: earliest wave start, latest wave end (100 MHz clock)
   const uint64_t xt1 = __builtin_amdgcn_s_memrealtime();

@@ -111,6 +111,8 @@ bool valid_pair(const aicp_pair& p);
 double ev_ms(hipEvent_t a, hipEvent_t b);
 bool read_order_enabled();
 bool force_trav1();
+// IcpParams::interleave for the NN launches: AICP_NN_INTERLEAVE=0/1 overrides the caller's default
+int nn_interleave(int dflt);
 
 // Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device (kernels_tree.hip).
 // launch = false: allocate the work space only (nothing enqueued; before a stream capture)

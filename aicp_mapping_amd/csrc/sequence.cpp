@@ -28,12 +28,14 @@
 //   r3   next reference points (k_seq_next_ref, k_transform), centroid + matcher kd-tree
 //   r2   raw kd-tree + SurfaceNormal, normals into the matcher tree's order
 //   icp  reference voxel map, overlap counts, ratio, ICP loop, corrections
-// Window w+1's reference waits for window w's corrections on the device: the ICP stream stores
-// w's ticket into signal memory as soon as no reading of w is active (k_active_list), and r3
-// waits for it (hipStreamWaitValue64); the host never blocks between windows and enqueues ahead
-// (where the runtime lacks stream wait-values, it polls each window's convergence instead).
-// The kd-tree builds and the ICP loop -- ~100 and ~160 short kernels -- are replayed from
-// hipGraphs captured per slot. Device buffers live in K window slots (reused with event waits);
+// Window w's ICP loop is enqueued iteration by iteration; k_active_list (fused into the previous
+// iteration's reduce) writes the active count into mapped host memory, and the host, one
+// iteration ahead, stops enqueueing once it reads 0. Window w+1's reference (r3) then waits for
+// w's ICP with an event. (AICP_SEQ_SYNC=signal instead enqueues all maxIterationCount launches
+// as one graph and makes r3 wait for w's ticket in signal memory, hipStreamWaitValue64: the
+// trailing no-op launches hold stream icp, 2.79 against 2.25 ms per window measured.)
+// The kd-tree builds -- ~100 short kernels each -- are replayed from hipGraphs captured per
+// slot. Device buffers live in K window slots (reused with event waits);
 // states and corrections of all readings are committed to sequence-wide arrays for the read-back.
 #include <hip/hip_runtime.h>
 
@@ -216,7 +218,8 @@ struct SeqState {
   uint64_t* sig = nullptr;
   uint64_t ticket = 0;
   std::vector<hipEvent_t> tev;  // seq_prof(): 5 timing events per window
-  bool use_wait = false;
+  bool use_wait = false;    // the window ticket is a device-side dependency (hipStreamWaitValue64)
+  bool loop_graph = false;  // AICP_SEQ_SYNC=signal: every maxIterationCount launch as one graph, no polls
   WorkerPool pool{std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1};
   aicp_sequence_timing last{};
   int device = 0;
@@ -658,17 +661,22 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   (void)dRst;                                                      \
   (void)dGst;                                                      \
   (void)dOutT;                                                     \
+  (void)np;                                                        \
+  (void)dDesc;                                                     \
+  (void)dState;                                                    \
   (void)dCap;                                                      \
   (void)bmp;                                                       \
   (void)res
 
-// The reference of the window (streams r3, r2) and the overlap + ICP set-up on stream icp.
-// The two kd-tree builds (+ SurfaceNormal) are replayed from graphs (graph_run).
-static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
+// The reference of the window on streams r3 and r2: its points (the previous window's last
+// reading corrected on the device, once that window's ticket is out), centroid, matcher kd-tree
+// and treelets (r3), raw kd-tree + SurfaceNormal scattered into the matcher's order (r2). The two
+// builds are replayed from graphs (graph_run). Nothing here runs on stream icp, so it can be
+// enqueued before the previous window's ICP loop.
+static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
                          const aicp_sequence_params* prm, WinRun& R) {
   WIN_REFS;
   const float4* src_pts = R.src_pts;
-  const float4* readS = R.readS;
   const bool use_tl = R.use_tl;
   const size_t tl_cap = R.tl_cap;
   TreeCtl* ctl_w = R.ctl_w;
@@ -694,17 +702,6 @@ static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_ref, s3));
-  // ---- icp: reference voxel map
-  hipStream_t si = S->s_icp;
-  if (doOvl) {
-    HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
-    launch_ovl_init(si, 1, dG, dGst, res, 1);
-    launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
-    launch_ovl_size(si, 1, dGst, dOvl, dCap);
-    launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
-    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
-    launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
-  }
   // work spaces first: nothing may be allocated inside a capture
   const int bucket = cfg->bucket_size;
   int rc = device_trees_begin(sl.tb[0], ctx->err, S->s_r2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0,
@@ -790,7 +787,29 @@ static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_s2, s2));
   if (R.tev) HIPC(hipEventRecord(R.tev[2], s2));
+  return AICP_OK;
+}
 
+// The window's set-up on stream icp: the reference voxel map (from the next reference's points,
+// ev_ref), the overlap counts and ratio (with the reading side, ev_rd), the pairs' frames (matcher
+// tree, ev_s3), the normals (ev_s2) and the centred readings. Enqueued after the previous window's
+// ICP loop, which runs on the same stream.
+static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                       WinRun& R) {
+  WIN_REFS;
+  (void)ctx;
+  (void)cfg;
+  const float4* readS = R.readS;
+  hipStream_t si = S->s_icp;
+  if (doOvl) {
+    HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
+    launch_ovl_init(si, 1, dG, dGst, res, 1);
+    launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
+    launch_ovl_size(si, 1, dGst, dOvl, dCap);
+    launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
+    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
+    launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
+  }
   HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));
   if (doOvl) {
     launch_ovl_intersect(si, (int)np, dDesc, dOvl + 1, dOvl, dState, bmp);
@@ -812,10 +831,19 @@ static int win_reference(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
 //     graph; k_active_list publishes the corrections and the window's ticket as soon as no pair is
 //     active, and the iterations after that find no active pair and return at once;
 //   polled mode: from iteration smoothLength on (no pair can stop earlier except on an error)
-//     k_active_list also writes the active count into mapped host memory; the host, kLookahead
+//     k_active_list also writes the active count into mapped host memory; the host, lookahead()
 //     iterations behind, stops enqueueing once it reads 0.
 // The window's states and corrections are then committed to the sequence's arrays.
-constexpr int kLookahead = 2;
+// iterations the host stays ahead of the polls it reads (AICP_SEQ_LOOKAHEAD, default 1): the
+// launches after the one that found no active pair are no-ops that still hold stream icp
+int lookahead() {
+  static const int v = [] {
+    const char* e = std::getenv("AICP_SEQ_LOOKAHEAD");
+    const int x = e ? std::atoi(e) : 1;
+    return x < 1 ? 1 : (x > 8 ? 8 : x);
+  }();
+  return v;
+}
 static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
                    WinRun& R, bool timeNN, int& nn_launches) {
   WIN_REFS;
@@ -831,9 +859,11 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
   ip.min_rot = cfg->min_diff_rot;
   ip.min_trans = cfg->min_diff_trans;
   ip.knn_normals = cfg->knn_normals;
+  ip.interleave = nn_interleave(0);  // (interleaved chunks measured equal on C2 windows, r03)
   ActiveList* al = sl.active.as<ActiveList>();
   uint32_t* ctr = sl.ctrs.as<uint32_t>();
-  const bool wait_mode = S->use_wait;
+  const bool wait_mode = S->use_wait;     // the ticket is signalled on the device
+  const bool loop_graph = S->loop_graph;  // no polls: every maxIterationCount launch, one graph
   uint64_t* tk = sl.wticket.as<uint64_t>();
   const bool fuse = icp_fuse_enabled();
   IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, 0);
@@ -875,7 +905,7 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
   };
   if (wait_mode) HIPC(hipStreamWriteValue64(si, tk, R.ticket, 0));
   if (R.tev) HIPC(hipEventRecord(R.tev[3], si));
-  if (wait_mode && !timeNN) {
+  if (loop_graph && !timeNN) {
     ip.prof_slot = 0;
     Key k;
     k << np << nread << use_tl << ip << R.m_sel.pair << R.m_sel.start << R.m_sel.n_blocks << R.m_red.pair
@@ -896,7 +926,7 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
     int n_pending = 0;
     bool stop = false;
     auto polled = [&](int q) {
-      return !wait_mode && !early_exit_disabled() && q >= cfg->smooth_length && q < kMaxPolls && q < cfg->max_iter;
+      return !loop_graph && !early_exit_disabled() && q >= cfg->smooth_length && q < kMaxPolls && q < cfg->max_iter;
     };
     for (int it = 0; it < cfg->max_iter && !stop; ++it) {
       ip.prof_slot = nn_launches;
@@ -927,9 +957,9 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
           HIPC(hipEventRecord(sl.ev_poll[q], si));
           pending[n_pending++] = q;
         }
-      if (wait_mode) continue;  // all maxIterationCount launches
-      // the poll kLookahead iterations back: the device is still busy with the ones since
-      while (n_pending > 0 && it + 1 - pending[0] >= kLookahead) {
+      if (loop_graph) continue;  // all maxIterationCount launches
+      // the poll lookahead() iterations back: the device is still busy with the ones since
+      while (n_pending > 0 && it + 1 - pending[0] >= lookahead()) {
         const int q = pending[0];
         for (int j = 1; j < n_pending; ++j) pending[j - 1] = pending[j];
         --n_pending;
@@ -978,10 +1008,17 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     }
     HIPC(hipEventCreate(&S->ev_begin));
     HIPC(hipEventCreate(&S->ev_end));
-    // AICP_SEQ_SYNC=poll: the host polls each window's convergence instead (A/B, fallback)
+    // Window dependency (AICP_SEQ_SYNC):
+    //   default (poll)  the host polls the active count to stop enqueueing a window's ICP
+    //                   iterations and enqueues the next reference after the loop (event order);
+    //   signal          every maxIterationCount launch enqueued at once as one graph; the next
+    //                   reference waits for the window's ticket on the device (wait-value). The
+    //                   trailing launches find no active pair but still hold stream icp: measured
+    //                   2.79 ms per window against 2.25 ms polled (r03).
     const char* e = std::getenv("AICP_SEQ_SYNC");
+    S->loop_graph = e && std::strcmp(e, "signal") == 0;
     int can = 0;
-    if (!(e && std::strcmp(e, "poll") == 0) &&
+    if (S->loop_graph &&
         hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, ctx->device) == hipSuccess && can &&
         hipExtMallocWithFlags((void**)&S->sig, 8, hipMallocSignalMemory) == hipSuccess) {
       HIPC(hipStreamWriteValue64(S->s_icp, S->sig, 0, 0));
@@ -1110,12 +1147,21 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       hp[slot] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
       return r;
     };
+    // The next reference is enqueued after the window's ICP loop: a wait-value enqueued earlier
+    // on a stream that shares a hardware queue with stream icp would block the loop behind it
+    // (HIP maps streams onto GPU_MAX_HW_QUEUES queues per priority; measured: a deadlock with
+    // several contexts alive).
+    const bool early_ref = false;
     rc = timed(0, [&] { return upload(0); });
-    if (!rc) rc = timed(1, [&] { return win_reference(ctx, S, cfg, prm, runs[0]); });
+    if (!rc) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[0]); });
+    if (!rc) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[0]); });
     for (size_t k = 0; k < plan.size() && !rc; ++k) {
-      if (k + 1 < plan.size()) rc = timed(0, [&] { return upload(k + 1); });
+      const bool next = k + 1 < plan.size();
+      if (next) rc = timed(0, [&] { return upload(k + 1); });
+      if (!rc && next && early_ref) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
       if (!rc) rc = timed(2, [&] { return win_icp(ctx, S, cfg, prm, runs[k], timeNN, nn_launches); });
-      if (!rc && k + 1 < plan.size()) rc = timed(1, [&] { return win_reference(ctx, S, cfg, prm, runs[k + 1]); });
+      if (!rc && next && !early_ref) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
+      if (!rc && next) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
       ++windows;
     }
     if (prof)
