@@ -2464,6 +2464,19 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce_f(
   pair_done(y);
 }
 
+// k_icp_update + (last pair of the group) the next active list. Kept out of the reduce kernel:
+// the update's solve (pivoted QR, LLT / min-norm QR / SVD fallback, fp64) needs 256 VGPRs, and a
+// kernel's register allocation is its largest path's, so k_icp_reduce_f ran its gathers at one
+// wave per SIMD (35-40 us per C2 window iteration against 12.5 + 12.3 us for the two kernels).
+__global__ __launch_bounds__(256) void k_icp_update_f(const PairDesc* __restrict__ pd, PairState* st,
+                                                      const double* __restrict__ slab, IcpParams prm, IcpIterSync y) {
+  const int pair = blockIdx.x;
+  PairState& s = st[pair];
+  if (!s.active) return;
+  icp_update_body(pd[pair], s, slab, prm);
+  pair_done(y);
+}
+
 __global__ void k_finalize(int n_pairs, const PairDesc* __restrict__ pd,
                            PairState* __restrict__ st, float* __restrict__ outT) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2719,6 +2732,14 @@ void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* p
   k_sel_compact<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, cand, cand_cnt);
   k_sel_final<<<n_pairs, 1024, 0, s>>>(pd + p0, st + p0, cand, cand_cnt + p0);
 }
+static bool reduce_fuse_update() {  // AICP_REDUCE_FUSE_UPDATE=1: the update inside the reduce kernel (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_REDUCE_FUSE_UPDATE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 bool icp_fuse_enabled() {  // AICP_ICP_FUSE=0: one launch per step (A/B)
   static const bool on = [] {
     const char* e = std::getenv("AICP_ICP_FUSE");
@@ -2743,8 +2764,13 @@ void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairStat
 void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float4* read_c,
                          const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
                          const float4* bnrm, double* slab, const IcpParams& prm, const IcpIterSync& y) {
-  if (m.n_blocks)
+  if (!m.n_blocks) return;
+  if (reduce_fuse_update()) {
     k_icp_reduce_f<<<m.n_blocks, kNNBlock, 0, s>>>(m, pd, st, read_c, match, d2, touched, bpts, bnrm, slab, prm, y);
+    return;
+  }
+  k_icp_reduce<<<m.n_blocks, kNNBlock, 0, s>>>(m, pd, st, read_c, match, d2, touched, bpts, bnrm, slab);
+  k_icp_update_f<<<y.np, 256, 0, s>>>(y.pd, y.st, slab, prm, y);
 }
 void launch_icp_reduce(hipStream_t s, BlockMap m, const PairDesc* pd, const PairState* st, const float4* read_c,
                        const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,

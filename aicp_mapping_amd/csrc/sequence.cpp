@@ -182,6 +182,14 @@ struct Key {
 constexpr int kSlots = 3;  // window slots in flight (>= 2: a window reads the previous slot's reading)
 constexpr int kMaxPolls = 64;  // ICP iterations that can end a window's loop early
 
+bool seq_read_early() {  // AICP_SEQ_READ_LATE=1: the reading side after the next reference (A/B: slower)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_SEQ_READ_LATE");
+    return !(e && e[0] == '1');
+  }();
+  return on;
+}
+
 bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches
   const char* e = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
   return e && e[0] == '1';
@@ -460,7 +468,6 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   HIPC(ensure(sl.isync, icp_sync_words(np) * 4));
   PairDesc* dRdesc = sl.rd.as<PairDesc>();
   PairDesc* dDesc = sl.wdesc.as<PairDesc>();
-  PairState* dState = sl.wstate.as<PairState>();
 
   // ---- host: pack the readings (+ AABBs), descriptors, block maps
   HIPC(ensure(sl.pin_read, nread * 16));
@@ -589,37 +596,6 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   }
   HIPC(hipEventRecord(sl.ev_up, su));
 
-  // ---- rd: reading side
-  hipStream_t sr = S->s_rd;
-  HIPC(hipStreamWaitEvent(sr, sl.ev_up, 0));
-  launch_init_state(sr, (int)np, dDesc, dState);
-  const float4* readS = sl.read_raw.as<float4>();
-  if (read_order_enabled()) {
-    const size_t tb = read_order_temp_bytes(nread, (int)np);
-    HIPC(ensure(sl.ord_k0, nread * 8));
-    HIPC(ensure(sl.ord_k1, nread * 8));
-    HIPC(ensure(sl.ord_v0, nread * 4));
-    HIPC(ensure(sl.ord_v1, nread * 4));
-    HIPC(ensure(sl.ord_tmp, tb));
-    HIPC(launch_read_order(sr, m_read, (int)np, dDesc, sl.read_raw.as<float4>(), (uint32_t)nread,
-                           sl.ord_k0.as<uint64_t>(), sl.ord_k1.as<uint64_t>(), sl.ord_v0.as<uint32_t>(),
-                           sl.ord_v1.as<uint32_t>(), sl.ord_tmp.p, tb, sl.read_s.as<float4>()));
-    readS = sl.read_s.as<float4>();
-  }
-  OvlDesc* dOvl = doOvl ? sl.ovl.as<OvlDesc>() : nullptr;
-  const uint64_t* dCap = doOvl ? sl.caps.as<uint64_t>() : nullptr;
-  uint8_t* bmp = doOvl ? sl.bitmap.as<uint8_t>() : nullptr;
-  if (doOvl) {
-    launch_ovl_init(sr, (int)np, dDesc, dState, res, 2);
-    launch_ovl_bbox(sr, m_read, dDesc, dState, readS, 1, res);
-    launch_ovl_size(sr, (int)np, dState, dOvl + 1, dCap + 1);
-    launch_ovl_clear(sr, (int)np, dOvl + 1, bmp, cap_max);
-    launch_ovl_mark(sr, m_read, dDesc, dOvl + 1, dState, readS, 1, res, bmp);
-    launch_ovl_popcount(sr, (int)np, dOvl + 1, dState, 1, bmp);
-  }
-  HIPC(hipGetLastError());
-  HIPC(hipEventRecord(sl.ev_rd, sr));
-
   R.np = np;
   R.nread = nread;
   R.n_ref = n_ref;
@@ -632,9 +608,10 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   R.cap = cap;
   R.cap_max = cap_max;
   R.src_pts = src_pts;
-  R.readS = readS;
+  R.readS = sl.read_raw.as<float4>();
   return AICP_OK;
 }
+
 
 #define WIN_REFS                                                   \
   const Win& w = R.w;                                              \
@@ -667,6 +644,47 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   (void)dCap;                                                      \
   (void)bmp;                                                       \
   (void)res
+
+// The reading side of the window on stream rd (independent of the reference): state init, Morton
+// order, the readings' voxel maps. Enqueued after the window's reference, so that it fills the
+// CUs the kd-tree builds leave idle instead of competing with the previous window's ICP loop.
+static int win_read_side(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                         WinRun& R) {
+  WIN_REFS;
+  (void)ctx;
+  (void)cfg;
+  const uint64_t nread = R.nread;
+  const BlockMap m_read = R.m_read;
+  const uint64_t cap_max = R.cap_max;
+  hipStream_t sr = S->s_rd;
+  HIPC(hipStreamWaitEvent(sr, sl.ev_up, 0));
+  launch_init_state(sr, (int)np, dDesc, dState);
+  const float4* readS = sl.read_raw.as<float4>();
+  if (read_order_enabled()) {
+    const size_t tb = read_order_temp_bytes(nread, (int)np);
+    HIPC(ensure(sl.ord_k0, nread * 8));
+    HIPC(ensure(sl.ord_k1, nread * 8));
+    HIPC(ensure(sl.ord_v0, nread * 4));
+    HIPC(ensure(sl.ord_v1, nread * 4));
+    HIPC(ensure(sl.ord_tmp, tb));
+    HIPC(launch_read_order(sr, m_read, (int)np, dDesc, sl.read_raw.as<float4>(), (uint32_t)nread,
+                           sl.ord_k0.as<uint64_t>(), sl.ord_k1.as<uint64_t>(), sl.ord_v0.as<uint32_t>(),
+                           sl.ord_v1.as<uint32_t>(), sl.ord_tmp.p, tb, sl.read_s.as<float4>()));
+    readS = sl.read_s.as<float4>();
+  }
+  if (doOvl) {
+    launch_ovl_init(sr, (int)np, dDesc, dState, res, 2);
+    launch_ovl_bbox(sr, m_read, dDesc, dState, readS, 1, res);
+    launch_ovl_size(sr, (int)np, dState, dOvl + 1, dCap + 1);
+    launch_ovl_clear(sr, (int)np, dOvl + 1, bmp, cap_max);
+    launch_ovl_mark(sr, m_read, dDesc, dOvl + 1, dState, readS, 1, res, bmp);
+    launch_ovl_popcount(sr, (int)np, dOvl + 1, dState, 1, bmp);
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(sl.ev_rd, sr));
+  R.readS = readS;
+  return AICP_OK;
+}
 
 // The reference of the window on streams r3 and r2: its points (the previous window's last
 // reading corrected on the device, once that window's ticket is out), centroid, matcher kd-tree
@@ -1152,15 +1170,24 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     // (HIP maps streams onto GPU_MAX_HW_QUEUES queues per priority; measured: a deadlock with
     // several contexts alive).
     const bool early_ref = false;
+    // The reading side of window k + 1 (Morton order, voxel maps) is enqueued with its upload,
+    // before window k's loop. (AICP_SEQ_READ_LATE=1 enqueues it with the next reference instead, to
+    // keep it off the loop's CUs: measured 2.29 against 2.20 ms per window, since it then slows
+    // the kd-tree builds on the critical path.)
+    const bool read_early = seq_read_early();
+    auto read_side = [&](size_t k) { return win_read_side(ctx, S, cfg, prm, runs[k]); };
     rc = timed(0, [&] { return upload(0); });
+    if (!rc) rc = timed(0, [&] { return read_side(0); });
     if (!rc) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[0]); });
     if (!rc) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[0]); });
     for (size_t k = 0; k < plan.size() && !rc; ++k) {
       const bool next = k + 1 < plan.size();
       if (next) rc = timed(0, [&] { return upload(k + 1); });
+      if (!rc && next && read_early) rc = timed(0, [&] { return read_side(k + 1); });
       if (!rc && next && early_ref) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
       if (!rc) rc = timed(2, [&] { return win_icp(ctx, S, cfg, prm, runs[k], timeNN, nn_launches); });
       if (!rc && next && !early_ref) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
+      if (!rc && next && !read_early) rc = timed(0, [&] { return read_side(k + 1); });
       if (!rc && next) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
       ++windows;
     }
