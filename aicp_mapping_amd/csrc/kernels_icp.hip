@@ -1765,6 +1765,219 @@ __global__ __launch_bounds__(256, (K <= 10 ? 5 : (K <= 20 ? 4 : 3))) void k_knn_
   }
 }
 
+// ---- k-NN of a tree's own points with one query per octet of lanes -------------------------
+// libnabo recurseKnn (eps 0, the SurfaceNormal / pre-filter kNN) exactly as Trav<K>::advance
+// walks it, but the traversal state is held identically by the 8 lanes of an octet and the
+// k-best list (IndexHeapBruteForceVector, ascending, head = entry K-1) is spread over them:
+// lane j holds entries [j*M, j*M + M). replaceHead's shift loop becomes, for every entry i at
+// once, newA[i] = A[i-1] > v ? A[i-1] : (A[i] > v ? v : A[i]) (A[-1] = -inf), M selects per lane
+// and one DPP move of the previous lane's last entry; for v >= head it changes nothing, so the
+// `dist < head` test needs no broadcast. A bucket's points are loaded one per lane (one 128-byte
+// run per octet) and their distances broadcast in order by ds_swizzle. Per query this issues a
+// few hundred wave instructions with the octet's lanes all busy, against one lane doing K-long
+// compare-shift chains: on a single 120k-point reference (the C2 stream's window) the kNN is
+// bound by the longest query's latency, not by the chip's issue rate.
+constexpr int kOctFrames = 24;  // far frames per octet kept in LDS (deeper ones in scratch)
+
+template <int K>
+struct OctBest {
+  static constexpr int M = (K + 7) / 8;
+  float v[M];
+  int32_t id[M];
+};
+
+__device__ __forceinline__ float oct_prev_f(float x) {  // lane l - 1's value (row_shr:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xf, 0xf, false));
+}
+__device__ __forceinline__ int32_t oct_prev_i(int32_t x) {
+  return __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+}
+// lane (l & ~7) | I of the 32-lane half: ds_swizzle bit mode, and_mask 0x18, or_mask I
+template <int I>
+__device__ __forceinline__ float oct_bcast(float x) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x18 | (I << 5)));
+}
+
+template <int K>
+__device__ __forceinline__ void oct_insert(OctBest<K>& b, bool first_lane, float val, int32_t vid) {
+  constexpr int M = OctBest<K>::M;
+  float pv = oct_prev_f(b.v[M - 1]);
+  int32_t pid = oct_prev_i(b.id[M - 1]);
+  if (first_lane) pv = -__builtin_inff();
+  float nv[M];
+  int32_t ni[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const float a = i == 0 ? pv : b.v[i - 1];
+    const int32_t ai = i == 0 ? pid : b.id[i - 1];
+    const bool sh = a > val, pl = b.v[i] > val;
+    nv[i] = sh ? a : (pl ? val : b.v[i]);
+    ni[i] = sh ? ai : (pl ? vid : b.id[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    b.v[i] = nv[i];
+    b.id[i] = ni[i];
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
+                                                 const uint4* __restrict__ nodes_all,
+                                                 const float4* __restrict__ bpts, int32_t* __restrict__ ids,
+                                                 unsigned long long* touched) {
+  constexpr int M = OctBest<K>::M;
+  constexpr int kHeadLane = (K - 1) / M, kHeadSlot = (K - 1) % M;
+  __shared__ LdsFrame oframes[kOctFrames * 32];
+  const int lane = threadIdx.x & 63, j = lane & 7, oct = threadIdx.x >> 3;  // oct: 0..31 in the block
+  const uint32_t s = (blockIdx.x * 256u + threadIdx.x) >> 3;                 // the octet's query
+  const bool live = s < total;
+  uint32_t tp = 0, tn = 0;
+  if (live) {
+    const int pair = pair_of_ref(pd, n_pairs, s);
+    const PairDesc& d = pd[pair];
+    const uint4* nodes = nodes_all + d.node_off;
+    const float4* pts = bpts + d.ref_off;
+    const float4 qq = bpts[s];
+    const float q0 = qq.x, q1 = qq.y, q2 = qq.z;
+    OctBest<K> best;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      best.v[i] = __builtin_inff();
+      best.id[i] = -1;
+    }
+    float head = __builtin_inff();
+    float off0 = 0.f, off1 = 0.f, off2 = 0.f, rd = 0.f, minFar;
+    int32_t n = 0, start = 0, sp = 0;
+    FarStack fs;
+    LdsFrame* lf = oframes + oct;
+    const uint2* nodes2 = reinterpret_cast<const uint2*>(nodes);
+    for (;;) {
+      // descent (Trav<K>::advance)
+      minFar = __builtin_inff();
+      uint2 nd = nodes2[2 * n];
+      int32_t pl = -1;
+      while ((nd.y & 3u) != kLeaf) {
+        const uint32_t cd = nd.y & 3u;
+        const float no = sel3(cd, q0, q1, q2) - __uint_as_float(nd.x);
+        const float oc = sel3(cd, off0, off1, off2);
+        const float rdf = rd + (-oc * oc + no * no);
+        minFar = fminf(minFar, rdf);
+        pl = n;
+        n = (no > 0.f) ? (int32_t)(nd.y >> 2) : n + 1;
+        ++tn;
+        nd = nodes2[2 * n];
+      }
+      if (pl < 0) pl = (int32_t)nodes[n].z;
+      // bucket: lane j takes point c + j, the distances go round the octet in order
+      {
+        const uint32_t b0 = nd.y >> 2, cnt = nd.x;
+        for (uint32_t c = 0; c < cnt; c += 8) {
+          float dist = __builtin_inff();
+          if (c + (uint32_t)j < cnt) {
+            const float4 p = pts[b0 + c + j];
+            const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
+            dist = 0.f;
+            dist += d0 * d0;
+            dist += d1 * d1;
+            dist += d2 * d2;
+          }
+          float dv[8];
+          dv[0] = oct_bcast<0>(dist);
+          dv[1] = oct_bcast<1>(dist);
+          dv[2] = oct_bcast<2>(dist);
+          dv[3] = oct_bcast<3>(dist);
+          dv[4] = oct_bcast<4>(dist);
+          dv[5] = oct_bcast<5>(dist);
+          dv[6] = oct_bcast<6>(dist);
+          dv[7] = oct_bcast<7>(dist);
+          const uint32_t m = min(8u, cnt - c);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if ((uint32_t)i < m) oct_insert<K>(best, j == 0, dv[i], (int32_t)(b0 + c + i));
+        }
+        tp += cnt;
+        head = __shfl(best.v[kHeadSlot], (lane & ~7) | kHeadLane, 64);
+      }
+      // climb to the next far descent (or the end of the query)
+      int32_t cnode = n, pc = pl;
+      bool done = false;
+      if (!(minFar * 1.f < head)) cnode = start;
+      for (;;) {
+        if (cnode == start) {
+          if (sp == 0) {
+            done = true;
+            break;
+          }
+          --sp;
+          FarFrame f;
+          if (sp < kOctFrames) {
+            const LdsFrame g = lf[sp * 32];
+            f = FarFrame{g.Pcd, g.rd, g.old, g.mn, g.start, g.Pcd & 0x3fffffff, g.PP, 0};
+          } else {
+            f = fs.f[sp];
+          }
+          const uint32_t pcd = (uint32_t)f.F >> 30;
+          rd = f.rd;
+          const float old = f.old;
+          if (pcd == 0) off0 = old;
+          else if (pcd == 1) off1 = old;
+          else off2 = old;
+          minFar = f.mn;
+          start = f.start;
+          cnode = f.P;
+          pc = f.PP;
+          if (!(minFar * 1.f < head)) cnode = start;
+          continue;
+        }
+        const int32_t p = pc;
+        const uint4 pn = nodes[p];
+        const uint32_t cd = pn.y & 3u;
+        const float no = sel3(cd, q0, q1, q2) - __uint_as_float(pn.x);
+        const float oc = sel3(cd, off0, off1, off2);
+        const float rdf = rd + (-oc * oc + no * no);
+        if (rdf * 1.f < head) {
+          const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
+          if (sp < kOctFrames) {
+            if (j == 0)
+              lf[sp * 32] = LdsFrame{(int32_t)((uint32_t)p | (cd << 30)), rd, oc, minFar, start, (int32_t)pn.z};
+          } else {
+            fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, (int32_t)pn.z, 0};
+          }
+          ++sp;
+          if (cd == 0) off0 = no;
+          else if (cd == 1) off1 = no;
+          else off2 = no;
+          rd = rdf;
+          n = far;
+          start = far;
+          break;
+        }
+        cnode = p;
+        pc = (int32_t)pn.z;
+      }
+      if (done) break;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int e = j * M + i;
+      if (e < K) ids[(size_t)s * K + e] = best.v[i] != __builtin_inff() ? best.id[i] : -1;
+    }
+  }
+  if (touched) {
+    unsigned long long a = (live && j == 0) ? tp : 0, b = (live && j == 0) ? tn : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o, 64);
+      b += __shfl_xor(b, o, 64);
+    }
+    if (lane == 0) {
+      atomicAdd(&touched[0], a);
+      atomicAdd(&touched[1], b);
+    }
+  }
+}
+
 template <int K>
 __global__ __launch_bounds__(256) void k_normals_from_ids(int n_pairs, uint32_t total,
                                                           const PairDesc* __restrict__ pd, PairState* st,
@@ -2634,10 +2847,28 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   }
   return true;
 }
+static bool knn_oct_enabled() {  // AICP_KNN_OCT=0: one query per lane (k_knn_ids / k_knn_ids_tl)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_KNN_OCT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
                     const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
                     const uint4* tl, const uint2* link) {
   if (!total_ref) return true;
+  if (knn_oct_enabled()) {
+    const unsigned go = (unsigned)(((uint64_t)total_ref * 8 + 255) / 256);
+    switch (knn) {
+      case 10: k_knn_oct<10><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
+      case 20: k_knn_oct<20><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
+      case 30: k_knn_oct<30><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
+      default: return false;
+    }
+    return true;
+  }
   const int g = persistent_grid((int)total_ref);
   if (tl && link && knn_treelets_enabled()) {
     switch (knn) {
