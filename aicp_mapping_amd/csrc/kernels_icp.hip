@@ -1811,7 +1811,9 @@ __device__ __forceinline__ void oct_insert(OctBest<K>& b, bool first_lane, float
     const float a = i == 0 ? pv : b.v[i - 1];
     const int32_t ai = i == 0 ? pid : b.id[i - 1];
     const bool sh = a > val, pl = b.v[i] > val;
-    nv[i] = sh ? a : (pl ? val : b.v[i]);
+    // a <= b.v[i] (ascending): the median of (a, b.v[i], val) is a if val < a, val if it lies
+    // between, b.v[i] above (val is finite and not NaN: the caller filtered with `< head`)
+    nv[i] = __builtin_amdgcn_fmed3f(a, b.v[i], val);
     ni[i] = sh ? ai : (pl ? vid : b.id[i]);
   }
 #pragma unroll
@@ -1891,13 +1893,17 @@ __global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, co
           dv[5] = oct_bcast<5>(dist);
           dv[6] = oct_bcast<6>(dist);
           dv[7] = oct_bcast<7>(dist);
-          const uint32_t m = min(8u, cnt - c);
+          // candidates below the head as it stood before this run (libnabo's `dist < head`; a
+          // candidate the earlier insertions of the run pushed above the head is a no-op)
+          uint32_t m8 = 0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) m8 |= (dv[i] < head ? 1u : 0u) << i;
 #pragma unroll
           for (int i = 0; i < 8; ++i)
-            if ((uint32_t)i < m) oct_insert<K>(best, j == 0, dv[i], (int32_t)(b0 + c + i));
+            if ((m8 >> i) & 1u) oct_insert<K>(best, j == 0, dv[i], (int32_t)(b0 + c + i));
+          head = __shfl(best.v[kHeadSlot], (lane & ~7) | kHeadLane, 64);
         }
         tp += cnt;
-        head = __shfl(best.v[kHeadSlot], (lane & ~7) | kHeadLane, 64);
       }
       // climb to the next far descent (or the end of the query)
       int32_t cnode = n, pc = pl;
