@@ -2853,19 +2853,27 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   }
   return true;
 }
-static bool knn_oct_enabled() {  // AICP_KNN_OCT=0: one query per lane (k_knn_ids / k_knn_ids_tl)
-  static const bool on = [] {
+// k_knn_oct for launches of at most this many queries (AICP_KNN_OCT_MAX; AICP_KNN_OCT=0 never,
+// =1 always): with eight lanes per query it issues ~2.3x the VALU instructions of the per-lane
+// engine, which pays only while the per-lane launch leaves the chip short of waves (the C2
+// stream's single 120k-point reference: 377 -> 245 us); on C5's 61 M queries it ran 91.7 ms per
+// launch against the per-lane engine's throughput (C5 3962 -> 3097 clouds/s, r03c).
+static bool knn_oct_enabled(uint32_t n_queries) {
+  static const uint64_t lim = [] {
     const char* e = std::getenv("AICP_KNN_OCT");
-    return !(e && e[0] == '0');
+    if (e && e[0] == '0') return (uint64_t)0;
+    if (e && e[0] == '1') return ~(uint64_t)0;
+    const char* m = std::getenv("AICP_KNN_OCT_MAX");
+    return m ? (uint64_t)std::strtoull(m, nullptr, 10) : (uint64_t)300000;
   }();
-  return on;
+  return n_queries <= lim;
 }
 
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
                     const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
                     const uint4* tl, const uint2* link) {
   if (!total_ref) return true;
-  if (knn_oct_enabled()) {
+  if (knn_oct_enabled(total_ref)) {
     const unsigned go = (unsigned)(((uint64_t)total_ref * 8 + 255) / 256);
     switch (knn) {
       case 10: k_knn_oct<10><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;

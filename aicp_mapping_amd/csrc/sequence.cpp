@@ -47,6 +47,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -205,29 +206,25 @@ struct SeqSlot {
       wdesc, wstate, woutT, wticket, isync;  // the window's readings (committed to the sequence's arrays at its end)
   TreeBufs tb[2];
   PinBuf pin_read, pin_par, pin_src;
-  hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr;
-  // early exit of the ICP loop: active counts written by k_active_list into mapped host memory
-  uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), kMaxPolls words
+  hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr,
+            ev_crit = nullptr, ev_setup = nullptr;  // ev_crit: the last reading's correction; ev_setup: ready to iterate
+  // early exit of the ICP loops: active counts written by the update kernels into mapped host
+  // memory, kMaxPolls words per loop (two loops per window)
+  uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), 2 * kMaxPolls words
   uint32_t* poll_dev = nullptr;   // its device address
-  hipEvent_t ev_poll[kMaxPolls] = {};
+  hipEvent_t ev_poll[2 * kMaxPolls] = {};
   GraphCache g_raw, g_match, g_icp;
   bool used = false;
 };
 
 struct SeqState {
-  hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr;
+  hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr, s_icp2 = nullptr;
   SeqSlot slot[kSlots];
   DevBuf desc, state, outT;
   PinBuf pin_state, pin_out, pin_ctl;
   std::vector<hipEvent_t> nn_ev;
-  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
-  // device-side window dependency: window k's ICP stores ticket k to `sig` (signal memory) once
-  // its corrections are final; the next reference's stream waits for it (hipStreamWaitValue64)
-  uint64_t* sig = nullptr;
-  uint64_t ticket = 0;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_icp2 = nullptr;
   std::vector<hipEvent_t> tev;  // seq_prof(): 5 timing events per window
-  bool use_wait = false;    // the window ticket is a device-side dependency (hipStreamWaitValue64)
-  bool loop_graph = false;  // AICP_SEQ_SYNC=signal: every maxIterationCount launch as one graph, no polls
   WorkerPool pool{std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1};
   aicp_sequence_timing last{};
   int device = 0;
@@ -235,7 +232,7 @@ struct SeqState {
 
 void seq_state_free(SeqState* S) {
   if (!S) return;
-  for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp})
+  for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp, S->s_icp2})
     if (q) (void)hipStreamSynchronize(q);
   for (SeqSlot& sl : S->slot) {
     for (DevBuf* b : {&sl.read_raw, &sl.read_s, &sl.read_c, &sl.match, &sl.d2, &sl.touch, &sl.cand, &sl.slab,
@@ -248,20 +245,19 @@ void seq_state_free(SeqState* S) {
     for (auto& t : sl.tb) t.release_all();
     for (GraphCache* g : {&sl.g_raw, &sl.g_match, &sl.g_icp}) g->reset();
     for (PinBuf* b : {&sl.pin_read, &sl.pin_par, &sl.pin_src}) release(*b);
-    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done})
+    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done, sl.ev_crit, sl.ev_setup})
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : sl.ev_poll)
       if (e) (void)hipEventDestroy(e);
     if (sl.poll_host) (void)hipHostFree(sl.poll_host);
   }
   for (DevBuf* b : {&S->desc, &S->state, &S->outT}) release(*b);
-  if (S->sig) (void)hipFree(S->sig);
   for (PinBuf* b : {&S->pin_state, &S->pin_out, &S->pin_ctl}) release(*b);
   for (hipEvent_t e : S->nn_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : S->tev) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {S->ev_begin, S->ev_end})
+  for (hipEvent_t e : {S->ev_begin, S->ev_end, S->ev_icp2})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t q : {S->s_rd, S->s_icp})  // (s_up = s_rd; s_r2, s_r3 are the context's)
+  for (hipStream_t q : {S->s_rd, S->s_icp, S->s_icp2})  // (s_up = s_rd; s_r2, s_r3 are the context's)
     if (q) (void)hipStreamDestroy(q);
   delete S;
 }
@@ -376,10 +372,10 @@ struct WinRun {
   const float4* src_pts = nullptr;
   const float4* readS = nullptr;
   TreeCtl* ctl_w = nullptr;
-  uint64_t ticket = 0, src_ticket = 0;  // this window's ICP ticket; the previous window's
   const PairDesc* src_desc = nullptr;   // the reference source's descriptor and correction
   const float* src_T = nullptr;
   hipEvent_t* tev = nullptr;            // seq_prof(): ref start, matcher done, normals done, ICP start, ICP done
+  std::vector<uint32_t> n_read;         // the readings' point counts
 };
 
 // Run `enqueue` on stream s through the cache: replay the graph if the key matches, otherwise
@@ -452,7 +448,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   HIPC(ensure(sl.sel_hist, np * kHistBins * 4));
   HIPC(ensure(sl.sel_cnt, np * 4));
   HIPC(ensure(sl.ctrs, kCtrWords * 4));
-  HIPC(ensure(sl.active, sizeof(ActiveList)));
+  HIPC(ensure(sl.active, 2 * sizeof(ActiveList)));  // one per ICP loop
   HIPC(ensure(sl.ref_raw, (size_t)n_ref * 16));
   HIPC(ensure(sl.bpts, (size_t)n_ref * 16));
   HIPC(ensure(sl.bnrm, (size_t)n_ref * 16));
@@ -598,6 +594,8 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
 
   R.np = np;
   R.nread = nread;
+  R.n_read.resize(np);
+  for (size_t i = 0; i < np; ++i) R.n_read[i] = (uint32_t)rd[w.p0 + i].n;
   R.n_ref = n_ref;
   R.tl_cap = tl_cap;
   R.use_tl = use_tl;
@@ -705,12 +703,7 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     // the source's correction must be final: from the previous window of this pass (its ICP
     // signals the ticket as soon as every reading has stopped, before the loop's remaining no-op
     // launches; or, polled mode, its ev_done), or from an earlier pass (synchronised)
-    if (w.index > 0) {
-      if (S->use_wait)
-        HIPC(hipStreamWaitValue64(s3, S->sig, R.src_ticket, hipStreamWaitValueGte, ~0ull));
-      else
-        HIPC(hipStreamWaitEvent(s3, S->slot[(w.slot + kSlots - 1) % kSlots].ev_done, 0));
-    }
+    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, S->slot[(w.slot + kSlots - 1) % kSlots].ev_crit, 0));
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
     launch_seq_next_ref(s3, dG, R.src_desc, R.src_T, sl.tsrc.as<float>());
     launch_transform(s3, (int)n_ref, sl.tsrc.as<float>(), src_pts, sl.ref_raw.as<float4>());
@@ -840,20 +833,24 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   launch_prepare_read(si, R.m_read, dDesc, readS, sl.read_c.as<float4>());
   HIPC(hipMemsetAsync(sl.sel_hist.p, 0, np * kHistBins * 4, si));
   HIPC(hipMemsetAsync(sl.sel_cnt.p, 0, np * 4, si));
+  HIPC(hipMemsetAsync(sl.isync.p, 0, icp_sync_words(np) * 4, si));
   HIPC(hipGetLastError());
+  HIPC(hipEventRecord(sl.ev_setup, si));
   return AICP_OK;
 }
 
-// The ICP loop of the window on stream icp.
-//   signal mode (hipStreamWaitValue available): every maxIterationCount launch is enqueued, as one
-//     graph; k_active_list publishes the corrections and the window's ticket as soon as no pair is
-//     active, and the iterations after that find no active pair and return at once;
-//   polled mode: from iteration smoothLength on (no pair can stop earlier except on an error)
-//     k_active_list also writes the active count into mapped host memory; the host, lookahead()
-//     iterations behind, stops enqueueing once it reads 0.
-// The window's states and corrections are then committed to the sequence's arrays.
+// The ICP loops of a window. The next reference needs only the correction of the window's last
+// reading (app.cpp:375-391), so a window with a successor runs two loops: group 0, that reading,
+// on stream icp, which the next reference waits for (ev_crit); group 1, the other readings, on
+// stream icp2 (low priority), which nothing waits for before the read-back and which therefore
+// runs beside the next window's kd-trees and loop. (AICP_SEQ_SPLIT=0: one loop per window.)
+// Each loop is polled: from iteration smoothLength on (no pair can stop earlier except on an
+// error) the update kernel of the last pair to finish an iteration writes the next active count
+// into mapped host memory; the host, lookahead() iterations ahead, stops enqueueing once it
+// reads 0. The window's states and corrections are committed to the sequence's arrays once
+// both loops are done (ev_done).
 // iterations the host stays ahead of the polls it reads (AICP_SEQ_LOOKAHEAD, default 1): the
-// launches after the one that found no active pair are no-ops that still hold stream icp
+// launches after the one that found no active pair are no-ops that still hold the stream
 int lookahead() {
   static const int v = [] {
     const char* e = std::getenv("AICP_SEQ_LOOKAHEAD");
@@ -862,14 +859,37 @@ int lookahead() {
   }();
   return v;
 }
-static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
-                   WinRun& R, bool timeNN, int& nn_launches) {
-  WIN_REFS;
-  hipStream_t si = S->s_icp;
-  const bool use_tl = R.use_tl;
-  const uint64_t nread = R.nread;
+bool seq_split() {
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_SEQ_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+struct IcpLoop {
+  WinRun* R = nullptr;
+  int g = 0;             // 0: the critical group (or the whole window), 1: the others
+  size_t p0 = 0, np = 0; // the group's pairs [p0, p0 + np) of the window
+  uint64_t reads = 0;
+  hipStream_t st = nullptr;
+  BlockMap msel{}, mred{};
+  int it = 0;
+  bool stop = false;
+  std::deque<int> pending;  // poll slots recorded, oldest first
+};
+
+static BlockMap map_sub(const BlockMap& m, uint32_t off, uint32_t cnt) {
+  BlockMap r = m;
+  r.pair += off;
+  r.start += off;
+  r.n_blocks = cnt;
+  return r;
+}
+
+static IcpParams icp_params(const aicp_icp_config* cfg) {
   IcpParams ip;
-  std::memset(&ip, 0, sizeof(ip));  // (compared bytewise in the graph key)
+  std::memset(&ip, 0, sizeof(ip));
   ip.maxE2 = (1 + cfg->nn_epsilon) * (1 + cfg->nn_epsilon);
   ip.maxR2 = cfg->nn_max_dist * cfg->nn_max_dist;
   ip.max_iter = cfg->max_iter;
@@ -878,126 +898,143 @@ static int win_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, c
   ip.min_trans = cfg->min_diff_trans;
   ip.knn_normals = cfg->knn_normals;
   ip.interleave = nn_interleave(0);  // (interleaved chunks measured equal on C2 windows, r03)
-  ActiveList* al = sl.active.as<ActiveList>();
-  uint32_t* ctr = sl.ctrs.as<uint32_t>();
-  const bool wait_mode = S->use_wait;     // the ticket is signalled on the device
-  const bool loop_graph = S->loop_graph;  // no polls: every maxIterationCount launch, one graph
-  uint64_t* tk = sl.wticket.as<uint64_t>();
-  const bool fuse = icp_fuse_enabled();
-  IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, 0);
-  y.np = (int)np;
-  y.pd = dDesc;
-  y.st = dState;
+  return ip;
+}
+
+// the window's loops: one, or (split) the last reading on icp + the others on icp2
+static int win_loops(SeqState* S, WinRun& R, bool split, IcpLoop* L, int& n_loops) {
+  const size_t np = R.np;
+  split = split && np >= 2;
+  n_loops = split ? 2 : 1;
+  for (int g = 0; g < n_loops; ++g) {
+    IcpLoop& q = L[g];
+    q = IcpLoop{};
+    q.R = &R;
+    q.g = g;
+    q.p0 = split ? (g == 0 ? np - 1 : 0) : 0;
+    q.np = split ? (g == 0 ? 1 : np - 1) : np;
+    q.st = g == 0 ? S->s_icp : S->s_icp2;
+    uint32_t sel0 = 0, red0 = 0, sel_n = 0, red_n = 0;
+    for (size_t i = 0; i < np; ++i) {
+      const uint32_t a = (R.n_read[i] + kNNBlock * kSelPerThread - 1) / (kNNBlock * kSelPerThread);
+      const uint32_t b = (R.n_read[i] + kNNBlock * kReducePerThread * kReduceChunks - 1) /
+                         (kNNBlock * kReducePerThread * kReduceChunks);
+      if (i < q.p0) {
+        sel0 += a;
+        red0 += b;
+      } else if (i < q.p0 + q.np) {
+        sel_n += a;
+        red_n += b;
+        q.reads += R.n_read[i];
+      }
+    }
+    q.msel = map_sub(R.m_sel, sel0, sel_n);
+    q.mred = map_sub(R.m_red, red0, red_n);
+  }
+  return AICP_OK;
+}
+
+// enqueue the loop's next iteration (and its poll slots)
+static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm, IcpLoop& q,
+                          bool timeNN, int& nn_launches) {
+  WinRun& R = *q.R;
+  WIN_REFS;
+  const int it = q.it;
+  const PairDesc* gd = dDesc + q.p0;
+  PairState* gs = dState + q.p0;
+  ActiveList* al = sl.active.as<ActiveList>() + q.g;
+  uint32_t* ctr = sl.ctrs.as<uint32_t>() + (q.g ? 2 * kXcdGroups * kCtrStride : 0);
+  uint32_t* poll_host = sl.poll_host + q.g * kMaxPolls;
+  uint32_t* poll_dev = sl.poll_dev + q.g * kMaxPolls;
+  IcpParams ip = icp_params(cfg);
+  ip.prof_slot = nn_launches;
+  auto polled = [&](int k) {
+    return !early_exit_disabled() && k >= cfg->smooth_length && k < kMaxPolls && k < cfg->max_iter;
+  };
+  // poll slot k holds the active count at the start of iteration k, written by the launch that
+  // builds that iteration's active list (k_active_list at it = 0, else the previous update)
+  uint32_t* hn_this = nullptr;
+  uint32_t* hn_next = nullptr;
+  if (it == 0 && polled(it)) {
+    poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
+    hn_this = poll_dev + it;
+  }
+  if (polled(it + 1)) {
+    poll_host[it + 1] = 0xffffffffu;
+    hn_next = poll_dev + it + 1;
+  }
+  if (timeNN)
+    while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
+      hipEvent_t e;
+      HIPC(hipEventCreate(&e));
+      S->nn_ev.push_back(e);
+    }
+  hipStream_t st = q.st;
+  if (it == 0) launch_active_list(st, (int)q.np, gd, gs, al, ctr, hn_this, nullptr, nullptr, nullptr);
+  if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches], st));
+  launch_icp_nn(st, (int)q.reads, gd, gs, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
+                R.use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
+                R.use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
+                sl.touch.as<uint32_t>(), ctr, ip);
+  if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], st));
+  ++nn_launches;
+  IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, q.g);
+  y.np = (int)q.np;
+  y.pd = gd;
+  y.st = gs;
   y.al = al;
   y.ctr = ctr;
-  y.done_sig = wait_mode ? S->sig : nullptr;
-  y.ticket = tk;
-  y.outT = dOutT;
-  if (fuse) HIPC(hipMemsetAsync(sl.isync.p, 0, icp_sync_words(np) * 4, si));
-  // one iteration; fused: the active list of iteration it + 1 is built at the end of iteration it
-  // (host_n: the poll slot of it + 1)
-  auto iteration = [&](int it, uint32_t* host_n_this, uint32_t* host_n_next, hipEvent_t ev_a, hipEvent_t ev_b) {
-    if (!fuse || it == 0)
-      launch_active_list(si, (int)np, dDesc, dState, al, ctr, host_n_this, wait_mode ? S->sig : nullptr, tk, dOutT);
-    if (ev_a) (void)hipEventRecord(ev_a, si);
-    launch_icp_nn(si, (int)nread, dDesc, dState, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
-                  use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
-                  use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
-                  sl.touch.as<uint32_t>(), ctr, ip);
-    if (ev_b) (void)hipEventRecord(ev_b, si);
-    if (fuse) {
-      IcpIterSync yi = y;
-      yi.host_n = host_n_next;
-      launch_icp_select_f(si, R.m_sel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
-                          sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), yi);
-      launch_icp_reduce_f(si, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(),
-                          sl.d2.as<float>(), sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(),
-                          sl.slab.as<double>(), ip, yi);
-      return;
-    }
-    launch_icp_select(si, R.m_sel, (int)np, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
-                      sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), 0);
-    launch_icp_reduce(si, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
-                      sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>());
-    launch_icp_update(si, (int)np, dDesc, dState, sl.slab.as<double>(), ip);
-  };
-  if (wait_mode) HIPC(hipStreamWriteValue64(si, tk, R.ticket, 0));
-  if (R.tev) HIPC(hipEventRecord(R.tev[3], si));
-  if (loop_graph && !timeNN) {
-    ip.prof_slot = 0;
-    Key k;
-    k << np << nread << use_tl << ip << R.m_sel.pair << R.m_sel.start << R.m_sel.n_blocks << R.m_red.pair
-      << R.m_red.start << R.m_red.n_blocks << sl.wdesc.p << sl.wstate.p << sl.woutT.p << tk
-      << S->sig << sl.active.p << sl.ctrs.p << sl.read_c.p << sl.nodes.p << sl.tl.p << sl.bpts.p << sl.ptl.p
-      << sl.match.p << sl.d2.p << sl.touch.p << sl.sel_hist.p << sl.cand.p << sl.sel_cnt.p << sl.bnrm.p
-      << sl.slab.p << fuse << sl.isync.p;
-    const int rc = graph_run(ctx, sl.g_icp, si, k, [&]() -> int {
-      for (int it = 0; it < cfg->max_iter; ++it) iteration(it, nullptr, nullptr, nullptr, nullptr);
-      launch_finalize(si, (int)np, dDesc, dState, dOutT);
-      HIPC(hipGetLastError());
-      return AICP_OK;
-    });
-    if (rc) return rc;
-    nn_launches += cfg->max_iter;
-  } else {
-    int pending[kMaxPolls];
-    int n_pending = 0;
-    bool stop = false;
-    auto polled = [&](int q) {
-      return !loop_graph && !early_exit_disabled() && q >= cfg->smooth_length && q < kMaxPolls && q < cfg->max_iter;
-    };
-    for (int it = 0; it < cfg->max_iter && !stop; ++it) {
-      ip.prof_slot = nn_launches;
-      if (timeNN) {
-        while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
-          hipEvent_t e;
-          HIPC(hipEventCreate(&e));
-          S->nn_ev.push_back(e);
-        }
-      }
-      // poll slot q holds the active count at the start of iteration q, written by the launch
-      // that builds that iteration's active list (k_active_list; fused: the previous reduce)
-      uint32_t* hn_this = nullptr;
-      uint32_t* hn_next = nullptr;
-      if ((!fuse || it == 0) && polled(it)) {
-        sl.poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
-        hn_this = sl.poll_dev + it;
-      }
-      if (fuse && polled(it + 1)) {
-        sl.poll_host[it + 1] = 0xffffffffu;
-        hn_next = sl.poll_dev + it + 1;
-      }
-      iteration(it, hn_this, hn_next, timeNN ? S->nn_ev[2 * nn_launches] : nullptr,
-                timeNN ? S->nn_ev[2 * nn_launches + 1] : nullptr);
-      ++nn_launches;
-      for (int q : {hn_this ? it : -1, hn_next ? it + 1 : -1})
-        if (q >= 0) {
-          HIPC(hipEventRecord(sl.ev_poll[q], si));
-          pending[n_pending++] = q;
-        }
-      if (loop_graph) continue;  // all maxIterationCount launches
-      // the poll lookahead() iterations back: the device is still busy with the ones since
-      while (n_pending > 0 && it + 1 - pending[0] >= lookahead()) {
-        const int q = pending[0];
-        for (int j = 1; j < n_pending; ++j) pending[j - 1] = pending[j];
-        --n_pending;
-        HIPC(hipEventSynchronize(sl.ev_poll[q]));
-        if (sl.poll_host[q] == 0) {
-          stop = true;
-          break;
-        }
-      }
-    }
-    launch_finalize(si, (int)np, dDesc, dState, dOutT);
-  }
+  y.host_n = hn_next;
+  launch_icp_select_f(st, q.msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(), sl.cand.as<uint32_t>(),
+                      sl.sel_cnt.as<uint32_t>(), y);
+  launch_icp_reduce_f(st, q.mred, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
+                      sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>(), ip, y);
   HIPC(hipGetLastError());
-  // (a window whose loop ran all maxIterationCount launches never saw an empty active list)
-  if (wait_mode) HIPC(hipStreamWriteValue64(si, S->sig, R.ticket, 0));
-  launch_seq_commit(si, (int)np, dDesc, dState, dOutT, S->desc.as<PairDesc>() + w.p0,
+  for (int k : {hn_this ? it : -1, hn_next ? it + 1 : -1})
+    if (k >= 0) {
+      HIPC(hipEventRecord(sl.ev_poll[q.g * kMaxPolls + k], st));
+      q.pending.push_back(k);
+    }
+  ++q.it;
+  if (q.it >= cfg->max_iter) q.stop = true;
+  return AICP_OK;
+}
+
+// the group's corrections (and, once both groups are done, the window's commit and ev_done)
+static int loop_finish(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_params* prm, IcpLoop& q, int n_loops) {
+  WinRun& R = *q.R;
+  WIN_REFS;
+  launch_finalize(q.st, (int)q.np, dDesc + q.p0, dState + q.p0, dOutT + 16 * q.p0);
+  HIPC(hipGetLastError());
+  if (q.g == 0) {
+    HIPC(hipEventRecord(sl.ev_crit, q.st));
+    if (R.tev) HIPC(hipEventRecord(R.tev[4], q.st));
+  }
+  if (q.g + 1 < n_loops) return AICP_OK;  // group 1 commits the window
+  if (q.g == 1) HIPC(hipStreamWaitEvent(q.st, sl.ev_crit, 0));
+  launch_seq_commit(q.st, (int)np, dDesc, dState, dOutT, S->desc.as<PairDesc>() + w.p0,
                     S->state.as<PairState>() + w.p0, S->outT.as<float>() + 16 * w.p0);
   HIPC(hipGetLastError());
-  HIPC(hipEventRecord(sl.ev_done, si));
-  if (R.tev) HIPC(hipEventRecord(R.tev[4], si));
+  HIPC(hipEventRecord(sl.ev_done, q.st));
+  return AICP_OK;
+}
+
+// the oldest poll of the loop (got: it was read; q.stop set when it read 0)
+static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool block, bool& got) {
+  got = false;
+  SeqSlot& sl = S->slot[q.R->w.slot];
+  const int k = q.pending.front();
+  hipEvent_t e = sl.ev_poll[q.g * kMaxPolls + k];
+  if (block) {
+    HIPC(hipEventSynchronize(e));
+  } else {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipErrorNotReady) return AICP_OK;
+    HIPC(r);
+  }
+  q.pending.pop_front();
+  got = true;
+  if (sl.poll_host[q.g * kMaxPolls + k] == 0) q.stop = true;
   return AICP_OK;
 }
 
@@ -1014,35 +1051,20 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     // the third high-priority one; uploads and the reading side share one low-priority stream.
     HIPC(hipStreamCreateWithPriority(&S->s_rd, hipStreamNonBlocking, lo));
     HIPC(hipStreamCreateWithPriority(&S->s_icp, hipStreamNonBlocking, hi));
+    HIPC(hipStreamCreateWithPriority(&S->s_icp2, hipStreamNonBlocking, lo));  // the non-critical ICP loops
     S->s_up = S->s_rd;
     S->s_r2 = ctx->stream2;
     S->s_r3 = ctx->stream3;
     for (SeqSlot& sl : S->slot) {
-      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done})
+      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done, &sl.ev_crit, &sl.ev_setup})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
       for (hipEvent_t& e : sl.ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIPC(hipHostMalloc((void**)&sl.poll_host, kMaxPolls * 4, hipHostMallocMapped));
+      HIPC(hipHostMalloc((void**)&sl.poll_host, 2 * kMaxPolls * 4, hipHostMallocMapped));
       HIPC(hipHostGetDevicePointer((void**)&sl.poll_dev, sl.poll_host, 0));
     }
     HIPC(hipEventCreate(&S->ev_begin));
     HIPC(hipEventCreate(&S->ev_end));
-    // Window dependency (AICP_SEQ_SYNC):
-    //   default (poll)  the host polls the active count to stop enqueueing a window's ICP
-    //                   iterations and enqueues the next reference after the loop (event order);
-    //   signal          every maxIterationCount launch enqueued at once as one graph; the next
-    //                   reference waits for the window's ticket on the device (wait-value). The
-    //                   trailing launches find no active pair but still hold stream icp: measured
-    //                   2.79 ms per window against 2.25 ms polled (r03).
-    const char* e = std::getenv("AICP_SEQ_SYNC");
-    S->loop_graph = e && std::strcmp(e, "signal") == 0;
-    int can = 0;
-    if (S->loop_graph &&
-        hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, ctx->device) == hipSuccess && can &&
-        hipExtMallocWithFlags((void**)&S->sig, 8, hipMallocSignalMemory) == hipSuccess) {
-      HIPC(hipStreamWriteValue64(S->s_icp, S->sig, 0, 0));
-      HIPC(hipStreamSynchronize(S->s_icp));
-      S->use_wait = true;
-    }
+    HIPC(hipEventCreateWithFlags(&S->ev_icp2, hipEventDisableTiming));
     (void)hipGetLastError();
   }
   SeqState* S = ctx->seq;
@@ -1135,8 +1157,6 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       const Win& w = plan[k];
       runs[k].w = w;
       runs[k].ctl_w = ctl + 2 * k;
-      runs[k].ticket = ++S->ticket;
-      runs[k].src_ticket = k > 0 ? runs[k - 1].ticket : 0;
       if (k > 0) {  // the source is the previous window's last reading, still in its slot
         const Win& pw = plan[k - 1];
         const size_t off = (size_t)w.src - pw.p0;
@@ -1165,31 +1185,116 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       hp[slot] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
       return r;
     };
-    // The next reference is enqueued after the window's ICP loop: a wait-value enqueued earlier
-    // on a stream that shares a hardware queue with stream icp would block the loop behind it
-    // (HIP maps streams onto GPU_MAX_HW_QUEUES queues per priority; measured: a deadlock with
-    // several contexts alive).
-    const bool early_ref = false;
     // The reading side of window k + 1 (Morton order, voxel maps) is enqueued with its upload,
     // before window k's loop. (AICP_SEQ_READ_LATE=1 enqueues it with the next reference instead, to
     // keep it off the loop's CUs: measured 2.29 against 2.20 ms per window, since it then slows
     // the kd-tree builds on the critical path.)
     const bool read_early = seq_read_early();
     auto read_side = [&](size_t k) { return win_read_side(ctx, S, cfg, prm, runs[k]); };
+    // ICP loops (win_loops): the critical loop of the current window, and the non-critical loops
+    // of earlier windows in order on stream icp2 (only the front one is iterated)
+    const bool split = seq_split();
+    std::vector<std::array<IcpLoop, 2>> loops(plan.size());
+    std::vector<int> n_loops(plan.size(), 0);
+    std::vector<uint8_t> done_enq(plan.size(), 0);  // the window's ev_done recorded
+    std::deque<IcpLoop*> rest;
+    auto advance = [&](IcpLoop* q, bool& progress) -> int {
+      const int nl = n_loops[q->R->w.index];
+      if (q->g == 1 && q->it == 0 && q->pending.empty() && !q->stop) {
+        SeqSlot& sl = S->slot[q->R->w.slot];
+        if (hipStreamWaitEvent(q->st, sl.ev_setup, 0) != hipSuccess) return AICP_ERR_HIP;
+      }
+      for (;;) {
+        while (!q->stop && (q->pending.empty() || q->it - q->pending.front() < lookahead())) {
+          const int r = loop_iteration(ctx, S, cfg, prm, *q, timeNN, nn_launches);
+          if (r) return r;
+          progress = true;
+        }
+        if (q->stop || q->pending.empty()) break;
+        bool got = false;
+        const int r = loop_poll(ctx, S, *q, false, got);
+        if (r) return r;
+        if (!got) break;
+        progress = true;
+      }
+      if (q->stop && q->it >= 0) {
+        const int r = loop_finish(ctx, S, prm, *q, nl);
+        if (r) return r;
+        if (q->g + 1 == nl) done_enq[q->R->w.index] = 1;
+        q->it = -1;  // finished
+        progress = true;
+      }
+      return AICP_OK;
+    };
+    auto drive_rest = [&](bool& progress) -> int {
+      while (!rest.empty()) {
+        const int r = advance(rest.front(), progress);
+        if (r) return r;
+        if (rest.front()->it >= 0) break;
+        rest.pop_front();
+      }
+      return AICP_OK;
+    };
+    // upload(k + 1) reuses the slot of window k - 2 and waits (on the device) for ev_done of
+    // window k - 1, which exists once that window's last loop has been finished here
+    auto can_upload = [&](size_t k) { return k + 1 < plan.size() && (k < 1 || done_enq[k - 1]); };
     rc = timed(0, [&] { return upload(0); });
     if (!rc) rc = timed(0, [&] { return read_side(0); });
     if (!rc) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[0]); });
     if (!rc) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[0]); });
     for (size_t k = 0; k < plan.size() && !rc; ++k) {
       const bool next = k + 1 < plan.size();
-      if (next) rc = timed(0, [&] { return upload(k + 1); });
-      if (!rc && next && read_early) rc = timed(0, [&] { return read_side(k + 1); });
-      if (!rc && next && early_ref) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
-      if (!rc) rc = timed(2, [&] { return win_icp(ctx, S, cfg, prm, runs[k], timeNN, nn_launches); });
-      if (!rc && next && !early_ref) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
+      bool uploaded = !next;
+      auto try_upload = [&]() -> int {
+        if (uploaded || !can_upload(k)) return AICP_OK;
+        uploaded = true;
+        int r = timed(0, [&] { return upload(k + 1); });
+        if (!r && read_early) r = timed(0, [&] { return read_side(k + 1); });
+        return r;
+      };
+      rc = try_upload();
+      if (rc) break;
+      rc = win_loops(S, runs[k], split && next, loops[k].data(), n_loops[k]);
+      if (rc) break;
+      if (runs[k].tev) {
+        rc = hipEventRecord(runs[k].tev[3], S->s_icp) == hipSuccess ? AICP_OK : AICP_ERR_HIP;
+        if (rc) break;
+      }
+      IcpLoop* crit = &loops[k][0];
+      if (n_loops[k] == 2) rest.push_back(&loops[k][1]);
+      rc = timed(2, [&]() -> int {
+        while (crit->it >= 0) {
+          bool progress = false;
+          int r = advance(crit, progress);
+          if (!r) r = drive_rest(progress);
+          if (!r) r = try_upload();
+          if (r) return r;
+          if (!progress) std::this_thread::yield();
+        }
+        // the next window's upload needs the previous window's ev_done
+        while (!uploaded && !rc) {
+          bool progress = false;
+          int r = drive_rest(progress);
+          if (!r) r = try_upload();
+          if (r) return r;
+          if (!progress) std::this_thread::yield();
+        }
+        return AICP_OK;
+      });
+      if (!rc && next) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
       if (!rc && next && !read_early) rc = timed(0, [&] { return read_side(k + 1); });
       if (!rc && next) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
       ++windows;
+    }
+    while (!rc && !rest.empty()) {
+      bool progress = false;
+      rc = drive_rest(progress);
+      if (!rc && !progress) std::this_thread::yield();
+    }
+    if (!rc) {  // the read-back (stream icp) after every non-critical loop (stream icp2)
+      rc = hipEventRecord(S->ev_icp2, S->s_icp2) == hipSuccess && hipStreamWaitEvent(S->s_icp, S->ev_icp2, 0) == hipSuccess
+               ? AICP_OK
+               : AICP_ERR_HIP;
     }
     if (prof)
       std::fprintf(stderr, "[aicp seq] host ms: upload %.2f reference %.2f icp(incl. polls) %.2f over %zu windows\n",
