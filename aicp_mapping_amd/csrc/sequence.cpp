@@ -843,7 +843,10 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
 // reading (app.cpp:375-391), so a window with a successor runs two loops: group 0, that reading,
 // on stream icp, which the next reference waits for (ev_crit); group 1, the other readings, on
 // stream icp2 (low priority), which nothing waits for before the read-back and which therefore
-// runs beside the next window's kd-trees and loop. (AICP_SEQ_SPLIT=0: one loop per window.)
+// runs beside the next window's kd-trees and loop (AICP_SEQ_SPLIT=1). Measured on C2 (r03): the
+// one-reading loop takes 0.99 ms against 1.06 ms for all five (an iteration is latency-bound,
+// not work-bound), and the other readings' NN launches beside the next reference's kd-trees and
+// kNN slow those from 0.88 to 1.63 ms, so the default is one loop per window.
 // Each loop is polled: from iteration smoothLength on (no pair can stop earlier except on an
 // error) the update kernel of the last pair to finish an iteration writes the next active count
 // into mapped host memory; the host, lookahead() iterations ahead, stops enqueueing once it
@@ -862,7 +865,7 @@ int lookahead() {
 bool seq_split() {
   static const bool on = [] {
     const char* e = std::getenv("AICP_SEQ_SPLIT");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
