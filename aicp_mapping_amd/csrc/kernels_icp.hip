@@ -1777,11 +1777,17 @@ __global__ __launch_bounds__(256, (K <= 10 ? 5 : (K <= 20 ? 4 : 3))) void k_knn_
 // few hundred wave instructions with the octet's lanes all busy, against one lane doing K-long
 // compare-shift chains: on a single 120k-point reference (the C2 stream's window) the kNN is
 // bound by the longest query's latency, not by the chip's issue rate.
-constexpr int kOctFrames = 24;  // far frames per octet kept in LDS (deeper ones in scratch)
+// far frames per query group kept in LDS (deeper ones in scratch): 24 per octet, 12 per quad
+// (18 KB per 256-thread block either way: 8 blocks per CU)
+template <int G>
+struct GrpCfg {
+  static constexpr int kFrames = G == 8 ? 24 : 12;
+  static constexpr int kGroups = 256 / G;  // query groups per block
+};
 
-template <int K>
+template <int K, int G>
 struct OctBest {
-  static constexpr int M = (K + 7) / 8;
+  static constexpr int M = (K + G - 1) / G;
   float v[M];
   int32_t id[M];
 };
@@ -1797,10 +1803,17 @@ template <int I>
 __device__ __forceinline__ float oct_bcast(float x) {
   return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x18 | (I << 5)));
 }
+// lane (l & ~3) | I: DPP quad_perm [I, I, I, I]
+template <int I>
+__device__ __forceinline__ float quad_bcast(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), I | (I << 2) | (I << 4) | (I << 6), 0xf, 0xf, false));
+}
+template <int I>
+__device__ __forceinline__ float grp_bcast4(float x) { return quad_bcast<I>(x); }
 
-template <int K>
-__device__ __forceinline__ void oct_insert(OctBest<K>& b, bool first_lane, float val, int32_t vid) {
-  constexpr int M = OctBest<K>::M;
+template <int K, int G>
+__device__ __forceinline__ void oct_insert(OctBest<K, G>& b, bool first_lane, float val, int32_t vid) {
+  constexpr int M = OctBest<K, G>::M;
   float pv = oct_prev_f(b.v[M - 1]);
   int32_t pid = oct_prev_i(b.id[M - 1]);
   if (first_lane) pv = -__builtin_inff();
@@ -1823,16 +1836,58 @@ __device__ __forceinline__ void oct_insert(OctBest<K>& b, bool first_lane, float
   }
 }
 
-template <int K>
+// the distances of a bucket run of 8 points, in order, in every lane of the group: octets load
+// one point per lane and broadcast by ds_swizzle; quads load two per lane (j, j + 4) and
+// broadcast by DPP
+template <int G>
+__device__ __forceinline__ void grp_bucket_dists(const float4* __restrict__ pts, uint32_t base, uint32_t n, int j,
+                                                 float q0, float q1, float q2, float (&dv)[8]) {
+  auto dist_of = [&](uint32_t i) {
+    float d = __builtin_inff();
+    if (i < n) {
+      const float4 p = pts[base + i];
+      const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
+      d = 0.f;
+      d += d0 * d0;
+      d += d1 * d1;
+      d += d2 * d2;
+    }
+    return d;
+  };
+  if constexpr (G == 8) {
+    const float d = dist_of((uint32_t)j);
+    dv[0] = oct_bcast<0>(d);
+    dv[1] = oct_bcast<1>(d);
+    dv[2] = oct_bcast<2>(d);
+    dv[3] = oct_bcast<3>(d);
+    dv[4] = oct_bcast<4>(d);
+    dv[5] = oct_bcast<5>(d);
+    dv[6] = oct_bcast<6>(d);
+    dv[7] = oct_bcast<7>(d);
+  } else {
+    const float da = dist_of((uint32_t)j), db = dist_of((uint32_t)j + 4);
+    dv[0] = quad_bcast<0>(da);
+    dv[1] = quad_bcast<1>(da);
+    dv[2] = quad_bcast<2>(da);
+    dv[3] = quad_bcast<3>(da);
+    dv[4] = quad_bcast<0>(db);
+    dv[5] = quad_bcast<1>(db);
+    dv[6] = quad_bcast<2>(db);
+    dv[7] = quad_bcast<3>(db);
+  }
+}
+
+template <int K, int G>
 __global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
                                                  const uint4* __restrict__ nodes_all,
                                                  const float4* __restrict__ bpts, int32_t* __restrict__ ids,
                                                  unsigned long long* touched) {
-  constexpr int M = OctBest<K>::M;
+  constexpr int M = OctBest<K, G>::M;
   constexpr int kHeadLane = (K - 1) / M, kHeadSlot = (K - 1) % M;
-  __shared__ LdsFrame oframes[kOctFrames * 32];
-  const int lane = threadIdx.x & 63, j = lane & 7, oct = threadIdx.x >> 3;  // oct: 0..31 in the block
-  const uint32_t s = (blockIdx.x * 256u + threadIdx.x) >> 3;                 // the octet's query
+  constexpr int kFrames = GrpCfg<G>::kFrames, kGroups = GrpCfg<G>::kGroups;
+  __shared__ LdsFrame oframes[kFrames * kGroups];
+  const int lane = threadIdx.x & 63, j = lane & (G - 1), grp = threadIdx.x / G;  // grp: the block's group
+  const uint32_t s = (blockIdx.x * 256u + threadIdx.x) / G;                          // the group's query
   const bool live = s < total;
   uint32_t tp = 0, tn = 0;
   if (live) {
@@ -1842,7 +1897,7 @@ __global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, co
     const float4* pts = bpts + d.ref_off;
     const float4 qq = bpts[s];
     const float q0 = qq.x, q1 = qq.y, q2 = qq.z;
-    OctBest<K> best;
+    OctBest<K, G> best;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       best.v[i] = __builtin_inff();
@@ -1852,7 +1907,7 @@ __global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, co
     float off0 = 0.f, off1 = 0.f, off2 = 0.f, rd = 0.f, minFar;
     int32_t n = 0, start = 0, sp = 0;
     FarStack fs;
-    LdsFrame* lf = oframes + oct;
+    LdsFrame* lf = oframes + grp;
     const uint2* nodes2 = reinterpret_cast<const uint2*>(nodes);
     for (;;) {
       // descent (Trav<K>::advance)
@@ -1871,28 +1926,12 @@ __global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, co
         nd = nodes2[2 * n];
       }
       if (pl < 0) pl = (int32_t)nodes[n].z;
-      // bucket: lane j takes point c + j, the distances go round the octet in order
+      // bucket: runs of 8 points, their distances in every lane of the group, in order
       {
         const uint32_t b0 = nd.y >> 2, cnt = nd.x;
         for (uint32_t c = 0; c < cnt; c += 8) {
-          float dist = __builtin_inff();
-          if (c + (uint32_t)j < cnt) {
-            const float4 p = pts[b0 + c + j];
-            const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
-            dist = 0.f;
-            dist += d0 * d0;
-            dist += d1 * d1;
-            dist += d2 * d2;
-          }
           float dv[8];
-          dv[0] = oct_bcast<0>(dist);
-          dv[1] = oct_bcast<1>(dist);
-          dv[2] = oct_bcast<2>(dist);
-          dv[3] = oct_bcast<3>(dist);
-          dv[4] = oct_bcast<4>(dist);
-          dv[5] = oct_bcast<5>(dist);
-          dv[6] = oct_bcast<6>(dist);
-          dv[7] = oct_bcast<7>(dist);
+          grp_bucket_dists<G>(pts, b0 + c, cnt - c, j, q0, q1, q2, dv);
           // candidates below the head as it stood before this run (libnabo's `dist < head`; a
           // candidate the earlier insertions of the run pushed above the head is a no-op)
           uint32_t m8 = 0;
@@ -1900,8 +1939,8 @@ __global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, co
           for (int i = 0; i < 8; ++i) m8 |= (dv[i] < head ? 1u : 0u) << i;
 #pragma unroll
           for (int i = 0; i < 8; ++i)
-            if ((m8 >> i) & 1u) oct_insert<K>(best, j == 0, dv[i], (int32_t)(b0 + c + i));
-          head = __shfl(best.v[kHeadSlot], (lane & ~7) | kHeadLane, 64);
+            if ((m8 >> i) & 1u) oct_insert<K, G>(best, j == 0, dv[i], (int32_t)(b0 + c + i));
+          head = __shfl(best.v[kHeadSlot], (lane & ~(G - 1)) | kHeadLane, 64);
         }
         tp += cnt;
       }
@@ -1917,8 +1956,8 @@ __global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, co
           }
           --sp;
           FarFrame f;
-          if (sp < kOctFrames) {
-            const LdsFrame g = lf[sp * 32];
+          if (sp < kFrames) {
+            const LdsFrame g = lf[sp * kGroups];
             f = FarFrame{g.Pcd, g.rd, g.old, g.mn, g.start, g.Pcd & 0x3fffffff, g.PP, 0};
           } else {
             f = fs.f[sp];
@@ -1944,9 +1983,9 @@ __global__ __launch_bounds__(256) void k_knn_oct(int n_pairs, uint32_t total, co
         const float rdf = rd + (-oc * oc + no * no);
         if (rdf * 1.f < head) {
           const int32_t far = (no > 0.f) ? p + 1 : (int32_t)(pn.y >> 2);
-          if (sp < kOctFrames) {
+          if (sp < kFrames) {
             if (j == 0)
-              lf[sp * 32] = LdsFrame{(int32_t)((uint32_t)p | (cd << 30)), rd, oc, minFar, start, (int32_t)pn.z};
+              lf[sp * kGroups] = LdsFrame{(int32_t)((uint32_t)p | (cd << 30)), rd, oc, minFar, start, (int32_t)pn.z};
           } else {
             fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, (int32_t)pn.z, 0};
           }
@@ -2858,6 +2897,13 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
 // engine, which pays only while the per-lane launch leaves the chip short of waves (the C2
 // stream's single 120k-point reference: 377 -> 245 us); on C5's 61 M queries it ran 91.7 ms per
 // launch against the per-lane engine's throughput (C5 3962 -> 3097 clouds/s, r03c).
+static int knn_group_lanes() {  // AICP_KNN_GROUP=4|8: lanes per query of k_knn_oct (default 8)
+  static const int g = [] {
+    const char* e = std::getenv("AICP_KNN_GROUP");
+    return (e && e[0] == '4') ? 4 : 8;
+  }();
+  return g;
+}
 static bool knn_oct_enabled(uint32_t n_queries) {
   static const uint64_t lim = [] {
     const char* e = std::getenv("AICP_KNN_OCT");
@@ -2874,13 +2920,18 @@ bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
                     const uint4* tl, const uint2* link) {
   if (!total_ref) return true;
   if (knn_oct_enabled(total_ref)) {
-    const unsigned go = (unsigned)(((uint64_t)total_ref * 8 + 255) / 256);
+    const int G = knn_group_lanes();
+    const unsigned go = (unsigned)(((uint64_t)total_ref * G + 255) / 256);
+#define AICP_KNN_GRP(KK)                                                                        \
+  (G == 8 ? (k_knn_oct<KK, 8><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched)) \
+          : (k_knn_oct<KK, 4><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched)))
     switch (knn) {
-      case 10: k_knn_oct<10><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
-      case 20: k_knn_oct<20><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
-      case 30: k_knn_oct<30><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
+      case 10: AICP_KNN_GRP(10); break;
+      case 20: AICP_KNN_GRP(20); break;
+      case 30: AICP_KNN_GRP(30); break;
       default: return false;
     }
+#undef AICP_KNN_GRP
     return true;
   }
   const int g = persistent_grid((int)total_ref);
