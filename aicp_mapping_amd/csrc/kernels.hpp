@@ -68,6 +68,7 @@ struct IcpIterSync {
   float* outT;
 };
 bool icp_fuse_enabled();
+void iter_prof_dump();  // diagnostic builds (AICP_ITER_PROF): per-kernel body / tail times to stderr
 inline size_t icp_sync_words(size_t n_pairs) { return 3 * n_pairs + 2; }
 // sync words laid out for pairs [0, n_pairs): sel1 | sel2 | red | pairs (2: one per group)
 IcpIterSync icp_sync_layout(uint32_t* words, size_t n_pairs, int group);

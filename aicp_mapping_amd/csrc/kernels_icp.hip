@@ -1327,6 +1327,43 @@ __device__ unsigned long long g_xcd_prof[64 * kXcdGroups * 2];
 #if AICP_NN_PROF
 __device__ unsigned long long g_nn_prof[8];
 #endif
+#ifndef AICP_ITER_PROF
+#define AICP_ITER_PROF 0  // diagnostic builds: time the ICP iteration kernels' bodies and serial tails
+#endif
+#if AICP_ITER_PROF
+// per kernel k (0 hist_f, 1 compact_f, 2 reduce, 3 update_f): [4k] body sum, [4k+1] bodies,
+// [4k+2] tail sum, [4k+3] tails (s_memrealtime ticks, 10 ns)
+__device__ unsigned long long g_iter_prof[16];
+#define AICP_IP_T0 const uint64_t ip_t0 = __builtin_amdgcn_s_memrealtime()
+#define AICP_IP_BODY(k)                                                                          \
+  do {                                                                                           \
+    if (threadIdx.x == 0) {                                                                      \
+      atomicAdd(&g_iter_prof[4 * (k)], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - ip_t0)); \
+      atomicAdd(&g_iter_prof[4 * (k) + 1], 1ull);                                                \
+    }                                                                                            \
+  } while (0)
+#define AICP_IP_TAIL0 const uint64_t ip_t1 = __builtin_amdgcn_s_memrealtime()
+#define AICP_IP_TAIL(k)                                                                          \
+  do {                                                                                           \
+    if (threadIdx.x == 0) {                                                                      \
+      atomicAdd(&g_iter_prof[4 * (k) + 2], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - ip_t1)); \
+      atomicAdd(&g_iter_prof[4 * (k) + 3], 1ull);                                                \
+    }                                                                                            \
+  } while (0)
+#else
+#define AICP_IP_T0 \
+  do {             \
+  } while (0)
+#define AICP_IP_BODY(k) \
+  do {                  \
+  } while (0)
+#define AICP_IP_TAIL0 \
+  do {                \
+  } while (0)
+#define AICP_IP_TAIL(k) \
+  do {                  \
+  } while (0)
+#endif
 
 // Persistent waves with XCD-affine work: the slot space [0, total) is cut into kXcdGroups
 // contiguous ranges (64-slot aligned) and group g is served only by blocks with
@@ -2249,11 +2286,23 @@ __device__ bool sel_find1_body(PairState& s, uint32_t* __restrict__ g) {
   __shared__ uint32_t res[2];
   const int t = threadIdx.x, lane = t & 63, nt = (int)blockDim.x;
   uint32_t v = 0;
-  for (int i = t; i < kHistBins; i += nt) {
-    const uint32_t c = __hip_atomic_load(&g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h[i] = c;
-    g[i] = 0;  // ready for the next iteration
-    v += c;
+  // eight agent-scope loads in flight per thread (each is a fabric round trip), then the stores
+  for (int i0 = 0; i0 < kHistBins; i0 += 8 * nt) {
+    uint32_t c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * nt + t;
+      c[u] = i < kHistBins ? __hip_atomic_load(&g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * nt + t;
+      if (i < kHistBins) {
+        h[i] = c[u];
+        g[i] = 0;  // ready for the next iteration
+        v += c[u];
+      }
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -2310,6 +2359,7 @@ __device__ void pair_done(const IcpIterSync& y) {
 __global__ __launch_bounds__(256) void k_sel_hist_f(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
                                                     const float* __restrict__ d2, uint32_t* __restrict__ hist1,
                                                     IcpIterSync y) {
+  AICP_IP_T0;
   const int pair = m.pair[blockIdx.x];
   if (!st[pair].active) return;
   __shared__ uint32_t h[2][kHistBins];  // one sub-histogram per wave pair (LDS atomic conflicts)
@@ -2339,8 +2389,11 @@ __global__ __launch_bounds__(256) void k_sel_hist_f(BlockMap m, const PairDesc* 
     if (c) atomicAdd(&g[b], c);
   }
   const uint32_t nblk = (d.n_read + 256u * kSelPerThread - 1) / (256u * kSelPerThread);
+  AICP_IP_BODY(0);
   if (!last_arrival(&y.sel1[pair], nblk)) return;
+  AICP_IP_TAIL0;
   if (!sel_find1_body(st[pair], g)) pair_done(y);
+  AICP_IP_TAIL(0);
 }
 
 __global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc* __restrict__ pd,
@@ -2387,16 +2440,38 @@ __global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc*
   }
 }
 
-// per pair (one workgroup, any size): digits 2 (bits 20..10) and 3 (bits 9..0) over the candidates
+// per pair (one workgroup, any size): digits 2 (bits 20..10) and 3 (bits 9..0) over the candidates.
+// The candidates were written by the other workgroups (other XCDs: each load is a fabric round
+// trip), so up to kFinalLds of them are read once, eight loads in flight per thread, into LDS and
+// both passes run there (the passes over global memory took ~11 us of a C2 iteration, r03).
+constexpr uint32_t kFinalLds = 8192;
 __device__ void sel_final_body(PairState& s, const uint32_t* __restrict__ cv, uint32_t* cand_cnt) {
   __shared__ uint32_t h[kHistBins];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t res[2];
+  __shared__ uint32_t cl[kFinalLds];
   const int t = threadIdx.x, nt = (int)blockDim.x;
   const uint32_t c = __hip_atomic_load(cand_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool lds = c <= kFinalLds;
+  const uint32_t* src = lds ? cl : cv;
+  if (lds) {
+    for (uint32_t i0 = 0; i0 < c; i0 += 8u * (uint32_t)nt) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t i = i0 + (uint32_t)(u * nt + t);
+        v[u] = i < c ? cv[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t i = i0 + (uint32_t)(u * nt + t);
+        if (i < c) cl[i] = v[u];
+      }
+    }
+  }
   for (int i = t; i < kHistBins; i += nt) h[i] = 0;
   __syncthreads();
-  for (uint32_t i = t; i < c; i += nt) atomicAdd(&h[(cv[i] >> 10) & 2047u], 1u);
+  for (uint32_t i = t; i < c; i += nt) atomicAdd(&h[(src[i] >> 10) & 2047u], 1u);
   __syncthreads();
   block_find_rank(h, kHistBins, s.sel_r1, res, wsum);
   const uint32_t b2 = res[0], r2 = res[1];
@@ -2405,7 +2480,7 @@ __device__ void sel_final_body(PairState& s, const uint32_t* __restrict__ cv, ui
   __syncthreads();
   const uint32_t hi21 = (s.sel_b1 << 11) | b2;
   for (uint32_t i = t; i < c; i += nt) {
-    const uint32_t v = cv[i];
+    const uint32_t v = src[i];
     if ((v >> 10) == hi21) atomicAdd(&h[v & 1023u], 1u);
   }
   __syncthreads();
@@ -2428,6 +2503,7 @@ __global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__
 __global__ __launch_bounds__(256) void k_sel_compact_f(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
                                                        const float* __restrict__ d2, uint32_t* __restrict__ cand,
                                                        uint32_t* __restrict__ cand_cnt, IcpIterSync y) {
+  AICP_IP_T0;
   const int pair = m.pair[blockIdx.x];
   PairState& s = st[pair];
   if (!s.active) return;
@@ -2468,8 +2544,11 @@ __global__ __launch_bounds__(256) void k_sel_compact_f(BlockMap m, const PairDes
     }
   }
   const uint32_t nblk = (d.n_read + 256u * kSelPerThread - 1) / (256u * kSelPerThread);
+  AICP_IP_BODY(1);
   if (!last_arrival(&y.sel2[pair], nblk)) return;
+  AICP_IP_TAIL0;
   sel_final_body(s, cand + d.read_off, cand_cnt + pair);
+  AICP_IP_TAIL(1);
 }
 
 // DPP lane moves of a double (both halves with the same control); lanes outside the
@@ -2592,10 +2671,12 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
     const float4* __restrict__ read_c, const int32_t* __restrict__ match,
     const float* __restrict__ d2, const uint32_t* __restrict__ touched, const float4* __restrict__ bpts,
     const float4* __restrict__ bnrm, double* __restrict__ slab) {
+  AICP_IP_T0;
   const int pair = m.pair[blockIdx.x];
   const PairState& s = st[pair];
   if (!s.active) return;
   icp_reduce_body(m, pd[pair], s, read_c, match, d2, touched, bpts, bnrm, slab);
+  AICP_IP_BODY(2);
 }
 
 // the serial part of an ICP update (one lane): solve, compose, checkers
@@ -2681,8 +2762,19 @@ __device__ void icp_update_body(const PairDesc& d, PairState& s, const double* _
     const int g = t / kRedCols, c = t - g * kRedCols;
     const double* col = slab + (size_t)d.red_blk_off * kRedCols + c;
     double v = 0.0;
-#pragma unroll 4
-    for (uint32_t r = g; r < d.n_red_blk; r += kGroups) v += col[(size_t)r * kRedCols];
+    // rows g, g + kGroups, ... in order; 16 loads in flight (the rows were written by the reduce
+    // workgroups on every XCD: each load is a fabric round trip)
+    for (uint32_t r0 = g; r0 < d.n_red_blk; r0 += 16u * kGroups) {
+      double x[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const uint32_t r = r0 + (uint32_t)u * kGroups;
+        x[u] = r < d.n_red_blk ? col[(size_t)r * kRedCols] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (r0 + (uint32_t)u * kGroups < d.n_red_blk) v += x[u];
+    }
     part[g][c] = v;
   }
   __syncthreads();
@@ -2728,11 +2820,15 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce_f(
 // wave per SIMD (35-40 us per C2 window iteration against 12.5 + 12.3 us for the two kernels).
 __global__ __launch_bounds__(256) void k_icp_update_f(const PairDesc* __restrict__ pd, PairState* st,
                                                       const double* __restrict__ slab, IcpParams prm, IcpIterSync y) {
+  AICP_IP_T0;
   const int pair = blockIdx.x;
   PairState& s = st[pair];
   if (!s.active) return;
   icp_update_body(pd[pair], s, slab, prm);
+  AICP_IP_BODY(3);
+  AICP_IP_TAIL0;
   pair_done(y);
+  AICP_IP_TAIL(3);
 }
 
 __global__ void k_finalize(int n_pairs, const PairDesc* __restrict__ pd,
@@ -2984,6 +3080,21 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
   else
     k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, nullptr, match, d2, touched, ctr, prm);
 }
+void iter_prof_dump() {
+#if AICP_ITER_PROF
+  unsigned long long h[16];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_iter_prof), sizeof(h)) == hipSuccess) {
+    const char* nm[4] = {"hist_f", "compact_f", "reduce", "update_f(body=slab+solve, tail=active list)"};
+    for (int k = 0; k < 4; ++k)
+      fprintf(stderr, "[iter prof] %s: body %.2f us avg over %llu, tail %.2f us avg over %llu\n", nm[k],
+              h[4 * k + 1] ? h[4 * k] / 100.0 / h[4 * k + 1] : 0.0, h[4 * k + 1],
+              h[4 * k + 3] ? h[4 * k + 2] / 100.0 / h[4 * k + 3] : 0.0, h[4 * k + 3]);
+  }
+  unsigned long long z[16] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_iter_prof), z, sizeof(z));
+#endif
+}
+
 void nn_prof_dump() {
 #if AICP_XCD_PROF
   static unsigned long long h[64 * kXcdGroups * 2];

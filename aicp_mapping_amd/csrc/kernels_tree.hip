@@ -711,13 +711,10 @@ __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t*
 
 // split: left-count rule, node event of this segment, children: leaf events, subtree segments
 // (count <= kSubMax), mid-size segments (<= kMidMax) or next-level segments
-__global__ __launch_bounds__(256) void k_tr_split(int level, int last, uint32_t total, TreeSeg* seg, TreeSeg* next,
-                                                  SubSeg* subs, SubSeg* mids, TreeCtl* ctl, const uint32_t* __restrict__ X2,
-                                                  NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
-                                                  int32_t* pair_depth, int bucket, uint32_t max_seg,
-                                                  uint32_t mid_max) {
-  const uint32_t si = blockIdx.x * blockDim.x + threadIdx.x;
-  if (si >= ctl->nseg[level]) return;
+__device__ void tr_split_seg(uint32_t si, int level, int last, uint32_t total, TreeSeg* seg, TreeSeg* next,
+                             SubSeg* subs, SubSeg* mids, TreeCtl* ctl, const uint32_t* __restrict__ X2,
+                             NodeEvent* ev, uint8_t* valid, uint32_t* ecnt, int32_t* pair_depth, int bucket,
+                             uint32_t max_seg, uint32_t mid_max) {
   TreeSeg& g = seg[si];
   if (g.count == 0) return;  // root handled elsewhere
   const uint32_t f = g.first, count = g.count;
@@ -804,6 +801,56 @@ __global__ __launch_bounds__(256) void k_tr_split(int level, int last, uint32_t 
     c.hi = 0u;
     g.child[side] = (int32_t)ni;
   }
+}
+
+__global__ __launch_bounds__(256) void k_tr_split(int level, int last, uint32_t total, TreeSeg* seg, TreeSeg* next,
+                                                  SubSeg* subs, SubSeg* mids, TreeCtl* ctl, const uint32_t* __restrict__ X2,
+                                                  NodeEvent* ev, uint8_t* valid, uint32_t* ecnt,
+                                                  int32_t* pair_depth, int bucket, uint32_t max_seg,
+                                                  uint32_t mid_max) {
+  const uint32_t si = blockIdx.x * blockDim.x + threadIdx.x;
+  if (si >= ctl->nseg[level]) return;
+  tr_split_seg(si, level, last, total, seg, next, subs, mids, ctl, X2, ev, valid, ecnt, pair_depth, bucket, max_seg,
+               mid_max);
+}
+
+// The pass-2 scan (k_tr_scan_counts) and the level's split in one launch: the last workgroup to
+// finish its part of the scan (arrival counter after the tile words, release / acquire at agent
+// scope) splits every segment of the level. Used when the level has few segments (the host
+// bound n_pairs << level), where a split launch of its own cost a kernel boundary for a handful
+// of threads.
+__device__ __forceinline__ bool tr_last_arrival(uint32_t* cnt, uint32_t n_expected) {
+  __shared__ uint32_t s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = atomicAdd(cnt, 1u);
+    const bool last = old + 1 == n_expected;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last ? 1u : 0u;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+__global__ __launch_bounds__(kLbThreads) void k_tr_scan2_split(uint32_t n, const uint32_t* __restrict__ c,
+                                                              uint32_t* __restrict__ X, uint64_t* st, int level,
+                                                              int last, uint32_t total, TreeSeg* seg, TreeSeg* next,
+                                                              SubSeg* subs, SubSeg* mids, TreeCtl* ctl, NodeEvent* ev,
+                                                              uint8_t* valid, uint32_t* ecnt, int32_t* pair_depth,
+                                                              int bucket, uint32_t max_seg, uint32_t mid_max) {
+  lookback_scan(n, [&](uint32_t i) -> uint32_t { return c[i]; }, X, st, ctl);
+  uint32_t* arrive = reinterpret_cast<uint32_t*>(st + lb_words(n));  // zeroed with the tile words
+  if (!tr_last_arrival(arrive, gridDim.x)) return;
+  const uint32_t ns = ctl->nseg[level];
+  for (uint32_t si = threadIdx.x; si < ns; si += blockDim.x)
+    tr_split_seg(si, level, last, total, seg, next, subs, mids, ctl, X, ev, valid, ecnt, pair_depth, bucket, max_seg,
+                 mid_max);
 }
 
 // pass 2 move; next level's segment map; points landing in leaves are final (bucket order)
@@ -1614,10 +1661,17 @@ void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, Pai
 }
 
 // look-back words of every scan of a build: two per global level and the node count scan
-size_t lb_stride_words(uint32_t total) { return lb_words(total + 2); }
+size_t lb_stride_words(uint32_t total) { return lb_words(total + 2) + 1; }  // + the fused split's arrival word
 bool tree_lookback_enabled() {  // AICP_TREE_LB=0: rocprim scans and a flag kernel (A/B)
   static const bool on = [] {
     const char* e = std::getenv("AICP_TREE_LB");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+bool tree_split_fuse_enabled() {  // AICP_TREE_SPLIT_FUSE=0: the split as its own launch (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_TREE_SPLIT_FUSE");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -1684,14 +1738,22 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   const bool bs = tree_bsearch_enabled();
   if (!bs) k_tr_pos<<<gp, 256, 0, s>>>(total, 1, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR);
   k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR, w.W[1], w.flag, bs ? 1 : 0);
-  if (lb) {
-    k_tr_scan_counts<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, w.ctl);
+  // few segments at this level (at most n_pairs << level): the split runs in the scan's last workgroup
+  const bool fuse_split = lb && tree_split_fuse_enabled() && ((size_t)w.n_pairs << std::min(level, 20)) <= 1024;
+  if (fuse_split) {
+    k_tr_scan2_split<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, level, last ? 1 : 0, total, seg, next,
+                                                w.subs, w.mids, w.ctl, w.ev, w.valid, w.ecnt, w.pair_depth, bucket,
+                                                (uint32_t)w.max_seg, w.mid_max);
   } else {
-    const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X2, (size_t)total + 1);
-    if (e != hipSuccess) return e;
+    if (lb) {
+      k_tr_scan_counts<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, w.ctl);
+    } else {
+      const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X2, (size_t)total + 1);
+      if (e != hipSuccess) return e;
+    }
+    k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.mids, w.ctl, w.X2, w.ev, w.valid,
+                                  w.ecnt, w.pair_depth, bucket, (uint32_t)w.max_seg, w.mid_max);
   }
-  k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.mids, w.ctl, w.X2, w.ev, w.valid, w.ecnt, w.pair_depth,
-                                bucket, (uint32_t)w.max_seg, w.mid_max);
   if (!bs) k_tr_pos<<<gp, 256, 0, s>>>(total, 2, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR);
   k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR, w.W[0], w.segof[b], bpts,
                                 bs ? 1 : 0);

@@ -1315,6 +1315,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     HIPC(hipEventRecord(S->ev_end, S->s_icp));
     rc = seq_sync(ctx, S);
     if (rc) return rc;
+    if (std::getenv("AICP_ITER_PROF_DUMP")) iter_prof_dump();
     if (prof && plan.size() > 2) {  // device phase times, averaged over the windows after the first
       double a[5] = {0, 0, 0, 0, 0};
       const size_t m = plan.size() - 1;
