@@ -181,6 +181,8 @@ void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const Pair
 void launch_normals_to_matcher(hipStream_t s, int n_refs, uint32_t total, const PairDesc* rd, const float4* bpts,
                                const float4* bpts_raw, const float4* nrm_raw, uint32_t* inv, float4* bnrm);
 void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst);
+void launch_pairs_degenerate_part(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst,
+                                  int what);
 
 // ---- overlap ------------------------------------------------------------------------------
 // Clouds: the reference side runs over overlap groups (one per distinct reference cloud and

@@ -2993,22 +2993,16 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
 // engine, which pays only while the per-lane launch leaves the chip short of waves (the C2
 // stream's single 120k-point reference: 377 -> 245 us); on C5's 61 M queries it ran 91.7 ms per
 // launch against the per-lane engine's throughput (C5 3962 -> 3097 clouds/s, r03c).
-static int knn_group_lanes() {  // AICP_KNN_GROUP=4|8: lanes per query of k_knn_oct (default 8)
-  static const int g = [] {
-    const char* e = std::getenv("AICP_KNN_GROUP");
-    return (e && e[0] == '4') ? 4 : 8;
-  }();
-  return g;
+static int knn_group_lanes() {  // AICP_KNN_GROUP=4|8: lanes per query of k_knn_oct (default 8), read per launch
+  const char* e = std::getenv("AICP_KNN_GROUP");
+  return (e && e[0] == '4') ? 4 : 8;
 }
-static bool knn_oct_enabled(uint32_t n_queries) {
-  static const uint64_t lim = [] {
-    const char* e = std::getenv("AICP_KNN_OCT");
-    if (e && e[0] == '0') return (uint64_t)0;
-    if (e && e[0] == '1') return ~(uint64_t)0;
-    const char* m = std::getenv("AICP_KNN_OCT_MAX");
-    return m ? (uint64_t)std::strtoull(m, nullptr, 10) : (uint64_t)300000;
-  }();
-  return n_queries <= lim;
+static bool knn_oct_enabled(uint32_t n_queries) {  // (the environment is read per launch: tests switch engines)
+  const char* e = std::getenv("AICP_KNN_OCT");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  const char* m = std::getenv("AICP_KNN_OCT_MAX");
+  return n_queries <= (m ? (uint64_t)std::strtoull(m, nullptr, 10) : (uint64_t)300000);
 }
 
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,

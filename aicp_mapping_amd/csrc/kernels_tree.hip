@@ -1507,14 +1507,16 @@ __global__ __launch_bounds__(256) void k_scatter_normals(int n_refs, uint32_t to
   bnrm[inv[ro + (uint32_t)__float_as_int(bpts_raw[j].w)]] = nrm_raw[j];
 }
 
+// what: 1 = the reference's degenerate-normal count (needs SurfaceNormal), 2 = the initial
+// transform's rigidity check (needs only the pair frames; before the first active list)
 __global__ void k_pairs_degenerate(int n_pairs, const PairDesc* __restrict__ pd, PairState* st,
-                                   const PairState* __restrict__ rst) {
+                                   const PairState* __restrict__ rst, int what) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
-  st[p].degenerate = rst[pd[p].ref_id].degenerate;
+  if (what & 1) st[p].degenerate = rst[pd[p].ref_id].degenerate;
   // ICP::compute applies T_refMean_dataIn to the reading first: RigidTransformation's
   // checkParameters throws TransformationError for a non-rigid initial transform
-  if (!rigid_ok(pd[p].Tinit)) {
+  if ((what & 2) && !rigid_ok(pd[p].Tinit)) {
     st[p].status = 5;
     st[p].active = 0;
   }
@@ -1657,7 +1659,11 @@ void launch_normals_to_matcher(hipStream_t s, int n_refs, uint32_t total, const 
   k_scatter_normals<<<grid_of(total), 256, 0, s>>>(n_refs, total, rd, bpts_raw, nrm_raw, inv, bnrm);
 }
 void launch_pairs_degenerate(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst) {
-  k_pairs_degenerate<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, rst);
+  k_pairs_degenerate<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, rst, 3);
+}
+void launch_pairs_degenerate_part(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* rst,
+                                  int what) {
+  k_pairs_degenerate<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, rst, what);
 }
 
 // look-back words of every scan of a build: two per global level and the node count scan

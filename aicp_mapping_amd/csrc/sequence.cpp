@@ -191,6 +191,14 @@ bool seq_read_early() {  // AICP_SEQ_READ_LATE=1: the reading side after the nex
   return on;
 }
 
+bool seq_early_nn() {  // AICP_SEQ_EARLY_NN=0: the window's loop waits for the normals before its first NN
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_SEQ_EARLY_NN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches
   const char* e = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
   return e && e[0] == '1';
@@ -828,8 +836,10 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   }
   HIPC(hipStreamWaitEvent(si, sl.ev_s3, 0));
   launch_pairs_from_refs(si, (int)np, dDesc, dRdesc);
-  HIPC(hipStreamWaitEvent(si, sl.ev_s2, 0));
-  launch_pairs_degenerate(si, (int)np, dDesc, dState, dRst);
+  if (!seq_early_nn()) HIPC(hipStreamWaitEvent(si, sl.ev_s2, 0));  // (A/B: the loop after the normals)
+  launch_pairs_degenerate_part(si, (int)np, dDesc, dState, dRst, 2);
+  // the normals (ev_s2) are waited for by the first iteration's reduce (loop_iteration): the
+  // first NN and select need only the matcher tree, which is ready ~0.2 ms earlier on C2
   launch_prepare_read(si, R.m_read, dDesc, readS, sl.read_c.as<float4>());
   HIPC(hipMemsetAsync(sl.sel_hist.p, 0, np * kHistBins * 4, si));
   HIPC(hipMemsetAsync(sl.sel_cnt.p, 0, np * 4, si));
@@ -862,12 +872,9 @@ int lookahead() {
   }();
   return v;
 }
-bool seq_split() {
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_SEQ_SPLIT");
-    return e && e[0] == '1';
-  }();
-  return on;
+bool seq_split() {  // read per sequence run (tests compare both schedules)
+  const char* e = std::getenv("AICP_SEQ_SPLIT");
+  return e && e[0] == '1';
 }
 
 struct IcpLoop {
@@ -990,6 +997,10 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   y.host_n = hn_next;
   launch_icp_select_f(st, q.msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(), sl.cand.as<uint32_t>(),
                       sl.sel_cnt.as<uint32_t>(), y);
+  if (it == 0) {  // the reduce gathers the reference normals (stream r2, scattered into matcher order)
+    HIPC(hipStreamWaitEvent(st, sl.ev_s2, 0));
+    launch_pairs_degenerate_part(st, (int)q.np, gd, gs, dRst, 1);
+  }
   launch_icp_reduce_f(st, q.mred, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
                       sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>(), ip, y);
   HIPC(hipGetLastError());
@@ -1054,7 +1065,20 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     // the third high-priority one; uploads and the reading side share one low-priority stream.
     HIPC(hipStreamCreateWithPriority(&S->s_rd, hipStreamNonBlocking, lo));
     HIPC(hipStreamCreateWithPriority(&S->s_icp, hipStreamNonBlocking, hi));
-    HIPC(hipStreamCreateWithPriority(&S->s_icp2, hipStreamNonBlocking, lo));  // the non-critical ICP loops
+    // the non-critical ICP loops (AICP_SEQ_SPLIT=1); AICP_SEQ_ICP2_CUS=k in 1..7 restricts that
+    // stream to k of every 8 CUs (hipExtStreamCreateWithCUMask), leaving the rest to the critical path
+    const char* cm = std::getenv("AICP_SEQ_ICP2_CUS");
+    const int k8 = cm ? std::atoi(cm) : 8;
+    if (k8 >= 1 && k8 <= 7) {
+      int ncu = 0;
+      HIPC(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int c = 0; c < ncu; ++c)
+        if (c % 8 < k8) mask[c / 32] |= 1u << (c % 32);
+      HIPC(hipExtStreamCreateWithCUMask(&S->s_icp2, (uint32_t)mask.size(), mask.data()));
+    } else {
+      HIPC(hipStreamCreateWithPriority(&S->s_icp2, hipStreamNonBlocking, lo));
+    }
     S->s_up = S->s_rd;
     S->s_r2 = ctx->stream2;
     S->s_r3 = ctx->stream3;

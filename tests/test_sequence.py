@@ -161,3 +161,23 @@ def test_sequence_c2_full_size(ctx, oracle, L):
         rr, tt = sy.rot_err(ref[k]["T"], T[i])
         assert rr < 1e-6 and tt < 1e-5, (i, rr, tt)
         assert out[i]["icp"]["iterations"] == ref[k]["stats"].iterations
+
+
+def test_sequence_split_loops_identical(ctx, L, monkeypatch):
+    """AICP_SEQ_SPLIT=1 runs each window's last reading (the next reference's source) in a loop
+    of its own on stream icp and the other readings on stream icp2. Every pair's
+    arithmetic is per pair, so the two schedules give bit-identical corrections and statistics,
+    also across a dropped reading (re-plan)."""
+    st = sy.make_stream(n_readings=12, n_points=5000, seed=8, half=18.0, jumps={2: (0.6, 0, 0), 6: (0, -0.6, 0)})
+    prm = L.default_sequence_params(max_correction_magnitude=0.4)  # readings 2 and 6 drop: two re-plans
+    monkeypatch.delenv("AICP_SEQ_SPLIT", raising=False)
+    T0, out0, done0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    monkeypatch.setenv("AICP_SEQ_SPLIT", "1")
+    T1, out1, done1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    assert (rc0, done0) == (rc1, done1) == (0, 12)
+    assert sum(1 - o["accepted"] for o in out1) == 2
+    assert np.array_equal(T0, T1)
+    for a, b in zip(out0, out1):
+        assert a["accepted"] == b["accepted"] and a["reference"] == b["reference"]
+        assert a["icp"]["iterations"] == b["icp"]["iterations"]
+        assert a["icp"]["nn_points_touched"] == b["icp"]["nn_points_touched"]
