@@ -226,7 +226,8 @@ struct SeqSlot {
 };
 
 struct SeqState {
-  hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr, s_icp2 = nullptr;
+  hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr, s_icp2 = nullptr,
+              s_r3_own = nullptr;
   SeqSlot slot[kSlots];
   DevBuf desc, state, outT;
   PinBuf pin_state, pin_out, pin_ctl;
@@ -265,7 +266,7 @@ void seq_state_free(SeqState* S) {
   for (hipEvent_t e : S->tev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {S->ev_begin, S->ev_end, S->ev_icp2})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t q : {S->s_rd, S->s_icp, S->s_icp2})  // (s_up = s_rd; s_r2, s_r3 are the context's)
+  for (hipStream_t q : {S->s_rd, S->s_icp, S->s_icp2, S->s_r3_own})  // (s_up = s_rd; s_r2, s_r3: the context's)
     if (q) (void)hipStreamDestroy(q);
   delete S;
 }
@@ -1082,6 +1083,10 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     S->s_up = S->s_rd;
     S->s_r2 = ctx->stream2;
     S->s_r3 = ctx->stream3;
+    if (const char* e = std::getenv("AICP_SEQ_R3_PRIO")) {  // A/B: the matcher-tree stream at priority lo|hi of its own
+      HIPC(hipStreamCreateWithPriority(&S->s_r3_own, hipStreamNonBlocking, e[0] == 'l' ? lo : hi));
+      S->s_r3 = S->s_r3_own;
+    }
     for (SeqSlot& sl : S->slot) {
       for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done, &sl.ev_crit, &sl.ev_setup})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));

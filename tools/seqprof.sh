@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 for v in "$@"; do
   echo "== $v"
-  env $v AICP_SEQ_PROF=1 timeout -k 10 120 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-batched > gpurun_out/seqprof.json 2> gpurun_out/seqprof.err || { tail -20 gpurun_out/seqprof.err; exit 1; }
+  env $v AICP_SEQ_PROF=1 timeout -k 10 120 python bench.py --steps ${SEQPROF_STEPS:-5} --warmup 2 --no-cpu-baseline --no-batched > gpurun_out/seqprof.json 2> gpurun_out/seqprof.err || { tail -20 gpurun_out/seqprof.err; exit 1; }
   grep 'aicp seq' gpurun_out/seqprof.err | tail -2
   python -c "import json; d=json.load(open('gpurun_out/seqprof.json')); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['mean_iterations'])"
 done
