@@ -199,6 +199,34 @@ bool seq_early_nn() {  // AICP_SEQ_EARLY_NN=0: the window's loop waits for the n
   return on;
 }
 
+bool seq_ovl_low() {  // AICP_SEQ_OVL_LOW=1: the reference's voxel map on the low-priority stream (A/B)
+  const char* e = std::getenv("AICP_SEQ_OVL_LOW");
+  return e && e[0] == '1';
+}
+
+bool seq_match_first() {  // AICP_SEQ_MATCH_FIRST=0: the raw tree is enqueued before the matcher tree
+  const char* e = std::getenv("AICP_SEQ_MATCH_FIRST");
+  return !(e && e[0] == '0');
+}
+
+// The raw tree + SurfaceNormal run as direct launches (AICP_SEQ_RAW_GRAPH=1: replayed from a graph):
+// on the device the ~100 short kernels finished 0.08 ms sooner than the graph's replay (ref ->
+// normals 0.95 -> 0.87 ms on C2), and enqueued after the matcher tree's graph they do not delay
+// it (measured: 2450-2470 against 2400-2440 clouds/s; both direct from two host threads: equal)
+bool seq_raw_graph() {
+  const char* e = std::getenv("AICP_SEQ_RAW_GRAPH");
+  return e && e[0] == '1';
+}
+
+bool seq_match_graph() {  // AICP_SEQ_MATCH_GRAPH=0: the matcher tree as direct launches
+  const char* e = std::getenv("AICP_SEQ_MATCH_GRAPH");
+  return !(e && e[0] == '0');
+}
+bool seq_trees_mt() {  // AICP_SEQ_TREES_MT=1: the two builds enqueued from two host threads
+  const char* e = std::getenv("AICP_SEQ_TREES_MT");
+  return e && e[0] == '1';
+}
+
 bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches
   const char* e = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
   return e && e[0] == '1';
@@ -215,7 +243,8 @@ struct SeqSlot {
   TreeBufs tb[2];
   PinBuf pin_read, pin_par, pin_src;
   hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr,
-            ev_crit = nullptr, ev_setup = nullptr;  // ev_crit: the last reading's correction; ev_setup: ready to iterate
+            ev_crit = nullptr, ev_setup = nullptr,  // ev_crit: the last reading's correction; ev_setup: ready to iterate
+            ev_ovl = nullptr;                       // the reference's voxel map (AICP_SEQ_OVL_LOW)
   // early exit of the ICP loops: active counts written by the update kernels into mapped host
   // memory, kMaxPolls words per loop (two loops per window)
   uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), 2 * kMaxPolls words
@@ -254,7 +283,7 @@ void seq_state_free(SeqState* S) {
     for (auto& t : sl.tb) t.release_all();
     for (GraphCache* g : {&sl.g_raw, &sl.g_match, &sl.g_icp}) g->reset();
     for (PinBuf* b : {&sl.pin_read, &sl.pin_par, &sl.pin_src}) release(*b);
-    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done, sl.ev_crit, sl.ev_setup})
+    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done, sl.ev_crit, sl.ev_setup, sl.ev_ovl})
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : sl.ev_poll)
       if (e) (void)hipEventDestroy(e);
@@ -760,17 +789,21 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     HIPC(hipGetLastError());
     return AICP_OK;
   };
-  if (capturable) {
-    Key k;
-    k << n_ref << plan0 << cfg->knn_normals << dRraw << sl.ref_raw.p << sl.bpts_raw.p << sl.nodes_raw.p
-      << sl.nrm_raw.p << sl.nbids.p << sl.ctrs.p << sl.tb[0].tw;
-    rc = graph_run(ctx, sl.g_raw, s2, k, raw_build);
-    if (rc) return rc;
+  auto raw_enqueue = [&]() -> int {
+    if (capturable && seq_raw_graph()) {
+      Key k;
+      k << n_ref << plan0 << cfg->knn_normals << dRraw << sl.ref_raw.p << sl.bpts_raw.p << sl.nodes_raw.p
+        << sl.nrm_raw.p << sl.nbids.p << sl.ctrs.p << sl.tb[0].tw;
+      const int r = graph_run(ctx, sl.g_raw, s2, k, raw_build);
+      if (r) return r;
+      HIPC(hipMemcpyAsync(ctl_w, sl.tb[0].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
+      return AICP_OK;
+    }
+    const int r = raw_build();
+    if (r || !capturable) return r;
     HIPC(hipMemcpyAsync(ctl_w, sl.tb[0].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
-  } else {
-    rc = raw_build();
-    if (rc) return rc;
-  }
+    return AICP_OK;
+  };
   // ---- r3: centroid + matcher tree + treelets
   auto match_build = [&]() -> int {
     int r = device_trees_begin(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, sl.ref_raw.as<float4>(), 1, bucket, sl.bpts,
@@ -786,20 +819,38 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     HIPC(hipGetLastError());
     return AICP_OK;
   };
-  if (capturable) {
-    Key k;
-    k << n_ref << plan1 << bucket << use_tl << tl_cap << dRdesc << sl.ref_raw.p << sl.bpts.p << sl.nodes.p
-      << sl.tb[1].tw;
-    if (use_tl) k << sl.tl.p << sl.ptl.p << sl.tl_flag.p << sl.tl_rank.p << sl.tl_temp.p << tlb;
-    rc = graph_run(ctx, sl.g_match, s3, k, match_build);
+  auto match_enqueue = [&]() -> int {
+    int r;
+    if (capturable && seq_match_graph()) {
+      Key k;
+      k << n_ref << plan1 << bucket << use_tl << tl_cap << dRdesc << sl.ref_raw.p << sl.bpts.p << sl.nodes.p
+        << sl.tb[1].tw;
+      if (use_tl) k << sl.tl.p << sl.ptl.p << sl.tl_flag.p << sl.tl_rank.p << sl.tl_temp.p << tlb;
+      r = graph_run(ctx, sl.g_match, s3, k, match_build);
+    } else {
+      r = match_build();
+    }
+    if (r) return r;
+    if (capturable || use_tl)
+      HIPC(hipMemcpyAsync(ctl_w + 1, sl.tb[1].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
+    HIPC(hipEventRecord(sl.ev_s3, s3));
+    if (R.tev) HIPC(hipEventRecord(R.tev[1], s3));
+    return AICP_OK;
+  };
+  // the two graphs' host launches take tens of us each: the matcher tree, which the window's
+  // loop starts on, can go first (AICP_SEQ_MATCH_FIRST)
+  if (seq_trees_mt()) {  // both builds enqueued at once from two host threads (streams r2, r3)
+    int rr[2] = {AICP_OK, AICP_OK};
+    S->pool.run(2, [&](size_t t) { rr[t] = t == 0 ? match_enqueue() : raw_enqueue(); });
+    rc = rr[0] ? rr[0] : rr[1];
+  } else if (seq_match_first()) {
+    rc = match_enqueue();
+    if (!rc) rc = raw_enqueue();
   } else {
-    rc = match_build();
+    rc = raw_enqueue();
+    if (!rc) rc = match_enqueue();
   }
   if (rc) return rc;
-  if (capturable || use_tl)
-    HIPC(hipMemcpyAsync(ctl_w + 1, sl.tb[1].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
-  HIPC(hipEventRecord(sl.ev_s3, s3));
-  if (R.tev) HIPC(hipEventRecord(R.tev[1], s3));
 
   HIPC(hipStreamWaitEvent(s2, sl.ev_s3, 0));
   launch_normals_to_matcher(s2, 1, n_ref, dRdesc, sl.bpts.as<float4>(), sl.bpts_raw.as<float4>(),
@@ -821,14 +872,21 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   (void)cfg;
   const float4* readS = R.readS;
   hipStream_t si = S->s_icp;
+  // the reference's voxel map: on stream icp, or (AICP_SEQ_OVL_LOW=1) on the low-priority reading
+  // stream, so that its marking yields the CUs to the kd-tree builds
+  hipStream_t so = seq_ovl_low() ? S->s_rd : si;
   if (doOvl) {
-    HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
-    launch_ovl_init(si, 1, dG, dGst, res, 1);
-    launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
-    launch_ovl_size(si, 1, dGst, dOvl, dCap);
-    launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
-    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
-    launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
+    HIPC(hipStreamWaitEvent(so, sl.ev_ref, 0));
+    launch_ovl_init(so, 1, dG, dGst, res, 1);
+    launch_ovl_bbox(so, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
+    launch_ovl_size(so, 1, dGst, dOvl, dCap);
+    launch_ovl_clear(so, 1, dOvl, bmp, R.cap[0]);
+    launch_ovl_mark(so, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
+    launch_ovl_popcount(so, 1, dOvl, dGst, 0, bmp);
+    if (so != si) {
+      HIPC(hipEventRecord(sl.ev_ovl, so));
+      HIPC(hipStreamWaitEvent(si, sl.ev_ovl, 0));
+    }
   }
   HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));
   if (doOvl) {
@@ -1088,7 +1146,8 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
       S->s_r3 = S->s_r3_own;
     }
     for (SeqSlot& sl : S->slot) {
-      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done, &sl.ev_crit, &sl.ev_setup})
+      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done, &sl.ev_crit, &sl.ev_setup,
+                            &sl.ev_ovl})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
       for (hipEvent_t& e : sl.ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       HIPC(hipHostMalloc((void**)&sl.poll_host, 2 * kMaxPolls * 4, hipHostMallocMapped));
