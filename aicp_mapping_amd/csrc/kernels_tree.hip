@@ -853,40 +853,99 @@ __global__ __launch_bounds__(kLbThreads) void k_tr_scan2_split(uint32_t n, const
                  mid_max);
 }
 
-// pass 2 move; next level's segment map; points landing in leaves are final (bucket order)
+// The next level's segment boxes along their split dimensions (what k_tr_minmax computes at the
+// start of a level), folded into the move that assigns the points to those segments: each wave
+// reduces per next-level segment (ballot over the lanes with the same key), the workgroup merges
+// its few keys in LDS, and one atomic per key and workgroup goes to the segment.
+constexpr int kMmKeys = 8;
+__device__ __forceinline__ void move2_minmax(bool has, int key, float v, TreeSeg* next) {
+  __shared__ int mk[kMmKeys];
+  __shared__ uint32_t mlo[kMmKeys], mhi[kMmKeys];
+  const int t = threadIdx.x, lane = t & 63;
+  if (t < kMmKeys) {
+    mk[t] = -1;
+    mlo[t] = 0xffffffffu;
+    mhi[t] = 0u;
+  }
+  __syncthreads();
+  uint64_t act = __ballot(has);
+  while (act) {
+    const int leader = __ffsll((long long)act) - 1;
+    const int k = __shfl(key, leader, 64);
+    const bool m = has && key == k;
+    const uint64_t mm = __ballot(m);
+    uint32_t e = m ? ord_enc(v) : 0xffffffffu, f = m ? ord_enc(v) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      e = min(e, (uint32_t)__shfl_xor((int)e, o, 64));
+      f = max(f, (uint32_t)__shfl_xor((int)f, o, 64));
+    }
+    if (lane == 0) {
+      int slot = -1;
+      for (int q = 0; q < kMmKeys && slot < 0; ++q) {
+        const int old = atomicCAS(&mk[q], -1, k);
+        if (old == -1 || old == k) slot = q;
+      }
+      if (slot >= 0) {
+        atomicMin(&mlo[slot], e);
+        atomicMax(&mhi[slot], f);
+      } else {  // more keys than slots (not expected: a workgroup spans at most two parents)
+        atomicMin(&next[k].lo, e);
+        atomicMax(&next[k].hi, f);
+      }
+    }
+    act &= ~mm;
+  }
+  __syncthreads();
+  if (t < kMmKeys && mk[t] >= 0) {
+    atomicMin(&next[mk[t]].lo, mlo[t]);
+    atomicMax(&next[mk[t]].hi, mhi[t]);
+  }
+}
+
+// pass 2 move; next level's segment map; points landing in leaves are final (bucket order);
+// next != nullptr: also the next level's segment boxes (move2_minmax)
 __global__ __launch_bounds__(256) void k_tr_move2(uint32_t total, const int32_t* __restrict__ segof,
                                                   const float4* __restrict__ W1, const TreeSeg* __restrict__ seg,
                                                   const uint32_t* __restrict__ X2, const uint32_t* __restrict__ posL,
                                                   const uint32_t* __restrict__ posR, float4* __restrict__ W2,
                                                   int32_t* __restrict__ segof_next, float4* __restrict__ bpts,
-                                                  int bsearch) {
+                                                  int bsearch, TreeSeg* next) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int s = segof[i];
+  const int s = i < total ? segof[i] : -1;
+  bool has = false;  // the point lands in a next-level segment (key, coordinate mv)
+  int key = -1;
+  float mv = 0.f;
   if (s < 0) {
-    segof_next[i] = -1;
-    return;
-  }
-  const TreeSeg& g = seg[s];
-  const float4 p = W1[i];
-  const float v = coord(p, g.cd), cut = seg_cut(g);
-  const uint32_t f = g.first, li = i - f;
-  uint32_t p2 = li;
-  if (li >= g.br1) {
-    if (bsearch) {
-      p2 = hoare_partner(li, v == cut, f, g.br1, g.br2, g.count, X2);
-    } else {
-      bool left;
-      const int32_t k = HoareRanks::rank(li, v == cut, f, g.br1, g.br2, g.count, X2, left);
-      if (k >= 0) p2 = left ? posR[f + k] : posL[f + k];
+    if (i < total) segof_next[i] = -1;
+  } else {
+    const TreeSeg& g = seg[s];
+    const float4 p = W1[i];
+    const float v = coord(p, g.cd), cut = seg_cut(g);
+    const uint32_t f = g.first, li = i - f;
+    uint32_t p2 = li;
+    if (li >= g.br1) {
+      if (bsearch) {
+        p2 = hoare_partner(li, v == cut, f, g.br1, g.br2, g.count, X2);
+      } else {
+        bool left;
+        const int32_t k = HoareRanks::rank(li, v == cut, f, g.br1, g.br2, g.count, X2, left);
+        if (k >= 0) p2 = left ? posR[f + k] : posL[f + k];
+      }
+      if (p2 >= g.count) p2 = li;  // unreachable for a consistent scan; keeps stores in range
     }
-    if (p2 >= g.count) p2 = li;  // unreachable for a consistent scan; keeps stores in range
+    const uint32_t q = f + p2;
+    W2[q] = p;
+    const int32_t child = g.child[p2 < g.left ? 0 : 1];
+    segof_next[q] = child >= 0 ? child : -1;
+    if (child == -1) bpts[q] = p;  // leaf: final; -2: the wave subtree builder takes it from W
+    if (next && child >= 0) {
+      has = true;
+      key = child;
+      mv = coord(p, next[child].cd);
+    }
   }
-  const uint32_t q = f + p2;
-  W2[q] = p;
-  const int32_t child = g.child[p2 < g.left ? 0 : 1];
-  segof_next[q] = child >= 0 ? child : -1;
-  if (child == -1) bpts[q] = p;  // leaf: final; -2: the wave subtree builder takes it from W
+  if (next) move2_minmax(has, key, mv, next);  // every thread of the workgroup, once
 }
 
 // ---- wave subtree builder ----------------------------------------------------------------------
@@ -1675,6 +1734,13 @@ bool tree_lookback_enabled() {  // AICP_TREE_LB=0: rocprim scans and a flag kern
   }();
   return on;
 }
+bool tree_mm_fuse_enabled() {  // AICP_TREE_MM_FUSE=0: the next level's boxes by k_tr_minmax (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_TREE_MM_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 bool tree_split_fuse_enabled() {  // AICP_TREE_SPLIT_FUSE=0: the split as its own launch (A/B)
   static const bool on = [] {
     const char* e = std::getenv("AICP_TREE_SPLIT_FUSE");
@@ -1733,7 +1799,8 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   uint64_t* st1 = w.lb + (size_t)(2 * level) * w.lb_stride;
   uint64_t* st2 = st1 + w.lb_stride;
   const bool lb = tree_lookback_enabled();
-  if (level > 0) k_tr_minmax<<<tiles_of(total), 256, 0, s>>>(total, w.segof[a], w.W[0], seg);  // (level 0: roots)
+  // level 0: the roots' boxes (k_tr_center); later levels: the previous level's move2 (move2_minmax)
+  if (level > 0 && !tree_mm_fuse_enabled()) k_tr_minmax<<<tiles_of(total), 256, 0, s>>>(total, w.segof[a], w.W[0], seg);
   if (lb) {
     k_tr_scan1<<<nt1, kLbThreads, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, st1, w.ctl);
   } else {
@@ -1762,7 +1829,7 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   }
   if (!bs) k_tr_pos<<<gp, 256, 0, s>>>(total, 2, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR);
   k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR, w.W[0], w.segof[b], bpts,
-                                bs ? 1 : 0);
+                                bs ? 1 : 0, tree_mm_fuse_enabled() ? next : nullptr);
   return hipGetLastError();
 }
 
