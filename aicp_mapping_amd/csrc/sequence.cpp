@@ -227,6 +227,11 @@ bool seq_trees_mt() {  // AICP_SEQ_TREES_MT=1: the two builds enqueued from two 
   return e && e[0] == '1';
 }
 
+bool seq_upload_late() {  // AICP_SEQ_UPLOAD_LATE=0: the next window's upload before this window's loop
+  const char* e = std::getenv("AICP_SEQ_UPLOAD_LATE");
+  return !(e && e[0] == '0');
+}
+
 bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches
   const char* e = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
   return e && e[0] == '1';
@@ -1343,7 +1348,9 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         if (!r && read_early) r = timed(0, [&] { return read_side(k + 1); });
         return r;
       };
-      rc = try_upload();
+      // (the next window's upload -- host packing of its readings -- goes after this window's first
+      // iterations are enqueued: before them it delayed the loop start on the host by ~0.4 ms)
+      if (!seq_upload_late()) rc = try_upload();
       if (rc) break;
       rc = win_loops(S, runs[k], split && next, loops[k].data(), n_loops[k]);
       if (rc) break;
