@@ -930,11 +930,14 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
         if (!fuse || it == 0) launch_active_list(q.st, q.np, gd, gs, q.al, q.ctr);
         if (G == 2 && icp_serial_nn()) HIPC(hipStreamWaitEvent(q.st, grp[1 - g].nn_done, 0));
         prm.prof_slot = nn_launches;
-        if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches], q.st));
+        const bool ext = timeNN && nn_ext_events();  // events on the NN's own dispatch
+        if (timeNN && !ext) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches], q.st));
         launch_icp_nn(q.st, (int)q.reads, gd, gs, q.al, readc, nodes, ctx->tl_total ? ctx->tl.as<uint4>() : nullptr,
                       parent, bpts, ctx->tl_total ? ctx->ptl.as<uint2>() : nullptr, ctx->match.as<int32_t>(),
-                      ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), q.ctr, prm);
-        if (timeNN) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches + 1], q.st));
+                      ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), q.ctr, prm,
+                      ext ? ctx->nn_ev[2 * nn_launches] : nullptr, ext ? ctx->nn_ev[2 * nn_launches + 1] : nullptr);
+        HIPC(hipGetLastError());
+        if (timeNN && !ext) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches + 1], q.st));
         if (G == 2) HIPC(hipEventRecord(q.nn_done, q.st));
         ++nn_launches;
         if (fuse) {  // select + reduce with the per-pair steps and the next active list inside

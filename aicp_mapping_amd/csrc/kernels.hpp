@@ -68,6 +68,7 @@ struct IcpIterSync {
   float* outT;
 };
 bool icp_fuse_enabled();
+void tree_prof_dump();  // diagnostic builds (AICP_ITER_PROF): k_tr_mid phase times to stderr
 void iter_prof_dump();  // diagnostic builds (AICP_ITER_PROF): per-kernel body / tail times to stderr
 inline size_t icp_sync_words(size_t n_pairs) { return 3 * n_pairs + 2; }
 // sync words laid out for pairs [0, n_pairs): sel1 | sel2 | red | pairs (2: one per group)
@@ -80,7 +81,9 @@ void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairStat
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st,
                    const ActiveList* al, const float4* read_c, const uint4* nodes, const uint4* tl,
                    const int32_t* parent, const float4* bpts, const uint2* ptl, int32_t* match, float* d2,
-                   uint32_t* touched, uint32_t* ctr, const IcpParams& prm);
+                   uint32_t* touched, uint32_t* ctr, const IcpParams& prm, hipEvent_t e0 = nullptr,
+                   hipEvent_t e1 = nullptr);
+bool nn_ext_events();  // timed NN launches carry their events on the dispatch (AICP_NN_EXT_EVENTS)
 // TrimmedDist limit per active pair. m: blocks of kNNBlock * kSelPerThread readings;
 // hist1: n_pairs * kHistBins zeroed words, cand: total_read words, cand_cnt: n_pairs zeroed
 // words (both left zeroed for the next call).
@@ -229,6 +232,8 @@ void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const
 // the window's descriptors, states and corrections into the sequence's arrays (np readings)
 void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState* st, const float* T, PairDesc* gd,
                        PairState* gst, float* gT);
+// a[0, na), b[0, nb), c[0, nc) = 0 in one launch
+void launch_zero_words3(hipStream_t s, uint32_t* a, size_t na, uint32_t* b, size_t nb, uint32_t* c, size_t nc);
 // od[i] (min, dim, bytes) from st[i].ovl_bbox; od[i].off preset; bytes > cap[i]: ovl_err, empty map
 void launch_ovl_size(hipStream_t s, int n, PairState* st, OvlDesc* od, const uint64_t* cap);
 // zero the n maps of od[] (device-side sizes, each at most max_bytes)

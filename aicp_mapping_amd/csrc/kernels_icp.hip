@@ -16,6 +16,7 @@
 //                  Counter + Differential checkers, per-pair active flag
 // SurfaceNormal: k_knn_ids (persistent kNN, eps 0, ids only) + k_normals_from_ids (uniform
 // covariance / eigen work per point).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -3058,21 +3059,51 @@ static int nn_engine() {
   return e;
 }
 
+// Timed launches (e0, e1 given) carry the events on the kernel's own dispatch
+// (hipExtLaunchKernelGGL): the elapsed time is the kernel's execution, as rocprofv3 reports it,
+// and no marker packets sit between the NN and its neighbours (two separate hipEventRecord
+// calls left ~6 us gaps on each side of every timed NN launch). AICP_NN_EXT_EVENTS=0: the
+// separate records (A/B).
+bool nn_ext_events() {
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_NN_EXT_EVENTS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <class E, class Tree>
+static void nn_launch(hipStream_t s, int g, hipEvent_t e0, hipEvent_t e1, const PairDesc* pd, const PairState* st,
+                      const ActiveList* al, const float4* read_c, const Tree* tree, const int32_t* parent,
+                      const float4* bpts, const uint2* ptl, int32_t* match, float* d2, uint32_t* touched,
+                      uint32_t* ctr, const IcpParams& prm) {
+  if (e0)
+    hipExtLaunchKernelGGL(k_icp_nn<E>, dim3(g), dim3(256), 0, s, e0, e1, 0, pd, st, al, read_c, tree, parent, bpts,
+                          ptl, match, d2, touched, ctr, prm);
+  else
+    k_icp_nn<E><<<g, 256, 0, s>>>(pd, st, al, read_c, tree, parent, bpts, ptl, match, d2, touched, ctr, prm);
+}
+
 void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const PairState* st, const ActiveList* al,
                    const float4* read_c, const uint4* nodes, const uint4* tl, const int32_t* parent,
                    const float4* bpts, const uint2* ptl, int32_t* match, float* d2, uint32_t* touched,
-                   uint32_t* ctr, const IcpParams& prm) {
+                   uint32_t* ctr, const IcpParams& prm, hipEvent_t e0, hipEvent_t e1) {
   const int g = persistent_grid(grid_items, AICP_NN_WAVES);
-  if (g == 0) return;  // a pair group without readings
+  if (g == 0) {  // a pair group without readings (the timing events still complete)
+    if (e0) (void)hipEventRecord(e0, s);
+    if (e1) (void)hipEventRecord(e1, s);
+    return;
+  }
   if (nn_engine() == 4 && tl && ptl)
-    k_icp_nn<Trav2S><<<g, 256, 0, s>>>(pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
+    nn_launch<Trav2S>(s, g, e0, e1, pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
   else if (nn_engine() == 3 && tl && ptl)
-    k_icp_nn<Trav2C><<<g, 256, 0, s>>>(pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
+    nn_launch<Trav2C>(s, g, e0, e1, pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
   else if (nn_engine() >= 1)
-    k_icp_nn<Trav<1>><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, nullptr, match, d2, touched, ctr,
-                                        prm);
+    nn_launch<Trav<1>>(s, g, e0, e1, pd, st, al, read_c, nodes, parent, bpts, (const uint2*)nullptr, match, d2,
+                       touched, ctr, prm);
   else
-    k_icp_nn<SM0><<<g, 256, 0, s>>>(pd, st, al, read_c, nodes, parent, bpts, nullptr, match, d2, touched, ctr, prm);
+    nn_launch<SM0>(s, g, e0, e1, pd, st, al, read_c, nodes, parent, bpts, (const uint2*)nullptr, match, d2, touched,
+                   ctr, prm);
 }
 void iter_prof_dump() {
 #if AICP_ITER_PROF

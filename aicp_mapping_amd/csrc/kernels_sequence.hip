@@ -7,6 +7,8 @@
 // capacity the host bounds from the source cloud's extent (a rigid motion keeps its diameter).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "aicp_common.hpp"
 #include "icp_math.hpp"
 #include "kernels.hpp"
@@ -71,6 +73,25 @@ __global__ __launch_bounds__(256) void k_seq_commit(int np, const uint32_t* __re
   for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) gd[i] = d[i];
   for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) gst[i] = st[i];
   for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) gT[i] = T[i];
+}
+
+// up to three word arrays zeroed by one launch (the loop's histogram, counts and hand-off words:
+// three hipMemsetAsync calls were five fill kernels of ~5 us each on the window's critical stream)
+__global__ __launch_bounds__(256) void k_zero_words3(uint32_t* a, uint32_t na, uint32_t* b, uint32_t nb, uint32_t* c,
+                                                     uint32_t nc) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na + nb + nc; i += stride) {
+    if (i < na) a[i] = 0u;
+    else if (i < na + nb) b[i - na] = 0u;
+    else c[i - na - nb] = 0u;
+  }
+}
+
+void launch_zero_words3(hipStream_t s, uint32_t* a, size_t na, uint32_t* b, size_t nb, uint32_t* c, size_t nc) {
+  const size_t n = na + nb + nc;
+  if (!n) return;
+  const unsigned g = (unsigned)std::min<size_t>(256, (n + 255) / 256);
+  k_zero_words3<<<g, 256, 0, s>>>(a, (uint32_t)na, b, (uint32_t)nb, c, (uint32_t)nc);
 }
 
 void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState* st, const float* T, PairDesc* gd,

@@ -30,6 +30,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "aicp_common.hpp"
@@ -1097,7 +1098,13 @@ __device__ void subtree_build(const SubSeg& g, uint32_t total, float4* pts, PosT
 // waves of a block take the nodes of one level each (a node is still split by one wave with the
 // same Hoare passes, so the swaps and the resulting order are the wave builder's), and a block
 // barrier separates the levels. Far fewer dependent steps per segment than depth-first by one wave.
-constexpr int kSubWaves = 8;
+// waves per block, one node each per level. 16 waves took k_tr_subtree_blk from 73 to 58 us on a
+// C2 reference but cost C5 (1024 pairs, tens of thousands of segments) 13 % of its clouds/s, and
+// the C2 stream's period did not move; 8 stays the default.
+#ifndef AICP_SUBWAVES
+#define AICP_SUBWAVES 8
+#endif
+constexpr int kSubWaves = AICP_SUBWAVES;
 constexpr int kSubLevelCap = 256;  // nodes above bucket per level (<= kSubMax / (bucket + 1))
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -1261,56 +1268,70 @@ __global__ __launch_bounds__(64 * kSubWaves) void k_tr_subtree_blk(uint32_t tota
 constexpr int kMidThreads = 1024;
 constexpr int kMidWaves = kMidThreads / 64;
 constexpr int kMidStack = 32;
+constexpr int kMidOut = 64;  // pieces of <= kSubMax points per mid segment (2 per split node > kSubMax)
 
-template <class T, class Op>
-__device__ __forceinline__ T mid_allreduce(T v, Op op, T* scratch) {
-  v = wave_reduce_dpp(v, op);
-  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
-  __syncthreads();
-  T r = scratch[0];
-#pragma unroll
-  for (int i = 1; i < kMidWaves; ++i) r = op(r, scratch[i]);
-  __syncthreads();
-  return r;
-}
+static_assert(kMidMax < 65536, "k_tr_mid packs two counts of a node into one word");
 
-// one Hoare pass over local [lo_b, end) with boundary br, the whole workgroup
-__device__ void mid_hoare(float4* pts, uint16_t* posA, uint16_t* posB, uint32_t* sA, uint32_t* sB, uint32_t lo_b,
-                          uint32_t br, uint32_t end, int cd, float cut, bool eq) {
+#ifndef AICP_ITER_PROF
+#define AICP_ITER_PROF 0
+#endif
+#if AICP_ITER_PROF
+// diagnostic builds: k_tr_mid's phases per segment (s_memrealtime ticks, 100 MHz): load, nodes,
+// store, node count, segments, and the slowest segment's total
+__device__ unsigned long long g_mid_prof[8];
+#endif
+
+// one Hoare pass over local [lo_b, end) with boundary br, the whole workgroup. A round covers
+// kMidSub chunks of kMidThreads elements with one barrier: the per-wave counts of the round's
+// chunks go to one of two count buffers (alternating rounds, so a round's writes never meet the
+// previous round's reads), and the offsets follow the element order (chunk, then wave, then
+// lane) -- the k-th misplaced element from the left still meets the k-th from the right.
+constexpr int kMidSub = 4;
+__device__ void mid_hoare(float4* pts, uint16_t* posA, uint16_t* posB, uint32_t (*sAB)[2][kMidSub][kMidWaves],
+                          uint32_t lo_b, uint32_t br, uint32_t end, int cd, float cut, bool eq) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   uint32_t ra = 0, rb = 0;
-  for (uint32_t jb = lo_b; jb < end; jb += kMidThreads) {
-    const uint32_t j = jb + t;
-    const bool ok = j < end;
-    bool pr = false;
-    if (ok) {
-      const float v = coord(pts[j], cd);
-      pr = eq ? (v == cut) : (v < cut);
-    }
-    const bool ml = ok && j < br && !pr, mr = ok && j >= br && pr;
-    const uint64_t ma = __ballot(ml), mb = __ballot(mr);
-    if (lane == 0) {
-      sA[wv] = (uint32_t)__popcll(ma);
-      sB[wv] = (uint32_t)__popcll(mb);
-    }
-    __syncthreads();
-    uint32_t oa = ra, ob = rb, ta = 0, tb = 0;
+  int buf = 0;
+  for (uint32_t jb = lo_b; jb < end; jb += kMidThreads * kMidSub, buf ^= 1) {
+    uint64_t ma[kMidSub], mb[kMidSub];
 #pragma unroll
-    for (int w = 0; w < kMidWaves; ++w) {
-      const uint32_t a = sA[w], b = sB[w];
-      if (w < wv) {
-        oa += a;
-        ob += b;
+    for (int u = 0; u < kMidSub; ++u) {
+      const uint32_t j = jb + u * kMidThreads + t;
+      const bool ok = j < end;
+      bool pr = false;
+      if (ok) {
+        const float v = coord(pts[j], cd);
+        pr = eq ? (v == cut) : (v < cut);
       }
-      ta += a;
-      tb += b;
+      ma[u] = __ballot(ok && j < br && !pr);
+      mb[u] = __ballot(ok && j >= br && pr);
+      if (lane == 0) {
+        sAB[buf][0][u][wv] = (uint32_t)__popcll(ma[u]);
+        sAB[buf][1][u][wv] = (uint32_t)__popcll(mb[u]);
+      }
     }
-    if (ml) posA[oa + popc_lt(ma)] = (uint16_t)j;
-    if (mr) posB[ob + popc_lt(mb)] = (uint16_t)j;
-    ra += ta;
-    rb += tb;
     __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kMidSub; ++u) {
+      uint32_t oa = ra, ob = rb, ta = 0, tb = 0;
+#pragma unroll
+      for (int w = 0; w < kMidWaves; ++w) {
+        const uint32_t x = sAB[buf][0][u][w], y = sAB[buf][1][u][w];
+        if (w < wv) {
+          oa += x;
+          ob += y;
+        }
+        ta += x;
+        tb += y;
+      }
+      const uint32_t j = jb + u * kMidThreads + t;
+      if ((ma[u] >> lane) & 1) posA[oa + popc_lt(ma[u])] = (uint16_t)j;
+      if ((mb[u] >> lane) & 1) posB[ob + popc_lt(mb[u])] = (uint16_t)j;
+      ra += ta;
+      rb += tb;
+    }
   }
+  __syncthreads();  // every position written
   for (uint32_t k = t; k < ra; k += kMidThreads) {
     const uint32_t a = posA[k], b = posB[rb - 1 - k];
     const float4 x = pts[a];
@@ -1326,11 +1347,12 @@ __global__ __launch_bounds__(kMidThreads) void k_tr_mid(uint32_t total, TreeCtl*
                                                         int32_t* pair_depth, int bucket, uint32_t max_seg) {
   __shared__ float4 pts[kMidMax];
   __shared__ uint16_t posA[kMidMax / 2], posB[kMidMax / 2];
-  __shared__ uint32_t sA[kMidWaves], sB[kMidWaves];
-  __shared__ float sF[kMidWaves];
+  __shared__ uint32_t sAB[2][2][kMidSub][kMidWaves];
+  __shared__ float sMn[kMidWaves], sMx[kMidWaves];
   __shared__ uint32_t sU[kMidWaves];
   __shared__ SubNode stk[kMidStack];
-  __shared__ int sp_s;
+  __shared__ SubSeg outq[kMidOut];  // the segment's pieces for the subtree builders, written at its end
+  __shared__ int sp_s, nout_s;
   __shared__ int32_t maxd_s;
   const int t = threadIdx.x;
   const uint32_t n_mid = ctl->n_mid;
@@ -1338,6 +1360,11 @@ __global__ __launch_bounds__(kMidThreads) void k_tr_mid(uint32_t total, TreeCtl*
     __syncthreads();  // the previous segment's last LDS reads precede this one's loads
     const SubSeg g = mids[mi];
     const uint32_t gf = g.f;
+#if AICP_ITER_PROF
+    const unsigned long long mp0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long mp1 = 0, mp2 = 0;
+    unsigned int mp_nodes = 0;
+#endif
     for (uint32_t j = t; j < g.c; j += kMidThreads) pts[j] = W[gf + j];
     if (t == 0) {
       SubNode& r = stk[0];
@@ -1351,12 +1378,19 @@ __global__ __launch_bounds__(kMidThreads) void k_tr_mid(uint32_t total, TreeCtl*
       r.pf = g.parent_f;
       r.pdepth = g.parent_depth;
       sp_s = 1;
+      nout_s = 0;
       maxd_s = g.depth;
     }
     __syncthreads();
+#if AICP_ITER_PROF
+    mp1 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (;;) {
       const int sp = sp_s;
       if (sp == 0) break;
+#if AICP_ITER_PROF
+      ++mp_nodes;
+#endif
       const SubNode nd = stk[sp - 1];  // count > kSubMax: split here
       __syncthreads();
       int cd;
@@ -1369,20 +1403,37 @@ __global__ __launch_bounds__(kMidThreads) void k_tr_mid(uint32_t total, TreeCtl*
         mn = fminf(mn, v);
         mx = fmaxf(mx, v);
       }
-      const float lo = mid_allreduce(mn, [](float a, float b) { return fminf(a, b); }, sF);
-      const float hi = mid_allreduce(mx, [](float a, float b) { return fmaxf(a, b); }, sF);
+      // min and max in one barrier, then the two counts packed in one word (count <= kMidMax <
+      // 2^16) in one more; sMn / sMx / sU are written again only after this node's later barriers
+      mn = wave_min(mn);
+      mx = wave_max(mx);
+      if ((t & 63) == 0) {
+        sMn[t >> 6] = mn;
+        sMx[t >> 6] = mx;
+      }
+      __syncthreads();
+      float lo = sMn[0], hi = sMx[0];
+#pragma unroll
+      for (int i = 1; i < kMidWaves; ++i) {
+        lo = fminf(lo, sMn[i]);
+        hi = fmaxf(hi, sMx[i]);
+      }
       const float cut = ideal < lo ? lo : (ideal > hi ? hi : ideal);
-      uint32_t nl = 0, ne = 0;
+      uint32_t nle = 0;
       for (uint32_t j = a0 + t; j < end; j += kMidThreads) {
         const float v = coord(pts[j], cd);
-        nl += v < cut ? 1u : 0u;
-        ne += v == cut ? 1u : 0u;
+        nle += v < cut ? 1u : (v == cut ? 0x10000u : 0u);
       }
-      nl = mid_allreduce(nl, [](uint32_t a, uint32_t b) { return a + b; }, sU);
-      ne = mid_allreduce(ne, [](uint32_t a, uint32_t b) { return a + b; }, sU);
+      nle = wave_sum_u(nle);
+      if ((t & 63) == 0) sU[t >> 6] = nle;
+      __syncthreads();
+      nle = 0;
+#pragma unroll
+      for (int i = 0; i < kMidWaves; ++i) nle += sU[i];
+      const uint32_t nl = nle & 0xffffu, ne = nle >> 16;
       const uint32_t br1 = nl, br2 = nl + ne;
-      mid_hoare(pts, posA, posB, sA, sB, a0, a0 + br1, end, cd, cut, false);
-      if (ne) mid_hoare(pts, posA, posB, sA, sB, a0 + br1, a0 + br2, end, cd, cut, true);
+      mid_hoare(pts, posA, posB, sAB, a0, a0 + br1, end, cd, cut, false);
+      if (ne) mid_hoare(pts, posA, posB, sAB, a0 + br1, a0 + br2, end, cd, cut, true);
       uint32_t left;
       if (ideal < lo) left = 1;
       else if (ideal > hi) left = count - 1;
@@ -1417,12 +1468,13 @@ __global__ __launch_bounds__(kMidThreads) void k_tr_mid(uint32_t total, TreeCtl*
           if (c.lc <= (uint32_t)bucket) {
             emit_event(ev, valid, ecnt, total, leaf_event(gf + c.lf, c.lc, c.depth, g.pair, c.pf, c.pdepth));
           } else if (c.lc <= (uint32_t)kSubMax) {
-            const uint32_t ni = atomicAdd(&ctl->n_small, 1u);
-            if (ni >= max_seg) {
-              atomicOr(&ctl->error, 4);
+            // queued in LDS: one slot reservation per segment at its end instead of a returning
+            // device atomic per piece on the workgroup's serial path
+            if (nout_s >= kMidOut) {
+              atomicOr(&ctl->error, 8);
               continue;
             }
-            SubSeg& o = subs[ni];
+            SubSeg& o = outq[nout_s++];
             o.f = gf + c.lf;
             o.c = c.lc;
             o.pair = g.pair;
@@ -1445,12 +1497,40 @@ __global__ __launch_bounds__(kMidThreads) void k_tr_mid(uint32_t total, TreeCtl*
     }
     // points back: W for the subtree builders, bpts for the leaves emitted here (the subtree
     // builders overwrite their ranges of bpts)
+#if AICP_ITER_PROF
+    mp2 = __builtin_amdgcn_s_memrealtime();
+#endif
+    {  // the queued pieces: one reservation, then a copy by the first nout threads
+      __shared__ uint32_t base_s;
+      const int nout = nout_s;
+      if (t == 0) base_s = nout ? atomicAdd(&ctl->n_small, (uint32_t)nout) : 0u;
+      __syncthreads();
+      const uint32_t base = base_s;
+      if (t < nout) {
+        if (base + (uint32_t)t < max_seg) subs[base + t] = outq[t];
+        else atomicOr(&ctl->error, 4);
+      }
+    }
     for (uint32_t j = t; j < g.c; j += kMidThreads) {
       const float4 p = pts[j];
       W[gf + j] = p;
       bpts[gf + j] = p;
     }
     if (t == 0 && pair_depth[g.pair] < maxd_s) atomicMax(&pair_depth[g.pair], maxd_s);
+#if AICP_ITER_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const unsigned long long mp3 = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(&g_mid_prof[0], mp1 - mp0);
+      atomicAdd(&g_mid_prof[1], mp2 - mp1);
+      atomicAdd(&g_mid_prof[2], mp3 - mp2);
+      atomicAdd(&g_mid_prof[3], (unsigned long long)mp_nodes);
+      atomicAdd(&g_mid_prof[4], 1ull);
+      atomicMax(&g_mid_prof[5], mp3 - mp0);
+      atomicMax(&g_mid_prof[6], (unsigned long long)mp_nodes);
+    }
+#endif
   }
 }
 
@@ -1741,12 +1821,15 @@ bool tree_mm_fuse_enabled() {  // AICP_TREE_MM_FUSE=0: the next level's boxes by
   }();
   return on;
 }
-bool tree_split_fuse_enabled() {  // AICP_TREE_SPLIT_FUSE=0: the split as its own launch (A/B)
-  static const bool on = [] {
+// the most segments a level may have for its split to run in the scan's last workgroup
+// (AICP_TREE_SPLIT_FUSE=N). Default 0, the split as its own launch: the fused kernel measured
+// 1.3 ms slower per C4 step already at N = 64 and no faster on C2.
+size_t tree_split_fuse_max() {
+  static const size_t v = [] {
     const char* e = std::getenv("AICP_TREE_SPLIT_FUSE");
-    return !(e && e[0] == '0');
+    return e ? (size_t)std::strtoul(e, nullptr, 10) : (size_t)0;
   }();
-  return on;
+  return v;
 }
 bool tree_bsearch_enabled() {  // AICP_TREE_BSEARCH=0: partner positions by k_tr_pos (A/B)
   static const bool on = [] {
@@ -1812,7 +1895,7 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   if (!bs) k_tr_pos<<<gp, 256, 0, s>>>(total, 1, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR);
   k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR, w.W[1], w.flag, bs ? 1 : 0);
   // few segments at this level (at most n_pairs << level): the split runs in the scan's last workgroup
-  const bool fuse_split = lb && tree_split_fuse_enabled() && ((size_t)w.n_pairs << std::min(level, 20)) <= 1024;
+  const bool fuse_split = lb && ((size_t)w.n_pairs << std::min(level, 20)) <= tree_split_fuse_max();
   if (fuse_split) {
     k_tr_scan2_split<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, level, last ? 1 : 0, total, seg, next,
                                                 w.subs, w.mids, w.ctl, w.ev, w.valid, w.ecnt, w.pair_depth, bucket,
@@ -1866,6 +1949,18 @@ hipError_t launch_tree_mid(hipStream_t s, uint32_t total, const TreeWork& w, flo
   k_tr_mid<<<g, kMidThreads, 0, s>>>(total, w.ctl, w.mids, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt, w.pair_depth,
                                      bucket, (uint32_t)w.max_seg);
   return hipGetLastError();
+}
+
+void tree_prof_dump() {
+#if AICP_ITER_PROF
+  unsigned long long h[8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mid_prof), sizeof(h)) == hipSuccess && h[4])
+    fprintf(stderr,
+            "[tree prof] k_tr_mid per segment: load %.2f us, nodes %.2f us (%.2f nodes), store %.2f us; "
+            "slowest segment %.2f us, most nodes %llu, segments %llu\n",
+            h[0] / 100.0 / h[4], h[1] / 100.0 / h[4], (double)h[3] / h[4], h[2] / 100.0 / h[4], h[5] / 100.0, h[6],
+            h[4]);
+#endif
 }
 
 hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const TreeWork& w,

@@ -893,7 +893,10 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
       HIPC(hipStreamWaitEvent(si, sl.ev_ovl, 0));
     }
   }
-  HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));
+  HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));  // (the slot's previous window is done: its upload waited)
+  // the loop's selection histogram, counts and hand-off words: before the wait on the trees
+  launch_zero_words3(si, sl.sel_hist.as<uint32_t>(), np * kHistBins, sl.sel_cnt.as<uint32_t>(), np,
+                     sl.isync.as<uint32_t>(), icp_sync_words(np));
   if (doOvl) {
     launch_ovl_intersect(si, (int)np, dDesc, dOvl + 1, dOvl, dState, bmp);
     launch_ovl_finish(si, (int)np, dDesc, dState, dGst, 1);
@@ -905,9 +908,6 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   // the normals (ev_s2) are waited for by the first iteration's reduce (loop_iteration): the
   // first NN and select need only the matcher tree, which is ready ~0.2 ms earlier on C2
   launch_prepare_read(si, R.m_read, dDesc, readS, sl.read_c.as<float4>());
-  HIPC(hipMemsetAsync(sl.sel_hist.p, 0, np * kHistBins * 4, si));
-  HIPC(hipMemsetAsync(sl.sel_cnt.p, 0, np * 4, si));
-  HIPC(hipMemsetAsync(sl.isync.p, 0, icp_sync_words(np) * 4, si));
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_setup, si));
   return AICP_OK;
@@ -1045,12 +1045,15 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
     }
   hipStream_t st = q.st;
   if (it == 0) launch_active_list(st, (int)q.np, gd, gs, al, ctr, hn_this, nullptr, nullptr, nullptr);
-  if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches], st));
+  const bool ext = timeNN && nn_ext_events();  // events on the NN's own dispatch
+  if (timeNN && !ext) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches], st));
   launch_icp_nn(st, (int)q.reads, gd, gs, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
                 R.use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
                 R.use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
-                sl.touch.as<uint32_t>(), ctr, ip);
-  if (timeNN) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], st));
+                sl.touch.as<uint32_t>(), ctr, ip, ext ? S->nn_ev[2 * nn_launches] : nullptr,
+                ext ? S->nn_ev[2 * nn_launches + 1] : nullptr);
+  HIPC(hipGetLastError());
+  if (timeNN && !ext) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], st));
   ++nn_launches;
   IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, q.g);
   y.np = (int)q.np;
@@ -1410,7 +1413,10 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     HIPC(hipEventRecord(S->ev_end, S->s_icp));
     rc = seq_sync(ctx, S);
     if (rc) return rc;
-    if (std::getenv("AICP_ITER_PROF_DUMP")) iter_prof_dump();
+    if (std::getenv("AICP_ITER_PROF_DUMP")) {
+      iter_prof_dump();
+      tree_prof_dump();
+    }
     if (prof && plan.size() > 2) {  // device phase times, averaged over the windows after the first
       double a[5] = {0, 0, 0, 0, 0};
       const size_t m = plan.size() - 1;
