@@ -228,7 +228,9 @@ hipError_t launch_ovl_sparse_sets(hipStream_t s, uint32_t n_blocks, const uint32
 // gd->ref_origin = translation of fromMatrix4fToIsometry3d(T) * prior pose of src (1 thread);
 // T is read at system scope (written by another stream's kernel, released through a signal)
 // and copied to Tcopy for the transform that follows on the same stream
-void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy);
+// T: the source's correction, or null and sst: its state (the correction composed on the device)
+void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, const PairState* sst,
+                         float* Tcopy);
 // the window's descriptors, states and corrections into the sequence's arrays (np readings)
 void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState* st, const float* T, PairDesc* gd,
                        PairState* gst, float* gT);

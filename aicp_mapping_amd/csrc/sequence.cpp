@@ -232,6 +232,16 @@ bool seq_upload_late() {  // AICP_SEQ_UPLOAD_LATE=0: the next window's upload be
   return !(e && e[0] == '0');
 }
 
+// AICP_SEQ_EARLY_REF=1: the next reference waits for the poll that found the loop finished instead
+// of the loop's end (after the trailing no-op iteration and the finalize); every correction is
+// final there, and k_seq_next_ref composes the source's correction from its state as k_finalize
+// does. Bit-identical results; measured 1 % slower on C2 (2521 against 2550 clouds/s over three
+// alternating runs each, r03), so off by default.
+bool seq_early_ref() {
+  const char* e = std::getenv("AICP_SEQ_EARLY_REF");
+  return e && e[0] == '1';
+}
+
 bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches
   const char* e = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
   return e && e[0] == '1';
@@ -255,6 +265,8 @@ struct SeqSlot {
   uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), 2 * kMaxPolls words
   uint32_t* poll_dev = nullptr;   // its device address
   hipEvent_t ev_poll[2 * kMaxPolls] = {};
+  hipEvent_t crit_wait = nullptr;  // what the next reference waits for: ev_crit, or the stop poll's event
+  bool crit_early = false;         // crit_wait is the stop poll's: the finalize has not run there
   GraphCache g_raw, g_match, g_icp;
   bool used = false;
 };
@@ -417,6 +429,7 @@ struct WinRun {
   TreeCtl* ctl_w = nullptr;
   const PairDesc* src_desc = nullptr;   // the reference source's descriptor and correction
   const float* src_T = nullptr;
+  const PairState* src_st = nullptr;    // its state (T_iter), for the early next reference
   hipEvent_t* tev = nullptr;            // seq_prof(): ref start, matcher done, normals done, ICP start, ICP done
   std::vector<uint32_t> n_read;         // the readings' point counts
 };
@@ -746,9 +759,12 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     // the source's correction must be final: from the previous window of this pass (its ICP
     // signals the ticket as soon as every reading has stopped, before the loop's remaining no-op
     // launches; or, polled mode, its ev_done), or from an earlier pass (synchronised)
-    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, S->slot[(w.slot + kSlots - 1) % kSlots].ev_crit, 0));
+    const SeqSlot& ps = S->slot[(w.slot + kSlots - 1) % kSlots];
+    const bool early = w.index > 0 && ps.crit_early && R.src_st;
+    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, ps.crit_wait, 0));
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
-    launch_seq_next_ref(s3, dG, R.src_desc, R.src_T, sl.tsrc.as<float>());
+    launch_seq_next_ref(s3, dG, R.src_desc, early ? nullptr : R.src_T, early ? R.src_st : nullptr,
+                        sl.tsrc.as<float>());
     launch_transform(s3, (int)n_ref, sl.tsrc.as<float>(), src_pts, sl.ref_raw.as<float4>());
   } else {
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
@@ -950,6 +966,7 @@ struct IcpLoop {
   BlockMap msel{}, mred{};
   int it = 0;
   bool stop = false;
+  int stop_poll = -1;       // the poll slot that read 0 (the loop's end), -1 otherwise
   std::deque<int> pending;  // poll slots recorded, oldest first
 };
 
@@ -1089,6 +1106,8 @@ static int loop_finish(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_param
   HIPC(hipGetLastError());
   if (q.g == 0) {
     HIPC(hipEventRecord(sl.ev_crit, q.st));
+    sl.crit_early = q.stop_poll >= 0 && seq_early_ref();
+    sl.crit_wait = sl.crit_early ? sl.ev_poll[q.g * kMaxPolls + q.stop_poll] : sl.ev_crit;
     if (R.tev) HIPC(hipEventRecord(R.tev[4], q.st));
   }
   if (q.g + 1 < n_loops) return AICP_OK;  // group 1 commits the window
@@ -1115,7 +1134,10 @@ static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool block, boo
   }
   q.pending.pop_front();
   got = true;
-  if (sl.poll_host[q.g * kMaxPolls + k] == 0) q.stop = true;
+  if (sl.poll_host[q.g * kMaxPolls + k] == 0) {
+    q.stop = true;
+    q.stop_poll = k;
+  }
   return AICP_OK;
 }
 
@@ -1261,6 +1283,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         const size_t off = (size_t)w.src - pw.p0;
         runs[k].src_desc = S->slot[pw.slot].wdesc.as<PairDesc>() + off;
         runs[k].src_T = S->slot[pw.slot].woutT.as<float>() + 16 * off;
+        runs[k].src_st = S->slot[pw.slot].wstate.as<PairState>() + off;
       } else if (w.src >= 0) {  // a reading of an earlier pass: committed
         runs[k].src_desc = S->desc.as<PairDesc>() + w.src;
         runs[k].src_T = S->outT.as<float>() + 16 * (size_t)w.src;

@@ -181,3 +181,25 @@ def test_sequence_split_loops_identical(ctx, L, monkeypatch):
         assert a["accepted"] == b["accepted"] and a["reference"] == b["reference"]
         assert a["icp"]["iterations"] == b["icp"]["iterations"]
         assert a["icp"]["nn_points_touched"] == b["icp"]["nn_points_touched"]
+
+
+@pytest.mark.parametrize("early", ["0", "1"])
+def test_sequence_early_reference_identical(ctx, L, monkeypatch, early):
+    """The next reference waits for the poll that found the window's loop finished and composes
+    the source's correction from its state (AICP_SEQ_EARLY_REF=1), or waits for the loop's end
+    and reads the finalize output (=0, the default). Both give the corrections of the split and
+    polled-off schedules bit for bit, across dropped readings."""
+    st = sy.make_stream(n_readings=12, n_points=5000, seed=8, half=18.0, jumps={2: (0.6, 0, 0), 6: (0, -0.6, 0)})
+    prm = L.default_sequence_params(max_correction_magnitude=0.4)  # readings 2 and 6 drop
+    monkeypatch.setenv("AICP_SEQ_NO_EARLY_EXIT", "1")  # no polls: the next reference after the loop
+    T0, out0, done0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    monkeypatch.delenv("AICP_SEQ_NO_EARLY_EXIT")
+    monkeypatch.setenv("AICP_SEQ_EARLY_REF", early)
+    T1, out1, done1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    assert (rc0, done0) == (rc1, done1) == (0, 12)
+    assert sum(1 - o["accepted"] for o in out1) == 2
+    assert np.array_equal(T0, T1)
+    for a, b in zip(out0, out1):
+        assert a["accepted"] == b["accepted"] and a["reference"] == b["reference"]
+        assert a["icp"]["iterations"] == b["icp"]["iterations"]
+        assert a["icp"]["nn_points_touched"] == b["icp"]["nn_points_touched"]
