@@ -33,47 +33,20 @@
 using namespace aicp;
 using namespace aicp::rt;
 
-namespace {
-
-// (function-local statics: initialised once, thread-safe under concurrent contexts)
-int icp_groups(size_t P) {
-  static const int g = [] {
-    const char* e = std::getenv("AICP_ICP_GROUPS");
-    return (e && std::atoi(e) == 2) ? 2 : 1;
-  }();
-  return P >= 2 ? g : 1;
-}
-bool icp_serial_nn() {
-  static const bool v = [] {
-    const char* e = std::getenv("AICP_ICP_SERIAL_NN");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return v;
-}
-struct IcpGroup {
-  int p0 = 0, np = 0;
-  uint32_t reads = 0;
-  BlockMap msel{}, mred{};
-  hipStream_t st = nullptr;
-  ActiveList* al = nullptr;
-  uint32_t* ctr = nullptr;
-  hipEvent_t nn_done = nullptr;
-};
-
-}  // namespace
-
 namespace aicp {
 namespace rt {
 
 // Test-only: AICP_FORCE_TRAV1=1 runs the ICP NN on node records (Trav<1>), the engine used when
 // treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records); read per
 // call so a test can switch it.
-int nn_interleave(int dflt) {
-  static const int v = [] {
-    const char* e = std::getenv("AICP_NN_INTERLEAVE");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
+// AICP_PROF=1: diagnostic output to stderr (the stream's phase times; the counters of the
+// diagnostic builds -DAICP_ITER_PROF / AICP_NN_PROF / AICP_XCD_PROF); never changes results
+bool prof_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("AICP_PROF");
+    return e && e[0] == '1';
   }();
-  return v < 0 ? dflt : v;
+  return on;
 }
 
 bool force_trav1() {
@@ -431,10 +404,7 @@ int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean) {
   // lean: the balanced estimate + 1, whatever the previous build used; the few segments still
   // above kSubMax go to the subtree kernel's global path (used for the raw-coordinate tree on
   // the critical stream: C2 +2 %, the leftovers cost less than the full-length levels)
-  if (lean) {
-    const char* e = std::getenv("AICP_TREE_LEAN");
-    if (!e || std::atoi(e) != 0) return std::min(kFarStack - 2, l + 1);
-  }
+  if (lean) return std::min(kFarStack - 2, l + 1);
   // with a previous build of this tree: the levels it used (a cloud that needs more leaves a few
   // segments above kSubMax to the subtree kernel's global path once, and the next plan grows);
   // without one: a margin of 4 levels over the balanced estimate
@@ -608,19 +578,6 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
   return AICP_OK;
 }
 
-bool stream_prio_enabled() {  // AICP_STREAM_PRIO=0: all streams at the default priority
-  const char* e = std::getenv("AICP_STREAM_PRIO");
-  return !(e && e[0] == '0');
-}
-
-bool read_order_enabled() {  // AICP_READ_ORDER=0 keeps the caller's order (A/B measurements)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_READ_ORDER");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 double ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
@@ -640,7 +597,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     if (!e) HIPC(hipEventCreate(&e));
   const bool timeNN = (flags & AICP_RUN_TIME_NN) && doIcp;
   if (timeNN)
-    while ((int)ctx->nn_ev.size() < 2 * 2 * cfg->max_iter) {  // up to two ICP groups
+    while ((int)ctx->nn_ev.size() < 2 * cfg->max_iter) {
       hipEvent_t e;
       HIPC(hipEventCreate(&e));
       ctx->nn_ev.push_back(e);
@@ -673,7 +630,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   // readings in Morton order inside each pair's range (kernels_order.hip): the overlap and
   // the ICP loop both visit the sorted copy
   const float4* readS = B->read_raw.as<float4>();
-  if (read_order_enabled()) {
+  {
     const size_t n = B->total_read;
     const size_t tb = read_order_temp_bytes(n, (int)P);
     HIPC(ensure(ctx->read_s, n * 16));
@@ -790,26 +747,6 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), kNormalsBucket,
                           ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0], true));
     if (rc) return join_worker(rc);
-    // the raw tree as treelet records too (the kNN's engine, TravT); errors into its control
-    // block (bit 4), copied again and checked after the batch
-    const uint4* tl_raw = nullptr;
-    const uint2* link_raw = nullptr;
-    if (ctx->tl_total && knn_treelets_enabled()) {
-      const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);
-      const size_t tbb = tree_scan_temp_bytes((size_t)cap + 1);
-      HIPC(ensure(ctx->tl_raw, ctx->tl_total * 16));
-      HIPC(ensure(ctx->link_raw, ctx->tl_total * 8));
-      HIPC(ensure(ctx->tlr_flag, ((size_t)cap + 1) * 4));
-      HIPC(ensure(ctx->tlr_rank, ((size_t)cap + 1) * 4));
-      HIPC(ensure(ctx->tlr_temp, tbb));
-      TreeBufs& T0 = ctx->tb[0];
-      HIPC(launch_treelets(s2, (int)R, cap, ctx->rdesc_raw.as<PairDesc>(), ctx->nodes_raw.as<uint4>(), kNormalsBucket,
-                           ctx->tlr_flag.as<uint32_t>(), ctx->tlr_rank.as<uint32_t>(), ctx->tlr_temp.p, tbb,
-                           ctx->tl_raw.as<uint4>(), ctx->link_raw.as<uint2>(), T0.tw.ctl));
-      HIPC(hipMemcpyAsync(T0.pin_ctl.p, T0.tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
-      tl_raw = ctx->tl_raw.as<uint4>();
-      link_raw = ctx->link_raw.as<uint2>();
-    }
     // normals on the raw tree (bucket order of that tree)
     HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
@@ -817,7 +754,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
     if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, ctx->rdesc_raw.as<PairDesc>(), dRstate,
                         ctx->nodes_raw.as<uint4>(), nullptr, ctx->bpts_raw.as<float4>(), ctx->nrm_raw.as<float4>(),
-                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr, tl_raw, link_raw))
+                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
     HIPC(hipEventRecord(ctx->ev[10], s2));
   }
@@ -846,16 +783,12 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(ensure(ctx->sel_cnt, P * 4));
     HIPC(hipMemsetAsync(ctx->sel_hist.p, 0, P * kHistBins * 4, s));
     HIPC(hipMemsetAsync(ctx->sel_cnt.p, 0, P * 4, s));
-    const bool fuse = icp_fuse_enabled();
-    if (fuse) {
-      HIPC(ensure(ctx->isync, icp_sync_words(P) * 4));
-      HIPC(hipMemsetAsync(ctx->isync.p, 0, icp_sync_words(P) * 4, s));
-    }
+    HIPC(ensure(ctx->isync, icp_sync_words(P) * 4));
+    HIPC(hipMemsetAsync(ctx->isync.p, 0, icp_sync_words(P) * 4, s));
     float4* bpts = ctx->bpts.as<float4>();
     float4* bnrm = ctx->bnrm.as<float4>();
     float4* readc = ctx->read_c.as<float4>();
     const uint4* nodes = ctx->nodes.as<uint4>();
-    const int32_t* parent = nullptr;
     HIPC(hipStreamWaitEvent(s2, ctx->ev[11], 0));
     launch_prepare_read(s2, B->m_read, dDesc, readS, readc);
     // normals from the raw tree's bucket order into the matcher tree's bucket order
@@ -873,99 +806,33 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     prm.min_rot = cfg->min_diff_rot;
     prm.min_trans = cfg->min_diff_trans;
     prm.knn_normals = cfg->knn_normals;
-    prm.interleave = nn_interleave(0);  // contiguous: each XCD's L2 keeps ~1/8 of the references
-    // The ICP loop in one pair group on s, or two on s and s2: group g's NN launch waits for the
-    // other group's previous NN launch, so the NN launches never share the chip with each other,
-    // and each group's select / reduce / update (short, low-occupancy kernels) runs underneath
-    // the other group's NN launch instead of between two NN launches.
-    const int G = icp_groups(P);
-    IcpGroup grp[2];
-    {
-      const std::vector<PairDesc>& hd = B->desc;
-      uint64_t tot = 0, acc = 0;
-      for (size_t i = 0; i < P; ++i) tot += hd[i].n_read;
-      size_t p1 = P;
-      if (G == 2) {
-        p1 = 1;
-        for (size_t i = 0; i + 1 < P; ++i) {  // first pair of group 1: about half the readings before it
-          acc += hd[i].n_read;
-          p1 = i + 1;
-          if (2 * acc >= tot) break;
-        }
-      }
-      uint32_t sel_blk = 0;
-      for (size_t i = 0; i < p1; ++i) sel_blk += (hd[i].n_read + kNNBlock * kSelPerThread - 1) / (kNNBlock * kSelPerThread);
-      const uint32_t red_blk = p1 < P ? hd[p1].red_blk_off : (uint32_t)B->n_red_total;
-      for (int g = 0; g < G; ++g) {
-        IcpGroup& q = grp[g];
-        q.p0 = g ? (int)p1 : 0;
-        q.np = g ? (int)(P - p1) : (int)p1;
-        q.reads = 0;
-        for (int i = q.p0; i < q.p0 + q.np; ++i) q.reads += hd[i].n_read;
-        q.msel = B->m_sel;
-        q.mred = B->m_red;
-        if (g == 0) {
-          q.msel.n_blocks = sel_blk;
-          q.mred.n_blocks = red_blk;
-        } else {
-          q.msel.pair += sel_blk;
-          q.msel.start += sel_blk;
-          q.msel.n_blocks -= sel_blk;
-          q.mred.pair += red_blk;
-          q.mred.start += red_blk;
-          q.mred.n_blocks -= red_blk;
-        }
-        q.st = g ? s2 : s;
-        q.al = ctx->active.as<ActiveList>() + g;
-        q.ctr = g ? dCtr + 2 * kXcdGroups * kCtrStride : dCtr;
-        q.nn_done = ctx->ev[13 + g];
-      }
-    }
-    if (G == 2) HIPC(hipStreamWaitEvent(s2, ctx->ev[9], 0));
+    // The ICP loop on s: per iteration the NN, then select + reduce with the per-pair steps and
+    // the next active list inside (launch_icp_select_f / _reduce_f)
+    uint32_t reads = 0;
+    for (size_t i = 0; i < P; ++i) reads += B->desc[i].n_read;
+    ActiveList* al = ctx->active.as<ActiveList>();
     for (int it = 0; it < cfg->max_iter; ++it) {
-      for (int g = 0; g < G; ++g) {
-        const IcpGroup& q = grp[g];
-        const PairDesc* gd = dDesc + q.p0;
-        PairState* gs = dState + q.p0;
-        if (!fuse || it == 0) launch_active_list(q.st, q.np, gd, gs, q.al, q.ctr);
-        if (G == 2 && icp_serial_nn()) HIPC(hipStreamWaitEvent(q.st, grp[1 - g].nn_done, 0));
-        prm.prof_slot = nn_launches;
-        const bool ext = timeNN && nn_ext_events();  // events on the NN's own dispatch
-        if (timeNN && !ext) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches], q.st));
-        launch_icp_nn(q.st, (int)q.reads, gd, gs, q.al, readc, nodes, ctx->tl_total ? ctx->tl.as<uint4>() : nullptr,
-                      parent, bpts, ctx->tl_total ? ctx->ptl.as<uint2>() : nullptr, ctx->match.as<int32_t>(),
-                      ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), q.ctr, prm,
-                      ext ? ctx->nn_ev[2 * nn_launches] : nullptr, ext ? ctx->nn_ev[2 * nn_launches + 1] : nullptr);
-        HIPC(hipGetLastError());
-        if (timeNN && !ext) HIPC(hipEventRecord(ctx->nn_ev[2 * nn_launches + 1], q.st));
-        if (G == 2) HIPC(hipEventRecord(q.nn_done, q.st));
-        ++nn_launches;
-        if (fuse) {  // select + reduce with the per-pair steps and the next active list inside
-          IcpIterSync y = icp_sync_layout(ctx->isync.as<uint32_t>(), P, g);
-          y.np = q.np;
-          y.pd = gd;
-          y.st = gs;
-          y.al = q.al;
-          y.ctr = q.ctr;
-          launch_icp_select_f(q.st, q.msel, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
-                              ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), y);
-          launch_icp_reduce_f(q.st, q.mred, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
-                              ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>(), prm, y);
-          continue;
-        }
-        launch_icp_select(q.st, q.msel, q.np, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
-                          ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), q.p0);
-        launch_icp_reduce(q.st, q.mred, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
-                          ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>());
-        launch_icp_update(q.st, q.np, gd, gs, ctx->slab.as<double>(), prm);
-      }
-    }
-    if (G == 2) {
-      HIPC(hipEventRecord(ctx->ev[15], s2));
-      HIPC(hipStreamWaitEvent(s, ctx->ev[15], 0));
+      if (it == 0) launch_active_list(s, (int)P, dDesc, dState, al, dCtr);
+      prm.prof_slot = nn_launches;
+      launch_icp_nn(s, (int)reads, dDesc, dState, al, readc, nodes, ctx->tl_total ? ctx->tl.as<uint4>() : nullptr,
+                    nullptr, bpts, ctx->tl_total ? ctx->ptl.as<uint2>() : nullptr, ctx->match.as<int32_t>(),
+                    ctx->d2.as<float>(), ctx->touch.as<uint32_t>(), dCtr, prm,
+                    timeNN ? ctx->nn_ev[2 * nn_launches] : nullptr, timeNN ? ctx->nn_ev[2 * nn_launches + 1] : nullptr);
+      HIPC(hipGetLastError());
+      ++nn_launches;
+      IcpIterSync y = icp_sync_layout(ctx->isync.as<uint32_t>(), P, 0);
+      y.np = (int)P;
+      y.pd = dDesc;
+      y.st = dState;
+      y.al = al;
+      y.ctr = dCtr;
+      launch_icp_select_f(s, B->m_sel, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
+                          ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), y);
+      launch_icp_reduce_f(s, B->m_red, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
+                          ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>(), prm, y);
     }
     launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
-    if (std::getenv("AICP_NN_PROF_DUMP")) {
+    if (prof_enabled()) {  // diagnostic builds' counters (AICP_XCD_PROF / AICP_NN_PROF)
       HIPC(hipStreamSynchronize(s));
       nn_prof_dump();
     }
@@ -989,8 +856,6 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     if (rc) return rc;
     if (ctx->tl_total && (ctx->tb[1].pin_ctl.as<TreeCtl>()->error & 4))
       FAIL(AICP_ERR_HIP, "matcher treelets exceed their allotment");
-    if (ctx->tl_total && knn_treelets_enabled() && (ctx->tb[0].pin_ctl.as<TreeCtl>()->error & 4))
-      FAIL(AICP_ERR_HIP, "normal-tree treelets exceed their allotment");
   }
   // results
   const PairState* hs = ctx->pin_state.as<PairState>();
@@ -1093,7 +958,6 @@ int aicp_hip_create(int device, aicp_hip_ctx** out) {
   // level kernels are the critical path before the ICP loop
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
-  if (!stream_prio_enabled()) prio_lo = prio_hi = 0;
   const int prio3 = prio_hi;  // (measured: stream 3 at the low priority is no faster)
   if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
@@ -1116,8 +980,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
                     &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->gdesc, &ctx->gstate, &ctx->tl, &ctx->ptl,
-                    &ctx->tl_flag, &ctx->tl_rank, &ctx->tl_temp, &ctx->pf_a, &ctx->pf_b, &ctx->tl_raw,
-                    &ctx->link_raw, &ctx->tlr_flag, &ctx->tlr_rank, &ctx->tlr_temp})
+                    &ctx->tl_flag, &ctx->tl_rank, &ctx->tl_temp, &ctx->pf_a, &ctx->pf_b})
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
   free_batch(ctx->oneshot);
@@ -1567,7 +1430,6 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   d.n_ref = V;
   d.ratio = 0.5f;
   d.tl_off = 0;
-  d.tl_cap = 4 * V + 4;  // treelet records allotted (the kNN engine's tree format)
   ident4(d.Tin);
   HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
@@ -1576,19 +1438,6 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   if (rc) return rc;
   rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes, 0);
   if (rc) return rc;
-  const bool use_tl = knn_treelets_enabled();
-  if (use_tl) {
-    const uint32_t cap = 2 * V + 2;
-    const size_t tbb = tree_scan_temp_bytes((size_t)cap + 1);
-    HIPC(ensure(ctx->tl_raw, ((size_t)V * 4 + 4) * 16));
-    HIPC(ensure(ctx->link_raw, ((size_t)V * 4 + 4) * 8));
-    HIPC(ensure(ctx->tlr_flag, ((size_t)cap + 1) * 4));
-    HIPC(ensure(ctx->tlr_rank, ((size_t)cap + 1) * 4));
-    HIPC(ensure(ctx->tlr_temp, tbb));
-    HIPC(launch_treelets(s, 1, cap, ctx->desc.as<PairDesc>(), ctx->nodes.as<uint4>(), 8, ctx->tlr_flag.as<uint32_t>(),
-                         ctx->tlr_rank.as<uint32_t>(), ctx->tlr_temp.p, tbb, ctx->tl_raw.as<uint4>(),
-                         ctx->link_raw.as<uint2>(), ctx->tb[0].tw.ctl));
-  }
   HIPC(ensure(ctx->match, (size_t)V * K * 4));
   HIPC(ensure(ctx->ctrs, kCtrWords * 4 + 16));
   HIPC(hipMemsetAsync(ctx->ctrs.p, 0, kCtrWords * 4 + 16, s));
@@ -1596,8 +1445,7 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   unsigned long long* dtouch = (unsigned long long*)(ctx->ctrs.as<uint32_t>() + kCtrWords);
   HIPC(hipEventRecord(E[2], s));
   if (!launch_knn_ids(s, 1, V, ctx->desc.as<PairDesc>(), ctx->nodes.as<uint4>(), bpts, K, ctx->match.as<int32_t>(),
-                      ctx->ctrs.as<uint32_t>(), dtouch, use_tl ? ctx->tl_raw.as<uint4>() : nullptr,
-                      use_tl ? ctx->link_raw.as<uint2>() : nullptr))
+                      ctx->ctrs.as<uint32_t>(), dtouch))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(E[3], s));

@@ -28,18 +28,14 @@ void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const floa
 void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st);
 // SurfaceNormal of the reference points (bucket order); ids: scratch of total_ref * knn;
 // ctr: zeroed work counter. Returns false if knn is unsupported.
-// tl / link (nullable): the same trees as treelet records (launch_treelets, pd[].tl_off) for the
-// treelet kNN engine, used when knn_treelets_enabled() (AICP_KNN_TREELETS=1, A/B only)
-bool knn_treelets_enabled();
 bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
-                    int32_t* ids, uint32_t* ctr, const uint4* tl = nullptr, const uint2* link = nullptr);
+                    int32_t* ids, uint32_t* ctr);
 // the kNN of every reference point in its own tree (bucket order in and out: ids are bucket
 // positions of the pair's tree, -1 past the cloud size); eps 0, self included. touched
 // (nullable, zeroed): += touched points, inner nodes
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
-                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
-                    const uint4* tl = nullptr, const uint2* link = nullptr);
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched);
 // host_n (nullable): device pointer of mapped host memory that receives the active count;
 // done_sig (nullable, signal memory): once no pair is active, the final corrections go to outT
 // and *ticket is stored to done_sig (the sequence's next reference waits on it)
@@ -67,7 +63,6 @@ struct IcpIterSync {
   const uint64_t* ticket;
   float* outT;
 };
-bool icp_fuse_enabled();
 void tree_prof_dump();  // diagnostic builds (AICP_ITER_PROF): k_tr_mid phase times to stderr
 void iter_prof_dump();  // diagnostic builds (AICP_ITER_PROF): per-kernel body / tail times to stderr
 inline size_t icp_sync_words(size_t n_pairs) { return 3 * n_pairs + 2; }
@@ -83,7 +78,6 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
                    const int32_t* parent, const float4* bpts, const uint2* ptl, int32_t* match, float* d2,
                    uint32_t* touched, uint32_t* ctr, const IcpParams& prm, hipEvent_t e0 = nullptr,
                    hipEvent_t e1 = nullptr);
-bool nn_ext_events();  // timed NN launches carry their events on the dispatch (AICP_NN_EXT_EVENTS)
 // TrimmedDist limit per active pair. m: blocks of kNNBlock * kSelPerThread readings;
 // hist1: n_pairs * kHistBins zeroed words, cand: total_read words, cand_cnt: n_pairs zeroed
 // words (both left zeroed for the next call).
@@ -149,8 +143,6 @@ struct TreeWork {
   size_t lb_stride;      // words per scan
   uint32_t mid_max;      // segments up to this size leave the global levels (kMidMax; kSubMax: no mid builder)
 };
-bool tree_lookback_enabled();
-bool tree_bsearch_enabled();
 uint32_t tree_mid_max();
 size_t tree_scan_temp_bytes(size_t n);
 size_t lb_bytes(uint32_t total);
@@ -224,13 +216,39 @@ hipError_t launch_ovl_sparse_sets(hipStream_t s, uint32_t n_blocks, const uint32
                                   int n_pairs, const PairDesc* pd, unsigned long long* per_cloud,
                                   unsigned long long* per_pair, PairState* gst, PairState* st);
 
+// The stream's sorted-key overlap: one side of a window (its readings, or its reference) as a
+// key list of `cap` words, cap = a host bound of the keys (no read-back of the true count).
+struct OvlKeySide {
+  OvlCloud* clouds;            // n_clouds (device)
+  int n_clouds;
+  const uint32_t* blk_cloud;   // n_blocks blocks of 256 points
+  const uint32_t* blk_start;
+  uint32_t n_blocks;
+  uint32_t n_points;           // count slots (clouds[c].slot + j)
+  uint32_t* cnt;               // n_points
+  uint64_t* off;               // n_points
+  uint64_t cap;
+  uint64_t* keys0;             // cap each
+  uint64_t* keys1;             // sorted
+  void* temp;                  // ovl_keys_temp_bytes
+  size_t temp_bytes;
+  unsigned long long* per_cloud;  // n_clouds
+};
+size_t ovl_keys_temp_bytes(size_t n_points, size_t cap, int n_clouds);
+// keys of the side's clouds (points at pts + clouds[c].pts_off), sorted; |S_c| into
+// st[c].ovl_counts[slot]; origin_of0 (nullable): clouds[0].origin := origin_of0->ref_origin first.
+// A cloud whose keys exceed cap reports st[c].ovl_err.
+hipError_t launch_ovl_keys(hipStream_t s, const OvlKeySide& k, const PairDesc* origin_of0, const float4* pts,
+                           double res, PairState* st, int slot);
+// |A ∩ B| of every reading of rd against the reference side (one cloud) into st[p].ovl_counts[2]
+hipError_t launch_ovl_keys_intersect(hipStream_t s, const OvlKeySide& rd, const OvlKeySide& ref,
+                                     unsigned long long* per_pair, PairState* st);
+
 // ---- frame-to-reference stream (kernels_sequence.hip) ---------------------------------------
 // gd->ref_origin = translation of fromMatrix4fToIsometry3d(T) * prior pose of src (1 thread);
-// T is read at system scope (written by another stream's kernel, released through a signal)
-// and copied to Tcopy for the transform that follows on the same stream
-// T: the source's correction, or null and sst: its state (the correction composed on the device)
-void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, const PairState* sst,
-                         float* Tcopy);
+// T (src's correction, written by another stream's kernel) is copied to Tcopy for the transform
+// that follows on the same stream
+void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy);
 // the window's descriptors, states and corrections into the sequence's arrays (np readings)
 void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState* st, const float* T, PairDesc* gd,
                        PairState* gst, float* gT);

@@ -141,9 +141,6 @@ constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #define AICP_KNN_LDS_FRAMES 6  // k_knn_ids (SurfaceNormal kNN): far frames per lane kept in LDS
 #endif
 constexpr int kKnnLdsFrames = AICP_KNN_LDS_FRAMES;
-#ifndef AICP_NN_BUCKET_MIN
-#define AICP_NN_BUCKET_MIN 16  // Trav2S: lanes at a leaf before a cooperative bucket pass
-#endif
 
 template <int K>
 struct Trav {
@@ -753,368 +750,12 @@ struct Trav2C {
 #endif
 };
 
-// k-NN over the same treelet records (the SurfaceNormal and pre-filter kNN, eps 0): Trav2C's
-// descent (one record per two levels) and one-treelet climb with libnabo's k-best list
-// (IndexHeapBruteForceVector: the head is v[K-1]) instead of the 1-NN best. Visit order, far
-// tests and results are Trav<K>'s over the node records.
-template <int K>
-struct TravT {
-  const uint4* tl;
-  const uint2* ptl;
-  const float4* pts;
-  float q0, q1, q2;
-  float noc0, noc1, noc2, rd, minFar;
-  int32_t n, start, sp, pl;
-  uint32_t lb0, lcnt;
-  uint32_t tp, tn;
-  Best<K> best;
-  NnLdsFrame* lf = nullptr;
-  int32_t nlf = 0;
-
-  __device__ __forceinline__ void reset(float a, float b, float c) {
-    q0 = a;
-    q1 = b;
-    q2 = c;
-    noc0 = noc1 = noc2 = rd = 0.f;
-    n = start = sp = 0;
-    pl = -1;
-    tp = tn = 0;
-    best_init<K>(best);
-  }
-  __device__ __forceinline__ bool decide(uint32_t w, uint32_t cd) {
-    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
-    minFar = min_bound(minFar, rd + (sel3(cd, noc0, noc1, noc2) + no * no));
-    ++tn;
-    return no > 0.f;
-  }
-  __device__ __forceinline__ void descend() {
-    minFar = __builtin_inff();
-    uint32_t T = (uint32_t)n >> 2, s = (uint32_t)n & 3u;
-    uint4 r = ld_rec(tl + T);
-    uint32_t w = r.x, cd = r.w & 3u;
-    if (s == 0 && cd != kLeaf) {
-      s = decide(w, cd) ? 2u : 1u;
-      pl = n;
-      n = (int32_t)(T << 2 | s);
-    }
-    while (s != 0) {
-      w = s == 1 ? r.y : r.z;
-      cd = (r.w >> (2 * s)) & 3u;
-      if (cd == kLeaf) break;
-      const bool right = decide(w, cd);
-      pl = n;
-      T = (r.w >> 6) + 2 * (s - 1) + (right ? 1u : 0u);
-      n = (int32_t)(T << 2);
-      r = ld_rec(tl + T);
-      w = r.x;
-      cd = r.w & 3u;
-      if (cd == kLeaf) break;
-      s = decide(w, cd) ? 2u : 1u;
-      pl = n;
-      n = (int32_t)(T << 2 | s);
-    }
-    lb0 = w & 0x0FFFFFFFu;
-    lcnt = w >> 28;
-  }
-  __device__ __forceinline__ void bucket(float maxR2) {
-    float3 P[kLeafBatch];
-#pragma unroll
-    for (int i = 0; i < kLeafBatch; ++i)
-      if ((uint32_t)i < lcnt) {
-        const float4 p = pts[lb0 + i];
-        P[i] = make_float3(p.x, p.y, p.z);
-      }
-#pragma unroll
-    for (int i = 0; i < kLeafBatch; ++i)
-      if ((uint32_t)i < lcnt) {
-        const float d0 = q0 - P[i].x, d1 = q1 - P[i].y, d2 = q2 - P[i].z;
-        float dist = 0.f;
-        dist += d0 * d0;
-        dist += d1 * d1;
-        dist += d2 * d2;
-        if (dist <= maxR2 && dist < best.v[K - 1]) best_replace<K>(best, (int32_t)(lb0 + i), dist);
-      }
-    for (uint32_t i = kLeafBatch; i < lcnt; ++i) {
-      const float4 p = pts[lb0 + i];
-      const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
-      float dist = 0.f;
-      dist += d0 * d0;
-      dist += d1 * d1;
-      dist += d2 * d2;
-      if (dist <= maxR2 && dist < best.v[K - 1]) best_replace<K>(best, (int32_t)(lb0 + i), dist);
-    }
-    tp += lcnt;
-  }
-  __device__ __forceinline__ bool far_push(FarStack& fs, const uint4& r, int32_t p, uint32_t s, int32_t pp,
-                                           float maxE2, float maxR2) {
-    const uint32_t T = (uint32_t)p >> 2;
-    const uint32_t w = s == 0 ? r.x : (s == 1 ? r.y : r.z), cd = (r.w >> (2 * s)) & 3u;
-    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
-    const float oc = sel3(cd, noc0, noc1, noc2);
-    const float rdf = rd + (oc + no * no);
-    if (!(rdf <= maxR2 && rdf * maxE2 < best.v[K - 1])) return false;
-    const uint32_t fr = no > 0.f ? 0u : 1u;
-    const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
-    if (sp < nlf)
-      lf[sp * kNNBlock] = NnLdsFrame{(int32_t)(((uint32_t)pp & 0x3fffffffu) | (cd << 30)), rd, oc, start,
-                                     __int_as_float(max(__float_as_int(minFar), 0) | (p == start ? (int32_t)0x80000000 : 0))};
-    else
-      fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, 0};
-    ++sp;
-    const float nn = -no * no;
-    if (cd == 0) noc0 = nn;
-    else if (cd == 1) noc1 = nn;
-    else noc2 = nn;
-    rd = rdf;
-    n = far;
-    start = far;
-    pl = p;
-    return true;
-  }
-  __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
-    int32_t c = n, pc = pl;
-    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
-    for (;;) {
-      if (c == start) {
-        if (sp == 0) return true;
-        --sp;
-        FarFrame f;
-        if (sp < nlf) {
-          const NnLdsFrame g = lf[sp * kNNBlock];
-          const int32_t mi = __float_as_int(g.mnf);
-          f = FarFrame{g.PPcd, g.rd, g.old, __int_as_float(mi & 0x7fffffff), g.start, mi < 0 ? g.start : -2,
-                       g.PPcd & 0x3fffffff, 0};
-        } else {
-          f = fs.f[sp];
-        }
-        const uint32_t pcd = (uint32_t)f.F >> 30;
-        rd = f.rd;
-        if (pcd == 0) noc0 = f.old;
-        else if (pcd == 1) noc1 = f.old;
-        else noc2 = f.old;
-        minFar = f.mn;
-        start = f.start;
-        c = f.P;
-        pc = f.PP;
-        if (!(minFar <= maxR2 && minFar * maxE2 < best.v[K - 1])) c = start;
-        continue;
-      }
-      const int32_t p = pc;
-      const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
-      int32_t rootpp;
-      const uint4 r = ld_rec_up(tl + T, ptl + T, rootpp);
-      const int32_t root = (int32_t)(T << 2);
-      if (far_push(fs, r, p, s, s != 0 ? root : rootpp, maxE2, maxR2)) return false;
-      c = p;
-      pc = s != 0 ? root : rootpp;
-      if (s == 0 || c == start) continue;
-      if (far_push(fs, r, root, 0, rootpp, maxE2, maxR2)) return false;
-      c = root;
-      pc = rootpp;
-    }
-  }
-  // one round: a descent, its bucket and the climb to the next far descent; true when done
-  __device__ __forceinline__ bool advance(FarStack& fs, float maxE2, float maxR2, const uint4*, const float4*) {
-    descend();
-    bucket(maxR2);
-    return climb(fs, maxE2, maxR2);
-  }
-};
-
-// Trav2C's traversal as a per-lane state machine ("if-if"): every iteration of the persistent
-// loop each lane takes one step of its own phase -- a descent step (one treelet record, up to two
-// levels) or a climb step (one record: the node and, for a child slot, its treelet root) -- with
-// one record load instruction shared by both phases. Lanes that reach a leaf wait until enough of
-// the wave is at a leaf (or nothing else can step) and then scan their buckets in one
-// cooperative pass. While-while loops make a wave wait for its slowest lane at every phase; here
-// a lane's dependent chain advances every round trip (tools/experiments/wavesim.cpp: 23 instead of 41 round
-// trips per 64 queries). Visit order, far tests, counts and results are Trav2C's.
-enum : int32_t { kPhDesc = 0, kPhLeaf = 1, kPhClimb = 2 };
-
-struct Trav2S {
-  const uint4* tl;
-  const uint2* ptl;
-  uint32_t pbase;
-  float q0, q1, q2;
-  float off0, off1, off2, rd, minFar;
-  int32_t n, start, sp, pl;  // descent: current node, climb frame start, far-stack depth, parent of n
-  int32_t c, pc;             // climb: node climbed from, node to test next
-  int32_t ph;
-  uint32_t lb0, lcnt;
-  uint32_t tp, tn;
-  Best<1> best;
-
-  __device__ __forceinline__ void bind(const uint4* t, const uint2* b, uint32_t tl_off, uint32_t ref_off) {
-    tl = t + tl_off;
-    ptl = b + tl_off;
-    pbase = ref_off;
-  }
-  __device__ __forceinline__ float res_d2() const { return best.v[0]; }
-  __device__ __forceinline__ int32_t res_id() const { return best.id[0]; }
-
-  __device__ __forceinline__ void reset(float a, float b, float cc) {
-    q0 = a;
-    q1 = b;
-    q2 = cc;
-    off0 = off1 = off2 = rd = 0.f;
-    minFar = __builtin_inff();
-    n = start = sp = 0;
-    pl = -1;
-    c = pc = 0;
-    ph = kPhDesc;
-    tp = tn = 0;
-    best_init<1>(best);
-  }
-
-  __device__ __forceinline__ bool decide(uint32_t w, uint32_t cd) {
-    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
-    const float oc = sel3(cd, off0, off1, off2);
-    minFar = fminf(minFar, rd + (-oc * oc + no * no));
-    ++tn;
-    return no > 0.f;
-  }
-
-  // the record this lane needs this round: its descent node's or its next climb node's treelet
-  __device__ __forceinline__ uint32_t need() const { return (uint32_t)(ph == kPhDesc ? n : pc) >> 2; }
-
-  // one descent step with n's record: up to two levels, then the next treelet or the leaf
-  __device__ __forceinline__ void desc_step(const uint4& r) {
-    const uint32_t T = (uint32_t)n >> 2;
-    uint32_t s = (uint32_t)n & 3u, w, cd;
-    if (s == 0) {
-      w = r.x;
-      cd = r.w & 3u;
-      if (cd == kLeaf) {
-        lb0 = w & 0x0FFFFFFFu;
-        lcnt = w >> 28;
-        ph = kPhLeaf;
-        return;
-      }
-      s = decide(w, cd) ? 2u : 1u;
-      pl = n;
-      n = (int32_t)(T << 2 | s);
-    }
-    w = s == 1 ? r.y : r.z;
-    cd = (r.w >> (2 * s)) & 3u;
-    if (cd == kLeaf) {
-      lb0 = w & 0x0FFFFFFFu;
-      lcnt = w >> 28;
-      ph = kPhLeaf;
-      return;
-    }
-    const bool right = decide(w, cd);
-    pl = n;
-    n = (int32_t)(((r.w >> 6) + 2 * (s - 1) + (right ? 1u : 0u)) << 2);
-  }
-
-  __device__ __forceinline__ void bucket_tail(const float4* __restrict__ pts, float maxR2) {
-    for (uint32_t i = kLeafBatch; i < lcnt; ++i) {
-      const float4 p = pts[pbase + lb0 + i];
-      const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
-      float dist = 0.f;
-      dist += d0 * d0;
-      dist += d1 * d1;
-      dist += d2 * d2;
-      if (dist <= maxR2 && dist < best.v[0]) best_replace<1>(best, (int32_t)(lb0 + i), dist);
-    }
-    tp += lcnt;
-  }
-
-  // after the bucket: climb from the leaf unless no ancestor's far bound can pass
-  __device__ __forceinline__ void start_climb(float maxE2, float maxR2) {
-    c = n;
-    pc = pl;
-    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
-    ph = kPhClimb;
-  }
-
-  // frames whose climb reached their start are popped without loads; true when the query is done
-  __device__ __forceinline__ bool climb_pops(FarStack& fs, float maxE2, float maxR2) {
-    while (c == start) {
-      if (sp == 0) return true;
-      --sp;
-      const uint32_t pcd = (uint32_t)fs.f[sp].F >> 30;
-      rd = fs.f[sp].rd;
-      const float old = fs.f[sp].old;
-      if (pcd == 0) off0 = old;
-      else if (pcd == 1) off1 = old;
-      else off2 = old;
-      minFar = fs.f[sp].mn;
-      start = fs.f[sp].start;
-      c = fs.f[sp].P;
-      pc = fs.f[sp].PP;
-      if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
-    }
-    return false;
-  }
-
-  // far test of node p (slot s of the record r); on a pass, push the frame and start the far
-  // descent. pp = p's parent.
-  __device__ __forceinline__ bool far_test(FarStack& fs, const uint4& r, int32_t p, uint32_t s, int32_t pp,
-                                           float maxE2, float maxR2) {
-    const uint32_t T = (uint32_t)p >> 2;
-    const uint32_t w = s == 0 ? r.x : (s == 1 ? r.y : r.z), cd = (r.w >> (2 * s)) & 3u;
-    const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
-    const float oc = sel3(cd, off0, off1, off2);
-    const float rdf = rd + (-oc * oc + no * no);
-    if (!(rdf <= maxR2 && rdf * maxE2 < best.v[0])) return false;
-    const uint32_t fr = no > 0.f ? 0u : 1u;  // far child = the left one when the query is right of the cut
-    const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr)) : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
-    fs.f[sp].F = (int32_t)((uint32_t)far | (cd << 30));
-    fs.f[sp].rd = rd;
-    fs.f[sp].old = oc;
-    fs.f[sp].mn = minFar;
-    fs.f[sp].start = start;
-    fs.f[sp].P = p;
-    fs.f[sp].PP = pp;
-    ++sp;
-    if (cd == 0) off0 = no;
-    else if (cd == 1) off1 = no;
-    else off2 = no;
-    rd = rdf;
-    n = far;
-    start = far;
-    pl = p;
-    minFar = __builtin_inff();
-    ph = kPhDesc;
-    return true;
-  }
-
-  // one climb step with pc's record r and its treelet root's parent rootpp: node pc, and if pc
-  // is a child slot and the climb goes on, its treelet root (same record)
-  __device__ __forceinline__ void climb_step(FarStack& fs, const uint4& r, int32_t rootpp, float maxE2,
-                                             float maxR2) {
-    const int32_t p = pc;
-    const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
-    const int32_t pp = s != 0 ? (int32_t)(T << 2) : rootpp;
-    if (far_test(fs, r, p, s, pp, maxE2, maxR2)) return;
-    c = p;
-    pc = pp;
-    if (s == 0 || c == start) return;
-    if (far_test(fs, r, pp, 0, rootpp, maxE2, maxR2)) return;
-    c = pp;
-    pc = rootpp;
-  }
-};
-
 template <class E>
 struct is_coop {
   static constexpr bool value = false;
 };
 template <>
 struct is_coop<Trav2C> {
-  static constexpr bool value = true;
-};
-template <>
-struct is_coop<Trav2S> {
-  static constexpr bool value = true;
-};
-template <class E>
-struct is_sm {
-  static constexpr bool value = false;
-};
-template <>
-struct is_sm<Trav2S> {
   static constexpr bool value = true;
 };
 
@@ -1174,147 +815,6 @@ __device__ __forceinline__ void coop_bucket(Eng& t, bool act, const float4* __re
   __builtin_amdgcn_wave_barrier();  // every lane's reads of xch precede the next round's writes
   if (act && res_d < t.best.v[0]) best_replace<1>(t.best, (int32_t)(t.lb0 + res_i), res_d);
 }
-
-// 1-NN (the ICP matcher) as a one-load-per-step state machine: each iteration a lane issues
-// exactly one 16-byte load -- a node record or a bucket point, chosen per lane -- and then
-// advances its own phase (descent / bucket / climb), so lanes in different phases of their
-// traversals share every load instruction instead of serialising whole loops. Visit order,
-// far tests and results are those of Trav<1> (libnabo recurseKnn).
-enum : int32_t { kDesc = 0, kClimb = 2 };
-
-struct SM0 {
-  uint32_t nb, pb;  // node / bucket offsets of the query's pair
-  float q0, q1, q2;
-  float off0, off1, off2, rd, minFar;
-  int32_t n, start, sp, phase;
-  float bestd;
-  int32_t bid;
-  uint32_t tp, tn;
-
-  __device__ __forceinline__ void bind(const uint4*, const float4*, uint32_t node_off, uint32_t ref_off) {
-    nb = node_off;
-    pb = ref_off;
-  }
-  __device__ __forceinline__ float res_d2() const { return bestd; }
-  __device__ __forceinline__ int32_t res_id() const { return bid; }
-
-  __device__ __forceinline__ void reset(float a, float bb, float cc) {
-    q0 = a;
-    q1 = bb;
-    q2 = cc;
-    off0 = off1 = off2 = rd = 0.f;
-    minFar = __builtin_inff();
-    n = start = sp = 0;
-    phase = kDesc;
-    bestd = __builtin_inff();
-    bid = -1;
-    tp = tn = 0;
-  }
-
-  // branch-free: a store through a selected member pointer would keep the struct in scratch
-  __device__ __forceinline__ void set_off(uint32_t cd, float v) {
-    off0 = (cd == 0) ? v : off0;
-    off1 = (cd == 1) ? v : off1;
-    off2 = (cd == 2) ? v : off2;
-  }
-
-  __device__ __forceinline__ bool advance(FarStack& fs, float E, float R, const uint4* __restrict__ nodes,
-                                          const float4* __restrict__ pts) {
-    const uint4 v = nodes[nb + n];
-    int32_t c, pc;
-    if (phase == kDesc) {
-      if ((v.y & 3u) != kLeaf) {
-        const uint32_t cd = v.y & 3u;
-        const float no = sel3(cd, q0, q1, q2) - __uint_as_float(v.x);
-        const float oc = sel3(cd, off0, off1, off2);
-        minFar = fminf(minFar, rd + (-oc * oc + no * no));
-        n = (no > 0.f) ? (int32_t)(v.y >> 2) : n + 1;
-        ++tn;
-        return false;
-      }
-      // bucket: all points loaded first (one round trip), then scanned in order
-      const uint32_t b0 = v.y >> 2, cn = v.x;
-      float3 P[kLeafBatch];
-#pragma unroll
-      for (int i = 0; i < kLeafBatch; ++i)
-        if ((uint32_t)i < cn) {
-          const float4 p = pts[pb + b0 + i];
-          P[i] = make_float3(p.x, p.y, p.z);
-        }
-#pragma unroll
-      for (int i = 0; i < kLeafBatch; ++i)
-        if ((uint32_t)i < cn) {
-          const float d0 = q0 - P[i].x, d1 = q1 - P[i].y, d2 = q2 - P[i].z;
-          float dist = 0.f;
-          dist += d0 * d0;
-          dist += d1 * d1;
-          dist += d2 * d2;
-          if (dist <= R && dist < bestd) {
-            bestd = dist;
-            bid = (int32_t)(b0 + i);
-          }
-        }
-      for (uint32_t i = kLeafBatch; i < cn; ++i) {
-        const float4 p = pts[pb + b0 + i];
-        const float d0 = q0 - p.x, d1 = q1 - p.y, d2 = q2 - p.z;
-        float dist = 0.f;
-        dist += d0 * d0;
-        dist += d1 * d1;
-        dist += d2 * d2;
-        if (dist <= R && dist < bestd) {
-          bestd = dist;
-          bid = (int32_t)(b0 + i);
-        }
-      }
-      tp += cn;
-      c = n;
-      pc = (int32_t)v.z;
-      if (!(minFar <= R && minFar * E < bestd)) c = start;
-    } else {  // kClimb: v = record of node n, parent of the finished near child
-      const uint32_t cd = v.y & 3u;
-      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(v.x);
-      const float oc = sel3(cd, off0, off1, off2);
-      const float rdf = rd + (-oc * oc + no * no);
-      if (rdf <= R && rdf * E < bestd) {
-        const int32_t far = (no > 0.f) ? n + 1 : (int32_t)(v.y >> 2);
-        const int k = sp;
-        fs.f[k].F = (int32_t)((uint32_t)far | (cd << 30));
-        fs.f[k].rd = rd;
-        fs.f[k].old = oc;
-        fs.f[k].mn = minFar;
-        fs.f[k].start = start;
-        fs.f[k].P = n;
-        fs.f[k].PP = (int32_t)v.z;
-        sp = k + 1;
-        set_off(cd, no);
-        rd = rdf;
-        start = far;
-        n = far;
-        minFar = __builtin_inff();
-        phase = kDesc;
-        return false;
-      }
-      c = n;
-      pc = (int32_t)v.z;
-    }
-    for (;;) {  // frame completions need no loads
-      if (c != start) {
-        n = pc;
-        phase = kClimb;
-        return false;
-      }
-      if (sp == 0) return true;
-      const int k = --sp;
-      rd = fs.f[k].rd;
-      set_off((uint32_t)fs.f[k].F >> 30, fs.f[k].old);
-      minFar = fs.f[k].mn;
-      start = fs.f[k].start;
-      c = fs.f[k].P;
-      pc = fs.f[k].PP;
-      if (!(minFar <= R && minFar * E < bestd)) c = start;
-    }
-  }
-};
 
 #ifndef AICP_XCD_PROF
 #define AICP_XCD_PROF 0  // diagnostic builds: per-XCD-group first start / last end of each NN launch
@@ -1442,30 +942,7 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
     ++pf_rounds;
     pf_lanes += __popcll(__ballot(has));
 #endif
-    if constexpr (is_sm<Eng>::value) {
-      __shared__ float4 xch_sm[kNNBlock];
-      const bool leaf = has && t.ph == kPhLeaf;
-      const uint32_t n_leaf = (uint32_t)__popcll(__ballot(leaf));
-      const uint32_t n_step = (uint32_t)__popcll(__ballot(has && t.ph != kPhLeaf));
-      if (n_leaf != 0 && (n_leaf >= (uint32_t)AICP_NN_BUCKET_MIN || n_step == 0)) {
-        coop_bucket(t, leaf, pts, maxR2, xch_sm + (threadIdx.x & ~63));
-        if (leaf) {
-          t.bucket_tail(pts, maxR2);
-          t.start_climb(maxE2, maxR2);
-        }
-      }
-      if (has && t.ph == kPhClimb && t.climb_pops(fs, maxE2, maxR2)) {
-        done(my, t);
-        has = false;
-      }
-      if (has && t.ph != kPhLeaf) {
-        const uint32_t T = t.need();
-        int32_t rootpp;
-        const uint4 r = ld_rec_up(t.tl + T, t.ptl + T, rootpp);
-        if (t.ph == kPhDesc) t.desc_step(r);
-        else t.climb_step(fs, r, rootpp, maxE2, maxR2);
-      }
-    } else if constexpr (is_coop<Eng>::value) {
+    if constexpr (is_coop<Eng>::value) {
 #if AICP_NN_PREFMIN
       __shared__ uint16_t pm_lds[kPmDepth * kNNBlock];
       t.pm = pm_lds + threadIdx.x;
@@ -1485,7 +962,7 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       }
       AICP_PF(pf_buck);
 #if AICP_NN_LDS_FRAMES > 0
-      if constexpr (is_coop<Eng>::value && !is_sm<Eng>::value) {  // used by the climb only
+      {  // used by the climb only
         __shared__ NnLdsFrame lds_frames[AICP_NN_LDS_FRAMES * kNNBlock];
         t.lf = lds_frames + threadIdx.x;
       }
@@ -1737,59 +1214,6 @@ __global__ __launch_bounds__(256) AICP_KNN_ATTR void k_knn_ids(int n_pairs, uint
         tn += t.tn;
       });
   if (touched) {  // touched points / inner nodes (the algorithmic bytes of the roofline), optional
-    unsigned long long a = tp, b = tn;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      a += __shfl_xor(a, o, 64);
-      b += __shfl_xor(b, o, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      atomicAdd(&touched[0], a);
-      atomicAdd(&touched[1], b);
-    }
-  }
-}
-
-// k_knn_ids over the treelet records (TravT<K>); pd[].tl_off locates each reference's records
-// occupancy of the node-record engine at each K (its register count sits just under the
-// 4 / 3 waves-per-SIMD steps; the treelet engine's few extra registers would cost a wave)
-template <int K>
-__global__ __launch_bounds__(256, (K <= 10 ? 5 : (K <= 20 ? 4 : 3))) void k_knn_ids_tl(int n_pairs, uint32_t total,
-                                                                 const PairDesc* __restrict__ pd,
-                                                                 const uint4* __restrict__ tl,
-                                                                 const uint2* __restrict__ link,
-                                                                 const float4* __restrict__ bpts,
-                                                                 int32_t* __restrict__ ids, uint32_t* ctr,
-                                                                 unsigned long long* touched) {
-  __shared__ NnLdsFrame knn_frames[(kKnnLdsFrames > 0 ? kKnnLdsFrames : 1) * kNNBlock];
-  uint32_t tp = 0, tn = 0;
-  int cur = -1;
-  uint32_t cur_end = 0, cur_off = 0;
-  persistent_xcd<TravT<K>>(
-      total, ctr, 1.f, __builtin_inff(), nullptr, bpts, [](uint32_t) {},
-      [&](uint32_t s, TravT<K>& t) {
-        if (cur < 0 || s < cur_off || s >= cur_end) {
-          cur = pair_of_ref(pd, n_pairs, s);
-          cur_off = pd[cur].ref_off;
-          cur_end = cur_off + pd[cur].n_ref;
-        }
-        const PairDesc& d = pd[cur];
-        t.tl = tl + d.tl_off;
-        t.ptl = link + d.tl_off;
-        t.pts = bpts + d.ref_off;
-        const float4 q = bpts[s];
-        t.reset(q.x, q.y, q.z);
-        t.lf = knn_frames + threadIdx.x;
-        t.nlf = kKnnLdsFrames;
-        return true;
-      },
-      [&](uint32_t s, TravT<K>& t) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) ids[(size_t)s * K + i] = (t.best.v[i] != __builtin_inff()) ? t.best.id[i] : -1;
-        tp += t.tp;
-        tn += t.tn;
-      });
-  if (touched) {
     unsigned long long a = tp, b = tn;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -2797,27 +2221,9 @@ __global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__
   icp_update_body(pd[pair], s, slab, prm);
 }
 
-// k_icp_reduce + (last workgroup of the pair) k_icp_update + (last pair of the group) the next
-// active list
-__global__ __launch_bounds__(kNNBlock) void k_icp_reduce_f(
-    BlockMap m, const PairDesc* __restrict__ pd, PairState* st, const float4* __restrict__ read_c,
-    const int32_t* __restrict__ match, const float* __restrict__ d2, const uint32_t* __restrict__ touched,
-    const float4* __restrict__ bpts, const float4* __restrict__ bnrm, double* __restrict__ slab, IcpParams prm,
-    IcpIterSync y) {
-  static_assert(kNNBlock == 256, "icp_update_body: 256 threads");
-  const int pair = m.pair[blockIdx.x];
-  PairState& s = st[pair];
-  if (!s.active) return;
-  const PairDesc& d = pd[pair];
-  icp_reduce_body(m, d, s, read_c, match, d2, touched, bpts, bnrm, slab);
-  if (!last_arrival(&y.red[pair], d.n_red_blk)) return;
-  icp_update_body(d, s, slab, prm);
-  pair_done(y);
-}
-
 // k_icp_update + (last pair of the group) the next active list. Kept out of the reduce kernel:
 // the update's solve (pivoted QR, LLT / min-norm QR / SVD fallback, fp64) needs 256 VGPRs, and a
-// kernel's register allocation is its largest path's, so k_icp_reduce_f ran its gathers at one
+// kernel's register allocation is its largest path's, so a fused reduce ran its gathers at one
 // wave per SIMD (35-40 us per C2 window iteration against 12.5 + 12.3 us for the two kernels).
 __global__ __launch_bounds__(256) void k_icp_update_f(const PairDesc* __restrict__ pd, PairState* st,
                                                       const double* __restrict__ slab, IcpParams prm, IcpIterSync y) {
@@ -2886,7 +2292,7 @@ __global__ __launch_bounds__(256) void k_knn_generic(uint32_t nq, const float4* 
   }
 }
 
-// 1-NN through either engine (SM0: the ICP matcher's one-load-per-step traversal)
+// 1-NN over the node records (Trav<1>)
 template <class Eng>
 __global__ __launch_bounds__(256) void k_knn1_generic(uint32_t nq, const float4* __restrict__ q,
                                                       const uint4* __restrict__ nodes,
@@ -2964,22 +2370,11 @@ void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const floa
 void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st) {
   k_init_state<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st);
 }
-// kNN over treelet records (TravT) only with AICP_KNN_TREELETS=1: measured no faster than the
-// node-record engine at equal occupancy (C2 normals and the pre-filter's k = 30 within 1 %), as
-// the k-best insertions, not the record loads, dominate these kernels
-bool knn_treelets_enabled() {
-  static int e = -1;
-  if (e < 0) {
-    const char* v = getenv("AICP_KNN_TREELETS");
-    e = (v && v[0] == '1') ? 1 : 0;
-  }
-  return e == 1;
-}
 bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
-                    int32_t* ids, uint32_t* ctr, const uint4* tl, const uint2* link) {
+                    int32_t* ids, uint32_t* ctr) {
   if (!total_ref) return true;
-  if (!launch_knn_ids(s, n_pairs, total_ref, pd, nodes, bpts, knn, ids, ctr, nullptr, tl, link)) return false;
+  if (!launch_knn_ids(s, n_pairs, total_ref, pd, nodes, bpts, knn, ids, ctr, nullptr)) return false;
   const int gu = (int)((total_ref + 255) / 256);
   switch (knn) {
     case 10: k_normals_from_ids<10><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm); break;
@@ -2989,52 +2384,34 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   }
   return true;
 }
-// k_knn_oct for launches of at most this many queries (AICP_KNN_OCT_MAX; AICP_KNN_OCT=0 never,
-// =1 always): with eight lanes per query it issues ~2.3x the VALU instructions of the per-lane
-// engine, which pays only while the per-lane launch leaves the chip short of waves (the C2
-// stream's single 120k-point reference: 377 -> 245 us); on C5's 61 M queries it ran 91.7 ms per
-// launch against the per-lane engine's throughput (C5 3962 -> 3097 clouds/s, r03c).
-static int knn_group_lanes() {  // AICP_KNN_GROUP=4|8: lanes per query of k_knn_oct (default 8), read per launch
-  const char* e = std::getenv("AICP_KNN_GROUP");
-  return (e && e[0] == '4') ? 4 : 8;
-}
+// k_knn_oct for launches of at most kKnnOctMax queries (AICP_KNN_OCT=0: never, =1: always --
+// tests compare the engines): with eight lanes per query it issues ~2.3x the VALU instructions of
+// the per-lane engine, which pays only while the per-lane launch leaves the chip short of waves
+// (the C2 stream's single 120k-point reference: 377 -> 245 us); on C5's 61 M queries it ran
+// 91.7 ms per launch against the per-lane engine's throughput (C5 3962 -> 3097 clouds/s, r03c).
+// (Quads, 4 lanes per query, measured equal to octets on C2, r03.)
+constexpr uint32_t kKnnOctMax = 300000;
 static bool knn_oct_enabled(uint32_t n_queries) {  // (the environment is read per launch: tests switch engines)
   const char* e = std::getenv("AICP_KNN_OCT");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  const char* m = std::getenv("AICP_KNN_OCT_MAX");
-  return n_queries <= (m ? (uint64_t)std::strtoull(m, nullptr, 10) : (uint64_t)300000);
+  return n_queries <= kKnnOctMax;
 }
 
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
-                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
-                    const uint4* tl, const uint2* link) {
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched) {
   if (!total_ref) return true;
   if (knn_oct_enabled(total_ref)) {
-    const int G = knn_group_lanes();
-    const unsigned go = (unsigned)(((uint64_t)total_ref * G + 255) / 256);
-#define AICP_KNN_GRP(KK)                                                                        \
-  (G == 8 ? (k_knn_oct<KK, 8><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched)) \
-          : (k_knn_oct<KK, 4><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched)))
+    const unsigned go = (unsigned)(((uint64_t)total_ref * 8 + 255) / 256);
     switch (knn) {
-      case 10: AICP_KNN_GRP(10); break;
-      case 20: AICP_KNN_GRP(20); break;
-      case 30: AICP_KNN_GRP(30); break;
+      case 10: k_knn_oct<10, 8><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
+      case 20: k_knn_oct<20, 8><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
+      case 30: k_knn_oct<30, 8><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
       default: return false;
     }
-#undef AICP_KNN_GRP
     return true;
   }
   const int g = persistent_grid((int)total_ref);
-  if (tl && link && knn_treelets_enabled()) {
-    switch (knn) {
-      case 10: k_knn_ids_tl<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, tl, link, bpts, ids, ctr, touched); break;
-      case 20: k_knn_ids_tl<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, tl, link, bpts, ids, ctr, touched); break;
-      case 30: k_knn_ids_tl<30><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, tl, link, bpts, ids, ctr, touched); break;
-      default: return false;
-    }
-    return true;
-  }
   switch (knn) {
     case 10: k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr, touched); break;
     case 20: k_knn_ids<20><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr, touched); break;
@@ -3047,31 +2424,12 @@ void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const Pa
                         uint32_t* ctr, uint32_t* host_n, uint64_t* done_sig, const uint64_t* ticket, float* outT) {
   k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT);
 }
-// NN engine of the ICP matcher: 4 = Trav2S, 3 = Trav2C (default), 1 = Trav<1>, 0 = SM0; AICP_NN_ENGINE overrides
-// (design experiments, tools/experiments/microbench.hip). Measured on MI355X, C2 batch of 16 pairs:
-// Trav<1> 230 us per NN launch, SM0 436 us (profiles/README.md).
-static int nn_engine() {
-  static int e = -1;
-  if (e < 0) {
-    const char* v = getenv("AICP_NN_ENGINE");
-    e = (v && (v[0] == '0' || v[0] == '1' || v[0] == '3' || v[0] == '4')) ? v[0] - '0' : 3;
-  }
-  return e;
-}
-
-// Timed launches (e0, e1 given) carry the events on the kernel's own dispatch
-// (hipExtLaunchKernelGGL): the elapsed time is the kernel's execution, as rocprofv3 reports it,
-// and no marker packets sit between the NN and its neighbours (two separate hipEventRecord
-// calls left ~6 us gaps on each side of every timed NN launch). AICP_NN_EXT_EVENTS=0: the
-// separate records (A/B).
-bool nn_ext_events() {
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_NN_EXT_EVENTS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
+// The ICP matcher's NN engine: Trav2C on the treelet records; Trav<1> on the node records where
+// treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records) or
+// AICP_FORCE_TRAV1 (tests). Timed launches (e0, e1 given) carry the events on the kernel's own
+// dispatch (hipExtLaunchKernelGGL): the elapsed time is the kernel's execution, as rocprofv3
+// reports it, with no marker packets between the NN and its neighbours (separate
+// hipEventRecord calls left ~6 us gaps on each side of every timed launch).
 template <class E, class Tree>
 static void nn_launch(hipStream_t s, int g, hipEvent_t e0, hipEvent_t e1, const PairDesc* pd, const PairState* st,
                       const ActiveList* al, const float4* read_c, const Tree* tree, const int32_t* parent,
@@ -3094,16 +2452,11 @@ void launch_icp_nn(hipStream_t s, int grid_items, const PairDesc* pd, const Pair
     if (e1) (void)hipEventRecord(e1, s);
     return;
   }
-  if (nn_engine() == 4 && tl && ptl)
-    nn_launch<Trav2S>(s, g, e0, e1, pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
-  else if (nn_engine() == 3 && tl && ptl)
+  if (tl && ptl)
     nn_launch<Trav2C>(s, g, e0, e1, pd, st, al, read_c, tl, parent, bpts, ptl, match, d2, touched, ctr, prm);
-  else if (nn_engine() >= 1)
+  else
     nn_launch<Trav<1>>(s, g, e0, e1, pd, st, al, read_c, nodes, parent, bpts, (const uint2*)nullptr, match, d2,
                        touched, ctr, prm);
-  else
-    nn_launch<SM0>(s, g, e0, e1, pd, st, al, read_c, nodes, parent, bpts, (const uint2*)nullptr, match, d2, touched,
-                   ctr, prm);
 }
 void iter_prof_dump() {
 #if AICP_ITER_PROF
@@ -3164,21 +2517,6 @@ void launch_icp_select(hipStream_t s, BlockMap m, int n_pairs, const PairDesc* p
   k_sel_compact<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, cand, cand_cnt);
   k_sel_final<<<n_pairs, 1024, 0, s>>>(pd + p0, st + p0, cand, cand_cnt + p0);
 }
-static bool reduce_fuse_update() {  // AICP_REDUCE_FUSE_UPDATE=1: the update inside the reduce kernel (A/B)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_REDUCE_FUSE_UPDATE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-bool icp_fuse_enabled() {  // AICP_ICP_FUSE=0: one launch per step (A/B)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_ICP_FUSE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 IcpIterSync icp_sync_layout(uint32_t* words, size_t n_pairs, int group) {
   IcpIterSync y{};
   y.sel1 = words;
@@ -3197,10 +2535,6 @@ void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairStat
                          const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
                          const float4* bnrm, double* slab, const IcpParams& prm, const IcpIterSync& y) {
   if (!m.n_blocks) return;
-  if (reduce_fuse_update()) {
-    k_icp_reduce_f<<<m.n_blocks, kNNBlock, 0, s>>>(m, pd, st, read_c, match, d2, touched, bpts, bnrm, slab, prm, y);
-    return;
-  }
   k_icp_reduce<<<m.n_blocks, kNNBlock, 0, s>>>(m, pd, st, read_c, match, d2, touched, bpts, bnrm, slab);
   k_icp_update_f<<<y.np, 256, 0, s>>>(y.pd, y.st, slab, prm, y);
 }
@@ -3223,12 +2557,7 @@ bool launch_knn_generic(hipStream_t s, uint32_t nq, const float4* q, const uint4
   if (!nq) return true;
   const int g = persistent_grid((int)nq);
   switch (k) {
-    case 1:
-      if (nn_engine() >= 1)
-        k_knn1_generic<Trav<1>><<<g, 256, 0, s>>>(nq, q, nodes, bpts, maxE2, maxR2, ids, d2, touched, ctr);
-      else
-        k_knn1_generic<SM0><<<g, 256, 0, s>>>(nq, q, nodes, bpts, maxE2, maxR2, ids, d2, touched, ctr);
-      break;
+    case 1: k_knn1_generic<Trav<1>><<<g, 256, 0, s>>>(nq, q, nodes, bpts, maxE2, maxR2, ids, d2, touched, ctr); break;
     case 4: k_knn_generic<4><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched, ctr); break;
     case 10: k_knn_generic<10><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched, ctr); break;
     case 20: k_knn_generic<20><<<g, 256, 0, s>>>(nq, q, nodes, parent, bpts, maxE2, maxR2, ids, d2, touched, ctr); break;

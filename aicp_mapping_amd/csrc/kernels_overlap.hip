@@ -23,13 +23,14 @@ namespace aicp {
 
 constexpr int kTreeMaxVal = 32768;
 
+// coordToKeyChecked: the key exists iff floor(c / res) is in [-32768, 32768) (x86 converts NaN
+// and out-of-range values to INT_MIN, which octomap's range test rejects; written out here so a
+// NaN coordinate is rejected on the device as well, instead of converting to 0)
 __device__ __forceinline__ bool key_checked(double rf, float c, int& key) {
-  const int sc = (int)floor(rf * (double)c) + kTreeMaxVal;
-  if (sc >= 0 && sc < 2 * kTreeMaxVal) {
-    key = sc;
-    return true;
-  }
-  return false;
+  const double f = floor(rf * (double)c);
+  if (!(f >= -(double)kTreeMaxVal && f < (double)kTreeMaxVal)) return false;
+  key = (int)f + kTreeMaxVal;
+  return true;
 }
 
 // sides: 1 = the reference origin, 2 = the reading origin

@@ -24,13 +24,14 @@ namespace {
 
 constexpr int kKeyMax = 32768;
 
+// coordToKeyChecked: the key exists iff floor(c / res) is in [-32768, 32768). (x86's int
+// conversion of NaN or of a value beyond int range gives INT_MIN, which octomap's range test
+// rejects; the test is written out here so NaN coordinates are rejected on the device too.)
 __device__ __forceinline__ bool key_ok(double rf, float c, int& key) {
-  const int sc = (int)floor(rf * (double)c) + kKeyMax;
-  if (sc >= 0 && sc < 2 * kKeyMax) {
-    key = sc;
-    return true;
-  }
-  return false;
+  const double f = floor(rf * (double)c);
+  if (!(f >= -(double)kKeyMax && f < (double)kKeyMax)) return false;
+  key = (int)f + kKeyMax;
+  return true;
 }
 
 // computeRayKeys(origin, end) + the endpoint key, in k_ovl_mark's order and arithmetic
@@ -169,6 +170,101 @@ __global__ void k_spo_counts(int n_groups, int n_pairs, const unsigned long long
   }
 }
 
+// ---- the stream's sorted-key overlap (sequence.cpp): one key list per side of a window ----
+// The clouds of one side (a window's readings, or its reference) write their words
+// cloud << 48 | key into a list of `cap` words, a host bound of the keys the rays can visit
+// (no read-back of the true count: the stream stays free of host synchronisation); the words
+// past the true total are padding (n_clouds << 48, sorted last, never counted).
+
+// the reference's origin, written on the device by k_seq_next_ref
+__global__ void k_spo_origin(OvlCloud* c, const PairDesc* __restrict__ g) {
+  if (threadIdx.x < 3) c->origin[threadIdx.x] = g->ref_origin[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void k_spo_emit_cap(const uint32_t* __restrict__ blk_cloud,
+                                                      const uint32_t* __restrict__ blk_start,
+                                                      const OvlCloud* __restrict__ clouds,
+                                                      const float4* __restrict__ pts, double res,
+                                                      const uint64_t* __restrict__ off, uint64_t cap,
+                                                      uint64_t* __restrict__ keys, PairState* est) {
+  const uint32_t ci = blk_cloud[blockIdx.x];
+  const OvlCloud& c = clouds[ci];
+  const uint32_t j = blk_start[blockIdx.x] + threadIdx.x;
+  if (j >= c.n) return;
+  uint64_t o = off[c.slot + j];
+  const uint64_t hi = (uint64_t)ci << 48;
+  bool over = false;
+  ray_keys(res, c.origin, pts[c.pts_off + j], [&](int a, int b, int d) {
+    if (o < cap)
+      keys[o++] = hi | ((uint64_t)a << 32) | ((uint64_t)b << 16) | (uint64_t)d;
+    else
+      over = true;
+  });
+  if (over) atomicOr(&est[ci].ovl_err, 1);  // the host bound was wrong: reported, never written past
+}
+
+// words [total, cap) := pad, total = off[n - 1] + cnt[n - 1]
+__global__ __launch_bounds__(256) void k_spo_pad(const uint64_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+                                                 uint32_t n, uint64_t cap, uint64_t pad, uint64_t* keys) {
+  const uint64_t total = n ? off[n - 1] + cnt[n - 1] : 0;
+  for (uint64_t i = total + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    keys[i] = pad;
+}
+
+// distinct words per cloud of a padded sorted list
+__global__ __launch_bounds__(256) void k_spo_unique_cap(const uint64_t* __restrict__ keys, uint64_t cap,
+                                                        uint32_t n_clouds, unsigned long long* __restrict__ per_cloud) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t k = i < cap ? keys[i] : ~0ull;
+  const uint32_t cloud = (uint32_t)(k >> 48);
+  const bool uniq = cloud < n_clouds && (i == 0 || keys[i - 1] != k);
+  const uint32_t c0 = __shfl(cloud, 0, 64);
+  if (__all(cloud == c0)) {
+    const uint64_t m = __ballot(uniq);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&per_cloud[c0], (unsigned long long)__popcll(m));
+  } else if (uniq) {
+    atomicAdd(&per_cloud[cloud], 1ull);
+  }
+}
+
+// |A ∩ B| per reading: its distinct words whose key is in the reference's list (cloud 0)
+__global__ __launch_bounds__(256) void k_spo_intersect_ref(const uint64_t* __restrict__ rk, uint64_t cap_r,
+                                                           uint32_t n_read, const uint64_t* __restrict__ gk,
+                                                           uint64_t cap_g, unsigned long long* __restrict__ per_pair) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap_r) return;
+  const uint64_t k = rk[i];
+  const uint32_t cloud = (uint32_t)(k >> 48);
+  if (cloud >= n_read || (i > 0 && rk[i - 1] == k)) return;
+  const uint64_t want = k & 0xFFFFFFFFFFFFull;
+  uint64_t lo = 0, hi = cap_g;  // first position with gk[pos] >= want
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (gk[mid] < want)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  if (lo < cap_g && gk[lo] == want) atomicAdd(&per_pair[(uint32_t)cloud], 1ull);
+}
+
+__global__ void k_spo_store(int n, const unsigned long long* __restrict__ v, PairState* st, int slot) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) st[i].ovl_counts[slot] = v[i];
+}
+
+__global__ void k_spo_zero(unsigned long long* v, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = 0ull;
+}
+
+int key_end_bit(int n_clouds) {
+  int b = 1;
+  while ((1 << b) <= n_clouds) ++b;
+  return 48 + b;
+}
+
 }  // namespace
 
 size_t ovl_sparse_scan_bytes(size_t n_points) {
@@ -212,6 +308,53 @@ hipError_t launch_ovl_sparse_sets(hipStream_t s, uint32_t n_blocks, const uint32
   }
   const int m = n_groups > n_pairs ? n_groups : n_pairs;
   k_spo_counts<<<(m + 63) / 64, 64, 0, s>>>(n_groups, n_pairs, per_cloud, per_pair, gst, st);
+  return hipGetLastError();
+}
+
+size_t ovl_keys_temp_bytes(size_t n_points, size_t cap, int n_clouds) {
+  size_t a = 0, b = 0;
+  (void)rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, n_points,
+                                rocprim::plus<uint64_t>());
+  (void)rocprim::radix_sort_keys(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr, cap, 0,
+                                 key_end_bit(n_clouds));
+  return a > b ? a : b;
+}
+
+hipError_t launch_ovl_keys(hipStream_t s, const OvlKeySide& k, const PairDesc* origin_of0, const float4* pts,
+                           double res, PairState* st, int slot) {
+  if (origin_of0) k_spo_origin<<<1, 64, 0, s>>>(k.clouds, origin_of0);
+  if (k.n_blocks) {
+    k_spo_count<<<k.n_blocks, 256, 0, s>>>(k.blk_cloud, k.blk_start, k.clouds, pts, pts, res, k.cnt);
+    size_t b = k.temp_bytes;
+    hipError_t e = rocprim::exclusive_scan(k.temp, b, k.cnt, k.off, (uint64_t)0, k.n_points,
+                                           rocprim::plus<uint64_t>(), s);
+    if (e != hipSuccess) return e;
+    k_spo_emit_cap<<<k.n_blocks, 256, 0, s>>>(k.blk_cloud, k.blk_start, k.clouds, pts, res, k.off, k.cap, k.keys0,
+                                              st);
+  }
+  const uint64_t pad = (uint64_t)k.n_clouds << 48;
+  const uint64_t pb = (k.cap + 255) / 256;
+  if (k.cap) k_spo_pad<<<(unsigned)(pb < 4096 ? pb : 4096), 256, 0, s>>>(k.off, k.cnt, k.n_points, k.cap, pad, k.keys0);
+  k_spo_zero<<<(k.n_clouds + 63) / 64, 64, 0, s>>>(k.per_cloud, k.n_clouds);
+  if (k.cap) {
+    size_t b = k.temp_bytes;
+    const hipError_t e =
+        rocprim::radix_sort_keys(k.temp, b, k.keys0, k.keys1, k.cap, 0, key_end_bit(k.n_clouds), s);
+    if (e != hipSuccess) return e;
+    k_spo_unique_cap<<<(unsigned)((k.cap + 255) / 256), 256, 0, s>>>(k.keys1, k.cap, (uint32_t)k.n_clouds,
+                                                                     k.per_cloud);
+  }
+  k_spo_store<<<(k.n_clouds + 63) / 64, 64, 0, s>>>(k.n_clouds, k.per_cloud, st, slot);
+  return hipGetLastError();
+}
+
+hipError_t launch_ovl_keys_intersect(hipStream_t s, const OvlKeySide& rd, const OvlKeySide& ref,
+                                     unsigned long long* per_pair, PairState* st) {
+  k_spo_zero<<<(rd.n_clouds + 63) / 64, 64, 0, s>>>(per_pair, rd.n_clouds);
+  if (rd.cap)
+    k_spo_intersect_ref<<<(unsigned)((rd.cap + 255) / 256), 256, 0, s>>>(rd.keys1, rd.cap, (uint32_t)rd.n_clouds,
+                                                                         ref.keys1, ref.cap, per_pair);
+  k_spo_store<<<(rd.n_clouds + 63) / 64, 64, 0, s>>>(rd.n_clouds, per_pair, st, 2);
   return hipGetLastError();
 }
 

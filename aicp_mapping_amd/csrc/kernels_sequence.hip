@@ -16,19 +16,11 @@
 namespace aicp {
 
 // gd: the new window's overlap group; src: the reading that becomes the reference; T: its
-// correction (column-major, the finalize output), or (T null) its state, whose T_iter is final:
-// the correction is then composed here in k_finalize's order (Tmean * T_iter * Tinit)
-__global__ void k_seq_next_ref(PairDesc* gd, const PairDesc* __restrict__ src, const float* T,
-                               const PairState* __restrict__ sst, float* Tcopy) {
+// correction (column-major, the finalize output)
+__global__ void k_seq_next_ref(PairDesc* gd, const PairDesc* __restrict__ src, const float* T, float* Tcopy) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   float Tl[16];
-  if (T) {
-    for (int k = 0; k < 16; ++k) Tl[k] = __hip_atomic_load(T + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  } else {
-    float tmp[16];
-    mul4(src->Tmean, sst->T, tmp);
-    mul4(tmp, src->Tinit, Tl);
-  }
+  for (int k = 0; k < 16; ++k) Tl[k] = __hip_atomic_load(T + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (int k = 0; k < 16; ++k) Tcopy[k] = Tl[k];
   double o[3];
   corrected_origin(Tl, src->read_origin, o);
@@ -107,9 +99,8 @@ void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState
     k_seq_commit<<<1, 256, 0, s>>>(np, (const uint32_t*)d, (const uint32_t*)st, (const uint32_t*)T, (uint32_t*)gd,
                                    (uint32_t*)gst, (uint32_t*)gT);
 }
-void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, const PairState* sst,
-                         float* Tcopy) {
-  k_seq_next_ref<<<1, 64, 0, s>>>(gd, src, T, sst, Tcopy);
+void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy) {
+  k_seq_next_ref<<<1, 64, 0, s>>>(gd, src, T, Tcopy);
 }
 void launch_ovl_size(hipStream_t s, int n, PairState* st, OvlDesc* od, const uint64_t* cap) {
   if (n) k_ovl_size<<<(n + 63) / 64, 64, 0, s>>>(n, st, od, cap);

@@ -517,60 +517,8 @@ __global__ void k_tr_roots(int n_pairs, uint32_t total, const PairDesc* __restri
 }
 
 // ---- one global level ------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_tr_minmax(uint32_t total, const int32_t* __restrict__ segof,
-                                                   const float4* __restrict__ W, TreeSeg* seg) {
-  const uint32_t base = blockIdx.x * kTile;
-  // tile inside one segment (contiguous ranges: first and last position suffice)
-  const int s_first = segof[base], s_last = segof[min(base + kTile - 1, total - 1)];
-  const bool uniform = s_first >= 0 && s_first == s_last;
-  if (uniform) {
-    const int cd = seg[s_first].cd;
-    float mn = __builtin_inff(), mx = -__builtin_inff();
-    for (int j = 0; j < kTileItems; ++j) {
-      const uint32_t i = base + (uint32_t)j * 256 + threadIdx.x;
-      if (i < total) {
-        const float v = coord(W[i], cd);
-        mn = fminf(mn, v);
-        mx = fmaxf(mx, v);
-      }
-    }
-    block_minmax(mn, mx);
-    if (threadIdx.x == 0) {  // top levels: many tiles per segment; see k_tr_center
-      const uint32_t emn = ord_enc(mn), emx = ord_enc(mx);
-      if (emn < seg[s_first].lo) atomicMin(&seg[s_first].lo, emn);
-      if (emx > seg[s_first].hi) atomicMax(&seg[s_first].hi, emx);
-    }
-    return;
-  }
-  for (int j = 0; j < kTileItems; ++j) {
-    const uint32_t i = base + (uint32_t)j * 256 + threadIdx.x;
-    const int s = i < total ? segof[i] : -1;
-    float v = 0.f;
-    if (s >= 0) v = coord(W[i], seg[s].cd);
-    float mn = s >= 0 ? v : __builtin_inff(), mx = s >= 0 ? v : -__builtin_inff();
-    const bool last = wave_seg_minmax(s, mn, mx);
-    if (s >= 0 && last) {
-      atomicMin(&seg[s].lo, ord_enc(mn));
-      atomicMax(&seg[s].hi, ord_enc(mx));
-    }
-  }
-}
-
-// pass-1 predicate (v < cut); position `total` stays 0
-__global__ __launch_bounds__(256) void k_tr_flag1(uint32_t total, const int32_t* __restrict__ segof,
-                                                  const float4* __restrict__ W, const TreeSeg* __restrict__ seg,
-                                                  uint32_t* __restrict__ flag) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > total) return;
-  uint32_t f = 0;
-  if (i < total) {
-    const int s = segof[i];
-    if (s >= 0) f = coord(W[i], seg[s].cd) < seg_cut(seg[s]) ? 1u : 0u;
-  }
-  flag[i] = f;
-}
-
-// X1 = exclusive scan of the pass-1 predicate (k_tr_flag1's) over positions [0, total]
+// ---- one global level ------------------------------------------------------------------------
+// X1 = exclusive scan of the pass-1 predicate (v < cut) over positions [0, total]
 __global__ __launch_bounds__(kLbThreads) void k_tr_scan1(uint32_t total, const int32_t* __restrict__ segof,
                                                         const float4* __restrict__ W, const TreeSeg* __restrict__ seg,
                                                         uint32_t* __restrict__ X, uint64_t* st, TreeCtl* ctl) {
@@ -590,32 +538,12 @@ __global__ __launch_bounds__(kLbThreads) void k_tr_scan_counts(uint32_t n, const
   lookback_scan(n, [&](uint32_t i) -> uint32_t { return c[i]; }, X, st, ctl);
 }
 
-// Destination of the element at local position li in a Hoare pass over [lo_b, count) with
-// boundary br (elements satisfying the predicate end up in [lo_b, br)), given the exclusive
-// scan X of the predicate: X[f + j] = #satisfying in [f, f + j).
-struct HoareRanks {
-  // misplaced-left rank (ascending) or misplaced-right rank (descending), -1 if in place
-  __device__ static int32_t rank(uint32_t li, bool pred, uint32_t f, uint32_t lo_b, uint32_t br, uint32_t count,
-                                 const uint32_t* X, bool& left_side) {
-    if (li < br) {
-      left_side = true;
-      if (pred) return -1;
-      return (int32_t)((li - lo_b) - (X[f + li] - X[f + lo_b]));  // non-satisfying in [lo_b, li)
-    }
-    left_side = false;
-    if (!pred) return -1;
-    const uint32_t kl = X[f + li] - X[f + br];
-    const uint32_t nmr = X[f + count] - X[f + br];
-    return (int32_t)(nmr - 1 - kl);
-  }
-};
-
 // The partner of the element at local position li directly, without the position arrays: the
 // k-th misplaced element from the left pairs with the k-th from the right, so the partner of a
 // misplaced-left element is the (nmr - 1 - k)-th predicate element of [br, count) and the partner
 // of a misplaced-right one the k-th non-predicate element of [lo_b, br); both are found by binary
-// search over the monotone counts X (L2-resident) instead of a scatter kernel (k_tr_pos) and a
-// kernel boundary.
+// search over the monotone counts X (L2-resident) instead of a scatter kernel and a kernel
+// boundary.
 __device__ __forceinline__ uint32_t hoare_partner(uint32_t li, bool pred, uint32_t f, uint32_t lo_b, uint32_t br,
                                                   uint32_t count, const uint32_t* __restrict__ X) {
   if (li < br) {
@@ -644,42 +572,11 @@ __device__ __forceinline__ uint32_t hoare_partner(uint32_t li, bool pred, uint32
   return lo - 1;
 }
 
-// partner positions of the misplaced elements of a pass
-__global__ __launch_bounds__(256) void k_tr_pos(uint32_t total, int pass, const int32_t* __restrict__ segof,
-                                                const float4* __restrict__ W, const TreeSeg* __restrict__ seg,
-                                                const uint32_t* __restrict__ X, uint32_t* __restrict__ posL,
-                                                uint32_t* __restrict__ posR) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int s = segof[i];
-  if (s < 0) return;
-  const TreeSeg& g = seg[s];
-  const float v = coord(W[i], g.cd), cut = seg_cut(g);
-  const uint32_t f = g.first, li = i - f;
-  uint32_t lo_b, br;
-  bool pred;
-  if (pass == 1) {
-    lo_b = 0;
-    br = X[f + g.count] - X[f];
-    pred = v < cut;
-  } else {
-    lo_b = g.br1;
-    br = g.br1 + (X[f + g.count] - X[f]);
-    if (li < lo_b) return;
-    pred = v == cut;  // v <= cut within [br1, count)
-  }
-  bool left;
-  const int32_t k = HoareRanks::rank(li, pred, f, lo_b, br, g.count, X, left);
-  if (k < 0 || (uint32_t)k >= g.count) return;
-  (left ? posL : posR)[f + k] = li;
-}
-
 // pass 1: move every element to its place, and write the pass-2 predicate at the new place
 __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t* __restrict__ segof,
                                                   const float4* __restrict__ W, TreeSeg* seg,
-                                                  const uint32_t* __restrict__ X, const uint32_t* __restrict__ posL,
-                                                  const uint32_t* __restrict__ posR, float4* __restrict__ W1,
-                                                  uint32_t* __restrict__ flag2, int bsearch) {
+                                                  const uint32_t* __restrict__ X, float4* __restrict__ W1,
+                                                  uint32_t* __restrict__ flag2) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > total) return;
   if (i == total) {
@@ -696,14 +593,7 @@ __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t*
   const float v = coord(p, g.cd), cut = seg_cut(g);
   const uint32_t f = g.first, li = i - f;
   const uint32_t br1 = X[f + g.count] - X[f];
-  uint32_t p1;
-  if (bsearch) {
-    p1 = hoare_partner(li, v < cut, f, 0, br1, g.count, X);
-  } else {
-    bool left;
-    const int32_t k = HoareRanks::rank(li, v < cut, f, 0, br1, g.count, X, left);
-    p1 = k < 0 ? li : (left ? posR[f + k] : posL[f + k]);
-  }
+  uint32_t p1 = hoare_partner(li, v < cut, f, 0, br1, g.count, X);
   if (p1 >= g.count) p1 = li;  // unreachable for a consistent scan; keeps stores in range
   W1[f + p1] = p;
   flag2[f + p1] = (p1 >= br1 && v == cut) ? 1u : 0u;
@@ -815,47 +705,8 @@ __global__ __launch_bounds__(256) void k_tr_split(int level, int last, uint32_t 
                mid_max);
 }
 
-// The pass-2 scan (k_tr_scan_counts) and the level's split in one launch: the last workgroup to
-// finish its part of the scan (arrival counter after the tile words, release / acquire at agent
-// scope) splits every segment of the level. Used when the level has few segments (the host
-// bound n_pairs << level), where a split launch of its own cost a kernel boundary for a handful
-// of threads.
-__device__ __forceinline__ bool tr_last_arrival(uint32_t* cnt, uint32_t n_expected) {
-  __shared__ uint32_t s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t old = atomicAdd(cnt, 1u);
-    const bool last = old + 1 == n_expected;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    s_last = last ? 1u : 0u;
-  }
-  __syncthreads();
-  return s_last != 0;
-}
-
-__global__ __launch_bounds__(kLbThreads) void k_tr_scan2_split(uint32_t n, const uint32_t* __restrict__ c,
-                                                              uint32_t* __restrict__ X, uint64_t* st, int level,
-                                                              int last, uint32_t total, TreeSeg* seg, TreeSeg* next,
-                                                              SubSeg* subs, SubSeg* mids, TreeCtl* ctl, NodeEvent* ev,
-                                                              uint8_t* valid, uint32_t* ecnt, int32_t* pair_depth,
-                                                              int bucket, uint32_t max_seg, uint32_t mid_max) {
-  lookback_scan(n, [&](uint32_t i) -> uint32_t { return c[i]; }, X, st, ctl);
-  uint32_t* arrive = reinterpret_cast<uint32_t*>(st + lb_words(n));  // zeroed with the tile words
-  if (!tr_last_arrival(arrive, gridDim.x)) return;
-  const uint32_t ns = ctl->nseg[level];
-  for (uint32_t si = threadIdx.x; si < ns; si += blockDim.x)
-    tr_split_seg(si, level, last, total, seg, next, subs, mids, ctl, X, ev, valid, ecnt, pair_depth, bucket, max_seg,
-                 mid_max);
-}
-
-// The next level's segment boxes along their split dimensions (what k_tr_minmax computes at the
-// start of a level), folded into the move that assigns the points to those segments: each wave
+// The next level's segment boxes along their split dimensions (a min/max pass at the start of a
+// level otherwise), folded into the move that assigns the points to those segments: each wave
 // reduces per next-level segment (ballot over the lanes with the same key), the workgroup merges
 // its few keys in LDS, and one atomic per key and workgroup goes to the segment.
 constexpr int kMmKeys = 8;
@@ -905,13 +756,12 @@ __device__ __forceinline__ void move2_minmax(bool has, int key, float v, TreeSeg
 }
 
 // pass 2 move; next level's segment map; points landing in leaves are final (bucket order);
-// next != nullptr: also the next level's segment boxes (move2_minmax)
+// also the next level's segment boxes (move2_minmax)
 __global__ __launch_bounds__(256) void k_tr_move2(uint32_t total, const int32_t* __restrict__ segof,
                                                   const float4* __restrict__ W1, const TreeSeg* __restrict__ seg,
-                                                  const uint32_t* __restrict__ X2, const uint32_t* __restrict__ posL,
-                                                  const uint32_t* __restrict__ posR, float4* __restrict__ W2,
+                                                  const uint32_t* __restrict__ X2, float4* __restrict__ W2,
                                                   int32_t* __restrict__ segof_next, float4* __restrict__ bpts,
-                                                  int bsearch, TreeSeg* next) {
+                                                  TreeSeg* next) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = i < total ? segof[i] : -1;
   bool has = false;  // the point lands in a next-level segment (key, coordinate mv)
@@ -926,13 +776,7 @@ __global__ __launch_bounds__(256) void k_tr_move2(uint32_t total, const int32_t*
     const uint32_t f = g.first, li = i - f;
     uint32_t p2 = li;
     if (li >= g.br1) {
-      if (bsearch) {
-        p2 = hoare_partner(li, v == cut, f, g.br1, g.br2, g.count, X2);
-      } else {
-        bool left;
-        const int32_t k = HoareRanks::rank(li, v == cut, f, g.br1, g.br2, g.count, X2, left);
-        if (k >= 0) p2 = left ? posR[f + k] : posL[f + k];
-      }
+      p2 = hoare_partner(li, v == cut, f, g.br1, g.br2, g.count, X2);
       if (p2 >= g.count) p2 = li;  // unreachable for a consistent scan; keeps stores in range
     }
     const uint32_t q = f + p2;
@@ -940,13 +784,13 @@ __global__ __launch_bounds__(256) void k_tr_move2(uint32_t total, const int32_t*
     const int32_t child = g.child[p2 < g.left ? 0 : 1];
     segof_next[q] = child >= 0 ? child : -1;
     if (child == -1) bpts[q] = p;  // leaf: final; -2: the wave subtree builder takes it from W
-    if (next && child >= 0) {
+    if (child >= 0) {
       has = true;
       key = child;
       mv = coord(p, next[child].cd);
     }
   }
-  if (next) move2_minmax(has, key, mv, next);  // every thread of the workgroup, once
+  move2_minmax(has, key, mv, next);  // every thread of the workgroup, once
 }
 
 // ---- wave subtree builder ----------------------------------------------------------------------
@@ -1806,45 +1650,8 @@ void launch_pairs_degenerate_part(hipStream_t s, int n_pairs, const PairDesc* pd
 }
 
 // look-back words of every scan of a build: two per global level and the node count scan
-size_t lb_stride_words(uint32_t total) { return lb_words(total + 2) + 1; }  // + the fused split's arrival word
-bool tree_lookback_enabled() {  // AICP_TREE_LB=0: rocprim scans and a flag kernel (A/B)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_TREE_LB");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-bool tree_mm_fuse_enabled() {  // AICP_TREE_MM_FUSE=0: the next level's boxes by k_tr_minmax (A/B)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_TREE_MM_FUSE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-// the most segments a level may have for its split to run in the scan's last workgroup
-// (AICP_TREE_SPLIT_FUSE=N). Default 0, the split as its own launch: the fused kernel measured
-// 1.3 ms slower per C4 step already at N = 64 and no faster on C2.
-size_t tree_split_fuse_max() {
-  static const size_t v = [] {
-    const char* e = std::getenv("AICP_TREE_SPLIT_FUSE");
-    return e ? (size_t)std::strtoul(e, nullptr, 10) : (size_t)0;
-  }();
-  return v;
-}
-bool tree_bsearch_enabled() {  // AICP_TREE_BSEARCH=0: partner positions by k_tr_pos (A/B)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_TREE_BSEARCH");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-uint32_t tree_mid_max() {  // AICP_TREE_MID=0: no mid-size builder, global levels down to kSubMax (A/B)
-  static const uint32_t v = [] {
-    const char* e = std::getenv("AICP_TREE_MID");
-    return (e && e[0] == '0') ? (uint32_t)kSubMax : (uint32_t)kMidMax;
-  }();
-  return v;
-}
+size_t lb_stride_words(uint32_t total) { return lb_words(total + 2); }
+uint32_t tree_mid_max() { return (uint32_t)kMidMax; }
 size_t lb_bytes(uint32_t total) { return (size_t)(2 * kFarStack + 1) * lb_stride_words(total) * 8; }
 
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
@@ -1881,54 +1688,21 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   const uint32_t nt1 = lb_words(total + 1) - 1;  // tiles of a scan over [0, total]
   uint64_t* st1 = w.lb + (size_t)(2 * level) * w.lb_stride;
   uint64_t* st2 = st1 + w.lb_stride;
-  const bool lb = tree_lookback_enabled();
   // level 0: the roots' boxes (k_tr_center); later levels: the previous level's move2 (move2_minmax)
-  if (level > 0 && !tree_mm_fuse_enabled()) k_tr_minmax<<<tiles_of(total), 256, 0, s>>>(total, w.segof[a], w.W[0], seg);
-  if (lb) {
-    k_tr_scan1<<<nt1, kLbThreads, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, st1, w.ctl);
-  } else {
-    k_tr_flag1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.flag);
-    const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X1, (size_t)total + 1);
-    if (e != hipSuccess) return e;
-  }
-  const bool bs = tree_bsearch_enabled();
-  if (!bs) k_tr_pos<<<gp, 256, 0, s>>>(total, 1, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR);
-  k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR, w.W[1], w.flag, bs ? 1 : 0);
-  // few segments at this level (at most n_pairs << level): the split runs in the scan's last workgroup
-  const bool fuse_split = lb && ((size_t)w.n_pairs << std::min(level, 20)) <= tree_split_fuse_max();
-  if (fuse_split) {
-    k_tr_scan2_split<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, level, last ? 1 : 0, total, seg, next,
-                                                w.subs, w.mids, w.ctl, w.ev, w.valid, w.ecnt, w.pair_depth, bucket,
-                                                (uint32_t)w.max_seg, w.mid_max);
-  } else {
-    if (lb) {
-      k_tr_scan_counts<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, w.ctl);
-    } else {
-      const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.flag, w.X2, (size_t)total + 1);
-      if (e != hipSuccess) return e;
-    }
-    k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.mids, w.ctl, w.X2, w.ev, w.valid,
-                                  w.ecnt, w.pair_depth, bucket, (uint32_t)w.max_seg, w.mid_max);
-  }
-  if (!bs) k_tr_pos<<<gp, 256, 0, s>>>(total, 2, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR);
-  k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.posL, w.posR, w.W[0], w.segof[b], bpts,
-                                bs ? 1 : 0, tree_mm_fuse_enabled() ? next : nullptr);
+  k_tr_scan1<<<nt1, kLbThreads, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, st1, w.ctl);
+  k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.W[1], w.flag);
+  k_tr_scan_counts<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, w.ctl);
+  k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.mids, w.ctl, w.X2, w.ev, w.valid,
+                                w.ecnt, w.pair_depth, bucket, (uint32_t)w.max_seg, w.mid_max);
+  k_tr_move2<<<gp, 256, 0, s>>>(total, w.segof[a], w.W[1], seg, w.X2, w.W[0], w.segof[b], bpts, next);
   return hipGetLastError();
 }
 
 // grid: an upper bound of the small-segment count (<= total / (bucket + 1) + pairs), capped;
 // the kernel strides over the device-side count
-bool subtree_blk_enabled() {  // AICP_SUBTREE_BLK=0: the depth-first wave builder for every segment
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_SUBTREE_BLK");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts, int bucket) {
   const size_t bound = std::min<size_t>(w.max_seg, (size_t)total / (size_t)(bucket + 1) + (size_t)w.n_pairs + 1);
-  const bool blk = subtree_blk_enabled() && bucket >= 4;  // level widths fit kSubLevelCap
+  const bool blk = bucket >= 4;  // level widths fit kSubLevelCap
   if (blk) {
     const unsigned gb = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, 2048));
     k_tr_subtree_blk<<<gb, 64 * kSubWaves, 0, s>>>(total, w.ctl, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt,
@@ -1966,13 +1740,8 @@ void tree_prof_dump() {
 hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const TreeWork& w,
                               uint4* nodes) {
   // S[p] = #nodes with end < p  (exclusive scan over end positions 0..total+1)
-  if (tree_lookback_enabled()) {
-    k_tr_scan_counts<<<lb_words(total + 2) - 1, kLbThreads, 0, s>>>(total + 2, w.ecnt, w.X1,
-                                                                      w.lb + (size_t)(2 * kFarStack) * w.lb_stride, w.ctl);
-  } else {
-    const hipError_t e = scan_u32(s, w.scan_temp, w.scan_temp_bytes, w.ecnt, w.X1, (size_t)total + 2);
-    if (e != hipSuccess) return e;
-  }
+  k_tr_scan_counts<<<lb_words(total + 2) - 1, kLbThreads, 0, s>>>(total + 2, w.ecnt, w.X1,
+                                                                    w.lb + (size_t)(2 * kFarStack) * w.lb_stride, w.ctl);
   k_tr_emit<<<grid_of(2 * (size_t)total), 256, 0, s>>>(total, w.ev, w.valid, w.X1, pd, nodes, w.ctl);
   k_tr_desc<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.X1, w.pair_depth, w.ctl);
   return hipGetLastError();

@@ -109,10 +109,9 @@ void pack_many(const std::vector<PackSeg>& segs);
 void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4);
 bool valid_pair(const aicp_pair& p);
 double ev_ms(hipEvent_t a, hipEvent_t b);
-bool read_order_enabled();
 bool force_trav1();
-// IcpParams::interleave for the NN launches: AICP_NN_INTERLEAVE=0/1 overrides the caller's default
-int nn_interleave(int dflt);
+bool force_sparse_overlap();  // AICP_OVL_SPARSE=1: every overlap on the sorted-key path (tests)
+bool prof_enabled();  // AICP_PROF=1: diagnostic output (stderr) only
 
 // Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device (kernels_tree.hip).
 // launch = false: allocate the work space only (nothing enqueued; before a stream capture)
@@ -161,7 +160,7 @@ struct aicp_hip_ctx {
   aicp::rt::DevBuf read_c, bpts, bnrm, nodes, match, d2, desc, state, touch, slab, bitmap, outT, scratch, active,
       ctrs, nbids, ref1, sel_hist, sel_cand, sel_cnt, qmap, ovl, rdesc, rstate, rdesc_raw, bpts_raw, nodes_raw,
       nrm_raw, inv, gdesc, gstate, read_s, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, tl, ptl, tl_flag,
-      tl_rank, tl_temp, pf_a, pf_b, tl_raw, link_raw, tlr_flag, tlr_rank, tlr_temp;
+      tl_rank, tl_temp, pf_a, pf_b;
   uint64_t tl_total = 0;  // matcher treelet records allotted for this batch (0: no treelets, Trav<1>)
   aicp::rt::TreeBufs tb[2];  // [0] raw-coordinate tree (stream2), [1] centred matcher tree (stream3)
   aicp::rt::PinBuf pin_desc, pin_state, pin_out, pin_io, pin_ovl, pin_rdesc, pin_gdesc, pin_gstate;

@@ -31,10 +31,10 @@
 // Window w's ICP loop is enqueued iteration by iteration; k_active_list (fused into the previous
 // iteration's reduce) writes the active count into mapped host memory, and the host, one
 // iteration ahead, stops enqueueing once it reads 0. Window w+1's reference (r3) then waits for
-// w's ICP with an event. (AICP_SEQ_SYNC=signal instead enqueues all maxIterationCount launches
-// as one graph and makes r3 wait for w's ticket in signal memory, hipStreamWaitValue64: the
-// trailing no-op launches hold stream icp, 2.79 against 2.25 ms per window measured.)
-// The kd-tree builds -- ~100 short kernels each -- are replayed from hipGraphs captured per
+// w's ICP with an event. (r03: all maxIterationCount launches as one graph with r3 waiting for a
+// ticket in signal memory, hipStreamWaitValue64, measured 2.79 against 2.25 ms per window: the
+// trailing no-op launches held stream icp.)
+// The matcher kd-tree build -- ~100 short kernels -- is replayed from a hipGraph captured per
 // slot. Device buffers live in K window slots (reused with event waits);
 // states and corrections of all readings are committed to sequence-wide arrays for the read-back.
 #include <hip/hip_runtime.h>
@@ -152,21 +152,7 @@ struct GraphCache {
   }
 };
 
-bool seq_prof() {  // AICP_SEQ_PROF=1: host time per part and device phase times (stderr)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_SEQ_PROF");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-bool graphs_enabled() {  // AICP_SEQ_GRAPHS=0: direct launches (A/B)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_SEQ_GRAPHS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+bool seq_prof() { return prof_enabled(); }  // AICP_PROF=1: host time per part and device phase times (stderr)
 
 struct Key {
   std::vector<uint64_t> v;
@@ -183,66 +169,7 @@ struct Key {
 constexpr int kSlots = 3;  // window slots in flight (>= 2: a window reads the previous slot's reading)
 constexpr int kMaxPolls = 64;  // ICP iterations that can end a window's loop early
 
-bool seq_read_early() {  // AICP_SEQ_READ_LATE=1: the reading side after the next reference (A/B: slower)
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_SEQ_READ_LATE");
-    return !(e && e[0] == '1');
-  }();
-  return on;
-}
-
-bool seq_early_nn() {  // AICP_SEQ_EARLY_NN=0: the window's loop waits for the normals before its first NN
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_SEQ_EARLY_NN");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-bool seq_ovl_low() {  // AICP_SEQ_OVL_LOW=1: the reference's voxel map on the low-priority stream (A/B)
-  const char* e = std::getenv("AICP_SEQ_OVL_LOW");
-  return e && e[0] == '1';
-}
-
-bool seq_match_first() {  // AICP_SEQ_MATCH_FIRST=0: the raw tree is enqueued before the matcher tree
-  const char* e = std::getenv("AICP_SEQ_MATCH_FIRST");
-  return !(e && e[0] == '0');
-}
-
-// The raw tree + SurfaceNormal run as direct launches (AICP_SEQ_RAW_GRAPH=1: replayed from a graph):
-// on the device the ~100 short kernels finished 0.08 ms sooner than the graph's replay (ref ->
-// normals 0.95 -> 0.87 ms on C2), and enqueued after the matcher tree's graph they do not delay
-// it (measured: 2450-2470 against 2400-2440 clouds/s; both direct from two host threads: equal)
-bool seq_raw_graph() {
-  const char* e = std::getenv("AICP_SEQ_RAW_GRAPH");
-  return e && e[0] == '1';
-}
-
-bool seq_match_graph() {  // AICP_SEQ_MATCH_GRAPH=0: the matcher tree as direct launches
-  const char* e = std::getenv("AICP_SEQ_MATCH_GRAPH");
-  return !(e && e[0] == '0');
-}
-bool seq_trees_mt() {  // AICP_SEQ_TREES_MT=1: the two builds enqueued from two host threads
-  const char* e = std::getenv("AICP_SEQ_TREES_MT");
-  return e && e[0] == '1';
-}
-
-bool seq_upload_late() {  // AICP_SEQ_UPLOAD_LATE=0: the next window's upload before this window's loop
-  const char* e = std::getenv("AICP_SEQ_UPLOAD_LATE");
-  return !(e && e[0] == '0');
-}
-
-// AICP_SEQ_EARLY_REF=1: the next reference waits for the poll that found the loop finished instead
-// of the loop's end (after the trailing no-op iteration and the finalize); every correction is
-// final there, and k_seq_next_ref composes the source's correction from its state as k_finalize
-// does. Bit-identical results; measured 1 % slower on C2 (2521 against 2550 clouds/s over three
-// alternating runs each, r03), so off by default.
-bool seq_early_ref() {
-  const char* e = std::getenv("AICP_SEQ_EARLY_REF");
-  return e && e[0] == '1';
-}
-
-bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches
+bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches (tests)
   const char* e = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
   return e && e[0] == '1';
 }
@@ -254,31 +181,27 @@ struct SeqSlot {
   // reference side
   DevBuf ref_src, ref_raw, bpts, bnrm, nodes, tl, ptl, tl_flag, tl_rank, tl_temp, bpts_raw, nodes_raw, nrm_raw, nbids,
       inv, rd, tsrc,  // rd: rdesc, rdesc_raw, gdesc (PairDesc) + rstate, gstate (PairState); tsrc: source T
-      wdesc, wstate, woutT, wticket, isync;  // the window's readings (committed to the sequence's arrays at its end)
+      wdesc, wstate, woutT, isync,  // the window's readings (committed to the sequence's arrays at its end)
+      sp_par, sp_cnt, sp_off, sp_keys_r, sp_keys_g, sp_tmp_r, sp_tmp_g, sp_pc;  // sorted-key overlap (sparse windows)
   TreeBufs tb[2];
   PinBuf pin_read, pin_par, pin_src;
-  hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr,
-            ev_crit = nullptr, ev_setup = nullptr,  // ev_crit: the last reading's correction; ev_setup: ready to iterate
-            ev_ovl = nullptr;                       // the reference's voxel map (AICP_SEQ_OVL_LOW)
-  // early exit of the ICP loops: active counts written by the update kernels into mapped host
-  // memory, kMaxPolls words per loop (two loops per window)
-  uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), 2 * kMaxPolls words
+  hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr;
+  // early exit of the ICP loop: active counts written by the update kernels into mapped host
+  // memory, one word per iteration
+  uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), kMaxPolls words
   uint32_t* poll_dev = nullptr;   // its device address
-  hipEvent_t ev_poll[2 * kMaxPolls] = {};
-  hipEvent_t crit_wait = nullptr;  // what the next reference waits for: ev_crit, or the stop poll's event
-  bool crit_early = false;         // crit_wait is the stop poll's: the finalize has not run there
-  GraphCache g_raw, g_match, g_icp;
+  hipEvent_t ev_poll[kMaxPolls] = {};
+  GraphCache g_match;
   bool used = false;
 };
 
 struct SeqState {
-  hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr, s_icp2 = nullptr,
-              s_r3_own = nullptr;
+  hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr;
   SeqSlot slot[kSlots];
   DevBuf desc, state, outT;
   PinBuf pin_state, pin_out, pin_ctl;
   std::vector<hipEvent_t> nn_ev;
-  hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_icp2 = nullptr;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
   std::vector<hipEvent_t> tev;  // seq_prof(): 5 timing events per window
   WorkerPool pool{std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1};
   aicp_sequence_timing last{};
@@ -287,7 +210,7 @@ struct SeqState {
 
 void seq_state_free(SeqState* S) {
   if (!S) return;
-  for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp, S->s_icp2})
+  for (hipStream_t q : {S->s_up, S->s_rd, S->s_r2, S->s_r3, S->s_icp})
     if (q) (void)hipStreamSynchronize(q);
   for (SeqSlot& sl : S->slot) {
     for (DevBuf* b : {&sl.read_raw, &sl.read_s, &sl.read_c, &sl.match, &sl.d2, &sl.touch, &sl.cand, &sl.slab,
@@ -295,12 +218,13 @@ void seq_state_free(SeqState* S) {
                       &sl.caps, &sl.sel_hist, &sl.sel_cnt, &sl.ctrs, &sl.active, &sl.ref_src, &sl.ref_raw, &sl.bpts,
                       &sl.bnrm, &sl.nodes, &sl.tl, &sl.ptl, &sl.tl_flag, &sl.tl_rank, &sl.tl_temp, &sl.bpts_raw,
                       &sl.nodes_raw, &sl.nrm_raw, &sl.nbids, &sl.inv, &sl.rd, &sl.tsrc, &sl.wdesc, &sl.wstate,
-                      &sl.woutT, &sl.wticket, &sl.isync})
+                      &sl.woutT, &sl.isync, &sl.sp_par, &sl.sp_cnt, &sl.sp_off, &sl.sp_keys_r,
+                      &sl.sp_keys_g, &sl.sp_tmp_r, &sl.sp_tmp_g, &sl.sp_pc})
       release(*b);
     for (auto& t : sl.tb) t.release_all();
-    for (GraphCache* g : {&sl.g_raw, &sl.g_match, &sl.g_icp}) g->reset();
+    sl.g_match.reset();
     for (PinBuf* b : {&sl.pin_read, &sl.pin_par, &sl.pin_src}) release(*b);
-    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done, sl.ev_crit, sl.ev_setup, sl.ev_ovl})
+    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done})
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : sl.ev_poll)
       if (e) (void)hipEventDestroy(e);
@@ -310,9 +234,9 @@ void seq_state_free(SeqState* S) {
   for (PinBuf* b : {&S->pin_state, &S->pin_out, &S->pin_ctl}) release(*b);
   for (hipEvent_t e : S->nn_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : S->tev) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {S->ev_begin, S->ev_end, S->ev_icp2})
+  for (hipEvent_t e : {S->ev_begin, S->ev_end})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t q : {S->s_rd, S->s_icp, S->s_icp2, S->s_r3_own})  // (s_up = s_rd; s_r2, s_r3: the context's)
+  for (hipStream_t q : {S->s_rd, S->s_icp})  // (s_up = s_rd; s_r2, s_r3: the context's)
     if (q) (void)hipStreamDestroy(q);
   delete S;
 }
@@ -399,6 +323,50 @@ uint64_t map_cap(const Box& b0, const double* o, double res, bool rigid) {
   return (vox + 15) / 16 * 16;
 }
 
+// A window's voxel maps beyond this many bytes (all of them together) take the sorted-key path
+// instead: a far return (a key box of 10^9+ voxels) or a very wide scan. The C2/C3 scenes need
+// ~3 MB per reading map and ~80 MB for a reference (sized for any rotation of its source).
+constexpr uint64_t kSeqMapBudget = uint64_t(1) << 30;
+constexpr uint64_t kMaxRayKeys = 3 * 65536 + 8;  // keys are 16-bit per axis: a ray's walk is bounded
+
+// Upper bound of the keys computeRayKeys(o, p) + p's own key visit, summed over a cloud: one
+// step per key crossed on an axis, plus the origin, the endpoint and a margin for the walk's
+// float overshoot. rigid: for any rigid motion of both cloud and origin (the corrected reference
+// of the next window), from the distance: sum_i |dk_i| <= sqrt(3) |p - o| / res + 3.
+// A point without a key (non-finite or beyond the key range) visits nothing.
+uint64_t key_bound(WorkerPool& pool, const aicp_cloud& c, const double* org, double res, bool rigid) {
+  constexpr uint64_t kChunk = 1 << 15;
+  const size_t tasks = (size_t)((c.n + kChunk - 1) / kChunk);
+  std::vector<uint64_t> part(tasks, 0);
+  const double rf = 1.0 / res;
+  const float of[3] = {(float)org[0], (float)org[1], (float)org[2]};
+  double ko[3];
+  for (int k = 0; k < 3; ++k) ko[k] = std::floor(rf * (double)of[k]);
+  pool.run(tasks, [&](size_t t) {
+    const char* src = reinterpret_cast<const char*>(c.pts);
+    uint64_t sum = 0;
+    const uint64_t a = t * kChunk, b = std::min<uint64_t>(c.n, a + kChunk);
+    for (uint64_t i = a; i < b; ++i) {
+      const float* p = reinterpret_cast<const float*>(src + i * c.stride);
+      if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]))) continue;
+      double v;
+      if (rigid) {
+        double d2 = 0;
+        for (int k = 0; k < 3; ++k) d2 += ((double)p[k] - org[k]) * ((double)p[k] - org[k]);
+        v = std::ceil(1.7320508075688772 * (std::sqrt(d2) * (1 + 1e-5) + 1e-3) * rf) + 8;
+      } else {
+        v = 8;
+        for (int k = 0; k < 3; ++k) v += std::fabs(std::floor(rf * (double)p[k]) - ko[k]);
+      }
+      sum += v < (double)kMaxRayKeys ? (uint64_t)v : kMaxRayKeys;
+    }
+    part[t] = sum;
+  });
+  uint64_t s = 0;
+  for (uint64_t v : part) s += v;
+  return s;
+}
+
 struct Win {
   size_t p0, np;
   int src;  // -1: the first cloud; else the reading whose corrected cloud is the reference
@@ -429,9 +397,11 @@ struct WinRun {
   TreeCtl* ctl_w = nullptr;
   const PairDesc* src_desc = nullptr;   // the reference source's descriptor and correction
   const float* src_T = nullptr;
-  const PairState* src_st = nullptr;    // its state (T_iter), for the early next reference
   hipEvent_t* tev = nullptr;            // seq_prof(): ref start, matcher done, normals done, ICP start, ICP done
   std::vector<uint32_t> n_read;         // the readings' point counts
+  bool sparse = false;                  // overlap on sorted key lists (a map over kSeqMapBudget)
+  OvlKeySide kr{}, kg{};                // its readings' and reference's sides
+  unsigned long long* per_pair = nullptr;
 };
 
 // Run `enqueue` on stream s through the cache: replay the graph if the key matches, otherwise
@@ -439,7 +409,7 @@ struct WinRun {
 // graphs are off or a capture failed.
 static int graph_run(aicp_hip_ctx* ctx, GraphCache& gc, hipStream_t s, const Key& key,
                      const std::function<int()>& enqueue) {
-  if (!graphs_enabled() || gc.broken) return enqueue();
+  if (gc.broken) return enqueue();
   if (!gc.exec || gc.key != key.v) {
     gc.reset();
     if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) != hipSuccess) {
@@ -504,7 +474,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   HIPC(ensure(sl.sel_hist, np * kHistBins * 4));
   HIPC(ensure(sl.sel_cnt, np * 4));
   HIPC(ensure(sl.ctrs, kCtrWords * 4));
-  HIPC(ensure(sl.active, 2 * sizeof(ActiveList)));  // one per ICP loop
+  HIPC(ensure(sl.active, sizeof(ActiveList)));
   HIPC(ensure(sl.ref_raw, (size_t)n_ref * 16));
   HIPC(ensure(sl.bpts, (size_t)n_ref * 16));
   HIPC(ensure(sl.bnrm, (size_t)n_ref * 16));
@@ -516,7 +486,6 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   HIPC(ensure(sl.wdesc, np * sizeof(PairDesc)));
   HIPC(ensure(sl.wstate, np * sizeof(PairState)));
   HIPC(ensure(sl.woutT, np * 64));
-  HIPC(ensure(sl.wticket, 8));
   HIPC(ensure(sl.isync, icp_sync_words(np) * 4));
   PairDesc* dRdesc = sl.rd.as<PairDesc>();
   PairDesc* dDesc = sl.wdesc.as<PairDesc>();
@@ -591,7 +560,50 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
     bm += cap[i];
     cap_max = std::max(cap_max, cap[i]);
   }
-  if (doOvl) {
+  // a window whose maps do not fit the budget runs its overlap on sorted key lists: sized by host
+  // bounds of the rays' keys (readings from their own points; the reference for any rigid
+  // motion of its source), so the stream needs no read-back
+  const bool sparse = doOvl && (force_sparse_overlap() || bm > kSeqMapBudget);
+  std::vector<OvlCloud> scl;
+  std::vector<uint32_t> sbc, sbs;
+  uint64_t cap_r = 0, cap_g = 0;
+  size_t tmp_r = 0, tmp_g = 0;
+  if (sparse) {
+    uint64_t slot = 0;
+    for (size_t i = 0; i <= np; ++i) {  // readings 0..np-1, then the reference
+      const bool ref = i == np;
+      const aicp_cloud& c = ref ? src : rd[w.p0 + i];
+      OvlCloud o{};
+      o.pts_off = ref ? 0u : loff[i];
+      o.n = (uint32_t)c.n;
+      o.side = ref ? 0u : 1u;
+      for (int k = 0; k < 3; ++k) o.origin[k] = ref ? (w.src < 0 ? first->origin[k] : 0.0) : c.origin[k];
+      o.slot = ref ? 0 : slot;
+      slot += ref ? 0 : c.n;
+      scl.push_back(o);
+      const uint32_t ci = ref ? 0u : (uint32_t)i;
+      for (uint32_t j = 0; j < o.n; j += 256) {
+        sbc.push_back(ci);
+        sbs.push_back(j);
+      }
+      const uint64_t kb = key_bound(S->pool, c, c.origin, res, ref && w.src >= 0);
+      (ref ? cap_g : cap_r) += kb;
+    }
+    tmp_r = ovl_keys_temp_bytes(nread, cap_r, (int)np);
+    tmp_g = ovl_keys_temp_bytes(n_ref, cap_g, 1);
+    size_t free_b = 0, total_b = 0;
+    HIPC(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t need = 16 * (cap_r + cap_g) + tmp_r + tmp_g;
+    if (need > sl.sp_keys_r.cap + sl.sp_keys_g.cap + sl.sp_tmp_r.cap + sl.sp_tmp_g.cap + free_b / 2)
+      FAIL(AICP_ERR_UNSUPPORTED, "sparse overlap: " + std::to_string(cap_r + cap_g) + " ray keys do not fit");
+    HIPC(ensure(sl.sp_cnt, (nread + n_ref) * 4));
+    HIPC(ensure(sl.sp_off, (nread + n_ref) * 8));
+    HIPC(ensure(sl.sp_keys_r, cap_r * 16 + 16));
+    HIPC(ensure(sl.sp_keys_g, cap_g * 16 + 16));
+    HIPC(ensure(sl.sp_tmp_r, tmp_r));
+    HIPC(ensure(sl.sp_tmp_g, tmp_g));
+    HIPC(ensure(sl.sp_pc, (2 * np + 1) * 8));
+  } else if (doOvl) {
     HIPC(ensure(sl.bitmap, bm));
     HIPC(ensure(sl.ovl, (np + 1) * sizeof(OvlDesc)));
     HIPC(ensure(sl.caps, (np + 1) * 8));
@@ -600,7 +612,9 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   const size_t nr = mr.pair.size(), nf = mg.pair.size(), nd = md.pair.size(), ns = ms.pair.size();
   const size_t words = 2 * (nr + nf + nd + ns);
   const size_t o_desc = 0, o_r = o_desc + np * sizeof(PairDesc), o_ovl = o_r + 3 * sizeof(PairDesc),
-               o_cap = o_ovl + (np + 1) * sizeof(OvlDesc), o_maps = o_cap + (np + 1) * 8, total = o_maps + words * 4;
+               o_cap = o_ovl + (np + 1) * sizeof(OvlDesc), o_maps = o_cap + (np + 1) * 8,
+               o_sp = (o_maps + words * 4 + 15) & ~size_t(15),
+               sp_bytes = scl.size() * sizeof(OvlCloud) + 8 * sbc.size(), total = o_sp + sp_bytes;
   HIPC(ensure(sl.pin_par, total));
   HIPC(ensure(sl.maps, words * 4));
   char* P = sl.pin_par.as<char>();
@@ -629,6 +643,26 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
     put(ms, m_sel);
   }
   HIPC(ensure(sl.slab, (size_t)red * kRedCols * 8));
+  if (sparse) {  // clouds (readings, reference) | block clouds | block starts
+    const size_t nb = sbc.size(), ncl = scl.size();
+    std::memcpy(P + o_sp, scl.data(), ncl * sizeof(OvlCloud));
+    std::memcpy(P + o_sp + ncl * sizeof(OvlCloud), sbc.data(), nb * 4);
+    std::memcpy(P + o_sp + ncl * sizeof(OvlCloud) + nb * 4, sbs.data(), nb * 4);
+    HIPC(ensure(sl.sp_par, sp_bytes));
+    char* D = sl.sp_par.as<char>();
+    OvlCloud* dcl = reinterpret_cast<OvlCloud*>(D);
+    const uint32_t* dbc = reinterpret_cast<const uint32_t*>(D + ncl * sizeof(OvlCloud));
+    const uint32_t* dbs = dbc + nb;
+    const uint32_t nbr = (uint32_t)(nb - (n_ref + 255) / 256);  // the readings' blocks come first
+    unsigned long long* pc = sl.sp_pc.as<unsigned long long>();
+    R.kr = OvlKeySide{dcl, (int)np, dbc, dbs, nbr, (uint32_t)nread, sl.sp_cnt.as<uint32_t>(),
+                      sl.sp_off.as<uint64_t>(), cap_r, sl.sp_keys_r.as<uint64_t>(),
+                      sl.sp_keys_r.as<uint64_t>() + cap_r, sl.sp_tmp_r.p, tmp_r, pc};
+    R.kg = OvlKeySide{dcl + np, 1, dbc + nbr, dbs + nbr, (uint32_t)(nb - nbr), n_ref,
+                      sl.sp_cnt.as<uint32_t>() + nread, sl.sp_off.as<uint64_t>() + nread, cap_g,
+                      sl.sp_keys_g.as<uint64_t>(), sl.sp_keys_g.as<uint64_t>() + cap_g, sl.sp_tmp_g.p, tmp_g, pc + np};
+    R.per_pair = pc + np + 1;
+  }
 
   // ---- up: readings, descriptors, maps (and a non-resident reference source)
   hipStream_t su = S->s_up;
@@ -640,6 +674,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
     HIPC(hipMemcpyAsync(sl.caps.p, P + o_cap, (np + 1) * 8, hipMemcpyHostToDevice, su));
   }
   HIPC(hipMemcpyAsync(sl.maps.p, P + o_maps, words * 4, hipMemcpyHostToDevice, su));
+  if (sparse) HIPC(hipMemcpyAsync(sl.sp_par.p, P + o_sp, sp_bytes, hipMemcpyHostToDevice, su));
   const float4* src_pts = src_resident;
   if (upload_src) {
     HIPC(ensure(sl.ref_src, (size_t)n_ref * 16));
@@ -663,6 +698,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   R.cap_max = cap_max;
   R.src_pts = src_pts;
   R.readS = sl.read_raw.as<float4>();
+  R.sparse = sparse;
   return AICP_OK;
 }
 
@@ -714,7 +750,7 @@ static int win_read_side(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   HIPC(hipStreamWaitEvent(sr, sl.ev_up, 0));
   launch_init_state(sr, (int)np, dDesc, dState);
   const float4* readS = sl.read_raw.as<float4>();
-  if (read_order_enabled()) {
+  {
     const size_t tb = read_order_temp_bytes(nread, (int)np);
     HIPC(ensure(sl.ord_k0, nread * 8));
     HIPC(ensure(sl.ord_k1, nread * 8));
@@ -726,7 +762,10 @@ static int win_read_side(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
                            sl.ord_v1.as<uint32_t>(), sl.ord_tmp.p, tb, sl.read_s.as<float4>()));
     readS = sl.read_s.as<float4>();
   }
-  if (doOvl) {
+  if (doOvl && R.sparse) {
+    launch_ovl_init(sr, (int)np, dDesc, dState, res, 2);
+    HIPC(launch_ovl_keys(sr, R.kr, nullptr, readS, res, dState, 1));
+  } else if (doOvl) {
     launch_ovl_init(sr, (int)np, dDesc, dState, res, 2);
     launch_ovl_bbox(sr, m_read, dDesc, dState, readS, 1, res);
     launch_ovl_size(sr, (int)np, dState, dOvl + 1, dCap + 1);
@@ -756,15 +795,12 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   hipStream_t s3 = S->s_r3;
   HIPC(hipStreamWaitEvent(s3, sl.ev_up, 0));
   if (w.src >= 0) {
-    // the source's correction must be final: from the previous window of this pass (its ICP
-    // signals the ticket as soon as every reading has stopped, before the loop's remaining no-op
-    // launches; or, polled mode, its ev_done), or from an earlier pass (synchronised)
+    // the source's correction must be final: from the previous window of this pass (its loop's
+    // end, ev_done), or from an earlier pass (synchronised)
     const SeqSlot& ps = S->slot[(w.slot + kSlots - 1) % kSlots];
-    const bool early = w.index > 0 && ps.crit_early && R.src_st;
-    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, ps.crit_wait, 0));
+    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, ps.ev_done, 0));
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
-    launch_seq_next_ref(s3, dG, R.src_desc, early ? nullptr : R.src_T, early ? R.src_st : nullptr,
-                        sl.tsrc.as<float>());
+    launch_seq_next_ref(s3, dG, R.src_desc, R.src_T, sl.tsrc.as<float>());
     launch_transform(s3, (int)n_ref, sl.tsrc.as<float>(), src_pts, sl.ref_raw.as<float4>());
   } else {
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
@@ -810,16 +846,9 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     HIPC(hipGetLastError());
     return AICP_OK;
   };
+  // the raw tree + SurfaceNormal as direct launches (replayed from a graph they finished 0.08 ms
+  // later on the device, r03), enqueued after the matcher tree's graph
   auto raw_enqueue = [&]() -> int {
-    if (capturable && seq_raw_graph()) {
-      Key k;
-      k << n_ref << plan0 << cfg->knn_normals << dRraw << sl.ref_raw.p << sl.bpts_raw.p << sl.nodes_raw.p
-        << sl.nrm_raw.p << sl.nbids.p << sl.ctrs.p << sl.tb[0].tw;
-      const int r = graph_run(ctx, sl.g_raw, s2, k, raw_build);
-      if (r) return r;
-      HIPC(hipMemcpyAsync(ctl_w, sl.tb[0].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
-      return AICP_OK;
-    }
     const int r = raw_build();
     if (r || !capturable) return r;
     HIPC(hipMemcpyAsync(ctl_w, sl.tb[0].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
@@ -842,7 +871,7 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   };
   auto match_enqueue = [&]() -> int {
     int r;
-    if (capturable && seq_match_graph()) {
+    if (capturable) {
       Key k;
       k << n_ref << plan1 << bucket << use_tl << tl_cap << dRdesc << sl.ref_raw.p << sl.bpts.p << sl.nodes.p
         << sl.tb[1].tw;
@@ -858,19 +887,9 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     if (R.tev) HIPC(hipEventRecord(R.tev[1], s3));
     return AICP_OK;
   };
-  // the two graphs' host launches take tens of us each: the matcher tree, which the window's
-  // loop starts on, can go first (AICP_SEQ_MATCH_FIRST)
-  if (seq_trees_mt()) {  // both builds enqueued at once from two host threads (streams r2, r3)
-    int rr[2] = {AICP_OK, AICP_OK};
-    S->pool.run(2, [&](size_t t) { rr[t] = t == 0 ? match_enqueue() : raw_enqueue(); });
-    rc = rr[0] ? rr[0] : rr[1];
-  } else if (seq_match_first()) {
-    rc = match_enqueue();
-    if (!rc) rc = raw_enqueue();
-  } else {
-    rc = raw_enqueue();
-    if (!rc) rc = match_enqueue();
-  }
+  // the matcher tree, which the window's loop starts on, goes first
+  rc = match_enqueue();
+  if (!rc) rc = raw_enqueue();
   if (rc) return rc;
 
   HIPC(hipStreamWaitEvent(s2, sl.ev_s3, 0));
@@ -893,90 +912,57 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   (void)cfg;
   const float4* readS = R.readS;
   hipStream_t si = S->s_icp;
-  // the reference's voxel map: on stream icp, or (AICP_SEQ_OVL_LOW=1) on the low-priority reading
-  // stream, so that its marking yields the CUs to the kd-tree builds
-  hipStream_t so = seq_ovl_low() ? S->s_rd : si;
-  if (doOvl) {
-    HIPC(hipStreamWaitEvent(so, sl.ev_ref, 0));
-    launch_ovl_init(so, 1, dG, dGst, res, 1);
-    launch_ovl_bbox(so, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
-    launch_ovl_size(so, 1, dGst, dOvl, dCap);
-    launch_ovl_clear(so, 1, dOvl, bmp, R.cap[0]);
-    launch_ovl_mark(so, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
-    launch_ovl_popcount(so, 1, dOvl, dGst, 0, bmp);
-    if (so != si) {
-      HIPC(hipEventRecord(sl.ev_ovl, so));
-      HIPC(hipStreamWaitEvent(si, sl.ev_ovl, 0));
-    }
+  // the reference's voxel map (or key list)
+  if (doOvl && R.sparse) {
+    HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
+    launch_ovl_init(si, 1, dG, dGst, res, 1);
+    HIPC(launch_ovl_keys(si, R.kg, w.src >= 0 ? dG : nullptr, sl.ref_raw.as<float4>(), res, dGst, 0));
+  } else if (doOvl) {
+    HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
+    launch_ovl_init(si, 1, dG, dGst, res, 1);
+    launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
+    launch_ovl_size(si, 1, dGst, dOvl, dCap);
+    launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
+    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
+    launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
   }
   HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));  // (the slot's previous window is done: its upload waited)
   // the loop's selection histogram, counts and hand-off words: before the wait on the trees
   launch_zero_words3(si, sl.sel_hist.as<uint32_t>(), np * kHistBins, sl.sel_cnt.as<uint32_t>(), np,
                      sl.isync.as<uint32_t>(), icp_sync_words(np));
   if (doOvl) {
-    launch_ovl_intersect(si, (int)np, dDesc, dOvl + 1, dOvl, dState, bmp);
+    if (R.sparse)
+      HIPC(launch_ovl_keys_intersect(si, R.kr, R.kg, R.per_pair, dState));
+    else
+      launch_ovl_intersect(si, (int)np, dDesc, dOvl + 1, dOvl, dState, bmp);
     launch_ovl_finish(si, (int)np, dDesc, dState, dGst, 1);
   }
   HIPC(hipStreamWaitEvent(si, sl.ev_s3, 0));
   launch_pairs_from_refs(si, (int)np, dDesc, dRdesc);
-  if (!seq_early_nn()) HIPC(hipStreamWaitEvent(si, sl.ev_s2, 0));  // (A/B: the loop after the normals)
   launch_pairs_degenerate_part(si, (int)np, dDesc, dState, dRst, 2);
   // the normals (ev_s2) are waited for by the first iteration's reduce (loop_iteration): the
   // first NN and select need only the matcher tree, which is ready ~0.2 ms earlier on C2
   launch_prepare_read(si, R.m_read, dDesc, readS, sl.read_c.as<float4>());
   HIPC(hipGetLastError());
-  HIPC(hipEventRecord(sl.ev_setup, si));
   return AICP_OK;
 }
 
-// The ICP loops of a window. The next reference needs only the correction of the window's last
-// reading (app.cpp:375-391), so a window with a successor runs two loops: group 0, that reading,
-// on stream icp, which the next reference waits for (ev_crit); group 1, the other readings, on
-// stream icp2 (low priority), which nothing waits for before the read-back and which therefore
-// runs beside the next window's kd-trees and loop (AICP_SEQ_SPLIT=1). Measured on C2 (r03): the
-// one-reading loop takes 0.99 ms against 1.06 ms for all five (an iteration is latency-bound,
-// not work-bound), and the other readings' NN launches beside the next reference's kd-trees and
-// kNN slow those from 0.88 to 1.63 ms, so the default is one loop per window.
-// Each loop is polled: from iteration smoothLength on (no pair can stop earlier except on an
-// error) the update kernel of the last pair to finish an iteration writes the next active count
-// into mapped host memory; the host, lookahead() iterations ahead, stops enqueueing once it
-// reads 0. The window's states and corrections are committed to the sequence's arrays once
-// both loops are done (ev_done).
-// iterations the host stays ahead of the polls it reads (AICP_SEQ_LOOKAHEAD, default 1): the
-// launches after the one that found no active pair are no-ops that still hold the stream
-int lookahead() {
-  static const int v = [] {
-    const char* e = std::getenv("AICP_SEQ_LOOKAHEAD");
-    const int x = e ? std::atoi(e) : 1;
-    return x < 1 ? 1 : (x > 8 ? 8 : x);
-  }();
-  return v;
-}
-bool seq_split() {  // read per sequence run (tests compare both schedules)
-  const char* e = std::getenv("AICP_SEQ_SPLIT");
-  return e && e[0] == '1';
-}
-
+// The ICP loop of a window, polled: from iteration smoothLength on (no pair can stop earlier
+// except on an error) the update kernel of the last pair to finish an iteration writes the next
+// active count into mapped host memory; the host, one iteration ahead, stops enqueueing once it
+// reads 0 (the launch after the one that found no active pair is a no-op that still holds the
+// stream). The window's states and corrections are then committed to the sequence's arrays
+// (ev_done), which the next reference waits for.
+// (r03, measured and removed: the window's last reading -- the next reference's source -- in a
+// loop of its own with the others on a second stream: the one-reading loop took 0.99 against
+// 1.06 ms, but the others' NN launches beside the next reference's kd-trees slowed those from 0.88
+// to 1.63 ms; the next reference started on the stop poll instead of the loop's end: 1 % slower.)
 struct IcpLoop {
   WinRun* R = nullptr;
-  int g = 0;             // 0: the critical group (or the whole window), 1: the others
-  size_t p0 = 0, np = 0; // the group's pairs [p0, p0 + np) of the window
-  uint64_t reads = 0;
-  hipStream_t st = nullptr;
-  BlockMap msel{}, mred{};
   int it = 0;
   bool stop = false;
-  int stop_poll = -1;       // the poll slot that read 0 (the loop's end), -1 otherwise
   std::deque<int> pending;  // poll slots recorded, oldest first
 };
-
-static BlockMap map_sub(const BlockMap& m, uint32_t off, uint32_t cnt) {
-  BlockMap r = m;
-  r.pair += off;
-  r.start += off;
-  r.n_blocks = cnt;
-  return r;
-}
 
 static IcpParams icp_params(const aicp_icp_config* cfg) {
   IcpParams ip;
@@ -988,55 +974,17 @@ static IcpParams icp_params(const aicp_icp_config* cfg) {
   ip.min_rot = cfg->min_diff_rot;
   ip.min_trans = cfg->min_diff_trans;
   ip.knn_normals = cfg->knn_normals;
-  ip.interleave = nn_interleave(0);  // (interleaved chunks measured equal on C2 windows, r03)
   return ip;
 }
 
-// the window's loops: one, or (split) the last reading on icp + the others on icp2
-static int win_loops(SeqState* S, WinRun& R, bool split, IcpLoop* L, int& n_loops) {
-  const size_t np = R.np;
-  split = split && np >= 2;
-  n_loops = split ? 2 : 1;
-  for (int g = 0; g < n_loops; ++g) {
-    IcpLoop& q = L[g];
-    q = IcpLoop{};
-    q.R = &R;
-    q.g = g;
-    q.p0 = split ? (g == 0 ? np - 1 : 0) : 0;
-    q.np = split ? (g == 0 ? 1 : np - 1) : np;
-    q.st = g == 0 ? S->s_icp : S->s_icp2;
-    uint32_t sel0 = 0, red0 = 0, sel_n = 0, red_n = 0;
-    for (size_t i = 0; i < np; ++i) {
-      const uint32_t a = (R.n_read[i] + kNNBlock * kSelPerThread - 1) / (kNNBlock * kSelPerThread);
-      const uint32_t b = (R.n_read[i] + kNNBlock * kReducePerThread * kReduceChunks - 1) /
-                         (kNNBlock * kReducePerThread * kReduceChunks);
-      if (i < q.p0) {
-        sel0 += a;
-        red0 += b;
-      } else if (i < q.p0 + q.np) {
-        sel_n += a;
-        red_n += b;
-        q.reads += R.n_read[i];
-      }
-    }
-    q.msel = map_sub(R.m_sel, sel0, sel_n);
-    q.mred = map_sub(R.m_red, red0, red_n);
-  }
-  return AICP_OK;
-}
-
 // enqueue the loop's next iteration (and its poll slots)
-static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm, IcpLoop& q,
-                          bool timeNN, int& nn_launches) {
+static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                          IcpLoop& q, bool timeNN, int& nn_launches) {
   WinRun& R = *q.R;
   WIN_REFS;
   const int it = q.it;
-  const PairDesc* gd = dDesc + q.p0;
-  PairState* gs = dState + q.p0;
-  ActiveList* al = sl.active.as<ActiveList>() + q.g;
-  uint32_t* ctr = sl.ctrs.as<uint32_t>() + (q.g ? 2 * kXcdGroups * kCtrStride : 0);
-  uint32_t* poll_host = sl.poll_host + q.g * kMaxPolls;
-  uint32_t* poll_dev = sl.poll_dev + q.g * kMaxPolls;
+  ActiveList* al = sl.active.as<ActiveList>();
+  uint32_t* ctr = sl.ctrs.as<uint32_t>();
   IcpParams ip = icp_params(cfg);
   ip.prof_slot = nn_launches;
   auto polled = [&](int k) {
@@ -1047,12 +995,12 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   uint32_t* hn_this = nullptr;
   uint32_t* hn_next = nullptr;
   if (it == 0 && polled(it)) {
-    poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
-    hn_this = poll_dev + it;
+    sl.poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
+    hn_this = sl.poll_dev + it;
   }
   if (polled(it + 1)) {
-    poll_host[it + 1] = 0xffffffffu;
-    hn_next = poll_dev + it + 1;
+    sl.poll_host[it + 1] = 0xffffffffu;
+    hn_next = sl.poll_dev + it + 1;
   }
   if (timeNN)
     while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
@@ -1060,37 +1008,34 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
       HIPC(hipEventCreate(&e));
       S->nn_ev.push_back(e);
     }
-  hipStream_t st = q.st;
-  if (it == 0) launch_active_list(st, (int)q.np, gd, gs, al, ctr, hn_this, nullptr, nullptr, nullptr);
-  const bool ext = timeNN && nn_ext_events();  // events on the NN's own dispatch
-  if (timeNN && !ext) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches], st));
-  launch_icp_nn(st, (int)q.reads, gd, gs, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
+  hipStream_t st = S->s_icp;
+  if (it == 0) launch_active_list(st, (int)np, dDesc, dState, al, ctr, hn_this);
+  launch_icp_nn(st, (int)R.nread, dDesc, dState, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
                 R.use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
                 R.use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
-                sl.touch.as<uint32_t>(), ctr, ip, ext ? S->nn_ev[2 * nn_launches] : nullptr,
-                ext ? S->nn_ev[2 * nn_launches + 1] : nullptr);
+                sl.touch.as<uint32_t>(), ctr, ip, timeNN ? S->nn_ev[2 * nn_launches] : nullptr,
+                timeNN ? S->nn_ev[2 * nn_launches + 1] : nullptr);
   HIPC(hipGetLastError());
-  if (timeNN && !ext) HIPC(hipEventRecord(S->nn_ev[2 * nn_launches + 1], st));
   ++nn_launches;
-  IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, q.g);
-  y.np = (int)q.np;
-  y.pd = gd;
-  y.st = gs;
+  IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, 0);
+  y.np = (int)np;
+  y.pd = dDesc;
+  y.st = dState;
   y.al = al;
   y.ctr = ctr;
   y.host_n = hn_next;
-  launch_icp_select_f(st, q.msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(), sl.cand.as<uint32_t>(),
+  launch_icp_select_f(st, R.m_sel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(), sl.cand.as<uint32_t>(),
                       sl.sel_cnt.as<uint32_t>(), y);
   if (it == 0) {  // the reduce gathers the reference normals (stream r2, scattered into matcher order)
     HIPC(hipStreamWaitEvent(st, sl.ev_s2, 0));
-    launch_pairs_degenerate_part(st, (int)q.np, gd, gs, dRst, 1);
+    launch_pairs_degenerate_part(st, (int)np, dDesc, dState, dRst, 1);
   }
-  launch_icp_reduce_f(st, q.mred, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
+  launch_icp_reduce_f(st, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
                       sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>(), ip, y);
   HIPC(hipGetLastError());
   for (int k : {hn_this ? it : -1, hn_next ? it + 1 : -1})
     if (k >= 0) {
-      HIPC(hipEventRecord(sl.ev_poll[q.g * kMaxPolls + k], st));
+      HIPC(hipEventRecord(sl.ev_poll[k], st));
       q.pending.push_back(k);
     }
   ++q.it;
@@ -1098,46 +1043,31 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   return AICP_OK;
 }
 
-// the group's corrections (and, once both groups are done, the window's commit and ev_done)
-static int loop_finish(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_params* prm, IcpLoop& q, int n_loops) {
+// the window's corrections, its commit to the sequence's arrays and ev_done
+static int loop_finish(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_params* prm, IcpLoop& q) {
   WinRun& R = *q.R;
   WIN_REFS;
-  launch_finalize(q.st, (int)q.np, dDesc + q.p0, dState + q.p0, dOutT + 16 * q.p0);
+  hipStream_t st = S->s_icp;
+  launch_finalize(st, (int)np, dDesc, dState, dOutT);
+  if (R.tev) HIPC(hipEventRecord(R.tev[4], st));
+  launch_seq_commit(st, (int)np, dDesc, dState, dOutT, S->desc.as<PairDesc>() + w.p0, S->state.as<PairState>() + w.p0,
+                    S->outT.as<float>() + 16 * w.p0);
   HIPC(hipGetLastError());
-  if (q.g == 0) {
-    HIPC(hipEventRecord(sl.ev_crit, q.st));
-    sl.crit_early = q.stop_poll >= 0 && seq_early_ref();
-    sl.crit_wait = sl.crit_early ? sl.ev_poll[q.g * kMaxPolls + q.stop_poll] : sl.ev_crit;
-    if (R.tev) HIPC(hipEventRecord(R.tev[4], q.st));
-  }
-  if (q.g + 1 < n_loops) return AICP_OK;  // group 1 commits the window
-  if (q.g == 1) HIPC(hipStreamWaitEvent(q.st, sl.ev_crit, 0));
-  launch_seq_commit(q.st, (int)np, dDesc, dState, dOutT, S->desc.as<PairDesc>() + w.p0,
-                    S->state.as<PairState>() + w.p0, S->outT.as<float>() + 16 * w.p0);
-  HIPC(hipGetLastError());
-  HIPC(hipEventRecord(sl.ev_done, q.st));
+  HIPC(hipEventRecord(sl.ev_done, st));
   return AICP_OK;
 }
 
 // the oldest poll of the loop (got: it was read; q.stop set when it read 0)
-static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool block, bool& got) {
+static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool& got) {
   got = false;
   SeqSlot& sl = S->slot[q.R->w.slot];
   const int k = q.pending.front();
-  hipEvent_t e = sl.ev_poll[q.g * kMaxPolls + k];
-  if (block) {
-    HIPC(hipEventSynchronize(e));
-  } else {
-    const hipError_t r = hipEventQuery(e);
-    if (r == hipErrorNotReady) return AICP_OK;
-    HIPC(r);
-  }
+  const hipError_t r = hipEventQuery(sl.ev_poll[k]);
+  if (r == hipErrorNotReady) return AICP_OK;
+  HIPC(r);
   q.pending.pop_front();
   got = true;
-  if (sl.poll_host[q.g * kMaxPolls + k] == 0) {
-    q.stop = true;
-    q.stop_poll = k;
-  }
+  if (sl.poll_host[k] == 0) q.stop = true;
   return AICP_OK;
 }
 
@@ -1154,38 +1084,18 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     // the third high-priority one; uploads and the reading side share one low-priority stream.
     HIPC(hipStreamCreateWithPriority(&S->s_rd, hipStreamNonBlocking, lo));
     HIPC(hipStreamCreateWithPriority(&S->s_icp, hipStreamNonBlocking, hi));
-    // the non-critical ICP loops (AICP_SEQ_SPLIT=1); AICP_SEQ_ICP2_CUS=k in 1..7 restricts that
-    // stream to k of every 8 CUs (hipExtStreamCreateWithCUMask), leaving the rest to the critical path
-    const char* cm = std::getenv("AICP_SEQ_ICP2_CUS");
-    const int k8 = cm ? std::atoi(cm) : 8;
-    if (k8 >= 1 && k8 <= 7) {
-      int ncu = 0;
-      HIPC(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-      for (int c = 0; c < ncu; ++c)
-        if (c % 8 < k8) mask[c / 32] |= 1u << (c % 32);
-      HIPC(hipExtStreamCreateWithCUMask(&S->s_icp2, (uint32_t)mask.size(), mask.data()));
-    } else {
-      HIPC(hipStreamCreateWithPriority(&S->s_icp2, hipStreamNonBlocking, lo));
-    }
     S->s_up = S->s_rd;
     S->s_r2 = ctx->stream2;
     S->s_r3 = ctx->stream3;
-    if (const char* e = std::getenv("AICP_SEQ_R3_PRIO")) {  // A/B: the matcher-tree stream at priority lo|hi of its own
-      HIPC(hipStreamCreateWithPriority(&S->s_r3_own, hipStreamNonBlocking, e[0] == 'l' ? lo : hi));
-      S->s_r3 = S->s_r3_own;
-    }
     for (SeqSlot& sl : S->slot) {
-      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done, &sl.ev_crit, &sl.ev_setup,
-                            &sl.ev_ovl})
+      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
       for (hipEvent_t& e : sl.ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIPC(hipHostMalloc((void**)&sl.poll_host, 2 * kMaxPolls * 4, hipHostMallocMapped));
+      HIPC(hipHostMalloc((void**)&sl.poll_host, kMaxPolls * 4, hipHostMallocMapped));
       HIPC(hipHostGetDevicePointer((void**)&sl.poll_dev, sl.poll_host, 0));
     }
     HIPC(hipEventCreate(&S->ev_begin));
     HIPC(hipEventCreate(&S->ev_end));
-    HIPC(hipEventCreateWithFlags(&S->ev_icp2, hipEventDisableTiming));
     (void)hipGetLastError();
   }
   SeqState* S = ctx->seq;
@@ -1233,11 +1143,20 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
   for (size_t i = 0; i < n; ++i)
     if (!valid(readings[i])) FAIL(AICP_ERR_INVALID, "invalid reading " + std::to_string(i));
   if ((size_t)F > (size_t)kMaxPairs) FAIL(AICP_ERR_UNSUPPORTED, "reference_update_frequency above 4096");
+  {  // a window holds at most F consecutive readings: their points index 32-bit offsets
+    uint64_t run = 0;
+    for (size_t i = 0; i < n; ++i) {
+      run += readings[i].n;
+      if (i >= (size_t)F) run -= readings[i - F].n;
+      if (run >= (1ull << 31)) FAIL(AICP_ERR_UNSUPPORTED, "a window's readings exceed 2^31 points");
+    }
+  }
   if (n == 0) return AICP_OK;
   HIPC(hipSetDevice(ctx->device));
   rc = seq_init(ctx, n);
   if (rc) return rc;
   SeqState* S = ctx->seq;
+  S->last = aicp_sequence_timing{};  // (an error return leaves no stale timing behind)
   const bool timeNN = prm->flags & AICP_RUN_TIME_NN;
   int nn_launches = 0, windows = 0, replans = 0;
   HIPC(hipEventRecord(S->ev_begin, S->s_up));
@@ -1283,7 +1202,6 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         const size_t off = (size_t)w.src - pw.p0;
         runs[k].src_desc = S->slot[pw.slot].wdesc.as<PairDesc>() + off;
         runs[k].src_T = S->slot[pw.slot].woutT.as<float>() + 16 * off;
-        runs[k].src_st = S->slot[pw.slot].wstate.as<PairState>() + off;
       } else if (w.src >= 0) {  // a reading of an earlier pass: committed
         runs[k].src_desc = S->desc.as<PairDesc>() + w.src;
         runs[k].src_T = S->outT.as<float>() + 16 * (size_t)w.src;
@@ -1308,57 +1226,38 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       return r;
     };
     // The reading side of window k + 1 (Morton order, voxel maps) is enqueued with its upload,
-    // before window k's loop. (AICP_SEQ_READ_LATE=1 enqueues it with the next reference instead, to
-    // keep it off the loop's CUs: measured 2.29 against 2.20 ms per window, since it then slows
-    // the kd-tree builds on the critical path.)
-    const bool read_early = seq_read_early();
+    // during window k's loop. (Enqueued with the next reference instead, to keep it off the loop's
+    // CUs, it slowed the kd-tree builds on the critical path: 2.29 against 2.20 ms per window.)
     auto read_side = [&](size_t k) { return win_read_side(ctx, S, cfg, prm, runs[k]); };
-    // ICP loops (win_loops): the critical loop of the current window, and the non-critical loops
-    // of earlier windows in order on stream icp2 (only the front one is iterated)
-    const bool split = seq_split();
-    std::vector<std::array<IcpLoop, 2>> loops(plan.size());
-    std::vector<int> n_loops(plan.size(), 0);
+    std::vector<IcpLoop> loops(plan.size());
     std::vector<uint8_t> done_enq(plan.size(), 0);  // the window's ev_done recorded
-    std::deque<IcpLoop*> rest;
-    auto advance = [&](IcpLoop* q, bool& progress) -> int {
-      const int nl = n_loops[q->R->w.index];
-      if (q->g == 1 && q->it == 0 && q->pending.empty() && !q->stop) {
-        SeqSlot& sl = S->slot[q->R->w.slot];
-        if (hipStreamWaitEvent(q->st, sl.ev_setup, 0) != hipSuccess) return AICP_ERR_HIP;
-      }
+    // enqueue iterations while the host is less than one iteration ahead of the oldest poll, read
+    // the polls that have completed, finish the loop once one reads 0
+    auto advance = [&](IcpLoop& q, bool& progress) -> int {
       for (;;) {
-        while (!q->stop && (q->pending.empty() || q->it - q->pending.front() < lookahead())) {
-          const int r = loop_iteration(ctx, S, cfg, prm, *q, timeNN, nn_launches);
+        while (!q.stop && (q.pending.empty() || q.it - q.pending.front() < 1)) {
+          const int r = loop_iteration(ctx, S, cfg, prm, q, timeNN, nn_launches);
           if (r) return r;
           progress = true;
         }
-        if (q->stop || q->pending.empty()) break;
+        if (q.stop || q.pending.empty()) break;
         bool got = false;
-        const int r = loop_poll(ctx, S, *q, false, got);
+        const int r = loop_poll(ctx, S, q, got);
         if (r) return r;
         if (!got) break;
         progress = true;
       }
-      if (q->stop && q->it >= 0) {
-        const int r = loop_finish(ctx, S, prm, *q, nl);
+      if (q.stop && q.it >= 0) {
+        const int r = loop_finish(ctx, S, prm, q);
         if (r) return r;
-        if (q->g + 1 == nl) done_enq[q->R->w.index] = 1;
-        q->it = -1;  // finished
+        done_enq[q.R->w.index] = 1;
+        q.it = -1;  // finished
         progress = true;
       }
       return AICP_OK;
     };
-    auto drive_rest = [&](bool& progress) -> int {
-      while (!rest.empty()) {
-        const int r = advance(rest.front(), progress);
-        if (r) return r;
-        if (rest.front()->it >= 0) break;
-        rest.pop_front();
-      }
-      return AICP_OK;
-    };
     // upload(k + 1) reuses the slot of window k - 2 and waits (on the device) for ev_done of
-    // window k - 1, which exists once that window's last loop has been finished here
+    // window k - 1, which exists once that window's loop has been finished here
     auto can_upload = [&](size_t k) { return k + 1 < plan.size() && (k < 1 || done_enq[k - 1]); };
     rc = timed(0, [&] { return upload(0); });
     if (!rc) rc = timed(0, [&] { return read_side(0); });
@@ -1367,58 +1266,34 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     for (size_t k = 0; k < plan.size() && !rc; ++k) {
       const bool next = k + 1 < plan.size();
       bool uploaded = !next;
+      // (the next window's upload -- host packing of its readings -- goes after this window's first
+      // iterations are enqueued: before them it delayed the loop start on the host by ~0.4 ms)
       auto try_upload = [&]() -> int {
         if (uploaded || !can_upload(k)) return AICP_OK;
         uploaded = true;
         int r = timed(0, [&] { return upload(k + 1); });
-        if (!r && read_early) r = timed(0, [&] { return read_side(k + 1); });
+        if (!r) r = timed(0, [&] { return read_side(k + 1); });
         return r;
       };
-      // (the next window's upload -- host packing of its readings -- goes after this window's first
-      // iterations are enqueued: before them it delayed the loop start on the host by ~0.4 ms)
-      if (!seq_upload_late()) rc = try_upload();
-      if (rc) break;
-      rc = win_loops(S, runs[k], split && next, loops[k].data(), n_loops[k]);
-      if (rc) break;
       if (runs[k].tev) {
         rc = hipEventRecord(runs[k].tev[3], S->s_icp) == hipSuccess ? AICP_OK : AICP_ERR_HIP;
         if (rc) break;
       }
-      IcpLoop* crit = &loops[k][0];
-      if (n_loops[k] == 2) rest.push_back(&loops[k][1]);
+      IcpLoop& q = loops[k];
+      q.R = &runs[k];
       rc = timed(2, [&]() -> int {
-        while (crit->it >= 0) {
+        while (q.it >= 0) {
           bool progress = false;
-          int r = advance(crit, progress);
-          if (!r) r = drive_rest(progress);
+          int r = advance(q, progress);
           if (!r) r = try_upload();
           if (r) return r;
           if (!progress) std::this_thread::yield();
         }
-        // the next window's upload needs the previous window's ev_done
-        while (!uploaded && !rc) {
-          bool progress = false;
-          int r = drive_rest(progress);
-          if (!r) r = try_upload();
-          if (r) return r;
-          if (!progress) std::this_thread::yield();
-        }
-        return AICP_OK;
+        return try_upload();
       });
       if (!rc && next) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
-      if (!rc && next && !read_early) rc = timed(0, [&] { return read_side(k + 1); });
       if (!rc && next) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
       ++windows;
-    }
-    while (!rc && !rest.empty()) {
-      bool progress = false;
-      rc = drive_rest(progress);
-      if (!rc && !progress) std::this_thread::yield();
-    }
-    if (!rc) {  // the read-back (stream icp) after every non-critical loop (stream icp2)
-      rc = hipEventRecord(S->ev_icp2, S->s_icp2) == hipSuccess && hipStreamWaitEvent(S->s_icp, S->ev_icp2, 0) == hipSuccess
-               ? AICP_OK
-               : AICP_ERR_HIP;
     }
     if (prof)
       std::fprintf(stderr, "[aicp seq] host ms: upload %.2f reference %.2f icp(incl. polls) %.2f over %zu windows\n",
@@ -1436,7 +1311,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     HIPC(hipEventRecord(S->ev_end, S->s_icp));
     rc = seq_sync(ctx, S);
     if (rc) return rc;
-    if (std::getenv("AICP_ITER_PROF_DUMP")) {
+    if (prof) {  // diagnostic builds' counters (-DAICP_ITER_PROF)
       iter_prof_dump();
       tree_prof_dump();
     }

@@ -23,9 +23,14 @@
 //     resolution read as float (yaml_configurator.cpp:81); App ignores the returned tree
 //     (app.cpp:132-135), so nullptr is returned.
 //
-// AbstractRegistrator / AbstractOverlapper have no virtual destructor and the factories delete
-// through the base pointer, so the shims own nothing that needs a destructor to run: the HIP
-// context is one per process (hip_shared_ctx), created on first use.
+// Ownership. AbstractRegistrator / AbstractOverlapper declare no virtual destructor, and the
+// factories return std::unique_ptr to the base, so deleting a shim skips its members'
+// destructors: HipRegistration's RegistrationParams strings and the reading copy (read_xyz_),
+// HipOverlapper's OverlapParams. That leaks those host allocations once per registrator, as the
+// reference's PointmatcherRegistration leaks its DataPoints members the same way. App creates
+// one of each per process (app.cpp:32-34), so this is bounded; a maintainer removes it upstream
+// by adding `virtual ~AbstractRegistrator() = default;` (and the same to AbstractOverlapper).
+// Device memory is not involved: the HIP context is one per process (hip_shared_ctx).
 #ifndef AICP_HIP_REGISTRATION_HPP_
 #define AICP_HIP_REGISTRATION_HPP_
 
@@ -84,14 +89,14 @@ class HipRegistration : public AbstractRegistrator {
 
   void registerClouds(pcl::PointCloud<pcl::PointXYZ>& cloud_ref, pcl::PointCloud<pcl::PointXYZ>& cloud_read,
                       Eigen::Matrix4f& final_transform) override {
-    run(&cloud_ref.points[0].x, cloud_ref.width, sizeof(pcl::PointXYZ), &cloud_read.points[0].x, cloud_read.width,
+    run(first_x(cloud_ref), cloud_ref.width, sizeof(pcl::PointXYZ), first_x(cloud_read), cloud_read.width,
         sizeof(pcl::PointXYZ), final_transform);
   }
 
   void registerClouds(pcl::PointCloud<pcl::PointXYZRGB>& cloud_ref, pcl::PointCloud<pcl::PointXYZRGB>& cloud_read,
                       Eigen::Matrix4f& final_transform) override {
     // fromPCLToDataPoints keeps x, y, z only: the 32-B rows are read in place
-    run(&cloud_ref.points[0].x, cloud_ref.width, sizeof(pcl::PointXYZRGB), &cloud_read.points[0].x, cloud_read.width,
+    run(first_x(cloud_ref), cloud_ref.width, sizeof(pcl::PointXYZRGB), first_x(cloud_read), cloud_read.width,
         sizeof(pcl::PointXYZRGB), final_transform);
   }
 
@@ -115,6 +120,13 @@ class HipRegistration : public AbstractRegistrator {
   }
 
   const aicp_icp_stats& lastStats() const { return stats_; }
+
+  // &points[0].x, or nullptr for an empty cloud (points[0] of an empty vector is undefined);
+  // the C-ABI rejects a null cloud with AICP_ERR_INVALID, which throws below
+  template <class P>
+  static const float* first_x(const pcl::PointCloud<P>& c) {
+    return c.points.empty() ? nullptr : &c.points[0].x;
+  }
 
  private:
   static void to_cloud(const std::vector<float>& xyz, pcl::PointCloud<pcl::PointXYZ>& out) {
@@ -180,10 +192,10 @@ class HipOverlapper : public AbstractOverlapper {
                               Eigen::Isometry3d ref_pose, Eigen::Isometry3d read_pose,
                               ColorOcTree* /*reading_tree*/) override {
     aicp_pair p{};
-    p.ref = &ref_cloud.points[0].x;
+    p.ref = HipRegistration::first_x(ref_cloud);
     p.n_ref = ref_cloud.width;
     p.ref_stride = sizeof(pcl::PointXYZ);
-    p.read = &read_cloud.points[0].x;
+    p.read = HipRegistration::first_x(read_cloud);
     p.n_read = read_cloud.width;
     p.read_stride = sizeof(pcl::PointXYZ);
     for (int k = 0; k < 3; ++k) {

@@ -825,13 +825,14 @@ float quantile_impl(std::vector<float>& values, float quantile, int32_t* err) {
 struct OcGeom {
   double resolution, resolution_factor;
   static constexpr int tree_max_val = 32768;
+  // ((int)floor(factor * c)) + tree_max_val in [0, 2 * tree_max_val): x86's conversion gives
+  // INT_MIN for NaN and out-of-range values, so those are rejected; the test is written on the
+  // double to keep that behaviour without relying on the conversion
   bool coordToKeyChecked(double coordinate, uint32_t& key) const {
-    const int scaled = ((int)std::floor(resolution_factor * coordinate)) + tree_max_val;
-    if (scaled >= 0 && ((unsigned)scaled) < (unsigned)(2 * tree_max_val)) {
-      key = (uint32_t)scaled;
-      return true;
-    }
-    return false;
+    const double f = std::floor(resolution_factor * coordinate);
+    if (!(f >= -(double)tree_max_val && f < (double)tree_max_val)) return false;
+    key = (uint32_t)((int)f + tree_max_val);
+    return true;
   }
   bool coordToKeyChecked(const float* c, uint32_t* k) const {
     for (int i = 0; i < 3; ++i)

@@ -125,6 +125,23 @@ static int gpu_mode(int argc, char** argv) {
     read_pose.translation()(k) = std::atof(argv[8 + k]);
   }
   ovl->computeOverlap(ref_c, read_c, ref_pose, read_pose, nullptr);  // app.cpp:132-135
+  // an empty cloud: no points[0] access, the C-ABI's AICP_ERR_INVALID surfaces as an exception
+  pcl::PointCloud<pcl::PointXYZ> empty;
+  Eigen::Matrix4f T_empty;
+  bool threw = false;
+  try {
+    reg->registerClouds(empty, read_c, T_empty);
+  } catch (const std::runtime_error&) {
+    threw = true;
+  }
+  if (!threw) return fail("empty reference must throw");
+  threw = false;
+  try {
+    ovl->computeOverlap(ref_c, empty, ref_pose, read_pose, nullptr);
+  } catch (const std::runtime_error&) {
+    threw = true;
+  }
+  if (!threw) return fail("empty reading in the overlap must throw");
   std::printf("T");
   for (int k = 0; k < 16; ++k) std::printf(" %.9g", T.data()[k]);
   std::printf("\nT_rgb");

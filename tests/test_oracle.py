@@ -386,3 +386,36 @@ def test_icp_planar_scan_uses_min_norm_path(oracle):
     paths = [st.solve_path[i] for i in range(st.iterations)]
     assert 1 in paths or 2 in paths
     assert abs(Tout[2, 3]) < 1e-4  # unobservable z stays put (min-norm solution)
+
+
+def test_c2_stall_is_the_epsilon_approximation(oracle):
+    """The C2 stream's first pair (the first cloud vs reading 0, 120k points each; VERDICT r03
+    item 2). With libnabo's approximate search (eps 3.16) the Differential checker stops ICP
+    after ~10 iterations 0.025 rad / 0.13 m from the ground truth: the approximate matches
+    move T by less than 1e-3 rad / 1e-2 m per step. Removing the approximation (eps 0)
+    converges towards the ground truth in the oracle and in the independent numpy restatement
+    alike, so the stall is the chain's behaviour, not a bug shared by oracle and device."""
+    ref, o_ref = sy.stream_first(1, 120000)
+    read, o_read, T_gt = sy.stream_reading(1, 0, 120000)
+    ov, _ = oracle.overlap(ref, o_ref, read, o_read, float(np.float32(0.2)))
+    ratio = oracle.autotune_ratio(ov)
+    # eps 3.16 (the default chain): stops early, far from T_gt
+    rc, T_eps, st_eps = oracle.icp(ref, read, oracle.default_config(trimmed_ratio=ratio))
+    assert rc == 0 and st_eps.converged == 1 and st_eps.iterations < 20
+    r, t = sy.rot_err(T_gt, T_eps)
+    assert r > 0.01 and t > 0.05, (r, t)
+    # eps 0: oracle and numpy agree and approach T_gt within the 20 iterations
+    rc, T0, st0 = oracle.icp(ref, read, oracle.default_config(trimmed_ratio=ratio, nn_epsilon=0.0))
+    assert rc == 0
+    Tn, itn = numpy_icp(ref, read, ratio)
+    r, t = sy.rot_err(Tn, T0)
+    assert r < 2e-5 and t < 2e-4, (r, t)
+    assert abs(st0.iterations - itn) <= 1
+    for T in (T0, Tn):
+        r, t = sy.rot_err(T_gt, T)
+        assert r < 1e-3 and t < 1e-2, (r, t)
+    # and eps 3.16 given more iterations (checker off) gets there too: slow, not wrong
+    rc, T60, _ = oracle.icp(ref, read, oracle.default_config(trimmed_ratio=ratio, max_iter=60, min_diff_rot=1e-9,
+                                                             min_diff_trans=1e-9))
+    r, t = sy.rot_err(T_gt, T60)
+    assert rc == 0 and r < 1e-3 and t < 2e-3, (r, t)

@@ -163,43 +163,57 @@ def test_sequence_c2_full_size(ctx, oracle, L):
         assert out[i]["icp"]["iterations"] == ref[k]["stats"].iterations
 
 
-def test_sequence_split_loops_identical(ctx, L, monkeypatch):
-    """AICP_SEQ_SPLIT=1 runs each window's last reading (the next reference's source) in a loop
-    of its own on stream icp and the other readings on stream icp2. Every pair's
-    arithmetic is per pair, so the two schedules give bit-identical corrections and statistics,
-    also across a dropped reading (re-plan)."""
-    st = sy.make_stream(n_readings=12, n_points=5000, seed=8, half=18.0, jumps={2: (0.6, 0, 0), 6: (0, -0.6, 0)})
-    prm = L.default_sequence_params(max_correction_magnitude=0.4)  # readings 2 and 6 drop: two re-plans
-    monkeypatch.delenv("AICP_SEQ_SPLIT", raising=False)
-    T0, out0, done0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
-    monkeypatch.setenv("AICP_SEQ_SPLIT", "1")
-    T1, out1, done1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
-    assert (rc0, done0) == (rc1, done1) == (0, 12)
-    assert sum(1 - o["accepted"] for o in out1) == 2
-    assert np.array_equal(T0, T1)
-    for a, b in zip(out0, out1):
-        assert a["accepted"] == b["accepted"] and a["reference"] == b["reference"]
-        assert a["icp"]["iterations"] == b["icp"]["iterations"]
-        assert a["icp"]["nn_points_touched"] == b["icp"]["nn_points_touched"]
 
-
-@pytest.mark.parametrize("early", ["0", "1"])
-def test_sequence_early_reference_identical(ctx, L, monkeypatch, early):
-    """The next reference waits for the poll that found the window's loop finished and composes
-    the source's correction from its state (AICP_SEQ_EARLY_REF=1), or waits for the loop's end
-    and reads the finalize output (=0, the default). Both give the corrections of the split and
-    polled-off schedules bit for bit, across dropped readings."""
+def test_sequence_polled_loop_identical(ctx, L, monkeypatch):
+    """The polled loop (the host stops enqueueing a window's iterations once the update kernel
+    reports no active reading) gives the corrections and statistics of the unpolled schedule,
+    which runs maxIterationCount launches per window (AICP_SEQ_NO_EARLY_EXIT=1), bit for bit,
+    across dropped readings and re-plans."""
     st = sy.make_stream(n_readings=12, n_points=5000, seed=8, half=18.0, jumps={2: (0.6, 0, 0), 6: (0, -0.6, 0)})
     prm = L.default_sequence_params(max_correction_magnitude=0.4)  # readings 2 and 6 drop
-    monkeypatch.setenv("AICP_SEQ_NO_EARLY_EXIT", "1")  # no polls: the next reference after the loop
+    monkeypatch.setenv("AICP_SEQ_NO_EARLY_EXIT", "1")
     T0, out0, done0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
     monkeypatch.delenv("AICP_SEQ_NO_EARLY_EXIT")
-    monkeypatch.setenv("AICP_SEQ_EARLY_REF", early)
     T1, out1, done1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
     assert (rc0, done0) == (rc1, done1) == (0, 12)
     assert sum(1 - o["accepted"] for o in out1) == 2
+    assert ctx.last_sequence_timing()["replans"] == 2
     assert np.array_equal(T0, T1)
     for a, b in zip(out0, out1):
         assert a["accepted"] == b["accepted"] and a["reference"] == b["reference"]
         assert a["icp"]["iterations"] == b["icp"]["iterations"]
         assert a["icp"]["nn_points_touched"] == b["icp"]["nn_points_touched"]
+
+def test_sequence_far_return_sparse_overlap(ctx, oracle, L):
+    """One lidar return ~5 km away (octomap's insertPointCloud takes any key in range,
+    octrees_overlap.cpp:184): in reading 1 (a plain reading) and in reading 4 (window 0's last,
+    the source of window 1's reference). Its key box is ~10^10 voxels, so those windows' overlaps
+    take the sorted-key path (sequence.cpp, kSeqMapBudget) instead of failing: key counts exact,
+    the same decisions and references, transforms within 1e-6 rad / 1e-5 m."""
+    st = sy.make_stream(n_readings=10, n_points=5000, seed=12, half=18.0)
+    for i in (1, 4):
+        far = (np.asarray(st.origins[i], np.float64) + (3000.0, 4000.0, 25.0)).astype(np.float32)
+        st.readings[i] = np.r_[st.readings[i], far[None]].astype(np.float32)
+    T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins)
+    assert rc == 0 and done == 10
+    ref = oracle.sequence(st.first, st.first_origin, st.readings, st.origins, resolution=RES)
+    _compare(out, ref, T)
+    assert [i for i, o in enumerate(out) if o["is_reference"]] == [4, 9]
+    # the far ray's keys are in the counts: reading 1's set is ~25k keys larger than its neighbours'
+    assert out[1]["icp"]["overlap_keys"][1] > out[0]["icp"]["overlap_keys"][1] + 20000
+
+
+def test_sequence_sparse_overlap_identical(ctx, L, monkeypatch):
+    """Every window on the sorted-key path (AICP_OVL_SPARSE=1) gives the dense maps' key counts
+    and corrections bit for bit, across dropped readings and re-plans."""
+    st = sy.make_stream(n_readings=12, n_points=5000, seed=8, half=18.0, jumps={2: (0.6, 0, 0), 6: (0, -0.6, 0)})
+    prm = L.default_sequence_params(max_correction_magnitude=0.4)
+    monkeypatch.delenv("AICP_OVL_SPARSE", raising=False)
+    T0, out0, done0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    monkeypatch.setenv("AICP_OVL_SPARSE", "1")
+    T1, out1, done1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    assert (rc0, done0) == (rc1, done1) == (0, 12)
+    assert np.array_equal(T0, T1)
+    for a, b in zip(out0, out1):
+        assert a["icp"]["overlap_keys"] == b["icp"]["overlap_keys"]
+        assert a["accepted"] == b["accepted"] and a["reference"] == b["reference"]
