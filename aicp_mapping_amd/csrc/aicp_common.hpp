@@ -172,7 +172,6 @@ struct IcpParams {
   float min_rot, min_trans;
   int32_t knn_normals;
   int32_t prof_slot;  // diagnostic builds (AICP_XCD_PROF): the launch's record slot
-  int32_t interleave; // NN chunks dealt to the XCD groups round-robin instead of in contiguous ranges
 };
 
 }  // namespace aicp

@@ -880,16 +880,13 @@ __device__ unsigned long long g_iter_prof[16];
 template <class Eng, class OnChunk, class Fetch, class Done>
 __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, float maxE2, float maxR2,
                                                const uint4* __restrict__ nodes, const float4* __restrict__ pts,
-                                               OnChunk&& on_chunk, Fetch&& fetch, Done&& done,
-                                               bool interleave = false) {
+                                               OnChunk&& on_chunk, Fetch&& fetch, Done&& done) {
   const int lane = threadIdx.x & 63;
   const uint32_t g = blockIdx.x % kXcdGroups;
-  // contiguous: group g serves slots [lo, hi) (its references stay in its XCD's L2); interleaved:
-  // group g serves the 64-slot chunks c with c % kXcdGroups == g (a spatially clustered run of
-  // expensive queries is spread over all XCDs instead of making one group the straggler)
-  const uint32_t lo = interleave ? 0u : (uint32_t)(((uint64_t)total * g) / kXcdGroups) & ~63u;
-  const uint32_t hi =
-      interleave || g + 1 == kXcdGroups ? total : (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups) & ~63u;
+  // group g serves slots [lo, hi) (its data stays in its XCD's L2). (Chunks dealt to the groups
+  // round-robin instead measured equal on C2 windows, r03.)
+  const uint32_t lo = (uint32_t)(((uint64_t)total * g) / kXcdGroups) & ~63u;
+  const uint32_t hi = g + 1 == kXcdGroups ? total : (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups) & ~63u;
   uint32_t* gctr = ctr + g * kCtrStride;
   Eng t;
   FarStack fs;
@@ -917,7 +914,7 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       if (pool >= pool_end) {
         uint32_t base = 0;
         if (lane == 0)
-          base = interleave ? (g + kXcdGroups * atomicAdd(gctr, 1u)) * 64u : lo + atomicAdd(gctr, 64u);
+          base = lo + atomicAdd(gctr, 64u);
         base = __builtin_amdgcn_readfirstlane(base);
         if (base >= hi) {
           exhausted = true;
@@ -1069,7 +1066,10 @@ __device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, c
     const int p = base + t;
     const bool a = p < n_pairs && st[p].active;
     // each pair's slot range is padded to a multiple of 64: a 64-slot chunk of the NN work space
-    // then belongs to one pair, whose parameters the wave keeps in scalar registers
+    // then belongs to one pair, whose parameters the wave keeps in scalar registers. (r04: each
+    // XCD group serving the g-th eighth of every pair's Morton-ordered readings, so that a stream
+    // window's XCD touches ~1/8 of the reference tree, measured equal on C2 (87 us per launch)
+    // and 4 % slower on C5: the NN launch is bound by its queries' latency chains, not by L2 misses.)
     const uint32_t v = a ? (pd[p].n_read + 63u) & ~63u : 0u;
     uint32_t x = v, c = a ? 1u : 0u;
 #pragma unroll
@@ -1614,8 +1614,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
         match[qidx] = t.res_id();
         d2out[qidx] = t.res_d2();
         touched[qidx] = (min(t.tn, 65535u) << 16) | min(t.tp, 65535u);
-      },
-      prm.interleave != 0);
+      });
 #if AICP_XCD_PROF
   // per launch slot and XCD group: earliest wave start, latest wave end (100 MHz clock)
   const uint64_t xt1 = __builtin_amdgcn_s_memrealtime();
