@@ -23,6 +23,7 @@ AICP_ERR_TRANSFORMATION = 5
 AICP_RUN_OVERLAP = 1
 AICP_RUN_ICP = 2
 AICP_RUN_TIME_NN = 4
+AICP_SEQ_DEBUG = 8  # aicp_sequence_params.flags: App's "debug" working_mode
 
 EXPORTS = [
     "aicp_hip_create", "aicp_hip_destroy", "aicp_hip_last_error", "aicp_hip_version",

@@ -236,9 +236,9 @@ struct OvlKeySide {
 };
 size_t ovl_keys_temp_bytes(size_t n_points, size_t cap, int n_clouds);
 // keys of the side's clouds (points at pts + clouds[c].pts_off), sorted; |S_c| into
-// st[c].ovl_counts[slot]; origin_of0 (nullable): clouds[0].origin := origin_of0->ref_origin first.
+// st[c].ovl_counts[slot]; origin0 (nullable, 3 device doubles): clouds[0].origin := origin0 first.
 // A cloud whose keys exceed cap reports st[c].ovl_err.
-hipError_t launch_ovl_keys(hipStream_t s, const OvlKeySide& k, const PairDesc* origin_of0, const float4* pts,
+hipError_t launch_ovl_keys(hipStream_t s, const OvlKeySide& k, const double* origin0, const float4* pts,
                            double res, PairState* st, int slot);
 // |A ∩ B| of every reading of rd against the reference side (one cloud) into st[p].ovl_counts[2]
 hipError_t launch_ovl_keys_intersect(hipStream_t s, const OvlKeySide& rd, const OvlKeySide& ref,
@@ -254,6 +254,11 @@ void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState
                        PairState* gst, float* gT);
 // a[0, na), b[0, nb), c[0, nc) = 0 in one launch
 void launch_zero_words3(hipStream_t s, uint32_t* a, size_t na, uint32_t* b, size_t nb, uint32_t* c, size_t nc);
+// debug working mode (app.cpp:87-96, 414), one thread each: hist := initT, d's prior origin :=
+// translation of initT * prior pose; then outT := d's correction and, if it is accepted,
+// initT := correction * initT
+void launch_debug_prep(hipStream_t s, PairDesc* d, const float* initT, float* hist);
+void launch_debug_post(hipStream_t s, const PairDesc* d, PairState* st, float* outT, float* initT, float max_corr);
 // od[i] (min, dim, bytes) from st[i].ovl_bbox; od[i].off preset; bytes > cap[i]: ovl_err, empty map
 void launch_ovl_size(hipStream_t s, int n, PairState* st, OvlDesc* od, const uint64_t* cap);
 // zero the n maps of od[] (device-side sizes, each at most max_bytes)

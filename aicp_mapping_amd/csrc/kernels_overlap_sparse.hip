@@ -176,9 +176,10 @@ __global__ void k_spo_counts(int n_groups, int n_pairs, const unsigned long long
 // (no read-back of the true count: the stream stays free of host synchronisation); the words
 // past the true total are padding (n_clouds << 48, sorted last, never counted).
 
-// the reference's origin, written on the device by k_seq_next_ref
-__global__ void k_spo_origin(OvlCloud* c, const PairDesc* __restrict__ g) {
-  if (threadIdx.x < 3) c->origin[threadIdx.x] = g->ref_origin[threadIdx.x];
+// a cloud's origin written on the device: the reference's by k_seq_next_ref, a debug-mode
+// reading's by k_debug_prep
+__global__ void k_spo_origin(OvlCloud* c, const double* __restrict__ o) {
+  if (threadIdx.x < 3) c->origin[threadIdx.x] = o[threadIdx.x];
 }
 
 __global__ __launch_bounds__(256) void k_spo_emit_cap(const uint32_t* __restrict__ blk_cloud,
@@ -320,9 +321,9 @@ size_t ovl_keys_temp_bytes(size_t n_points, size_t cap, int n_clouds) {
   return a > b ? a : b;
 }
 
-hipError_t launch_ovl_keys(hipStream_t s, const OvlKeySide& k, const PairDesc* origin_of0, const float4* pts,
+hipError_t launch_ovl_keys(hipStream_t s, const OvlKeySide& k, const double* origin0, const float4* pts,
                            double res, PairState* st, int slot) {
-  if (origin_of0) k_spo_origin<<<1, 64, 0, s>>>(k.clouds, origin_of0);
+  if (origin0) k_spo_origin<<<1, 64, 0, s>>>(k.clouds, origin0);
   if (k.n_blocks) {
     k_spo_count<<<k.n_blocks, 256, 0, s>>>(k.blk_cloud, k.blk_start, k.clouds, pts, pts, res, k.cnt);
     size_t b = k.temp_bytes;

@@ -27,6 +27,39 @@ __global__ void k_seq_next_ref(PairDesc* gd, const PairDesc* __restrict__ src, c
   for (int k = 0; k < 3; ++k) gd->ref_origin[k] = o[k];
 }
 
+// App's debug working mode (app.cpp:87-96): before reading d is registered, initT (initialT_) is
+// kept in hist (its value before this reading, for a re-plan) and the reading's prior pose
+// becomes initialT_ * prior pose: its translation is the overlap's sensor origin
+// (fromMatrix4fToIsometry3d, common.cpp:4-23, as for a correction). The points follow with
+// k_transform(initT).
+__global__ void k_debug_prep(PairDesc* d, const float* initT, float* hist) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float T[16];
+  for (int k = 0; k < 16; ++k) T[k] = initT[k];
+  for (int k = 0; k < 16; ++k) hist[k] = T[k];
+  double o[3];
+  corrected_origin(T, d->read_origin, o);
+  for (int k = 0; k < 3; ++k) d->read_origin[k] = o[k];
+}
+
+// the reading's correction (k_finalize's arithmetic and rigidity check) and, when it is accepted
+// (|t_i| <= max_correction_magnitude, app.cpp:366-373), initialT_ = correction * initialT_
+// (app.cpp:414: a dropped reading returns before that line)
+__global__ void k_debug_post(const PairDesc* __restrict__ d, PairState* st, float* outT, float* initT,
+                             float max_corr) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float tmp[16], T[16];
+  mul4(d->Tmean, st->T, tmp);
+  mul4(tmp, d->Tinit, T);
+  for (int i = 0; i < 16; ++i) outT[i] = T[i];
+  if (st->status == 0 && !rigid_ok(T)) st->status = 5;
+  if (st->status != 0 || correction_rejected(T, max_corr)) return;
+  float I[16], N[16];
+  for (int i = 0; i < 16; ++i) I[i] = initT[i];
+  mul4(T, I, N);
+  for (int i = 0; i < 16; ++i) initT[i] = N[i];
+}
+
 // one map per entry from the key box in st[i].ovl_bbox (k_ovl_init + k_ovl_bbox), padded by 2
 // voxels below and 2 above like the batch path's host sizing; od[i].off is preset by the host.
 // A box beyond cap[i] bytes is reported (ovl_err) and gets an empty map: every mark and lookup
@@ -101,6 +134,12 @@ void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState
 }
 void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy) {
   k_seq_next_ref<<<1, 64, 0, s>>>(gd, src, T, Tcopy);
+}
+void launch_debug_prep(hipStream_t s, PairDesc* d, const float* initT, float* hist) {
+  k_debug_prep<<<1, 64, 0, s>>>(d, initT, hist);
+}
+void launch_debug_post(hipStream_t s, const PairDesc* d, PairState* st, float* outT, float* initT, float max_corr) {
+  k_debug_post<<<1, 64, 0, s>>>(d, st, outT, initT, max_corr);
 }
 void launch_ovl_size(hipStream_t s, int n, PairState* st, OvlDesc* od, const uint64_t* cap) {
   if (n) k_ovl_size<<<(n + 63) / 64, 64, 0, s>>>(n, st, od, cap);

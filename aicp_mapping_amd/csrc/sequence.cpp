@@ -186,11 +186,12 @@ struct SeqSlot {
   TreeBufs tb[2];
   PinBuf pin_read, pin_par, pin_src;
   hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr;
-  // early exit of the ICP loop: active counts written by the update kernels into mapped host
-  // memory, one word per iteration
-  uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), kMaxPolls words
+  // early exit of the ICP loops: active counts written by the update kernels into mapped host
+  // memory, one word per iteration, in two areas (debug mode's consecutive per-reading loops
+  // alternate, so a loop's trailing write never lands in its successor's words)
+  uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), 2 * kMaxPolls words
   uint32_t* poll_dev = nullptr;   // its device address
-  hipEvent_t ev_poll[kMaxPolls] = {};
+  hipEvent_t ev_poll[2 * kMaxPolls] = {};
   GraphCache g_match;
   bool used = false;
 };
@@ -199,7 +200,8 @@ struct SeqState {
   hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr;
   SeqSlot slot[kSlots];
   DevBuf desc, state, outT;
-  PinBuf pin_state, pin_out, pin_ctl;
+  DevBuf initT;  // debug working mode: initialT_ (16 floats), then its value before each reading
+  PinBuf pin_state, pin_out, pin_ctl, pin_desc;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;
   std::vector<hipEvent_t> tev;  // seq_prof(): 5 timing events per window
@@ -230,8 +232,8 @@ void seq_state_free(SeqState* S) {
       if (e) (void)hipEventDestroy(e);
     if (sl.poll_host) (void)hipHostFree(sl.poll_host);
   }
-  for (DevBuf* b : {&S->desc, &S->state, &S->outT}) release(*b);
-  for (PinBuf* b : {&S->pin_state, &S->pin_out, &S->pin_ctl}) release(*b);
+  for (DevBuf* b : {&S->desc, &S->state, &S->outT, &S->initT}) release(*b);
+  for (PinBuf* b : {&S->pin_state, &S->pin_out, &S->pin_ctl, &S->pin_desc}) release(*b);
   for (hipEvent_t e : S->nn_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : S->tev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {S->ev_begin, S->ev_end})
@@ -402,6 +404,11 @@ struct WinRun {
   bool sparse = false;                  // overlap on sorted key lists (a map over kSeqMapBudget)
   OvlKeySide kr{}, kg{};                // its readings' and reference's sides
   unsigned long long* per_pair = nullptr;
+  // debug working mode: the readings one after the other (per-reading loops and overlaps)
+  bool debug = false;
+  std::vector<uint32_t> loff;               // each reading's first point in the window
+  std::vector<uint32_t> b_read, b_sel, b_red;  // each reading's first block in m_read / m_sel / m_red (+ end)
+  std::vector<OvlKeySide> kr1;              // sparse: each reading's own key side
 };
 
 // Run `enqueue` on stream s through the cache: replay the graph if the key matches, otherwise
@@ -444,6 +451,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   const Win& w = R.w;
   SeqSlot& sl = S->slot[w.slot];
   const bool doOvl = prm->flags & AICP_RUN_OVERLAP;
+  const bool debug = prm->flags & AICP_SEQ_DEBUG;
   const double res = prm->resolution;
   const size_t np = w.np;
   const aicp_cloud& src = w.src < 0 ? *first : rd[w.src];
@@ -554,7 +562,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   uint64_t bm = 0, cap_max = 0;
   for (size_t i = 0; i <= np; ++i) {
     cap[i] = i == 0 ? map_cap(src_box, src.origin, res, w.src >= 0)
-                    : map_cap(boxes[i - 1], rd[w.p0 + i - 1].origin, res, false);
+                    : map_cap(boxes[i - 1], rd[w.p0 + i - 1].origin, res, debug);  // debug: moved by initialT_
     od[i] = OvlDesc{};
     od[i].off = bm;
     bm += cap[i];
@@ -568,6 +576,7 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   std::vector<uint32_t> sbc, sbs;
   uint64_t cap_r = 0, cap_g = 0;
   size_t tmp_r = 0, tmp_g = 0;
+  std::vector<uint64_t> kb_read;  // each reading's key bound
   if (sparse) {
     uint64_t slot = 0;
     for (size_t i = 0; i <= np; ++i) {  // readings 0..np-1, then the reference
@@ -586,10 +595,13 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
         sbc.push_back(ci);
         sbs.push_back(j);
       }
-      const uint64_t kb = key_bound(S->pool, c, c.origin, res, ref && w.src >= 0);
+      const uint64_t kb = key_bound(S->pool, c, c.origin, res, (ref && w.src >= 0) || (!ref && debug));
+      if (!ref) kb_read.push_back(kb);
       (ref ? cap_g : cap_r) += kb;
     }
     tmp_r = ovl_keys_temp_bytes(nread, cap_r, (int)np);
+    if (debug)  // the readings one at a time: each side's own scan / sort
+      for (size_t i = 0; i < np; ++i) tmp_r = std::max(tmp_r, ovl_keys_temp_bytes(rd[w.p0 + i].n, kb_read[i], 1));
     tmp_g = ovl_keys_temp_bytes(n_ref, cap_g, 1);
     size_t free_b = 0, total_b = 0;
     HIPC(hipMemGetInfo(&free_b, &total_b));
@@ -614,7 +626,9 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   const size_t o_desc = 0, o_r = o_desc + np * sizeof(PairDesc), o_ovl = o_r + 3 * sizeof(PairDesc),
                o_cap = o_ovl + (np + 1) * sizeof(OvlDesc), o_maps = o_cap + (np + 1) * 8,
                o_sp = (o_maps + words * 4 + 15) & ~size_t(15),
-               sp_bytes = scl.size() * sizeof(OvlCloud) + 8 * sbc.size(), total = o_sp + sp_bytes;
+               // clouds | block clouds | block starts [debug: | clouds with count slot 0 | zero tags]
+               sp_bytes = (scl.size() * sizeof(OvlCloud) + 8 * sbc.size()) * (debug ? 2 : 1),
+               total = o_sp + sp_bytes;
   HIPC(ensure(sl.pin_par, total));
   HIPC(ensure(sl.maps, words * 4));
   char* P = sl.pin_par.as<char>();
@@ -648,6 +662,12 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
     std::memcpy(P + o_sp, scl.data(), ncl * sizeof(OvlCloud));
     std::memcpy(P + o_sp + ncl * sizeof(OvlCloud), sbc.data(), nb * 4);
     std::memcpy(P + o_sp + ncl * sizeof(OvlCloud) + nb * 4, sbs.data(), nb * 4);
+    if (debug) {  // each reading alone: its counts start at its own first point, its words tagged 0
+      OvlCloud* c1 = reinterpret_cast<OvlCloud*>(P + o_sp + ncl * sizeof(OvlCloud) + 8 * nb);
+      std::memcpy(c1, scl.data(), ncl * sizeof(OvlCloud));
+      for (size_t c = 0; c < ncl; ++c) c1[c].slot = 0;
+      std::memset(P + o_sp + 2 * ncl * sizeof(OvlCloud) + 8 * nb, 0, 4 * nb);
+    }
     HIPC(ensure(sl.sp_par, sp_bytes));
     char* D = sl.sp_par.as<char>();
     OvlCloud* dcl = reinterpret_cast<OvlCloud*>(D);
@@ -662,6 +682,32 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
                       sl.sp_cnt.as<uint32_t>() + nread, sl.sp_off.as<uint64_t>() + nread, cap_g,
                       sl.sp_keys_g.as<uint64_t>(), sl.sp_keys_g.as<uint64_t>() + cap_g, sl.sp_tmp_g.p, tmp_g, pc + np};
     R.per_pair = pc + np + 1;
+    if (debug) {  // reading i alone: cloud i (its key words tagged 0), keys at its own offset
+      R.kr1.assign(np, OvlKeySide{});
+      OvlCloud* c1 = reinterpret_cast<OvlCloud*>(D + ncl * sizeof(OvlCloud) + 8 * nb);
+      const uint32_t* bc0 = reinterpret_cast<const uint32_t*>(D + 2 * ncl * sizeof(OvlCloud) + 8 * nb);
+      uint32_t b0 = 0;
+      uint64_t k0 = 0;
+      for (size_t i = 0; i < np; ++i) {
+        const uint32_t nbi = (uint32_t)((rd[w.p0 + i].n + 255) / 256);
+        OvlKeySide& k = R.kr1[i];
+        k = R.kr;
+        k.clouds = c1 + i;
+        k.n_clouds = 1;
+        k.blk_cloud = bc0 + b0;
+        k.blk_start = dbs + b0;
+        k.n_blocks = nbi;
+        k.n_points = (uint32_t)rd[w.p0 + i].n;
+        k.cnt = R.kr.cnt + loff[i];
+        k.off = R.kr.off + loff[i];
+        k.cap = kb_read[i];
+        k.keys0 = R.kr.keys0 + 2 * k0;  // (the readings' key area holds 2 * cap_r words: per reading keys0 | keys1)
+        k.keys1 = R.kr.keys0 + 2 * k0 + kb_read[i];
+        k.per_cloud = pc + i;
+        b0 += nbi;
+        k0 += kb_read[i];
+      }
+    }
   }
 
   // ---- up: readings, descriptors, maps (and a non-resident reference source)
@@ -699,6 +745,19 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
   R.src_pts = src_pts;
   R.readS = sl.read_raw.as<float4>();
   R.sparse = sparse;
+  R.debug = debug;
+  R.loff = loff;
+  {  // each reading's first block in the three block maps (pair-major), and the end
+    R.b_read.assign(np + 1, 0);
+    R.b_sel.assign(np + 1, 0);
+    R.b_red.assign(np + 1, 0);
+    for (size_t i = 0; i < np; ++i) {
+      const uint64_t n = rd[w.p0 + i].n;
+      R.b_read[i + 1] = R.b_read[i] + (uint32_t)((n + kNNBlock - 1) / kNNBlock);
+      R.b_sel[i + 1] = R.b_sel[i] + (uint32_t)((n + kNNBlock * kSelPerThread - 1) / (kNNBlock * kSelPerThread));
+      R.b_red[i + 1] = R.b_red[i] + (uint32_t)((n + kRedBlk - 1) / kRedBlk);
+    }
+  }
   return AICP_OK;
 }
 
@@ -750,6 +809,12 @@ static int win_read_side(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   HIPC(hipStreamWaitEvent(sr, sl.ev_up, 0));
   launch_init_state(sr, (int)np, dDesc, dState);
   const float4* readS = sl.read_raw.as<float4>();
+  if (R.debug) {  // the points move with initialT_ right before each reading's loop (in place)
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(sl.ev_rd, sr));
+    R.readS = readS;
+    return AICP_OK;
+  }
   {
     const size_t tb = read_order_temp_bytes(nread, (int)np);
     HIPC(ensure(sl.ord_k0, nread * 8));
@@ -800,6 +865,11 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     const SeqSlot& ps = S->slot[(w.slot + kSlots - 1) % kSlots];
     if (w.index > 0) HIPC(hipStreamWaitEvent(s3, ps.ev_done, 0));
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
+    // debug mode, a source from an earlier pass (uploaded as given): it was registered as
+    // initialT_ * its points (initialT_ as before it, kept by k_debug_prep)
+    if (R.debug && w.index == 0)
+      launch_transform(s3, (int)n_ref, S->initT.as<float>() + 16 * (1 + (size_t)w.src), src_pts,
+                       const_cast<float4*>(src_pts));
     launch_seq_next_ref(s3, dG, R.src_desc, R.src_T, sl.tsrc.as<float>());
     launch_transform(s3, (int)n_ref, sl.tsrc.as<float>(), src_pts, sl.ref_raw.as<float4>());
   } else {
@@ -916,7 +986,7 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   if (doOvl && R.sparse) {
     HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
     launch_ovl_init(si, 1, dG, dGst, res, 1);
-    HIPC(launch_ovl_keys(si, R.kg, w.src >= 0 ? dG : nullptr, sl.ref_raw.as<float4>(), res, dGst, 0));
+    HIPC(launch_ovl_keys(si, R.kg, w.src >= 0 ? dG->ref_origin : nullptr, sl.ref_raw.as<float4>(), res, dGst, 0));
   } else if (doOvl) {
     HIPC(hipStreamWaitEvent(si, sl.ev_ref, 0));
     launch_ovl_init(si, 1, dG, dGst, res, 1);
@@ -930,7 +1000,7 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   // the loop's selection histogram, counts and hand-off words: before the wait on the trees
   launch_zero_words3(si, sl.sel_hist.as<uint32_t>(), np * kHistBins, sl.sel_cnt.as<uint32_t>(), np,
                      sl.isync.as<uint32_t>(), icp_sync_words(np));
-  if (doOvl) {
+  if (doOvl && !R.debug) {
     if (R.sparse)
       HIPC(launch_ovl_keys_intersect(si, R.kr, R.kg, R.per_pair, dState));
     else
@@ -942,7 +1012,7 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   launch_pairs_degenerate_part(si, (int)np, dDesc, dState, dRst, 2);
   // the normals (ev_s2) are waited for by the first iteration's reduce (loop_iteration): the
   // first NN and select need only the matcher tree, which is ready ~0.2 ms earlier on C2
-  launch_prepare_read(si, R.m_read, dDesc, readS, sl.read_c.as<float4>());
+  if (!R.debug) launch_prepare_read(si, R.m_read, dDesc, readS, sl.read_c.as<float4>());
   HIPC(hipGetLastError());
   return AICP_OK;
 }
@@ -959,10 +1029,21 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
 // to 1.63 ms; the next reference started on the stop poll instead of the loop's end: 1 % slower.)
 struct IcpLoop {
   WinRun* R = nullptr;
+  int sub = -1;   // debug mode: the one reading of the window this loop registers
+  int area = 0;   // poll words / events used: [area * kMaxPolls, + kMaxPolls)
   int it = 0;
   bool stop = false;
   std::deque<int> pending;  // poll slots recorded, oldest first
 };
+
+// the blocks [off, off + cnt) of a block map
+static BlockMap map_sub(const BlockMap& m, uint32_t off, uint32_t cnt) {
+  BlockMap r = m;
+  r.pair += off;
+  r.start += off;
+  r.n_blocks = cnt;
+  return r;
+}
 
 static IcpParams icp_params(const aicp_icp_config* cfg) {
   IcpParams ip;
@@ -985,6 +1066,16 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   const int it = q.it;
   ActiveList* al = sl.active.as<ActiveList>();
   uint32_t* ctr = sl.ctrs.as<uint32_t>();
+  // the pairs this loop iterates: the window's, or (debug mode) reading q.sub alone
+  const int r = q.sub;
+  const int np_l = r >= 0 ? 1 : (int)np;
+  PairDesc* gd = r >= 0 ? dDesc + r : dDesc;
+  PairState* gs = r >= 0 ? dState + r : dState;
+  const uint64_t reads = r >= 0 ? R.n_read[r] : R.nread;
+  const BlockMap msel = r >= 0 ? map_sub(R.m_sel, R.b_sel[r], R.b_sel[r + 1] - R.b_sel[r]) : R.m_sel;
+  const BlockMap mred = r >= 0 ? map_sub(R.m_red, R.b_red[r], R.b_red[r + 1] - R.b_red[r]) : R.m_red;
+  uint32_t* poll_host = sl.poll_host + q.area * kMaxPolls;
+  uint32_t* poll_dev = sl.poll_dev + q.area * kMaxPolls;
   IcpParams ip = icp_params(cfg);
   ip.prof_slot = nn_launches;
   auto polled = [&](int k) {
@@ -995,12 +1086,12 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   uint32_t* hn_this = nullptr;
   uint32_t* hn_next = nullptr;
   if (it == 0 && polled(it)) {
-    sl.poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
-    hn_this = sl.poll_dev + it;
+    poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
+    hn_this = poll_dev + it;
   }
   if (polled(it + 1)) {
-    sl.poll_host[it + 1] = 0xffffffffu;
-    hn_next = sl.poll_dev + it + 1;
+    poll_host[it + 1] = 0xffffffffu;
+    hn_next = poll_dev + it + 1;
   }
   if (timeNN)
     while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
@@ -1009,8 +1100,8 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
       S->nn_ev.push_back(e);
     }
   hipStream_t st = S->s_icp;
-  if (it == 0) launch_active_list(st, (int)np, dDesc, dState, al, ctr, hn_this);
-  launch_icp_nn(st, (int)R.nread, dDesc, dState, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
+  if (it == 0) launch_active_list(st, np_l, gd, gs, al, ctr, hn_this);
+  launch_icp_nn(st, (int)reads, gd, gs, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
                 R.use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
                 R.use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
                 sl.touch.as<uint32_t>(), ctr, ip, timeNN ? S->nn_ev[2 * nn_launches] : nullptr,
@@ -1018,24 +1109,24 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   HIPC(hipGetLastError());
   ++nn_launches;
   IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, 0);
-  y.np = (int)np;
-  y.pd = dDesc;
-  y.st = dState;
+  y.np = np_l;
+  y.pd = gd;
+  y.st = gs;
   y.al = al;
   y.ctr = ctr;
   y.host_n = hn_next;
-  launch_icp_select_f(st, R.m_sel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(), sl.cand.as<uint32_t>(),
+  launch_icp_select_f(st, msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(), sl.cand.as<uint32_t>(),
                       sl.sel_cnt.as<uint32_t>(), y);
   if (it == 0) {  // the reduce gathers the reference normals (stream r2, scattered into matcher order)
     HIPC(hipStreamWaitEvent(st, sl.ev_s2, 0));
-    launch_pairs_degenerate_part(st, (int)np, dDesc, dState, dRst, 1);
+    launch_pairs_degenerate_part(st, np_l, gd, gs, dRst, 1);
   }
-  launch_icp_reduce_f(st, R.m_red, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
+  launch_icp_reduce_f(st, mred, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
                       sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>(), ip, y);
   HIPC(hipGetLastError());
   for (int k : {hn_this ? it : -1, hn_next ? it + 1 : -1})
     if (k >= 0) {
-      HIPC(hipEventRecord(sl.ev_poll[k], st));
+      HIPC(hipEventRecord(sl.ev_poll[q.area * kMaxPolls + k], st));
       q.pending.push_back(k);
     }
   ++q.it;
@@ -1048,7 +1139,7 @@ static int loop_finish(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_param
   WinRun& R = *q.R;
   WIN_REFS;
   hipStream_t st = S->s_icp;
-  launch_finalize(st, (int)np, dDesc, dState, dOutT);
+  if (!R.debug) launch_finalize(st, (int)np, dDesc, dState, dOutT);  // (debug: k_debug_post per reading)
   if (R.tev) HIPC(hipEventRecord(R.tev[4], st));
   launch_seq_commit(st, (int)np, dDesc, dState, dOutT, S->desc.as<PairDesc>() + w.p0, S->state.as<PairState>() + w.p0,
                     S->outT.as<float>() + 16 * w.p0);
@@ -1062,12 +1153,57 @@ static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool& got) {
   got = false;
   SeqSlot& sl = S->slot[q.R->w.slot];
   const int k = q.pending.front();
-  const hipError_t r = hipEventQuery(sl.ev_poll[k]);
+  const hipError_t r = hipEventQuery(sl.ev_poll[q.area * kMaxPolls + k]);
   if (r == hipErrorNotReady) return AICP_OK;
   HIPC(r);
   q.pending.pop_front();
   got = true;
-  if (sl.poll_host[k] == 0) q.stop = true;
+  if (sl.poll_host[q.area * kMaxPolls + k] == 0) q.stop = true;
+  return AICP_OK;
+}
+
+// Debug working mode, before reading q.sub's loop (app.cpp:87-96): initialT_ into its history
+// slot, the prior origin moved by it, its points moved in place (pcl::transformPointCloud), then
+// its overlap with the window's reference (the key box / bound allows any rigid motion) and
+// its centred copy
+static int sub_prep(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_params* prm, IcpLoop& q) {
+  WinRun& R = *q.R;
+  WIN_REFS;
+  const int r = q.sub;
+  hipStream_t si = S->s_icp;
+  float* initT = S->initT.as<float>();
+  float4* pts = sl.read_raw.as<float4>() + R.loff[r];
+  launch_debug_prep(si, dDesc + r, initT, initT + 16 * (1 + w.p0 + (size_t)r));
+  launch_transform(si, (int)R.n_read[r], initT, pts, pts);
+  const BlockMap mrd = map_sub(R.m_read, R.b_read[r], R.b_read[r + 1] - R.b_read[r]);
+  if (doOvl) {
+    launch_ovl_init(si, 1, dDesc + r, dState + r, res, 2);
+    if (R.sparse) {
+      HIPC(launch_ovl_keys(si, R.kr1[r], dDesc[r].read_origin, sl.read_raw.as<float4>(), res, dState + r, 1));
+      HIPC(launch_ovl_keys_intersect(si, R.kr1[r], R.kg, R.per_pair + r, dState + r));
+    } else {
+      launch_ovl_bbox(si, mrd, dDesc, dState, sl.read_raw.as<float4>(), 1, res);
+      launch_ovl_size(si, 1, dState + r, dOvl + 1 + r, dCap + 1 + r);
+      launch_ovl_clear(si, 1, dOvl + 1 + r, bmp, R.cap[1 + r]);
+      launch_ovl_mark(si, mrd, dDesc, dOvl + 1, dState, sl.read_raw.as<float4>(), 1, res, bmp);
+      launch_ovl_popcount(si, 1, dOvl + 1 + r, dState + r, 1, bmp);
+      launch_ovl_intersect(si, 1, dDesc + r, dOvl + 1 + r, dOvl, dState + r, bmp);
+    }
+    launch_ovl_finish(si, 1, dDesc + r, dState + r, dGst, 1);
+  }
+  launch_prepare_read(si, mrd, dDesc, sl.read_raw.as<float4>(), sl.read_c.as<float4>());
+  HIPC(hipGetLastError());
+  return AICP_OK;
+}
+
+// after reading q.sub's loop: its correction, and initialT_ = correction * initialT_ when it is
+// accepted (app.cpp:366-373, 414)
+static int sub_post(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_params* prm, IcpLoop& q) {
+  WinRun& R = *q.R;
+  WIN_REFS;
+  const int r = q.sub;
+  launch_debug_post(S->s_icp, dDesc + r, dState + r, dOutT + 16 * r, S->initT.as<float>(), prm->max_correction_magnitude);
+  HIPC(hipGetLastError());
   return AICP_OK;
 }
 
@@ -1091,7 +1227,7 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
       for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
       for (hipEvent_t& e : sl.ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIPC(hipHostMalloc((void**)&sl.poll_host, kMaxPolls * 4, hipHostMallocMapped));
+      HIPC(hipHostMalloc((void**)&sl.poll_host, 2 * kMaxPolls * 4, hipHostMallocMapped));
       HIPC(hipHostGetDevicePointer((void**)&sl.poll_dev, sl.poll_host, 0));
     }
     HIPC(hipEventCreate(&S->ev_begin));
@@ -1133,6 +1269,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
   const int F = prm->reference_update_frequency;
   if (F < 1) FAIL(AICP_ERR_INVALID, "reference_update_frequency must be >= 1");
   const bool doOvl = prm->flags & AICP_RUN_OVERLAP;
+  const bool debug = prm->flags & AICP_SEQ_DEBUG;
   if (doOvl && !(prm->resolution > 0)) FAIL(AICP_ERR_INVALID, "resolution");
   int rc = check_cfg(ctx, cfg, AICP_RUN_ICP | (doOvl ? AICP_RUN_OVERLAP : 0));
   if (rc) return rc;
@@ -1157,6 +1294,10 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
   if (rc) return rc;
   SeqState* S = ctx->seq;
   S->last = aicp_sequence_timing{};  // (an error return leaves no stale timing behind)
+  if (debug) {
+    HIPC(ensure(S->initT, 64 * (n + 1)));
+    HIPC(ensure(S->pin_desc, n * sizeof(PairDesc)));
+  }
   const bool timeNN = prm->flags & AICP_RUN_TIME_NN;
   int nn_launches = 0, windows = 0, replans = 0;
   HIPC(hipEventRecord(S->ev_begin, S->s_up));
@@ -1248,9 +1389,14 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         progress = true;
       }
       if (q.stop && q.it >= 0) {
-        const int r = loop_finish(ctx, S, prm, q);
+        // debug mode: this reading's correction / initialT_, and the window's commit after its
+        // last reading; otherwise the window's corrections and commit
+        int r = q.sub >= 0 ? sub_post(ctx, S, prm, q) : AICP_OK;
+        if (!r && (q.sub < 0 || q.sub + 1 == (int)q.R->np)) {
+          r = loop_finish(ctx, S, prm, q);
+          if (!r) done_enq[q.R->w.index] = 1;
+        }
         if (r) return r;
-        done_enq[q.R->w.index] = 1;
         q.it = -1;  // finished
         progress = true;
       }
@@ -1259,6 +1405,13 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     // upload(k + 1) reuses the slot of window k - 2 and waits (on the device) for ev_done of
     // window k - 1, which exists once that window's loop has been finished here
     auto can_upload = [&](size_t k) { return k + 1 < plan.size() && (k < 1 || done_enq[k - 1]); };
+    if (debug) {  // initialT_ at the pass's first reading: identity, or its value before reading p
+      static const float kI[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+      if (p == 0)
+        HIPC(hipMemcpyAsync(S->initT.p, kI, 64, hipMemcpyHostToDevice, S->s_icp));
+      else
+        HIPC(hipMemcpyAsync(S->initT.p, S->initT.as<float>() + 16 * (1 + p), 64, hipMemcpyDeviceToDevice, S->s_icp));
+    }
     rc = timed(0, [&] { return upload(0); });
     if (!rc) rc = timed(0, [&] { return read_side(0); });
     if (!rc) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[0]); });
@@ -1279,18 +1432,28 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         rc = hipEventRecord(runs[k].tev[3], S->s_icp) == hipSuccess ? AICP_OK : AICP_ERR_HIP;
         if (rc) break;
       }
-      IcpLoop& q = loops[k];
-      q.R = &runs[k];
-      rc = timed(2, [&]() -> int {
-        while (q.it >= 0) {
-          bool progress = false;
-          int r = advance(q, progress);
-          if (!r) r = try_upload();
-          if (r) return r;
-          if (!progress) std::this_thread::yield();
-        }
-        return try_upload();
-      });
+      // one loop per window; debug mode: one per reading, in order (reading i + 1 is moved by
+      // the initialT_ that reading i's correction updates)
+      const int n_sub = debug ? (int)runs[k].np : 1;
+      for (int sub = 0; sub < n_sub && !rc; ++sub) {
+        IcpLoop& q = loops[k];
+        q = IcpLoop{};
+        q.R = &runs[k];
+        q.sub = debug ? sub : -1;
+        q.area = sub & 1;
+        if (debug) rc = sub_prep(ctx, S, prm, q);
+        if (rc) break;
+        rc = timed(2, [&]() -> int {
+          while (q.it >= 0) {
+            bool progress = false;
+            int r = advance(q, progress);
+            if (!r) r = try_upload();
+            if (r) return r;
+            if (!progress) std::this_thread::yield();
+          }
+          return try_upload();
+        });
+      }
       if (!rc && next) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
       if (!rc && next) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
       ++windows;
@@ -1308,6 +1471,9 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
                         hipMemcpyDeviceToHost, S->s_icp));
     HIPC(hipMemcpyAsync(S->pin_out.as<float>() + 16 * p, S->outT.as<float>() + 16 * p, (pe - p) * 64,
                         hipMemcpyDeviceToHost, S->s_icp));
+    if (debug)  // the prior origins moved by initialT_ (k_debug_prep), for the corrected poses
+      HIPC(hipMemcpyAsync(S->pin_desc.as<PairDesc>() + p, S->desc.as<PairDesc>() + p, (pe - p) * sizeof(PairDesc),
+                          hipMemcpyDeviceToHost, S->s_icp));
     HIPC(hipEventRecord(S->ev_end, S->s_icp));
     rc = seq_sync(ctx, S);
     if (rc) return rc;
@@ -1386,7 +1552,9 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     aicp_sequence_result& r = out[i];
     r.accepted = accepted[i];
     for (int k = 0; k < 3; ++k) r.corrected_origin[k] = 0.0;
-    if (r.accepted) corrected_origin(hT + 16 * i, readings[i].origin, r.corrected_origin);
+    if (r.accepted)
+      corrected_origin(hT + 16 * i, debug ? S->pin_desc.as<PairDesc>()[i].read_origin : readings[i].origin,
+                       r.corrected_origin);
     const PairState& st = hs[i];
     aicp_icp_stats& o = r.icp;
     std::memset(&o, 0, sizeof(o));

@@ -347,8 +347,9 @@ def bench_stream(args):
         st = make_stream(n_read, n_pts, seed=1 + rank)
     ctx = L.Context(local_rank)
     cfg = L.default_config()
+    debug = args.working_mode == "debug"
     prm = L.default_sequence_params(reference_update_frequency=args.ref_every,
-                                    flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_TIME_NN)
+                                    flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_TIME_NN | (L.AICP_SEQ_DEBUG if debug else 0))
 
     def step():
         T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, cfg, prm)
@@ -414,6 +415,7 @@ def bench_stream(args):
                                   args.config.upper(), "ANYmal VLP-16" if args.config == "c2" else "KITTI HDL-64",
                                   n_pts, n_read, args.ref_every, prm.max_correction_magnitude),
                   "readings_per_step_per_gpu": n_read, "windows_per_step": windows, "replans": replans,
+                  "working_mode": args.working_mode,
                   "chain": CHAIN, "overlap": "octree-equivalent voxel sets at 0.2 m",
                   "timed_region": "host clouds -> packing -> H2D -> device -> corrections (aicp_hip_sequence_run)",
                   "parallelism": "one stream per rank (replicas), RCCL all_gather of T"}
@@ -432,7 +434,10 @@ def bench_stream(args):
             "accuracy_vs_ground_truth": {"median_rot_rad": float(np.median([e[0] for e in errs])),
                                          "median_trans_m": float(np.median([e[1] for e in errs])),
                                          "note": "the reference chain (eps 3.16 approximate NN) stalls on this "
-                                                 "scene; the oracle gives the same transforms (parity_vs_oracle)"},
+                                                 "scene; the oracle gives the same transforms (parity_vs_oracle), "
+                                                 "and with eps 0 the oracle reaches the ground truth "
+                                                 "(tests/test_oracle.py::test_c2_stall_is_the_epsilon_approximation"
+                                                 ", DESIGN.md §7)"},
             "roofline": roofline_nn(nn, "k_icp_nn (transform + libnabo-order 1-NN over treelets + bucket scan), "
                                         "one launch per ICP iteration of a reference window (5 readings)"),
             "batched_independent": batched,
@@ -465,7 +470,8 @@ def cpu_stream(st, T, out, args):
     def rep():
         t = time.perf_counter()
         last["r"] = po.sequence(st.first, st.first_origin, st.readings[:k], st.origins[:k],
-                                reference_update_frequency=args.ref_every, resolution=res)
+                                reference_update_frequency=args.ref_every, resolution=res,
+                                working_mode=args.working_mode)
         return k, time.perf_counter() - t
 
     med, rates = median_rate(rep, args.cpu_reps)
@@ -739,6 +745,8 @@ def main():
                     help="BASELINE.json workload (default c2: the metric's configuration)")
     ap.add_argument("--pairs", type=int, default=None, help="readings (pairs) per step per GPU")
     ap.add_argument("--ref-every", type=int, default=5, help="reference_update_frequency")
+    ap.add_argument("--working-mode", choices=["robot", "debug"], default="robot",
+                    help="App's working_mode for c2/c3 (debug: readings pre-transformed by initialT_, serial)")
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--data", default=None,
                     help="recorded directory (aicp_input_poses.csv + cloud_*.pcd) replayed as the stream")

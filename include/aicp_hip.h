@@ -253,12 +253,20 @@ int aicp_hip_last_phase_ms(const aicp_hip_ctx* ctx, double out_ms[5]);
  * Inputs are host buffers (pre-filtered clouds, as App passes read_prefiltered); everything
  * from the upload to the corrections runs on the device, the next reference included. */
 
+/* aicp_sequence_params.flags: App's "debug" working_mode (aicp.launch:36). Each reading is first
+ * transformed by initialT_ (pcl::transformPointCloud, float) and its prior pose becomes
+ * initialT_ * prior pose (app.cpp:87-96); after each accepted reading initialT_ = correction *
+ * initialT_ (app.cpp:414; identity at the start). The readings then depend on each other one by
+ * one, so the device registers them one after the other (the reference trees are still built
+ * once per window). Without the flag: "robot" mode, the node's default (aicp_ros_node.cpp:14). */
+#define AICP_SEQ_DEBUG 8
+
 typedef struct {
   int32_t reference_update_frequency; /* 5 (aicp.launch:61) */
   float max_correction_magnitude;     /* 1.0 (aicp.launch:63; aicp_ros_node.cpp:28 default 0.5) */
   double resolution;                  /* octomapResolution (0.2, aicp_config.yaml:21) */
   int32_t flags;                      /* AICP_RUN_OVERLAP: per-reading overlap + auto-tuned ratio
-                                         (else cfg->trimmed_ratio); AICP_RUN_TIME_NN */
+                                         (else cfg->trimmed_ratio); AICP_RUN_TIME_NN; AICP_SEQ_DEBUG */
 } aicp_sequence_params;
 
 typedef struct {
@@ -266,7 +274,8 @@ typedef struct {
   int32_t accepted;        /* 0: dropped, some |t_i| > max_correction_magnitude */
   int32_t reference;       /* cloud it was registered against: -1 the first cloud, else a reading */
   int32_t is_reference;    /* 1: it became the next reference */
-  double corrected_origin[3]; /* translation of correction * prior pose (accepted readings) */
+  double corrected_origin[3]; /* translation of correction * prior pose (accepted readings; in debug
+                                 mode the prior pose is initialT_ * the reading's prior pose) */
   aicp_icp_stats icp;
 } aicp_sequence_result;
 

@@ -357,25 +357,47 @@ def corrected_origin(T, prior_origin):
     return np.array([((R[r][0] * o[0] + R[r][1] * o[1]) + R[r][2] * o[2]) + float(Tt[r, 3]) for r in range(3)])
 
 
+def mul4(A, B):
+    """Eigen Matrix4f product A * B in float: each coefficient summed over k = 0..3 in order."""
+    A = np.asarray(A, np.float32)
+    B = np.asarray(B, np.float32)
+    C = np.zeros((4, 4), np.float32)
+    for r in range(4):
+        for c in range(4):
+            s = np.float32(A[r, 0] * B[0, c])
+            for k in range(1, 4):
+                s = np.float32(s + np.float32(A[r, k] * B[k, c]))
+            C[r, c] = s
+    return C
+
+
 def sequence(first, first_origin, readings, origins, cfg=None, reference_update_frequency=5,
-             max_correction_magnitude=1.0, resolution=0.2, overlap=True, stop=None):
+             max_correction_magnitude=1.0, resolution=0.2, overlap=True, stop=None, working_mode="robot"):
     """App::processCloud over a stream (app.cpp:282-414, robot mode): the first cloud is the
     reference; each reading: overlap -> ratio -> ICP against the current reference; dropped when
     some |T(i,3)| > max_correction_magnitude (float compare, app.cpp:366-373); an accepted reading
     is transformed by T and, as the reference_update_frequency-th accepted reading since the last
     update, becomes the reference with origin corrected_origin(T, its origin); a registration
     error ends the stream (app.cpp:210). stop: process only readings [0, stop).
+    working_mode "debug" (app.cpp:87-96, 414): each reading is first transformed by initialT_
+    (float, transform_cloud) and its prior pose becomes initialT_ * prior pose; after an accepted
+    reading initialT_ = correction * initialT_ (a dropped reading returns before that line).
     Returns a list of dicts (status, T, stats, accepted, reference, is_reference,
-    corrected_origin, overlap, counts, ratio)."""
+    corrected_origin, overlap, counts, ratio, prior_origin)."""
     cfg = cfg or default_config()
     ref, ref_origin, ref_id = _pts(first), np.asarray(first_origin, np.float64), -1
     acc = 0
     out = []
     mc = np.float32(max_correction_magnitude)
+    initT = np.eye(4, dtype=np.float32)
     for i, (r, o) in enumerate(zip(readings, origins)):
         if stop is not None and i >= stop:
             break
-        rec = dict(reference=ref_id, is_reference=0, accepted=0, corrected_origin=None)
+        if working_mode == "debug":
+            r = transform_cloud(initT, r)
+            o = corrected_origin(initT, o)
+        rec = dict(reference=ref_id, is_reference=0, accepted=0, corrected_origin=None,
+                   prior_origin=np.asarray(o, np.float64))
         if overlap:
             ov, cnt = globals()["overlap"](ref, ref_origin, r, o, resolution)
             ratio = autotune_ratio(ov)
@@ -399,4 +421,5 @@ def sequence(first, first_origin, readings, origins, cfg=None, reference_update_
             ref, ref_origin, ref_id = transform_cloud(Tf, r), rec["corrected_origin"], i
             rec["is_reference"] = 1
             acc = 0
+        initT = mul4(Tf, initT)
     return out

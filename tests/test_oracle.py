@@ -419,3 +419,27 @@ def test_c2_stall_is_the_epsilon_approximation(oracle):
                                                              min_diff_trans=1e-9))
     r, t = sy.rot_err(T_gt, T60)
     assert rc == 0 and r < 1e-3 and t < 2e-3, (r, t)
+
+
+def test_sequence_debug_mode_replay(oracle):
+    """The oracle's replay of App's debug working mode (app.cpp:87-96, 414) on a short stream:
+    reading 0 sees initialT_ = identity (so it equals robot mode's first registration); every
+    later reading is registered as initialT_ * reading with prior origin initialT_ * prior pose,
+    initialT_ being the float product of the accepted corrections so far; a dropped reading
+    leaves it unchanged."""
+    st = sy.make_stream(n_readings=6, n_points=3000, seed=5, half=12.0, jumps={3: (0.6, 0, 0)})
+    dbg = oracle.sequence(st.first, st.first_origin, st.readings, st.origins, max_correction_magnitude=0.4,
+                          resolution=RES, working_mode="debug")
+    rob = oracle.sequence(st.first, st.first_origin, st.readings[:1], st.origins[:1], max_correction_magnitude=0.4,
+                          resolution=RES)
+    np.testing.assert_array_equal(dbg[0]["T"], rob[0]["T"])
+    assert [r["accepted"] for r in dbg] == [1, 1, 1, 0, 1, 1]
+    initT = np.eye(4, dtype=np.float32)
+    for i, r in enumerate(dbg):
+        np.testing.assert_allclose(r["prior_origin"], oracle.corrected_origin(initT, st.origins[i]), rtol=0, atol=0)
+        if r["accepted"]:
+            initT = oracle.mul4(r["T"], initT)
+    # the drift is absorbed after the first correction: later accepted corrections are small
+    for r in dbg[1:]:
+        if r["accepted"]:
+            assert sy.rot_err(np.eye(4), r["T"])[0] < 5e-3

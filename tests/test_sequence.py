@@ -217,3 +217,41 @@ def test_sequence_sparse_overlap_identical(ctx, L, monkeypatch):
     for a, b in zip(out0, out1):
         assert a["icp"]["overlap_keys"] == b["icp"]["overlap_keys"]
         assert a["accepted"] == b["accepted"] and a["reference"] == b["reference"]
+
+
+@pytest.mark.parametrize("jumps", [None, {2: (0.6, 0, 0), 6: (0, -0.6, 0)}])
+def test_sequence_debug_mode_matches_oracle(ctx, oracle, L, jumps):
+    """App's "debug" working mode (aicp.launch:36; app.cpp:87-96, 414): every reading is first
+    moved by initialT_ (the product of the accepted corrections so far) and its prior pose with
+    it; a dropped reading leaves initialT_ as it was. The device registers the readings of a
+    window one after the other against the window's reference; the corrections, decisions,
+    references, corrected poses and key counts equal the oracle's replay of the same mode."""
+    st = sy.make_stream(n_readings=12, n_points=5000, seed=8, half=18.0, jumps=jumps)
+    prm = L.default_sequence_params(max_correction_magnitude=0.4, flags=L.AICP_RUN_OVERLAP | L.AICP_SEQ_DEBUG)
+    T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    assert rc == 0 and done == 12
+    ref = oracle.sequence(st.first, st.first_origin, st.readings, st.origins, max_correction_magnitude=0.4,
+                          resolution=RES, working_mode="debug")
+    _compare(out, ref, T)
+    assert ctx.last_sequence_timing()["replans"] == (2 if jumps else 0)
+    # after the first correction initialT_ carries the drift: the later corrections are small
+    if not jumps:
+        for i in range(2, 12):
+            rr, tt = sy.rot_err(np.eye(4), T[i])
+            assert rr < 5e-3 and tt < 5e-2, (i, rr, tt)
+
+
+def test_sequence_debug_mode_sparse_overlap(ctx, oracle, L, monkeypatch):
+    """Debug mode with every overlap on the sorted-key path (one key side per reading, bounds for
+    any rigid motion): the same results as the dense maps, and the oracle's."""
+    st = sy.make_stream(n_readings=7, n_points=4000, seed=9, half=15.0)
+    prm = L.default_sequence_params(flags=L.AICP_RUN_OVERLAP | L.AICP_SEQ_DEBUG)
+    monkeypatch.delenv("AICP_OVL_SPARSE", raising=False)
+    T0, out0, _, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    monkeypatch.setenv("AICP_OVL_SPARSE", "1")
+    T1, out1, _, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    assert rc0 == rc1 == 0
+    assert np.array_equal(T0, T1)
+    assert [o["icp"]["overlap_keys"] for o in out0] == [o["icp"]["overlap_keys"] for o in out1]
+    ref = oracle.sequence(st.first, st.first_origin, st.readings, st.origins, resolution=RES, working_mode="debug")
+    _compare(out1, ref, T1)

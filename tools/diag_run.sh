@@ -4,6 +4,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 for v in "$@"; do
-  AICP_NN_PROF_DUMP=1 AICP_HIP_LIB=$PWD/build_ab/lib_$v.so timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/diag_$v.out 2> gpurun_out/diag_$v.err || { tail -20 gpurun_out/diag_$v.err; exit 1; }
+  AICP_HIP_LIB=$PWD/build_ab/lib_$v.so timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/diag_$v.out 2> gpurun_out/diag_$v.err || { tail -20 gpurun_out/diag_$v.err; exit 1; }
   tail -25 gpurun_out/diag_$v.err
 done
