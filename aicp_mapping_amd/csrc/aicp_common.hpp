@@ -106,6 +106,9 @@ struct PairState {
   int32_t pad_;
   double qh[kHistRing][4];
   double th[kHistRing][3];
+  // per history entry i >= 1: |angdist(q_i, q_i-1)| and |t_i - t_i-1|, computed once when entry
+  // i is pushed (the Differential checker sums the last smoothLength of them every iteration)
+  double dq[kHistRing], dt[kHistRing];
 };
 
 // ---- device kd-tree construction (kernels_tree.hip) ----------------------------------------

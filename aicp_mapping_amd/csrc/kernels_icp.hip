@@ -2103,8 +2103,23 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
   AICP_IP_BODY(2);
 }
 
+// A x = b of the point-to-plane step from the reduced sums (upper triangle, then the rhs)
+__device__ __forceinline__ void normal_system(const double* tot, double* A, double* b) {
+  int c = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int bb = a; bb < 6; ++bb) {
+      A[a * 6 + bb] = tot[c];
+      A[bb * 6 + a] = tot[c];
+      ++c;
+    }
+  for (int a = 0; a < 6; ++a) b[a] = -tot[21 + a];
+}
+
 // the serial part of an ICP update (one lane): solve, compose, checkers
-__device__ void update_serial(const PairDesc& d, PairState& s, const double* tot, const IcpParams& prm) {
+// x_full: the LLT solution when the pivoted-QR rank is full (solve6's first path, computed by
+// two waves side by side in icp_update_body), or nullptr: solve6 here
+__device__ void update_serial(const PairDesc& d, PairState& s, const double* tot, const IcpParams& prm,
+                              const double* x_full) {
   s.touched_pts += (uint64_t)tot[28];
   s.touched_nodes += (uint64_t)tot[29];
   const int32_t kept = (int32_t)tot[27];
@@ -2114,17 +2129,14 @@ __device__ void update_serial(const PairDesc& d, PairState& s, const double* tot
     s.active = 0;
     return;
   }
-  double A[36], b[6];
-  int c = 0;
-  for (int a = 0; a < 6; ++a)
-    for (int bb = a; bb < 6; ++bb) {
-      A[a * 6 + bb] = tot[c];
-      A[bb * 6 + a] = tot[c];
-      ++c;
-    }
-  for (int a = 0; a < 6; ++a) b[a] = -tot[21 + a];
   double xd[6];
-  solve6(A, b, xd);
+  if (x_full) {
+    for (int a = 0; a < 6; ++a) xd[a] = x_full[a];
+  } else {
+    double A[36], b[6];
+    normal_system(tot, A, b);
+    solve6(A, b, xd);
+  }
   float x[6];
   for (int a = 0; a < 6; ++a) x[a] = (float)xd[a];
   float dT[16];
@@ -2146,17 +2158,22 @@ __device__ void update_serial(const PairDesc& d, PairState& s, const double* tot
   const int h = s.hist_count % kHistRing;
   quat_from_T(s.T, s.qh[h]);
   for (int i = 0; i < 3; ++i) s.th[h][i] = (double)s.T[12 + i];
+  if (s.hist_count >= 1) {  // entry i = hist_count against entry i - 1
+    const int bprev = (s.hist_count - 1) % kHistRing;
+    s.dq[h] = fabs(quat_angdist(s.qh[h], s.qh[bprev]));
+    const double dx = s.th[h][0] - s.th[bprev][0];
+    const double dy = s.th[h][1] - s.th[bprev][1];
+    const double dz = s.th[h][2] - s.th[bprev][2];
+    s.dt[h] = sqrt(dx * dx + dy * dy + dz * dz);
+  }
   s.hist_count += 1;
   const int sz = s.hist_count;
   if (sz > prm.smooth) {
     double cv0 = 0, cv1 = 0;
     for (int i = sz - 1; i >= sz - prm.smooth; --i) {
-      const int a = i % kHistRing, bprev = (i - 1) % kHistRing;
-      cv0 += fabs(quat_angdist(s.qh[a], s.qh[bprev]));
-      const double dx = s.th[a][0] - s.th[bprev][0];
-      const double dy = s.th[a][1] - s.th[bprev][1];
-      const double dz = s.th[a][2] - s.th[bprev][2];
-      cv1 += sqrt(dx * dx + dy * dy + dz * dz);
+      const int a = i % kHistRing;
+      cv0 += s.dq[a];
+      cv1 += s.dt[a];
     }
     cv0 /= prm.smooth;
     cv1 /= prm.smooth;
@@ -2209,7 +2226,26 @@ __device__ void icp_update_body(const PairDesc& d, PairState& s, const double* _
     tot[t] = v;
   }
   __syncthreads();
-  if (t == 0) update_serial(d, s, tot, prm);
+  // solve6's full-rank path with its two halves side by side: wave 0 the pivoted-QR rank, wave 1
+  // the LLT solve (each ~half of the serial solve); a rank below 6 or a failed LLT falls back
+  // to solve6 on lane 0
+  __shared__ int rank_llt[2];
+  __shared__ double xs[6];
+  if (t == 0 || t == 64) {
+    double A[36], b[6];
+    normal_system(tot, A, b);
+    if (t == 0) {
+      PivQR<6> q;
+      pivqr<6>(A, q);
+      rank_llt[0] = q.rank;
+    } else {
+      double x[6];
+      rank_llt[1] = llt_solve<6>(A, 6, b, x) ? 1 : 0;
+      for (int a = 0; a < 6; ++a) xs[a] = x[a];
+    }
+  }
+  __syncthreads();
+  if (t == 0) update_serial(d, s, tot, prm, rank_llt[0] == 6 && rank_llt[1] ? xs : nullptr);
 }
 
 __global__ __launch_bounds__(256) void k_icp_update(const PairDesc* __restrict__ pd, PairState* st,
