@@ -15,7 +15,7 @@ DEFAULT=("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_I
 [ ${#SETS[@]} -eq 0 ] && SETS=("${DEFAULT[@]}")
 for C in "${SETS[@]}"; do
   i=$((i+1))
-  timeout -k 10 150 rocprofv3 --pmc $C --kernel-include-regex "$R" --output-format csv -d gpurun_out/$N/p$i -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-batched > gpurun_out/$N/p$i.log 2>&1 || { tail -5 gpurun_out/$N/p$i.log; exit 1; }
+  timeout -k 10 150 rocprofv3 --pmc $C --kernel-include-regex "$R" --output-format csv -d gpurun_out/$N/p$i -o run -- python3 bench.py --config ${CFG:-c2} --steps 1 --warmup 0 --no-cpu-baseline --no-batched > gpurun_out/$N/p$i.log 2>&1 || { tail -5 gpurun_out/$N/p$i.log; exit 1; }
 done
 python3 - "$N" <<'PY'
 import csv, glob, sys, collections
