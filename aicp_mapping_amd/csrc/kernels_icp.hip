@@ -1106,7 +1106,9 @@ __device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, c
     al->n = carry_cnt;
     al->total = carry_off;
     al->off[carry_cnt] = carry_off;
-    if (host_n) *host_n = carry_cnt;  // mapped host memory: the sequence's early-exit poll
+    // mapped host memory: the sequence's early-exit poll, read by the host without an event
+    // (a system-scope store goes through to host memory; nothing else is published with it)
+    if (host_n) __hip_atomic_store(host_n, carry_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // every pair has stopped: their corrections are final (k_finalize's arithmetic), and the
   // sequence's next reference, waiting on done_sig on another stream, may start now

@@ -572,39 +572,11 @@ __device__ __forceinline__ uint32_t hoare_partner(uint32_t li, bool pred, uint32
   return lo - 1;
 }
 
-// Large builds (C5: 61 M points, segments of 60k and more): hoare_partner's binary search is ~16
-// dependent loads per misplaced element, so the misplaced elements of pass 1 first write their
-// local positions by rank (posL: non-predicate elements left of the boundary, posR: predicate
-// elements right of it) and k_tr_move1 reads its partner with one load.
-// (AICP_TREE_SCATTER_MIN overrides the threshold: the equivalence test builds small trees both ways)
-uint32_t tree_scatter_min() {  // read per build (tests switch it inside one process)
-  const char* e = std::getenv("AICP_TREE_SCATTER_MIN");
-  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (1u << 22);
-}
-__global__ __launch_bounds__(256) void k_tr_scatter1(uint32_t total, const int32_t* __restrict__ segof,
-                                                     const float4* __restrict__ W, const TreeSeg* __restrict__ seg,
-                                                     const uint32_t* __restrict__ X, uint32_t* __restrict__ posL,
-                                                     uint32_t* __restrict__ posR) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int s = segof[i];
-  if (s < 0) return;
-  const TreeSeg& g = seg[s];
-  const float v = coord(W[i], g.cd);
-  const bool pred = v < seg_cut(g);
-  const uint32_t f = g.first, li = i - f, x0 = X[f], xi = X[i];
-  const uint32_t br = X[f + g.count] - x0;
-  if (li < br && !pred) posL[f + (li - (xi - x0))] = li;
-  else if (li >= br && pred) posR[f + (xi - X[f + br])] = li;
-}
-
 // pass 1: move every element to its place, and write the pass-2 predicate at the new place
-// (posL / posR: the partner from k_tr_scatter1's lists; nullptr: hoare_partner)
 __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t* __restrict__ segof,
                                                   const float4* __restrict__ W, TreeSeg* seg,
                                                   const uint32_t* __restrict__ X, float4* __restrict__ W1,
-                                                  uint32_t* __restrict__ flag2, const uint32_t* __restrict__ posL,
-                                                  const uint32_t* __restrict__ posR) {
+                                                  uint32_t* __restrict__ flag2) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > total) return;
   if (i == total) {
@@ -621,20 +593,7 @@ __global__ __launch_bounds__(256) void k_tr_move1(uint32_t total, const int32_t*
   const float v = coord(p, g.cd), cut = seg_cut(g);
   const uint32_t f = g.first, li = i - f;
   const uint32_t br1 = X[f + g.count] - X[f];
-  uint32_t p1;
-  if (posL) {
-    const bool pred = v < cut;
-    p1 = li;
-    if (li < br1 && !pred) {
-      const uint32_t k = li - (X[i] - X[f]), nmr = X[f + g.count] - X[f + br1];
-      p1 = posR[f + (nmr - 1 - k)];
-    } else if (li >= br1 && pred) {
-      const uint32_t r = X[i] - X[f + br1], nmr = X[f + g.count] - X[f + br1];
-      p1 = posL[f + (nmr - 1 - r)];
-    }
-  } else {
-    p1 = hoare_partner(li, v < cut, f, 0, br1, g.count, X);
-  }
+  uint32_t p1 = hoare_partner(li, v < cut, f, 0, br1, g.count, X);
   if (p1 >= g.count) p1 = li;  // unreachable for a consistent scan; keeps stores in range
   W1[f + p1] = p;
   flag2[f + p1] = (p1 >= br1 && v == cut) ? 1u : 0u;
@@ -1428,312 +1387,6 @@ constexpr int kMidOut = 64;  // pieces of <= kSubMax points per mid segment (2 p
 
 static_assert(kMidMax < 65536, "k_tr_mid packs two counts of a node into one word");
 
-// ---- level-synchronous mid-size builder ---------------------------------------------------------
-// k_tr_mid's segments (<= kMidMax points) split down to pieces of <= kSubMax points, one level at
-// a time like k_tr_subtree_lvl: a level has at most kMidMax / kSubMax nodes. The coordinates stay
-// in LDS in input order (SoA) and the Hoare swaps move 16-bit indices (perm), so the segment fits
-// one workgroup's LDS; the points are gathered into their final order at the end (all reads
-// before the barrier, then the writes: the segment is rewritten in place).
-constexpr int kMlThreads = 1024;
-constexpr int kMlPer = kMidMax / kMlThreads;
-constexpr int kMlNodes = 2 * (kMidMax / (kSubMax + 1)) + 2;  // nodes above kSubMax in a level
-static_assert(kMidMax % kMlThreads == 0 && kMidMax <= 65536, "mid positions fit 16 bits");
-
-__global__ __launch_bounds__(kMlThreads) void k_tr_mid_lvl(uint32_t total, TreeCtl* ctl,
-                                                           const SubSeg* __restrict__ mids, SubSeg* subs,
-                                                           float4* W, float4* __restrict__ bpts, NodeEvent* ev,
-                                                           uint8_t* valid, uint32_t* ecnt, int32_t* pair_depth,
-                                                           int bucket, uint32_t max_seg) {
-  __shared__ float cx[3][kMidMax];      // coordinates, input order
-  __shared__ uint16_t perm[kMidMax];    // input index at each position
-  __shared__ uint16_t posB[kMidMax];
-  __shared__ uint8_t nid[kMidMax];      // node of each position in the level, 0xFF: done
-  __shared__ uint32_t wtot[kMlPer][kMlThreads / 64];
-  // the level's nodes: first / count, box, parent first; per level: cut dim, ideal, min / max,
-  // counts nl | ne << 16, misplaced-right count, rank base, left, children
-  __shared__ uint32_t nf[2][kMlNodes], nc[2][kMlNodes], npf[2][kMlNodes];
-  __shared__ float nmn[2][3][kMlNodes], nmx[2][3][kMlNodes];
-  __shared__ int ncd[kMlNodes];
-  __shared__ float nideal[kMlNodes];
-  __shared__ uint32_t nlo[kMlNodes], nhi[kMlNodes], ncnt[kMlNodes], nmr[kMlNodes], nbase[kMlNodes], nleft[kMlNodes];
-  __shared__ int nch[2][kMlNodes];
-  __shared__ SubSeg outq[kMidOut];
-  __shared__ uint32_t n_next, any_eq, nout_s, base_s;
-  const int t = threadIdx.x;
-  const uint32_t n_mid = ctl->n_mid;
-  for (uint32_t mi = blockIdx.x; mi < n_mid; mi += gridDim.x) {
-    __syncthreads();
-    const SubSeg g = mids[mi];
-    const uint32_t gf = g.f, n = g.c;
-    if (n > (uint32_t)kMidMax) {  // (mid_max above the LDS size: a configuration error)
-      if (t == 0) atomicOr(&ctl->error, 8);
-      continue;
-    }
-    for (uint32_t j = t; j < n; j += kMlThreads) {
-      const float4 q = W[gf + j];
-      cx[0][j] = q.x;
-      cx[1][j] = q.y;
-      cx[2][j] = q.z;
-      perm[j] = (uint16_t)j;
-      nid[j] = 0;
-    }
-    if (t == 0) {
-      nf[0][0] = 0;
-      nc[0][0] = n;
-      npf[0][0] = g.parent_f;
-      for (int k = 0; k < 3; ++k) {
-        nmn[0][k][0] = g.mn[k];
-        nmx[0][k][0] = g.mx[k];
-      }
-      nout_s = 0;
-    }
-    int cur = 0;
-    uint32_t nn = 1;
-    int depth = g.depth, maxd = g.depth;
-    for (;;) {
-      if ((uint32_t)t < nn) {
-        float mn[3], mx[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          mn[k] = nmn[cur][k][t];
-          mx[k] = nmx[cur][k][t];
-        }
-        int cd;
-        float ideal;
-        split_dim(mn, mx, cd, ideal);
-        ncd[t] = cd;
-        nideal[t] = ideal;
-        nlo[t] = 0xFFFFFFFFu;
-        nhi[t] = 0u;
-        ncnt[t] = 0u;
-      }
-      if (t == 0) {
-        n_next = 0;
-        any_eq = 0;
-      }
-      __syncthreads();
-      // the cut coordinate of position p (input order through perm) and the node's cut
-      auto val = [&](uint32_t p, int i) { return cx[ncd[i]][perm[p]]; };
-      auto cut_of = [&](int i) {
-        const float lo = ord_dec(nlo[i]), hi = ord_dec(nhi[i]), id = nideal[i];
-        return id < lo ? lo : (id > hi ? hi : id);
-      };
-      auto node_of = [&](uint32_t p) -> int {
-        const uint32_t i = p < n ? nid[p] : 0xFFu;
-        return i == 0xFFu ? -1 : (int)i;
-      };
-#pragma unroll 1
-      for (int u = 0; u < kMlPer; ++u) {
-        const uint32_t p = (uint32_t)(u * kMlThreads + t);
-        const int i = node_of(p);
-        const float v = i >= 0 ? val(p, i) : 0.f;
-        float a = i >= 0 ? v : __builtin_inff(), b = i >= 0 ? v : -__builtin_inff();
-        if (wave_seg_minmax(i, a, b) && i >= 0) {
-          atomicMin(&nlo[i], ord_enc(a));
-          atomicMax(&nhi[i], ord_enc(b));
-        }
-      }
-      __syncthreads();
-#pragma unroll 1
-      for (int u = 0; u < kMlPer; ++u) {
-        const uint32_t p = (uint32_t)(u * kMlThreads + t);
-        const int i = node_of(p);
-        uint32_t x = 0;
-        if (i >= 0) {
-          const float v = val(p, i), c = cut_of(i);
-          x = v < c ? 1u : (v == c ? 0x10000u : 0u);
-        }
-        if (wave_seg_sum(i, x) && i >= 0 && x) {
-          atomicAdd(&ncnt[i], x);
-          if (x >> 16) any_eq = 1;
-        }
-      }
-      __syncthreads();
-      for (int pass = 0; pass < 2; ++pass) {
-        if (pass == 1 && !any_eq) break;
-        if ((uint32_t)t < nn) nmr[t] = 0;
-        // the packed pass flag of position p: misplaced left (1) / right (1 << 16) of its node
-        auto flag = [&](uint32_t p) -> uint32_t {
-          const uint32_t i = p < n ? nid[p] : 0xFFu;
-          if (i == 0xFFu) return 0u;
-          const uint32_t loc = p - nf[cur][i], nl = ncnt[i] & 0xFFFFu, ne = ncnt[i] >> 16;
-          const float v = val(p, (int)i), c = cut_of((int)i);
-          const bool pr = pass == 0 ? v < c : v == c;
-          const uint32_t lo_b = pass == 0 ? 0u : nl, br = pass == 0 ? nl : nl + ne;
-          if (loc < lo_b) return 0u;
-          return (loc < br && !pr) ? 1u : ((loc >= br && pr) ? 0x10000u : 0u);
-        };
-        // block-wide exclusive scan of the packed flags (ml | mr << 16) in position order; the
-        // thread at a node's first position keeps the node's base, counts of mr per node
-        uint32_t ex[kMlPer];  // inclusive, then exclusive prefix
-        const int lane = t & 63, wv = t >> 6;
-#pragma unroll
-        for (int u = 0; u < kMlPer; ++u) {
-          uint32_t x = flag((uint32_t)(u * kMlThreads + t));
-#pragma unroll
-          for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off, 64);
-            if (lane >= off) x += y;
-          }
-          ex[u] = x;
-          if (lane == 63) wtot[u][wv] = x;
-        }
-        __syncthreads();
-        {
-          uint32_t base = 0;
-#pragma unroll
-          for (int u = 0; u < kMlPer; ++u) {
-            uint32_t b = base;
-#pragma unroll
-            for (int w = 0; w < kMlThreads / 64; ++w) {
-              if (w < wv) b += wtot[u][w];
-              base += wtot[u][w];
-            }
-            const uint32_t p = (uint32_t)(u * kMlThreads + t);
-            const uint32_t fl = flag(p);
-            ex[u] = b + ex[u] - fl;
-            const int kk = node_of(p);
-            if (kk >= 0 && p == nf[cur][kk]) nbase[kk] = ex[u];
-            uint32_t m = fl >> 16;
-            if (wave_seg_sum(kk, m) && kk >= 0 && m) atomicAdd(&nmr[kk], m);
-          }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kMlPer; ++u) {
-          const uint32_t p = (uint32_t)(u * kMlThreads + t);
-          if (flag(p) >> 16) {
-            const int i = nid[p];
-            posB[nf[cur][i] + ((ex[u] - nbase[i]) >> 16)] = (uint16_t)p;
-          }
-        }
-        __syncthreads();
-        uint32_t ml = 0;  // (the flags before any swap of this pass: one bit per u)
-#pragma unroll
-        for (int u = 0; u < kMlPer; ++u)
-          if (flag((uint32_t)(u * kMlThreads + t)) & 0xFFFFu) ml |= 1u << u;
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kMlPer; ++u)
-          if ((ml >> u) & 1u) {
-            const uint32_t p = (uint32_t)(u * kMlThreads + t);
-            const int i = nid[p];
-            const uint32_t f0 = nf[cur][i];
-            const uint32_t k = (ex[u] - nbase[i]) & 0xFFFFu;
-            const uint32_t b = posB[f0 + nmr[i] - 1 - k];
-            const uint16_t a = perm[p];
-            perm[p] = perm[b];
-            perm[b] = a;
-          }
-        __syncthreads();
-      }
-      if ((uint32_t)t < nn) {
-        const uint32_t count = nc[cur][t], nl = ncnt[t] & 0xFFFFu, ne = ncnt[t] >> 16;
-        const float lo = ord_dec(nlo[t]), hi = ord_dec(nhi[t]), ideal = nideal[t];
-        const float ct = ideal < lo ? lo : (ideal > hi ? hi : ideal);
-        const int cd = ncd[t];
-        const uint32_t br1 = nl, br2 = nl + ne;
-        uint32_t left;
-        if (ideal < lo) left = 1;
-        else if (ideal > hi) left = count - 1;
-        else if (br1 > count / 2) left = br1;
-        else if (br2 < count / 2) left = br2;
-        else left = count / 2;
-        nleft[t] = left;
-        const uint32_t f0 = nf[cur][t];
-        NodeEvent e{};
-        e.f = gf + f0;
-        e.c = count;
-        e.depth = depth;
-        e.pair = g.pair;
-        e.cut_bits = __float_as_uint(ct);
-        e.cd = cd;
-        e.left = left;
-        e.parent_f = npf[cur][t];
-        e.parent_depth = depth == g.depth ? g.parent_depth : depth - 1;
-        emit_event(ev, valid, ecnt, total, e);
-        for (int side = 0; side < 2; ++side) {
-          const uint32_t cf = side ? f0 + left : f0, cc = side ? count - left : left;
-          float cmn[3], cmx[3];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            cmn[k] = (side && k == cd) ? ct : nmn[cur][k][t];
-            cmx[k] = (!side && k == cd) ? ct : nmx[cur][k][t];
-          }
-          nch[side][t] = -1;
-          if (cc <= (uint32_t)bucket) {
-            emit_event(ev, valid, ecnt, total, leaf_event(gf + cf, cc, depth + 1, g.pair, gf + f0, depth));
-          } else if (cc <= (uint32_t)kSubMax) {
-            const uint32_t q = atomicAdd(&nout_s, 1u);
-            if (q >= (uint32_t)kMidOut) {
-              atomicOr(&ctl->error, 8);
-              continue;
-            }
-            SubSeg& o = outq[q];
-            o.f = gf + cf;
-            o.c = cc;
-            o.pair = g.pair;
-            o.depth = depth + 1;
-            for (int k = 0; k < 3; ++k) {
-              o.mn[k] = cmn[k];
-              o.mx[k] = cmx[k];
-            }
-            o.parent_f = gf + f0;
-            o.parent_depth = depth;
-          } else {
-            const uint32_t q = atomicAdd(&n_next, 1u);
-            if (q >= (uint32_t)kMlNodes) {
-              atomicOr(&ctl->error, 8);
-              continue;
-            }
-            nf[cur ^ 1][q] = cf;
-            nc[cur ^ 1][q] = cc;
-            npf[cur ^ 1][q] = gf + f0;
-            for (int k = 0; k < 3; ++k) {
-              nmn[cur ^ 1][k][q] = cmn[k];
-              nmx[cur ^ 1][k][q] = cmx[k];
-            }
-            nch[side][t] = (int)q;
-          }
-        }
-      }
-      __syncthreads();
-#pragma unroll 1
-      for (int u = 0; u < kMlPer; ++u) {
-        const uint32_t p = (uint32_t)(u * kMlThreads + t);
-        const int i = node_of(p);
-        if (i >= 0) {
-          const int c = nch[(p - nf[cur][i]) < nleft[i] ? 0 : 1][i];
-          nid[p] = c < 0 ? 0xFFu : (uint8_t)c;
-        }
-      }
-      maxd = depth + 1;
-      nn = n_next;
-      __syncthreads();
-      if (nn == 0) break;
-      cur ^= 1;
-      ++depth;
-    }
-    {  // the queued pieces: one reservation, then a copy by the first nout threads
-      const uint32_t nout = nout_s < (uint32_t)kMidOut ? nout_s : (uint32_t)kMidOut;
-      if (t == 0) base_s = nout ? atomicAdd(&ctl->n_small, nout) : 0u;
-      __syncthreads();
-      const uint32_t base = base_s;
-      if ((uint32_t)t < nout) {
-        if (base + (uint32_t)t < max_seg) subs[base + t] = outq[t];
-        else atomicOr(&ctl->error, 4);
-      }
-    }
-    // the points in their new order: bpts (the leaves emitted here) gathered from W, then W (for
-    // the subtree builders) copied back from bpts once every read of W has completed
-    for (uint32_t p = t; p < n; p += kMlThreads) bpts[gf + p] = W[gf + perm[p]];
-    __syncthreads();
-    for (uint32_t p = t; p < n; p += kMlThreads) W[gf + p] = bpts[gf + p];
-    if (t == 0 && pair_depth[g.pair] < maxd) atomicMax(&pair_depth[g.pair], maxd);
-  }
-}
-
-
 #ifndef AICP_ITER_PROF
 #define AICP_ITER_PROF 0
 #endif
@@ -2269,13 +1922,13 @@ void launch_pairs_degenerate_part(hipStream_t s, int n_pairs, const PairDesc* pd
 
 // look-back words of every scan of a build: two per global level and the node count scan
 size_t lb_stride_words(uint32_t total) { return lb_words(total + 2); }
-uint32_t tree_mid_max() {  // (A/B, temporary: AICP_TREE_MIDMAX)
-  const char* e = std::getenv("AICP_TREE_MIDMAX");
-  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)kMidMax;
-}
-bool tree_lvl_enabled() {  // (A/B, temporary: AICP_TREE_LVL=0 -> k_tr_subtree_blk)
-  const char* e = std::getenv("AICP_TREE_LVL");
-  return !e || std::atoi(e) != 0;
+uint32_t tree_mid_max() { return (uint32_t)kMidMax; }
+// k_tr_subtree_lvl from this many points of a build (C5: 61 M); smaller builds are latency-bound
+// and keep k_tr_subtree_blk (r04: C2 2620 against 2479 clouds/s with the level builder).
+// AICP_TREE_LVL_MIN overrides it (the equivalence test builds small trees both ways).
+uint32_t tree_lvl_min() {
+  const char* e = std::getenv("AICP_TREE_LVL_MIN");
+  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (1u << 22);
 }
 size_t lb_bytes(uint32_t total) { return (size_t)(2 * kFarStack + 1) * lb_stride_words(total) * 8; }
 
@@ -2315,10 +1968,7 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
   uint64_t* st2 = st1 + w.lb_stride;
   // level 0: the roots' boxes (k_tr_center); later levels: the previous level's move2 (move2_minmax)
   k_tr_scan1<<<nt1, kLbThreads, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, st1, w.ctl);
-  const bool scat = total >= tree_scatter_min() && w.posL && w.posR;
-  if (scat) k_tr_scatter1<<<(total + 255) / 256, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.posL, w.posR);
-  k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.W[1], w.flag, scat ? w.posL : nullptr,
-                                 scat ? w.posR : nullptr);
+  k_tr_move1<<<gp1, 256, 0, s>>>(total, w.segof[a], w.W[0], seg, w.X1, w.W[1], w.flag);
   k_tr_scan_counts<<<nt1, kLbThreads, 0, s>>>(total + 1, w.flag, w.X2, st2, w.ctl);
   k_tr_split<<<gs, 256, 0, s>>>(level, last ? 1 : 0, total, seg, next, w.subs, w.mids, w.ctl, w.X2, w.ev, w.valid,
                                 w.ecnt, w.pair_depth, bucket, (uint32_t)w.max_seg, w.mid_max);
@@ -2331,7 +1981,7 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
 hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts, int bucket) {
   const size_t bound = std::min<size_t>(w.max_seg, (size_t)total / (size_t)(bucket + 1) + (size_t)w.n_pairs + 1);
   const bool blk = bucket >= 4;  // level widths fit kSubLevelCap
-  if (bucket >= 8 && tree_lvl_enabled()) {  // level widths fit kLvlCap
+  if (bucket >= 8 && total >= tree_lvl_min()) {  // level widths fit kLvlCap
     const unsigned gl = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, 2048));
     k_tr_subtree_lvl<<<gl, kLvlThreads, 0, s>>>(total, w.ctl, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt,
                                                  w.pair_depth, bucket);
@@ -2352,12 +2002,8 @@ hipError_t launch_tree_mid(hipStream_t s, uint32_t total, const TreeWork& w, flo
   // device-side count)
   const size_t bound = std::min<size_t>(w.max_seg, (size_t)total / (size_t)(kSubMax + 1) + (size_t)w.n_pairs + 1);
   const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, 1024));
-  if (tree_lvl_enabled())
-    k_tr_mid_lvl<<<g, kMlThreads, 0, s>>>(total, w.ctl, w.mids, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt,
-                                          w.pair_depth, bucket, (uint32_t)w.max_seg);
-  else
-    k_tr_mid<<<g, kMidThreads, 0, s>>>(total, w.ctl, w.mids, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt,
-                                       w.pair_depth, bucket, (uint32_t)w.max_seg);
+  k_tr_mid<<<g, kMidThreads, 0, s>>>(total, w.ctl, w.mids, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt, w.pair_depth,
+                                     bucket, (uint32_t)w.max_seg);
   return hipGetLastError();
 }
 

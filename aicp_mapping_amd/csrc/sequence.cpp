@@ -191,7 +191,6 @@ struct SeqSlot {
   // alternate, so a loop's trailing write never lands in its successor's words)
   uint32_t* poll_host = nullptr;  // hipHostMalloc(mapped), 2 * kMaxPolls words
   uint32_t* poll_dev = nullptr;   // its device address
-  hipEvent_t ev_poll[2 * kMaxPolls] = {};
   GraphCache g_match;
   bool used = false;
 };
@@ -227,8 +226,6 @@ void seq_state_free(SeqState* S) {
     sl.g_match.reset();
     for (PinBuf* b : {&sl.pin_read, &sl.pin_par, &sl.pin_src}) release(*b);
     for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done})
-      if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : sl.ev_poll)
       if (e) (void)hipEventDestroy(e);
     if (sl.poll_host) (void)hipHostFree(sl.poll_host);
   }
@@ -1019,9 +1016,11 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
 
 // The ICP loop of a window, polled: from iteration smoothLength on (no pair can stop earlier
 // except on an error) the update kernel of the last pair to finish an iteration writes the next
-// active count into mapped host memory; the host, one iteration ahead, stops enqueueing once it
-// reads 0 (the launch after the one that found no active pair is a no-op that still holds the
-// stream). The window's states and corrections are then committed to the sequence's arrays
+// active count into mapped host memory (a system-scope store); the host, one iteration ahead,
+// reads the word itself and stops enqueueing once it reads 0 (the launch after the one that found
+// no active pair is a no-op that still holds the stream). (r03 recorded an event per poll and
+// queried it: each marker left a 5-10 us gap before the next NN launch, C2 2512 against 2620
+// clouds/s in r04.) The window's states and corrections are then committed to the sequence's arrays
 // (ev_done), which the next reference waits for.
 // (r03, measured and removed: the window's last reading -- the next reference's source -- in a
 // loop of its own with the others on a second stream: the one-reading loop took 0.99 against
@@ -1126,7 +1125,6 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   HIPC(hipGetLastError());
   for (int k : {hn_this ? it : -1, hn_next ? it + 1 : -1})
     if (k >= 0) {
-      HIPC(hipEventRecord(sl.ev_poll[q.area * kMaxPolls + k], st));
       q.pending.push_back(k);
     }
   ++q.it;
@@ -1153,12 +1151,24 @@ static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool& got) {
   got = false;
   SeqSlot& sl = S->slot[q.R->w.slot];
   const int k = q.pending.front();
-  const hipError_t r = hipEventQuery(sl.ev_poll[q.area * kMaxPolls + k]);
-  if (r == hipErrorNotReady) return AICP_OK;
-  HIPC(r);
+  volatile uint32_t* w = sl.poll_host + q.area * kMaxPolls + k;
+  if (*w == 0xffffffffu) {
+    // not written yet: still running, or the launch that writes it had no active pair (then
+    // the stream drains and the word stays unwritten: the loop is over)
+    const hipError_t r = hipStreamQuery(S->s_icp);
+    if (r == hipErrorNotReady) return AICP_OK;
+    HIPC(r);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (*w == 0xffffffffu) {
+      q.pending.pop_front();
+      got = true;
+      q.stop = true;
+      return AICP_OK;
+    }
+  }
   q.pending.pop_front();
   got = true;
-  if (sl.poll_host[q.area * kMaxPolls + k] == 0) q.stop = true;
+  if (*w == 0) q.stop = true;
   return AICP_OK;
 }
 
@@ -1226,7 +1236,6 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     for (SeqSlot& sl : S->slot) {
       for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
-      for (hipEvent_t& e : sl.ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       HIPC(hipHostMalloc((void**)&sl.poll_host, 2 * kMaxPolls * 4, hipHostMallocMapped));
       HIPC(hipHostGetDevicePointer((void**)&sl.poll_dev, sl.poll_host, 0));
     }

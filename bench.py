@@ -301,6 +301,19 @@ def load_traffic(name):
         return None
 
 
+def add_traffic(rf, name):
+    """PMC HBM bytes per launch (profiles/<name>, tools/profile.sh) into the roofline object, and
+    the fraction of peak they are at this run's launch time beside the algorithmic fraction (on
+    the C2 window the tree and the points stay in L2 / MALL, so the counters see far fewer bytes
+    than the algorithmic model counts)."""
+    tr = load_traffic(name)
+    if not tr or not tr.get("bytes_per_launch") or not rf.get("avg_launch_us"):
+        return
+    rf["traffic"] = tr["bytes_per_launch"]
+    rf["traffic_source"] = tr.get("source", name)
+    rf["traffic_frac"] = round(tr["bytes_per_launch"] / (rf["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+
+
 def base_line(args, world, metric, value, unit, ms_per_step, dtype, data, config, scaling="weak", hib=True):
     return {
         "metric": metric,
@@ -348,11 +361,17 @@ def bench_stream(args):
     ctx = L.Context(local_rank)
     cfg = L.default_config()
     debug = args.working_mode == "debug"
-    prm = L.default_sequence_params(reference_update_frequency=args.ref_every,
-                                    flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_TIME_NN | (L.AICP_SEQ_DEBUG if debug else 0))
+    flags = L.AICP_RUN_OVERLAP | (L.AICP_SEQ_DEBUG if debug else 0)
+    prm = L.default_sequence_params(reference_update_frequency=args.ref_every, flags=flags)
+    # HIP events on the NN launches (AICP_RUN_TIME_NN) only in the last timed step: each timed
+    # launch costs ~11 us of dispatch gaps around the NN on the ICP stream (r04 kernel trace:
+    # update -> NN 7 us, NN -> select 4.5 us, against ~0 between the other kernels), ~5 % of a
+    # C2 window, so the roofline's launch average comes from one step of the timed region
+    prm_t = L.default_sequence_params(reference_update_frequency=args.ref_every, flags=flags | L.AICP_RUN_TIME_NN)
 
-    def step():
-        T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, cfg, prm)
+    def step(timed=False):
+        T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, cfg,
+                                            prm_t if timed else prm)
         if dist is not None:
             sh.gather_records(sh.pack_records(T.transpose(0, 2, 1).reshape(-1, 16),
                                               [o["icp"]["iterations"] for o in out],
@@ -367,8 +386,8 @@ def bench_stream(args):
     dev_ms = wall_ms = 0.0
     windows = replans = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        T, out = step()
+    for k_step in range(args.steps):
+        T, out = step(timed=k_step == args.steps - 1)
         t = ctx.last_nn_timing()
         for k in ("launches", "total_ms", "bytes"):
             nn[k] += t[k]
@@ -442,10 +461,7 @@ def bench_stream(args):
                                         "one launch per ICP iteration of a reference window (5 readings)"),
             "batched_independent": batched,
         })
-        tr = load_traffic("r03_nn_traffic_%s.json" % args.config)
-        if tr:
-            out_line["roofline"]["traffic"] = tr.get("bytes_per_launch")
-            out_line["roofline"]["traffic_source"] = tr.get("source")
+        add_traffic(out_line["roofline"], "nn_traffic_%s.json" % args.config)
         if world == 1 and not args.no_cpu_baseline:
             out_line["cpu_baseline"], out_line["parity_vs_oracle"] = cpu_stream(st, T, out, args)
         print(json.dumps(out_line))
@@ -629,10 +645,7 @@ def bench_c5(args):
                      "accuracy_vs_ground_truth": {"median_rot_rad": float(np.median([e[0] for e in errs])),
                                                   "median_trans_m": float(np.median([e[1] for e in errs]))},
                      "roofline": roofline_nn(nn, "k_icp_nn, one launch per ICP iteration of the 1024-pair batch")})
-        tr = load_traffic("r03_nn_traffic_c5.json")
-        if tr:
-            line["roofline"]["traffic"] = tr.get("bytes_per_launch")
-            line["roofline"]["traffic_source"] = tr.get("source")
+        add_traffic(line["roofline"], "nn_traffic_c5.json")
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"], line["cpu_baseline_all_cores"], line["parity_vs_oracle"] = cpu_c5(pairs, T, args)
         print(json.dumps(line))

@@ -444,13 +444,18 @@ def test_block_subtree_builder_matches_oracle_trees(ctx, oracle, L):
         assert r < 1e-6 and t < 1e-5
 
 
-@pytest.mark.parametrize("bucket", [8, 6])
-def test_subtree_builders_match_oracle_trees(ctx, oracle, L, bucket):
-    """bucketSize 8: the level-synchronous subtree builder (k_tr_subtree_lvl); 6: the block
-    builder (k_tr_subtree_blk). Both give libnabo's trees: touch counts, depth, normals."""
+@pytest.mark.parametrize("builder", ["level", "block", "block_b6"])
+def test_subtree_builders_match_oracle_trees(ctx, oracle, L, monkeypatch, builder):
+    """The finishing builders below the global levels give libnabo's trees (touch counts, depth,
+    normals): k_tr_subtree_lvl (all nodes of a level per pass; builds of >= 4 M points, forced
+    here), k_tr_subtree_blk (a node per wave) with bucketSize 8 and 6."""
+    bucket = 6 if builder == "block_b6" else 8
+    if builder == "level":
+        monkeypatch.setenv("AICP_TREE_LVL_MIN", "1")
     prs = [sy.make_pair(20000, 20000, seed=90 + i) for i in range(2)]
     pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
     T, st, rc = ctx.align_batch(pairs, flags=L.AICP_RUN_ICP, cfg=L.default_config(trimmed_ratio=0.65, bucket_size=bucket))
+    monkeypatch.delenv("AICP_TREE_LVL_MIN", raising=False)
     assert rc == 0
     for i, p in enumerate(prs):
         rc1, T1, st1 = oracle.icp(p.ref, p.read, oracle.default_config(trimmed_ratio=0.65, bucket_size=bucket))
@@ -459,23 +464,6 @@ def test_subtree_builders_match_oracle_trees(ctx, oracle, L, bucket):
         assert st[i]["degenerate_normals"] == st1.degenerate_normals
         r, t = sy.rot_err(T1, T[i])
         assert r < 1e-6 and t < 1e-5
-
-
-def test_scatter_partner_levels_identical(ctx, L, monkeypatch):
-    """The global levels' pass-1 partners from rank lists (k_tr_scatter1, builds of >= 4 M points)
-    equal the binary-search partners: forced on a small batch, same transforms and touch counts."""
-    prs = [sy.make_pair(30000, 30000, seed=75 + i) for i in range(3)]
-    pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
-    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
-    Ta, sa, rca = ctx.align_batch(pairs, flags=flags, resolution=RES)
-    monkeypatch.setenv("AICP_TREE_SCATTER_MIN", "1")
-    Tb, sb, rcb = ctx.align_batch(pairs, flags=flags, resolution=RES)
-    monkeypatch.delenv("AICP_TREE_SCATTER_MIN")
-    assert rca == rcb == 0
-    np.testing.assert_array_equal(Ta, Tb)
-    for a, b in zip(sa, sb):
-        assert (a["iterations"], a["tree_depth"], a["nn_points_touched"], a["nn_nodes_touched"]) == \
-               (b["iterations"], b["tree_depth"], b["nn_points_touched"], b["nn_nodes_touched"])
 
 
 def test_resident_batch_full_size_round_trip(ctx, L):
