@@ -915,12 +915,7 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   };
   // the raw tree + SurfaceNormal as direct launches (replayed from a graph they finished 0.08 ms
   // later on the device, r03), enqueued after the matcher tree's graph
-  auto raw_enqueue = [&]() -> int {
-    const int r = raw_build();
-    if (r || !capturable) return r;
-    HIPC(hipMemcpyAsync(ctl_w, sl.tb[0].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
-    return AICP_OK;
-  };
+  auto raw_enqueue = [&]() -> int { return raw_build(); };
   // ---- r3: centroid + matcher tree + treelets
   auto match_build = [&]() -> int {
     int r = device_trees_begin(sl.tb[1], ctx->err, s3, 1, n_ref, dRdesc, sl.ref_raw.as<float4>(), 1, bucket, sl.bpts,
@@ -948,10 +943,12 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
       r = match_build();
     }
     if (r) return r;
-    if (capturable || use_tl)
-      HIPC(hipMemcpyAsync(ctl_w + 1, sl.tb[1].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
     HIPC(hipEventRecord(sl.ev_s3, s3));
     if (R.tev) HIPC(hipEventRecord(R.tev[1], s3));
+    // the build's control block for the host's check after the run, behind the event the loop
+    // waits for (in front of it, the D2H copy held the loop start ~15 us per window, r04 trace)
+    if (capturable || use_tl)
+      HIPC(hipMemcpyAsync(ctl_w + 1, sl.tb[1].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
     return AICP_OK;
   };
   // the matcher tree, which the window's loop starts on, goes first
@@ -965,6 +962,7 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_s2, s2));
   if (R.tev) HIPC(hipEventRecord(R.tev[2], s2));
+  if (capturable) HIPC(hipMemcpyAsync(ctl_w, sl.tb[0].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
   return AICP_OK;
 }
 
