@@ -1781,36 +1781,38 @@ __device__ void pair_done(const IcpIterSync& y) {
 }
 
 // k_sel_hist + (last workgroup of the pair) k_sel_find1; a pair that stops here is done with
-// the iteration
-__global__ __launch_bounds__(256) void k_sel_hist_f(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
-                                                    const float* __restrict__ d2, uint32_t* __restrict__ hist1,
-                                                    IcpIterSync y) {
+// the iteration. kT threads per workgroup over kNNBlock * kSelPerThread readings (two LDS
+// sub-histograms, one per half of the workgroup); the tail reads the pair's global histogram.
+// 256 threads: with 1024 the sub-histograms' atomic conflicts doubled the kernel (C2 r04,
+// rocprofv3: 21.1 against 11.3 us).
+template <int kT>
+__global__ __launch_bounds__(kT) void k_sel_hist_f(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
+                                                   const float* __restrict__ d2, uint32_t* __restrict__ hist1,
+                                                   IcpIterSync y) {
+  constexpr int kPer = kNNBlock * kSelPerThread / kT;
   AICP_IP_T0;
   const int pair = m.pair[blockIdx.x];
   if (!st[pair].active) return;
-  __shared__ uint32_t h[2][kHistBins];  // one sub-histogram per wave pair (LDS atomic conflicts)
+  __shared__ uint32_t h[2][kHistBins];  // one sub-histogram per half workgroup (LDS atomic conflicts)
   const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 2 * kHistBins / 256; ++i) (&h[0][0])[t + 256 * i] = 0;
+  for (int i = t; i < 2 * kHistBins; i += kT) (&h[0][0])[i] = 0;
   const PairDesc& d = pd[pair];
   const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
   const uint32_t j0 = m.start[blockIdx.x];
-  uint32_t v[kSelPerThread];
+  uint32_t v[kPer];
 #pragma unroll
-  for (int u = 0; u < kSelPerThread; ++u) {
-    const uint32_t j = j0 + t + 256u * u;
+  for (int u = 0; u < kPer; ++u) {
+    const uint32_t j = j0 + t + (uint32_t)kT * u;
     v[u] = j < d.n_read ? bits[j] : kInfBits;
   }
   __syncthreads();
-  uint32_t* mine = h[t >> 7];
+  uint32_t* mine = h[t / (kT / 2)];
 #pragma unroll
-  for (int u = 0; u < kSelPerThread; ++u)
+  for (int u = 0; u < kPer; ++u)
     if (v[u] != kInfBits) atomicAdd(&mine[v[u] >> 21], 1u);
   __syncthreads();
   uint32_t* g = hist1 + (size_t)pair * kHistBins;
-#pragma unroll
-  for (int i = 0; i < kHistBins / 256; ++i) {
-    const int b = t + 256 * i;
+  for (int b = t; b < kHistBins; b += kT) {
     const uint32_t c = h[0][b] + h[1][b];
     if (c) atomicAdd(&g[b], c);
   }
@@ -1821,6 +1823,10 @@ __global__ __launch_bounds__(256) void k_sel_hist_f(BlockMap m, const PairDesc* 
   if (!sel_find1_body(st[pair], g)) pair_done(y);
   AICP_IP_TAIL(0);
 }
+#ifndef AICP_SEL_HIST_THREADS
+#define AICP_SEL_HIST_THREADS 256
+#endif
+constexpr int kSelHistThreads = AICP_SEL_HIST_THREADS;
 
 __global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc* __restrict__ pd,
                                                      const PairState* __restrict__ st, const float* __restrict__ d2,
@@ -1925,35 +1931,41 @@ __global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__
   sel_final_body(s, cand + pd[pair].read_off, cand_cnt + pair);
 }
 
-// k_sel_compact + (last workgroup of the pair) k_sel_final
-__global__ __launch_bounds__(256) void k_sel_compact_f(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
-                                                       const float* __restrict__ d2, uint32_t* __restrict__ cand,
-                                                       uint32_t* __restrict__ cand_cnt, IcpIterSync y) {
+// k_sel_compact + (last workgroup of the pair) k_sel_final. kT threads per workgroup over the
+// same kNNBlock * kSelPerThread readings of a block-map entry: with 1024 the final select's tail
+// loads its ~6k candidates (written from every XCD) in one round of loads instead of three.
+template <int kT>
+__global__ __launch_bounds__(kT) void k_sel_compact_f(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
+                                                      const float* __restrict__ d2, uint32_t* __restrict__ cand,
+                                                      uint32_t* __restrict__ cand_cnt, IcpIterSync y) {
+  constexpr int kPer = kNNBlock * kSelPerThread / kT, kW = kT / 64;
   AICP_IP_T0;
   const int pair = m.pair[blockIdx.x];
   PairState& s = st[pair];
   if (!s.active) return;
-  __shared__ uint32_t wcount[4];
+  __shared__ uint32_t wcount[kW];
   __shared__ uint32_t base;
   const PairDesc& d = pd[pair];
   const uint32_t b1 = s.sel_b1;
   const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint32_t j0 = m.start[blockIdx.x];
-  uint32_t v[kSelPerThread];
+  uint32_t v[kPer];
 #pragma unroll
-  for (int u = 0; u < kSelPerThread; ++u) {
-    const uint32_t j = j0 + t + 256u * u;
+  for (int u = 0; u < kPer; ++u) {
+    const uint32_t j = j0 + t + (uint32_t)kT * u;
     v[u] = j < d.n_read ? bits[j] : kInfBits;
   }
   uint32_t mine = 0;  // this wave's hits
 #pragma unroll
-  for (int u = 0; u < kSelPerThread; ++u)
+  for (int u = 0; u < kPer; ++u)
     mine += (uint32_t)__popcll(__ballot(v[u] != kInfBits && (v[u] >> 21) == b1));
   if (lane == 0) wcount[w] = mine;
   __syncthreads();
   if (t == 0) {
-    const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < kW; ++k) tot += wcount[k];
     base = tot ? atomicAdd(&cand_cnt[pair], tot) : 0u;
   }
   __syncthreads();
@@ -1962,7 +1974,7 @@ __global__ __launch_bounds__(256) void k_sel_compact_f(BlockMap m, const PairDes
     for (int k = 0; k < w; ++k) o += wcount[k];
     const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int u = 0; u < kSelPerThread; ++u) {
+    for (int u = 0; u < kPer; ++u) {
       const bool hit = v[u] != kInfBits && (v[u] >> 21) == b1;
       const uint64_t mk = __ballot(hit);
       if (hit) cand[d.read_off + o + (uint32_t)__popcll(mk & below)] = v[u];
@@ -1976,6 +1988,10 @@ __global__ __launch_bounds__(256) void k_sel_compact_f(BlockMap m, const PairDes
   sel_final_body(s, cand + d.read_off, cand_cnt + pair);
   AICP_IP_TAIL(1);
 }
+#ifndef AICP_SEL_COMPACT_THREADS
+#define AICP_SEL_COMPACT_THREADS 1024
+#endif
+constexpr int kSelCompactThreads = AICP_SEL_COMPACT_THREADS;
 
 // DPP lane moves of a double (both halves with the same control); lanes outside the
 // pattern read 0 (bound_ctrl), which the sums below never use
@@ -2565,8 +2581,8 @@ IcpIterSync icp_sync_layout(uint32_t* words, size_t n_pairs, int group) {
 void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
                          uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y) {
   if (!m.n_blocks) return;
-  k_sel_hist_f<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, hist1, y);
-  k_sel_compact_f<<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, cand, cand_cnt, y);
+  k_sel_hist_f<kSelHistThreads><<<m.n_blocks, kSelHistThreads, 0, s>>>(m, pd, st, d2, hist1, y);
+  k_sel_compact_f<kSelCompactThreads><<<m.n_blocks, kSelCompactThreads, 0, s>>>(m, pd, st, d2, cand, cand_cnt, y);
 }
 void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float4* read_c,
                          const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
