@@ -535,8 +535,8 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
   uint8_t* bm = ctx->bitmap.as<uint8_t>();
   const OvlDesc* dOvl = ctx->ovl.as<OvlDesc>();
   TCHK(hipMemsetAsync(bm, 0, bm_bytes, s));
-  launch_ovl_mark(s, B->m_gref, dG, dOvl + P, dGst, B->ref_raw.as<float4>(), 0, res, bm);
-  launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm);
+  launch_ovl_mark(s, B->m_gref, dG, dOvl + P, dGst, B->ref_raw.as<float4>(), 0, res, bm, true);
+  launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm, true);
   launch_ovl_count(s, (int)P, (int)G, dDesc, dOvl, dOvl + P, dState, dGst, bm);
   launch_ovl_finish(s, (int)P, dDesc, dState, dGst, set_ratio ? 1 : 0);
   TCHK(hipGetLastError());
@@ -893,7 +893,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   if (timeNN)
     for (int it = 0; it < nn_launches; ++it) ctx->last_nn_ms += ev_ms(ctx->nn_ev[2 * it], ctx->nn_ev[2 * it + 1]);
   // N*(12 B query + 8 B id/d2) + V*16 B + W*8 B
-  ctx->last_nn_bytes = (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0;
+  ctx->last_nn_bytes = timeNN ? (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0 : 0.0;
   ctx->last_queries = queries;
   ctx->last_phase[0] = doOvl ? ev_ms(ctx->ev[0], ctx->ev[1]) + ev_ms(ctx->ev[6], ctx->ev[2]) : 0;
   // tree and normals run on the second stream, concurrently with the overlap

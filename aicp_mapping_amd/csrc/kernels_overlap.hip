@@ -108,7 +108,9 @@ __global__ __launch_bounds__(256) void k_ovl_bbox(BlockMap m, const PairDesc* __
 // bytes leave L2 every pass"), and the ~100 ray steps per point fall on far fewer distinct
 // voxels; a skipped store is always one that a lane of the workgroup has already issued, so
 // the map is the same union. C5 (r04, rocprofv3 + PMC WRITE_SIZE per dispatch): reference side
-// 111 -> 66 GB, reading side 17.5 -> 13.9 GB, time equal (24.0 vs 23.5 ms average). Measured
+// 111 -> 66 GB, reading side 17.5 -> 13.9 GB, time equal (24.0 vs 23.5 ms average). The batch
+// path (many clouds) uses it; the stream's window (6 clouds, latency-bound walks) does not: there
+// the cache's LDS round trip per step made the launch slower (C2: 182 against 162 us). Measured
 // and not kept: groups of 8 voxel bytes loaded and only the zero ones stored (WRITE_SIZE 109 ->
 // 19.6 GB, but 24.6 -> 30.5 ms: the loads' latency enters the walk).
 constexpr int kMarkCache = 4096;
@@ -323,8 +325,12 @@ void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* s
   if (m.n_blocks) k_ovl_bbox<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res);
 }
 void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDesc* od, PairState* st,
-                     const float4* pts, int side, double res, uint8_t* maps) {
-  if (m.n_blocks) k_ovl_mark<true><<<m.n_blocks, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
+                     const float4* pts, int side, double res, uint8_t* maps, bool filter) {
+  if (!m.n_blocks) return;
+  if (filter)
+    k_ovl_mark<true><<<m.n_blocks, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
+  else
+    k_ovl_mark<false><<<m.n_blocks, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
 }
 void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
                       const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps) {

@@ -832,7 +832,7 @@ static int win_read_side(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     launch_ovl_bbox(sr, m_read, dDesc, dState, readS, 1, res);
     launch_ovl_size(sr, (int)np, dState, dOvl + 1, dCap + 1);
     launch_ovl_clear(sr, (int)np, dOvl + 1, bmp, cap_max);
-    launch_ovl_mark(sr, m_read, dDesc, dOvl + 1, dState, readS, 1, res, bmp);
+    launch_ovl_mark(sr, m_read, dDesc, dOvl + 1, dState, readS, 1, res, bmp, false);
     launch_ovl_popcount(sr, (int)np, dOvl + 1, dState, 1, bmp);
   }
   HIPC(hipGetLastError());
@@ -988,7 +988,7 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
     launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
     launch_ovl_size(si, 1, dGst, dOvl, dCap);
     launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
-    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp);
+    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp, false);
     launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
   }
   HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));  // (the slot's previous window is done: its upload waited)
@@ -1193,7 +1193,7 @@ static int sub_prep(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_params* 
       launch_ovl_bbox(si, mrd, dDesc, dState, sl.read_raw.as<float4>(), 1, res);
       launch_ovl_size(si, 1, dState + r, dOvl + 1 + r, dCap + 1 + r);
       launch_ovl_clear(si, 1, dOvl + 1 + r, bmp, R.cap[1 + r]);
-      launch_ovl_mark(si, mrd, dDesc, dOvl + 1, dState, sl.read_raw.as<float4>(), 1, res, bmp);
+      launch_ovl_mark(si, mrd, dDesc, dOvl + 1, dState, sl.read_raw.as<float4>(), 1, res, bmp, false);
       launch_ovl_popcount(si, 1, dOvl + 1 + r, dState + r, 1, bmp);
       launch_ovl_intersect(si, 1, dDesc + r, dOvl + 1 + r, dOvl, dState + r, bmp);
     }
@@ -1587,7 +1587,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     tp += hs[i].touched_pts;
     tn += hs[i].touched_nodes;
   }
-  ctx->last_nn_bytes = (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0;
+  ctx->last_nn_bytes = timeNN ? (double)queries * 20.0 + (double)tp * 16.0 + (double)tn * 8.0 : 0.0;
   ctx->last_queries = queries;
   S->last.windows = windows;
   S->last.replans = replans;

@@ -389,8 +389,9 @@ def bench_stream(args):
     for k_step in range(args.steps):
         T, out = step(timed=k_step == args.steps - 1)
         t = ctx.last_nn_timing()
-        for k in ("launches", "total_ms", "bytes"):
-            nn[k] += t[k]
+        if t["launches"]:  # (the algorithmic bytes come with every step; the timing with the last)
+            for k in ("launches", "total_ms", "bytes"):
+                nn[k] += t[k]
         iters += sum(o["icp"]["iterations"] for o in out)
         tm = ctx.last_sequence_timing()
         dev_ms += tm["device_ms"]
