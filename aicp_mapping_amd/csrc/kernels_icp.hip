@@ -2121,6 +2121,121 @@ __global__ __launch_bounds__(kNNBlock) void k_icp_reduce(
   AICP_IP_BODY(2);
 }
 
+// a double of lane src (wave-uniform src) on every lane
+__device__ __forceinline__ double bcast_d(double v, int src) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, src);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), src);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// pivqr<6>'s rank (Eigen FullPivHouseholderQR: full pivoting, Householder steps, the rank
+// threshold) by one wave, lane c < 6 holding column c. Every element sees the operations of the
+// serial loops in their order (the pivot scan column-major with the first strict maximum, the
+// reflector sums over rows in order, no contraction), so the rank is pivqr<6>'s. get(r, c):
+// element (r, c) of A (a memory read: the column index is the lane's).
+template <class Get>
+__device__ int wave_pivqr_rank6(Get get) {
+  constexpr int N = 6;
+  const int lane = threadIdx.x & 63;
+  const int c = lane < N ? lane : 0;
+  double col[N];
+#pragma unroll
+  for (int r = 0; r < N; ++r) col[r] = get(r, c);
+  const double prec = (double)kFltEps * N;
+  int nonzero = N;
+  double maxpivot = 0, biggest = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    // this lane's first strict maximum over rows k.., then the lanes k.. in order
+    double bl = -1;
+    int rl = k;
+#pragma unroll
+    for (int r = k; r < N; ++r) {
+      const double v = fabs(col[r]);
+      if (v > bl) {
+        bl = v;
+        rl = r;
+      }
+    }
+    double bv = -1;
+    int br = k, bc = k;
+#pragma unroll
+    for (int cc = k; cc < N; ++cc) {
+      const double v = bcast_d(bl, cc);
+      const int rr = __builtin_amdgcn_readlane(rl, cc);
+      if (v > bv) {
+        bv = v;
+        br = rr;
+        bc = cc;
+      }
+    }
+    if (k == 0) biggest = bv;
+    if (bv <= biggest * prec) {  // (wave-uniform)
+      nonzero = k;
+      break;
+    }
+    // rows k <-> br on the columns k.., then columns k <-> bc on all rows
+    if (lane >= k && lane < N) {
+      double xk = col[k], xb = xk;
+#pragma unroll
+      for (int r = k + 1; r < N; ++r) xb = r == br ? col[r] : xb;
+#pragma unroll
+      for (int r = k + 1; r < N; ++r)
+        if (r == br) col[r] = xk;
+      col[k] = xb;
+    }
+    if (bc != k) {
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        const double xk = bcast_d(col[r], k), xb = bcast_d(col[r], bc);
+        col[r] = lane == k ? xb : (lane == bc ? xk : col[r]);
+      }
+    }
+    // the reflector of column k (lane k's values, on every lane)
+    double tailSq = 0;
+#pragma unroll
+    for (int r = k + 1; r < N; ++r) tailSq += col[r] * col[r];
+    tailSq = bcast_d(tailSq, k);
+    const double c0 = bcast_d(col[k], k);
+    double beta, tau;
+    const bool flat = tailSq <= kDblMin;
+    if (flat) {
+      tau = 0;
+      beta = c0;
+    } else {
+      beta = sqrt(c0 * c0 + tailSq);
+      if (c0 >= 0) beta = -beta;
+      tau = (beta - c0) / beta;
+    }
+    const double den = c0 - beta;
+    if (lane == k) {
+#pragma unroll
+      for (int r = k + 1; r < N; ++r) col[r] = flat ? 0.0 : col[r] / den;
+      col[k] = beta;
+    }
+    if (fabs(beta) > maxpivot) maxpivot = fabs(beta);
+    double v[N];
+#pragma unroll
+    for (int r = k + 1; r < N; ++r) v[r] = bcast_d(col[r], k);
+    if (lane > k && lane < N) {
+      double sum = col[k];
+#pragma unroll
+      for (int r = k + 1; r < N; ++r) sum += v[r] * col[r];
+      sum *= tau;
+      col[k] -= sum;
+#pragma unroll
+      for (int r = k + 1; r < N; ++r) col[r] -= sum * v[r];
+    }
+  }
+  const double thr = fabs(maxpivot) * ((double)kFltEps * N);
+  int rank = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (i < nonzero) rank += fabs(bcast_d(col[i], i)) > thr ? 1 : 0;
+  return rank;
+}
+
 // A x = b of the point-to-plane step from the reduced sums (upper triangle, then the rhs)
 __device__ __forceinline__ void normal_system(const double* tot, double* A, double* b) {
   int c = 0;
@@ -2249,18 +2364,18 @@ __device__ void icp_update_body(const PairDesc& d, PairState& s, const double* _
   // to solve6 on lane 0
   __shared__ int rank_llt[2];
   __shared__ double xs[6];
-  if (t == 0 || t == 64) {
-    double A[36], b[6];
+  if (t == 64) {  // wave 1: the LLT solve
+    double A[36], b[6], x[6];
     normal_system(tot, A, b);
-    if (t == 0) {
-      PivQR<6> q;
-      pivqr<6>(A, q);
-      rank_llt[0] = q.rank;
-    } else {
-      double x[6];
-      rank_llt[1] = llt_solve<6>(A, 6, b, x) ? 1 : 0;
-      for (int a = 0; a < 6; ++a) xs[a] = x[a];
-    }
+    rank_llt[1] = llt_solve<6>(A, 6, b, x) ? 1 : 0;
+    for (int a = 0; a < 6; ++a) xs[a] = x[a];
+  }
+  if (t < 64) {  // wave 0: the pivoted-QR rank, a lane per column (A from the upper triangle)
+    const int rk = wave_pivqr_rank6([&](int r, int c) {
+      const int a = r < c ? r : c, bb = r < c ? c : r;
+      return tot[a * 6 - a * (a - 1) / 2 + (bb - a)];
+    });
+    if (t == 0) rank_llt[0] = rk;
   }
   __syncthreads();
   if (t == 0) update_serial(d, s, tot, prm, rank_llt[0] == 6 && rank_llt[1] ? xs : nullptr);
@@ -2392,8 +2507,16 @@ __global__ void k_transform(int n, const float* __restrict__ T, const float4* __
   out[i] = make_float4(o[0], o[1], o[2], 1.f);
 }
 
+// solve6 as the update kernel takes it: the wave-parallel rank first (a path of 100 + its rank if
+// it ever disagrees with pivqr<6>'s, so the golden test fails loudly)
 __global__ __launch_bounds__(64) void k_solve6(const double* A, const double* b, double* x, int32_t* path) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *path = solve6(A, b, x);
+  const int rk = wave_pivqr_rank6([&](int r, int c) { return A[r * 6 + c]; });
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    PivQR<6> q;
+    pivqr<6>(A, q);
+    const int p = solve6(A, b, x);
+    *path = rk == q.rank ? p : 100 + rk;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
