@@ -2236,6 +2236,58 @@ __device__ int wave_pivqr_rank6(Get get) {
   return rank;
 }
 
+// llt_solve<6>(M, 6, b, x) by one wave, lane i holding row i of L (every element sees the serial
+// loops' operations in their order). get(r, c): element (r, c) of M; b on every lane. Returns
+// false where llt_solve would (a non-positive pivot); x on every lane.
+template <class Get>
+__device__ bool wave_llt_solve6(Get get, const double* b, double* x) {
+  constexpr int N = 6;
+  const int lane = threadIdx.x & 63;
+  const int i = lane < N ? lane : 0;
+  double L[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) L[k] = 0;
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double Lj[N];  // row j of L so far (lane j's)
+#pragma unroll
+    for (int k = 0; k < j; ++k) Lj[k] = bcast_d(L[k], j);
+    double d = get(j, j);
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= Lj[k] * Lj[k];
+    if (!(d > 0)) ok = false;
+    const double ljj = sqrt(d);
+    if (lane == j) L[j] = ljj;
+    if (lane > j && lane < N) {
+      double sum = get(i, j);
+#pragma unroll
+      for (int k = 0; k < j; ++k) sum -= L[k] * Lj[k];
+      L[j] = sum / ljj;
+    }
+  }
+  if (!ok) return false;
+  double y[N];
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    double Lr[N];
+#pragma unroll
+    for (int k = 0; k <= r; ++k) Lr[k] = bcast_d(L[k], r);
+    double sum = b[r];
+#pragma unroll
+    for (int k = 0; k < r; ++k) sum -= Lr[k] * y[k];
+    y[r] = sum / Lr[r];
+  }
+#pragma unroll
+  for (int r = N - 1; r >= 0; --r) {
+    double sum = y[r];
+#pragma unroll
+    for (int k = r + 1; k < N; ++k) sum -= bcast_d(L[r], k) * x[k];
+    x[r] = sum / bcast_d(L[r], r);
+  }
+  return true;
+}
+
 // A x = b of the point-to-plane step from the reduced sums (upper triangle, then the rhs)
 __device__ __forceinline__ void normal_system(const double* tot, double* A, double* b) {
   int c = 0;
@@ -2364,17 +2416,21 @@ __device__ void icp_update_body(const PairDesc& d, PairState& s, const double* _
   // to solve6 on lane 0
   __shared__ int rank_llt[2];
   __shared__ double xs[6];
-  if (t == 64) {  // wave 1: the LLT solve
-    double A[36], b[6], x[6];
-    normal_system(tot, A, b);
-    rank_llt[1] = llt_solve<6>(A, 6, b, x) ? 1 : 0;
-    for (int a = 0; a < 6; ++a) xs[a] = x[a];
+  auto tri = [&](int r, int c) {  // A from the upper triangle of the sums
+    const int a = r < c ? r : c, bb = r < c ? c : r;
+    return tot[a * 6 - a * (a - 1) / 2 + (bb - a)];
+  };
+  if (t >= 64 && t < 128) {  // wave 1: the LLT solve, a lane per row
+    double b[6], x[6];
+    for (int a = 0; a < 6; ++a) b[a] = -tot[21 + a];
+    const bool ok = wave_llt_solve6(tri, b, x);
+    if (t == 64) {
+      rank_llt[1] = ok ? 1 : 0;
+      for (int a = 0; a < 6; ++a) xs[a] = x[a];
+    }
   }
   if (t < 64) {  // wave 0: the pivoted-QR rank, a lane per column (A from the upper triangle)
-    const int rk = wave_pivqr_rank6([&](int r, int c) {
-      const int a = r < c ? r : c, bb = r < c ? c : r;
-      return tot[a * 6 - a * (a - 1) / 2 + (bb - a)];
-    });
+    const int rk = wave_pivqr_rank6(tri);
     if (t == 0) rank_llt[0] = rk;
   }
   __syncthreads();
@@ -2507,15 +2563,24 @@ __global__ void k_transform(int n, const float* __restrict__ T, const float4* __
   out[i] = make_float4(o[0], o[1], o[2], 1.f);
 }
 
-// solve6 as the update kernel takes it: the wave-parallel rank first (a path of 100 + its rank if
-// it ever disagrees with pivqr<6>'s, so the golden test fails loudly)
+// solve6 as the update kernel takes it: the wave-parallel rank and LLT first (a path of 100 + the
+// rank if the wave's rank ever disagrees with pivqr<6>'s, 200 if the wave's LLT differs from
+// llt_solve<6> in a bit, so the golden test fails loudly)
 __global__ __launch_bounds__(64) void k_solve6(const double* A, const double* b, double* x, int32_t* path) {
-  const int rk = wave_pivqr_rank6([&](int r, int c) { return A[r * 6 + c]; });
+  const auto get = [&](int r, int c) { return A[r * 6 + c]; };
+  const int rk = wave_pivqr_rank6(get);
+  double bl[6], xw[6];
+  for (int i = 0; i < 6; ++i) bl[i] = b[i];
+  const bool okw = wave_llt_solve6(get, bl, xw);
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     PivQR<6> q;
     pivqr<6>(A, q);
+    double xl[6];
+    const bool okl = llt_solve<6>(A, 6, b, xl);
+    bool same = okw == okl;
+    for (int i = 0; i < 6 && okl && okw; ++i) same &= __double_as_longlong(xl[i]) == __double_as_longlong(xw[i]);
     const int p = solve6(A, b, x);
-    *path = rk == q.rank ? p : 100 + rk;
+    *path = rk != q.rank ? 100 + rk : (!same ? 200 : p);
   }
 }
 
