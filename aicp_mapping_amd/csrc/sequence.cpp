@@ -1426,14 +1426,29 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     for (size_t k = 0; k < plan.size() && !rc; ++k) {
       const bool next = k + 1 < plan.size();
       bool uploaded = !next;
-      // (the next window's upload -- host packing of its readings -- goes after this window's first
-      // iterations are enqueued: before them it delayed the loop start on the host by ~0.4 ms)
+      // The next window's upload (host packing of its readings, ~0.35 ms per C2 window, then its
+      // H2D and reading side) runs on a host thread of its own, started once this window's first
+      // iterations are enqueued: on the polling thread it held the poll that enqueues iteration
+      // smoothLength + 1, and the device waited ~0.25 ms per window for it (r04 trace).
+      std::thread up_thr;
+      int up_rc = AICP_OK;
       auto try_upload = [&]() -> int {
         if (uploaded || !can_upload(k)) return AICP_OK;
         uploaded = true;
-        int r = timed(0, [&] { return upload(k + 1); });
-        if (!r) r = timed(0, [&] { return read_side(k + 1); });
-        return r;
+        up_thr = std::thread([&, k] {
+          if (hipSetDevice(S->device) != hipSuccess) {
+            up_rc = AICP_ERR_HIP;
+            return;
+          }
+          int r = timed(0, [&] { return upload(k + 1); });
+          if (!r) r = timed(0, [&] { return read_side(k + 1); });
+          up_rc = r;
+        });
+        return AICP_OK;
+      };
+      auto join_upload = [&]() -> int {
+        if (up_thr.joinable()) up_thr.join();
+        return up_rc;
       };
       if (runs[k].tev) {
         rc = hipEventRecord(runs[k].tev[3], S->s_icp) == hipSuccess ? AICP_OK : AICP_ERR_HIP;
@@ -1460,6 +1475,10 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
           }
           return try_upload();
         });
+      }
+      {
+        const int ur = join_upload();  // (before any return: the thread uses this scope)
+        if (!rc) rc = ur;
       }
       if (!rc && next) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
       if (!rc && next) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
