@@ -197,13 +197,14 @@ struct SeqSlot {
 
 struct SeqState {
   hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr;
+  hipStream_t s_probe = nullptr;  // seq_prof(): an idle stream whose markers time the host's enqueue
   SeqSlot slot[kSlots];
   DevBuf desc, state, outT;
   DevBuf initT;  // debug working mode: initialT_ (16 floats), then its value before each reading
   PinBuf pin_state, pin_out, pin_ctl, pin_desc;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;
-  std::vector<hipEvent_t> tev;  // seq_prof(): 5 timing events per window
+  std::vector<hipEvent_t> tev;  // seq_prof(): 8 timing events per window
   WorkerPool pool{std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1};
   aicp_sequence_timing last{};
   int device = 0;
@@ -235,7 +236,7 @@ void seq_state_free(SeqState* S) {
   for (hipEvent_t e : S->tev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {S->ev_begin, S->ev_end})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t q : {S->s_rd, S->s_icp})  // (s_up = s_rd; s_r2, s_r3: the context's)
+  for (hipStream_t q : {S->s_rd, S->s_icp, S->s_probe})  // (s_up = s_rd; s_r2, s_r3: the context's)
     if (q) (void)hipStreamDestroy(q);
   delete S;
 }
@@ -396,7 +397,9 @@ struct WinRun {
   TreeCtl* ctl_w = nullptr;
   const PairDesc* src_desc = nullptr;   // the reference source's descriptor and correction
   const float* src_T = nullptr;
-  hipEvent_t* tev = nullptr;            // seq_prof(): ref start, matcher done, normals done, ICP start, ICP done
+  // seq_prof(): ref start, matcher done, normals done, ICP start, ICP done, commit done, host at the
+  // next reference's enqueue (a marker on an idle stream), its upload ready on r3
+  hipEvent_t* tev = nullptr;
   std::vector<uint32_t> n_read;         // the readings' point counts
   bool sparse = false;                  // overlap on sorted key lists (a map over kSeqMapBudget)
   OvlKeySide kr{}, kg{};                // its readings' and reference's sides
@@ -855,7 +858,9 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   TreeCtl* ctl_w = R.ctl_w;
   // ---- r3: the reference points
   hipStream_t s3 = S->s_r3;
+  if (R.tev) HIPC(hipEventRecord(R.tev[6], S->s_probe));
   HIPC(hipStreamWaitEvent(s3, sl.ev_up, 0));
+  if (R.tev) HIPC(hipEventRecord(R.tev[7], s3));
   if (w.src >= 0) {
     // the source's correction must be final: from the previous window of this pass (its loop's
     // end, ev_done), or from an earlier pass (synchronised)
@@ -1140,6 +1145,7 @@ static int loop_finish(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_param
   launch_seq_commit(st, (int)np, dDesc, dState, dOutT, S->desc.as<PairDesc>() + w.p0, S->state.as<PairState>() + w.p0,
                     S->outT.as<float>() + 16 * w.p0);
   HIPC(hipGetLastError());
+  if (R.tev) HIPC(hipEventRecord(R.tev[5], st));
   HIPC(hipEventRecord(sl.ev_done, st));
   return AICP_OK;
 }
@@ -1334,12 +1340,13 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     std::memset(ctl, 0, plan.size() * 2 * sizeof(TreeCtl));
     std::vector<WinRun> runs(plan.size());
     if (seq_prof()) {
-      while (S->tev.size() < 5 * plan.size()) {
+      if (!S->s_probe) HIPC(hipStreamCreateWithFlags(&S->s_probe, hipStreamNonBlocking));
+      while (S->tev.size() < 8 * plan.size()) {
         hipEvent_t e;
         HIPC(hipEventCreate(&e));
         S->tev.push_back(e);
       }
-      for (size_t k = 0; k < plan.size(); ++k) runs[k].tev = S->tev.data() + 5 * k;
+      for (size_t k = 0; k < plan.size(); ++k) runs[k].tev = S->tev.data() + 8 * k;
     }
     auto upload = [&](size_t k) {
       const Win& w = plan[k];
@@ -1366,7 +1373,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       return win_upload(ctx, S, cfg, prm, first, readings, resident, rbox, runs[k]);
     };
     const bool prof = seq_prof();
-    double hp[3] = {0, 0, 0};
+    double hp[5] = {0, 0, 0, 0, 0};  // upload (its thread), reference trees, icp loop, join, reference icp
     auto timed = [&](int slot, const std::function<int()>& f) {
       const auto a = std::chrono::steady_clock::now();
       const int r = f();
@@ -1422,7 +1429,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     rc = timed(0, [&] { return upload(0); });
     if (!rc) rc = timed(0, [&] { return read_side(0); });
     if (!rc) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[0]); });
-    if (!rc) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[0]); });
+    if (!rc) rc = timed(4, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[0]); });
     for (size_t k = 0; k < plan.size() && !rc; ++k) {
       const bool next = k + 1 < plan.size();
       bool uploaded = !next;
@@ -1477,16 +1484,18 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         });
       }
       {
-        const int ur = join_upload();  // (before any return: the thread uses this scope)
+        const int ur = timed(3, join_upload);  // (before any return: the thread uses this scope)
         if (!rc) rc = ur;
       }
       if (!rc && next) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
-      if (!rc && next) rc = timed(1, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
+      if (!rc && next) rc = timed(4, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
       ++windows;
     }
     if (prof)
-      std::fprintf(stderr, "[aicp seq] host ms: upload %.2f reference %.2f icp(incl. polls) %.2f over %zu windows\n",
-                   hp[0], hp[1], hp[2], plan.size());
+      std::fprintf(stderr,
+                   "[aicp seq] host ms: upload %.2f reference trees %.2f reference icp %.2f icp(incl. polls) %.2f "
+                   "upload join %.2f over %zu windows\n",
+                   hp[0], hp[1], hp[4], hp[2], hp[3], plan.size());
     if (rc) {
       (void)seq_sync(ctx, S);
       return rc;
@@ -1508,7 +1517,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       tree_prof_dump();
     }
     if (prof && plan.size() > 2) {  // device phase times, averaged over the windows after the first
-      double a[5] = {0, 0, 0, 0, 0};
+      double a[5] = {0, 0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
       const size_t m = plan.size() - 1;
       for (size_t k = 1; k < plan.size(); ++k) {
         const hipEvent_t* t = runs[k].tev;
@@ -1517,7 +1526,16 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         a[2] += ev_ms(t[0], t[3]);
         a[3] += ev_ms(t[3], t[4]);
         a[4] += ev_ms(runs[k - 1].tev[0], t[0]);
+        const hipEvent_t* u = runs[k - 1].tev;  // the hand-off from window k - 1's commit
+        b[0] += ev_ms(u[4], u[5]);
+        b[1] += ev_ms(u[5], t[6]);
+        b[2] += ev_ms(u[5], t[7]);
+        b[3] += ev_ms(u[5], t[0]);
       }
+      std::fprintf(stderr,
+                   "[aicp seq] hand-off ms/window: commit %.3f, from its end: host enqueue %.3f upload ready %.3f "
+                   "reference start %.3f\n",
+                   b[0] / m, b[1] / m, b[2] / m, b[3] / m);
       std::fprintf(stderr,
                    "[aicp seq] device ms/window: ref->matcher %.3f ref->normals %.3f ref->icp start %.3f icp %.3f "
                    "period %.3f\n",
