@@ -287,7 +287,7 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
   TCHK(ensure(T.mids, max_seg * sizeof(SubSeg)));
   TCHK(ensure(T.lb, lb_bytes((uint32_t)n)));
   TCHK(ensure(T.ecnt, (n + 2) * 4));
-  TCHK(ensure(T.sums, P * 6 * 8));
+  TCHK(ensure(T.sums, (P + tree_sum_tiles(n)) * 6 * 8));  // per pair, then per tile (k_tr_sum)
   TCHK(ensure(T.pdepth, P * 4));
   TCHK(ensure(T.ctl, sizeof(TreeCtl)));
   const size_t tb = tree_scan_temp_bytes(n + 2);

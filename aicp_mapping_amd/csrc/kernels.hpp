@@ -132,7 +132,7 @@ struct TreeWork {
   SubSeg* subs;          // wave-subtree segments, max_seg
   SubSeg* mids;          // mid-size segments (kSubMax < count <= kMidMax), max_seg
   uint32_t* ecnt;        // nodes ending at each position, total + 2
-  uint64_t* sums;        // 6 per pair (128-bit fixed-point coordinate sums)
+  uint64_t* sums;        // 6 per pair (128-bit fixed-point coordinate sums), then 6 per tree_sum_tiles tile
   int32_t* pair_depth;   // per pair
   TreeCtl* ctl;
   void* scan_temp;
@@ -144,6 +144,7 @@ struct TreeWork {
   uint32_t mid_max;      // segments up to this size leave the global levels (kMidMax; kSubMax: no mid builder)
 };
 uint32_t tree_mid_max();
+size_t tree_sum_tiles(size_t n);  // k_tr_sum's tiles over n points
 size_t tree_scan_temp_bytes(size_t n);
 size_t lb_bytes(uint32_t total);
 size_t lb_stride_words(uint32_t total);

@@ -296,14 +296,18 @@ __device__ __forceinline__ void atomic_add128(uint64_t* w, uint64_t lo, int64_t 
 }
 
 // Per-pair reductions over the points use tiles of kTile positions per 256-thread block (8 per
-// thread): a tile inside one pair (the common case) reduces in registers + LDS and issues one
-// atomic per word, so a 120k-point cloud makes ~60 atomics per word instead of ~470.
+// thread): a tile inside one pair (the common case) reduces in registers + LDS.
 constexpr int kTileItems = 8;
 constexpr uint32_t kTile = 256 * kTileItems;
 inline unsigned tiles_of(size_t n) { return (unsigned)std::max<size_t>(1, (n + kTile - 1) / kTile); }
 
+// The centroid sums: a tile inside one pair stores its 128-bit partials (part[6 * tile ..]) and
+// k_tr_frames adds them per pair; a tile across pair boundaries adds its runs atomically into
+// sums[6 * pair ..]. (With one atomic per word and tile, a C2 reference's 60 tiles took 40-56 us
+// whenever the reading side's voxel marks ran beside it, r04 trace: same-address atomics wait
+// behind the marks' stores at the memory side.)
 __global__ __launch_bounds__(256) void k_tr_sum(int n_pairs, uint32_t total, const PairDesc* __restrict__ pd,
-                                                const float4* __restrict__ raw, uint64_t* sums) {
+                                                const float4* __restrict__ raw, uint64_t* sums, uint64_t* part) {
   __shared__ uint64_t slo[3][4];
   __shared__ int64_t shi[3][4];
   const uint32_t base = blockIdx.x * kTile;
@@ -362,21 +366,49 @@ __global__ __launch_bounds__(256) void k_tr_sum(int n_pairs, uint32_t total, con
     uint64_t lo = slo[d][0];
     int64_t hi = shi[d][0];
     for (int k = 1; k < 4; ++k) add128(lo, hi, slo[d][k], shi[d][k]);
-    atomic_add128(sums + (size_t)p_first * 6 + 2 * d, lo, hi);
+    part[(size_t)blockIdx.x * 6 + 2 * d] = lo;
+    part[(size_t)blockIdx.x * 6 + 2 * d + 1] = (uint64_t)hi;
   }
 }
 
 // mean, T_refIn_refMean, T_refMean_dataIn = T_refIn_refMean^-1 * T0 (A.1 steps 2, 5);
-// center == 0: the kernel-level kNN entry points build on the points as given.
-__global__ void k_tr_frames(int n_pairs, PairDesc* pd, const uint64_t* sums, int center) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// center == 0: the kernel-level kNN entry points build on the points as given. One wave per
+// pair: the atomic sums of the boundary tiles plus the partials of the pair's own tiles (integer
+// sums: the order does not matter).
+__global__ __launch_bounds__(64) void k_tr_frames(int n_pairs, uint32_t total, PairDesc* pd, const uint64_t* sums,
+                                                  const uint64_t* part, int center) {
+  const int p = blockIdx.x;
   if (p >= n_pairs) return;
   PairDesc& d = pd[p];
+  float mean[3] = {0.f, 0.f, 0.f};
+  if (center) {
+    const uint32_t ro = d.ref_off, re = d.ref_off + d.n_ref;
+    const uint32_t t0 = (ro + kTile - 1) / kTile;  // the first tile starting inside the pair
+    uint64_t lo[3] = {0, 0, 0};
+    int64_t hi[3] = {0, 0, 0};
+    for (uint32_t t = t0 + (uint32_t)threadIdx.x; (uint64_t)t * kTile < re; t += 64) {
+      if (min((uint64_t)t * kTile + kTile, (uint64_t)total) > re) break;  // straddles the pair's end
+#pragma unroll
+      for (int k = 0; k < 3; ++k) add128(lo[k], hi[k], part[(size_t)t * 6 + 2 * k], (int64_t)part[(size_t)t * 6 + 2 * k + 1]);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t lo_o = __shfl_xor(lo[k], off, 64);
+        const int64_t hi_o = __shfl_xor(hi[k], off, 64);
+        add128(lo[k], hi[k], lo_o, hi_o);
+      }
+      add128(lo[k], hi[k], sums[p * 6 + 2 * k], (int64_t)sums[p * 6 + 2 * k + 1]);
+      mean[k] = mean_from_fixed40(lo[k], (uint64_t)hi[k], d.n_ref);
+    }
+  }
+  if (threadIdx.x != 0) return;
   float Tm[16], Tmi[16];
   ident4(Tm);
   ident4(Tmi);
   for (int k = 0; k < 3; ++k) {
-    d.mean[k] = center ? mean_from_fixed40(sums[p * 6 + 2 * k], sums[p * 6 + 2 * k + 1], d.n_ref) : 0.f;
+    d.mean[k] = mean[k];
     Tm[12 + k] = d.mean[k];
     Tmi[12 + k] = -d.mean[k];
   }
@@ -1923,6 +1955,7 @@ void launch_pairs_degenerate_part(hipStream_t s, int n_pairs, const PairDesc* pd
 // look-back words of every scan of a build: two per global level and the node count scan
 size_t lb_stride_words(uint32_t total) { return lb_words(total + 2); }
 uint32_t tree_mid_max() { return (uint32_t)kMidMax; }
+size_t tree_sum_tiles(size_t n) { return tiles_of(n); }
 // k_tr_subtree_lvl from this many points of a build (C5: 61 M); smaller builds are latency-bound
 // and keep k_tr_subtree_blk (r04: C2 2620 against 2479 clouds/s with the level builder).
 // AICP_TREE_LVL_MIN overrides it (the equivalence test builds small trees both ways).
@@ -1946,8 +1979,9 @@ hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairD
   }
   k_tr_zero<<<(unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (most + 255) / 256)), 256, 0, s>>>(
       z, n_pairs, w.seg[0]);
-  if (center) k_tr_sum<<<tiles_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.sums);
-  k_tr_frames<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.sums, center);
+  uint64_t* part = w.sums + (size_t)n_pairs * 6;  // tile partials (TreeWork::sums)
+  if (center) k_tr_sum<<<tiles_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.sums, part);
+  k_tr_frames<<<n_pairs, 64, 0, s>>>(n_pairs, total, pd, w.sums, part, center);
   k_tr_center<<<tiles_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.W[0], w.segof[0], w.seg[0], bpts, bucket,
                                              w.mid_max);
   k_tr_roots<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, total, pd, w.seg[0], w.subs, w.mids, w.ctl, w.ev, w.valid, w.ecnt,

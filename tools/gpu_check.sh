@@ -1,10 +1,12 @@
-#!/bin/bash
-# GPU round-trip: parity tests, smoke, short bench. Each step bounded; stop at first failure.
-set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/parity.log 2>&1 || { tail -40 gpurun_out/parity.log; exit 1; }
-tail -3 gpurun_out/parity.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -30 gpurun_out/smoke.log; exit 1; }
-tail -1 gpurun_out/smoke.log
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
-cat gpurun_out/bench.log
+# GPU suite, then N alternating bench runs of the tree's library and build_var/lib_head.so (C2 stream,
+# AICP_PROF=1 phase times); steps chained so a failure stops the call
+cd $GRAFT_REPO_ROOT
+N=${1:-3}
+timeout -k 10 600 python3 -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_t.log 2>&1; rc=$?
+tail -2 gpurun_out/gpu_t.log; [ $rc -eq 0 ] || exit $rc
+for i in $(seq $N); do
+  for v in "" "$GRAFT_REPO_ROOT/build_var/lib_head.so"; do
+    AICP_HIP_LIB=$v AICP_PROF=1 timeout -k 10 200 python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-batched > gpurun_out/b.log 2>&1 || exit 1
+    echo "${v:-tree} $(grep -o '"value": [0-9.]*' gpurun_out/b.log | head -1) $(grep "device ms" gpurun_out/b.log | tail -1)"
+  done
+done
