@@ -204,7 +204,7 @@ struct SeqState {
   PinBuf pin_state, pin_out, pin_ctl, pin_desc;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;
-  std::vector<hipEvent_t> tev;  // seq_prof(): 8 timing events per window
+  std::vector<hipEvent_t> tev;  // seq_prof(): 10 timing events per window
   WorkerPool pool{std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1};
   aicp_sequence_timing last{};
   int device = 0;
@@ -398,7 +398,8 @@ struct WinRun {
   const PairDesc* src_desc = nullptr;   // the reference source's descriptor and correction
   const float* src_T = nullptr;
   // seq_prof(): ref start, matcher done, normals done, ICP start, ICP done, commit done, host at the
-  // next reference's enqueue (a marker on an idle stream), its upload ready on r3
+  // next reference's enqueue (a marker on an idle stream), its upload ready on r3, reading side
+  // start and end
   hipEvent_t* tev = nullptr;
   std::vector<uint32_t> n_read;         // the readings' point counts
   bool sparse = false;                  // overlap on sorted key lists (a map over kSeqMapBudget)
@@ -807,6 +808,7 @@ static int win_read_side(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   const uint64_t cap_max = R.cap_max;
   hipStream_t sr = S->s_rd;
   HIPC(hipStreamWaitEvent(sr, sl.ev_up, 0));
+  if (R.tev) HIPC(hipEventRecord(R.tev[8], sr));
   launch_init_state(sr, (int)np, dDesc, dState);
   const float4* readS = sl.read_raw.as<float4>();
   if (R.debug) {  // the points move with initialT_ right before each reading's loop (in place)
@@ -840,6 +842,7 @@ static int win_read_side(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_rd, sr));
+  if (R.tev) HIPC(hipEventRecord(R.tev[9], sr));
   R.readS = readS;
   return AICP_OK;
 }
@@ -1341,12 +1344,12 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     std::vector<WinRun> runs(plan.size());
     if (seq_prof()) {
       if (!S->s_probe) HIPC(hipStreamCreateWithFlags(&S->s_probe, hipStreamNonBlocking));
-      while (S->tev.size() < 8 * plan.size()) {
+      while (S->tev.size() < 10 * plan.size()) {
         hipEvent_t e;
         HIPC(hipEventCreate(&e));
         S->tev.push_back(e);
       }
-      for (size_t k = 0; k < plan.size(); ++k) runs[k].tev = S->tev.data() + 8 * k;
+      for (size_t k = 0; k < plan.size(); ++k) runs[k].tev = S->tev.data() + 10 * k;
     }
     auto upload = [&](size_t k) {
       const Win& w = plan[k];
@@ -1517,7 +1520,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       tree_prof_dump();
     }
     if (prof && plan.size() > 2) {  // device phase times, averaged over the windows after the first
-      double a[5] = {0, 0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+      double a[5] = {0, 0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, c[3] = {0, 0, 0};
       const size_t m = plan.size() - 1;
       for (size_t k = 1; k < plan.size(); ++k) {
         const hipEvent_t* t = runs[k].tev;
@@ -1531,7 +1534,15 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         b[1] += ev_ms(u[5], t[6]);
         b[2] += ev_ms(u[5], t[7]);
         b[3] += ev_ms(u[5], t[0]);
+        // window k's reading side (enqueued during window k - 1's loop) against that loop
+        c[0] += ev_ms(u[3], t[8]);
+        c[1] += ev_ms(t[8], t[9]);
+        c[2] += ev_ms(u[4], t[9]);
       }
+      std::fprintf(stderr,
+                   "[aicp seq] reading side ms/window: start after the previous loop's start %.3f, duration %.3f, "
+                   "end after that loop's end %.3f\n",
+                   c[0] / m, c[1] / m, c[2] / m);
       std::fprintf(stderr,
                    "[aicp seq] hand-off ms/window: commit %.3f, from its end: host enqueue %.3f upload ready %.3f "
                    "reference start %.3f\n",

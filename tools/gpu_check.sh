@@ -1,11 +1,15 @@
-# GPU suite, then N alternating bench runs of the tree's library and build_var/lib_head.so (C2 stream,
-# AICP_PROF=1 phase times); steps chained so a failure stops the call
+# GPU suite (TESTS=0 skips it), then N alternating C2 bench runs (AICP_PROF=1 phase times) of the
+# in-tree library and each library given: bash tools/gpu_check.sh N [path/to/lib.so ...]
+# Steps are chained so that a failure stops the call.
 cd $GRAFT_REPO_ROOT
 N=${1:-3}
-timeout -k 10 600 python3 -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_t.log 2>&1; rc=$?
-tail -2 gpurun_out/gpu_t.log; [ $rc -eq 0 ] || exit $rc
+shift
+if [ "${TESTS:-1}" != 0 ]; then
+  timeout -k 10 600 python3 -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_t.log 2>&1; rc=$?
+  tail -2 gpurun_out/gpu_t.log; [ $rc -eq 0 ] || exit $rc
+fi
 for i in $(seq $N); do
-  for v in "" "$GRAFT_REPO_ROOT/build_var/lib_head.so"; do
+  for v in "" "$@"; do
     AICP_HIP_LIB=$v AICP_PROF=1 timeout -k 10 200 python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-batched > gpurun_out/b.log 2>&1 || exit 1
     echo "${v:-tree} $(grep -o '"value": [0-9.]*' gpurun_out/b.log | head -1) $(grep "device ms" gpurun_out/b.log | tail -1)"
   done
