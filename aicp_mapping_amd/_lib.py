@@ -36,7 +36,8 @@ EXPORTS = [
     "aicp_hip_last_prefilter_stats", "aicp_hip_map_create", "aicp_hip_map_free", "aicp_hip_map_size",
     "aicp_hip_map_download", "aicp_hip_map_crop", "aicp_hip_map_merge", "aicp_hip_map_prefilter",
     "aicp_hip_default_sequence_params", "aicp_hip_sequence_run", "aicp_hip_last_sequence_timing",
-    "aicp_hip_map_register_batch",
+    "aicp_hip_map_register_batch", "aicp_hip_multi_create", "aicp_hip_multi_destroy", "aicp_hip_multi_size",
+    "aicp_hip_multi_context", "aicp_hip_multi_last_error", "aicp_hip_multi_align_batch",
 ]
 
 
@@ -231,6 +232,15 @@ def _load():
     L.aicp_hip_last_sequence_timing.argtypes = [vp, C.POINTER(SequenceTiming)]
     L.aicp_hip_map_register_batch.argtypes = [vp, cfgp, vp, C.c_float, C.c_float, C.POINTER(Cloud), fp, sz, C.c_int,
                                               fp, stp]
+    L.aicp_hip_multi_create.argtypes = [ip, C.c_int, C.POINTER(vp)]
+    L.aicp_hip_multi_destroy.argtypes = [vp]
+    L.aicp_hip_multi_destroy.restype = None
+    L.aicp_hip_multi_size.argtypes = [vp]
+    L.aicp_hip_multi_context.argtypes = [vp, C.c_int]
+    L.aicp_hip_multi_context.restype = vp
+    L.aicp_hip_multi_last_error.argtypes = [vp]
+    L.aicp_hip_multi_last_error.restype = C.c_char_p
+    L.aicp_hip_multi_align_batch.argtypes = [vp, cfgp, pp, sz, C.c_double, C.c_int, fp, stp, ip]
     return L
 
 
@@ -585,3 +595,51 @@ class ResidentBatch:
 
     def __del__(self):
         self.free()
+
+
+class MultiContext:
+    """aicp_hip_multi: one context and host thread per device for independent pairs (SURVEY §8(e));
+    the C++ host's form of the torch.distributed path in bench.py. `devices` may repeat a device."""
+
+    def __init__(self, devices=None, n_devices: int = 0):
+        h = C.c_void_p()
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*[int(d) for d in devices])
+            rc = lib.aicp_hip_multi_create(arr, len(devices), C.byref(h))
+        else:
+            rc = lib.aicp_hip_multi_create(None, int(n_devices), C.byref(h))
+        if rc != AICP_OK:
+            raise AicpError(rc, f"aicp_hip_multi_create(devices={devices}, n={n_devices}) failed")
+        self.h = h
+
+    def size(self) -> int:
+        return lib.aicp_hip_multi_size(self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.aicp_hip_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def align_batch(self, pairs, cfg=None, resolution=0.2, flags=AICP_RUN_ICP, raise_on_error=True):
+        """Context.align_batch over the devices. Returns (T[n,4,4] row-major, stats dicts, the
+        device of each pair, rc)."""
+        cfg = cfg or default_config()
+        arr = (Pair * len(pairs))()
+        keep = []
+        for i, pr in enumerate(pairs):
+            p, k = make_pair(pr["ref"], pr["read"], pr.get("ref_origin", (0, 0, 0)),
+                             pr.get("read_origin", (0, 0, 0)), pr.get("init_T"))
+            arr[i] = p
+            keep.append(k)
+        outT = np.zeros((len(pairs), 16), np.float32)
+        st = (IcpStats * len(pairs))()
+        dev = np.zeros(len(pairs), np.int32)
+        rc = lib.aicp_hip_multi_align_batch(self.h, C.byref(cfg), arr, len(pairs), float(resolution), int(flags),
+                                            _fptr(outT), st, dev.ctypes.data_as(C.POINTER(C.c_int)))
+        if raise_on_error and rc != AICP_OK:
+            raise AicpError(rc, lib.aicp_hip_multi_last_error(self.h).decode())
+        T = outT.reshape(-1, 4, 4).transpose(0, 2, 1).copy()
+        return T, [s.as_dict() for s in st], dev, rc

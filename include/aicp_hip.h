@@ -138,6 +138,24 @@ int aicp_hip_overlap_batch(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_p
 int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg,
                          const aicp_pair* pairs, size_t n_pairs, double resolution, int flags,
                          float* out_T /* 16*n */, aicp_icp_stats* stats /* n, nullable */);
+/* ---- several GPUs from one host process (C5) ----------------------------------
+ * Independent pairs shard across devices with no data-path exchange: one context and one host
+ * thread per device, longest-processing-time shards by n_read * log2(n_ref), and the per-pair
+ * results written at the pairs' own indices (the gather). Replaces nothing in the reference,
+ * which registers one pair at a time on the CPU (app.cpp:528-550); it is the C++ host's form of
+ * bench.py's torch.distributed path. devices = NULL: devices 0..n_devices-1 (n_devices <= 0:
+ * every visible device); a device may be listed more than once (several contexts on one GPU). */
+typedef struct aicp_hip_multi aicp_hip_multi;
+int aicp_hip_multi_create(const int* devices, int n_devices, aicp_hip_multi** out);
+void aicp_hip_multi_destroy(aicp_hip_multi* m);
+int aicp_hip_multi_size(const aicp_hip_multi* m);
+aicp_hip_ctx* aicp_hip_multi_context(aicp_hip_multi* m, int i);
+const char* aicp_hip_multi_last_error(const aicp_hip_multi* m);
+/* aicp_hip_align_batch over the devices; out_device (n, nullable): the device of each pair */
+int aicp_hip_multi_align_batch(aicp_hip_multi* m, const aicp_icp_config* cfg, const aicp_pair* pairs,
+                               size_t n_pairs, double resolution, int flags, float* out_T /* 16*n */,
+                               aicp_icp_stats* stats /* n, nullable */, int* out_device /* n, nullable */);
+
 /* getOutputReading: out = T * in (float, pad row 1), pointmatcher_registration.cpp:128-131. */
 int aicp_hip_transform(aicp_hip_ctx* ctx, const float T[16], const float* in, size_t n,
                        size_t stride, float* out /* packed xyz, 3*n */);
