@@ -561,16 +561,12 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
   // reports into its error word, checked after the batch
   if (ctx->tl_total) {
     const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);  // node records allotted
-    const size_t tb = tree_scan_temp_bytes((size_t)cap + 1);
     TCHK(ensure(ctx->tl, ctx->tl_total * 16));
     TCHK(ensure(ctx->ptl, ctx->tl_total * 8));  // treelet links {parent, grandparent}
-    TCHK(ensure(ctx->tl_flag, ((size_t)cap + 1) * 4));
     TCHK(ensure(ctx->tl_rank, ((size_t)cap + 1) * 4));
-    TCHK(ensure(ctx->tl_temp, tb));
     TreeBufs& T = ctx->tb[1];
-    TCHK(launch_treelets(s3, (int)R, cap, dRdesc, ctx->nodes.as<uint4>(), bucket, ctx->tl_flag.as<uint32_t>(),
-                         ctx->tl_rank.as<uint32_t>(), ctx->tl_temp.p, tb, ctx->tl.as<uint4>(),
-                         ctx->ptl.as<uint2>(), T.tw.ctl));
+    TCHK(launch_treelets(s3, (int)R, cap, dRdesc, ctx->nodes.as<uint4>(), bucket, ctx->tl_rank.as<uint32_t>(),
+                         ctx->tl.as<uint4>(), ctx->ptl.as<uint2>(), T.tw));
     TCHK(hipMemcpyAsync(T.pin_ctl.p, T.tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
   }
   launch_pairs_from_refs(s3, (int)B->P, dDesc, dRdesc);
@@ -980,7 +976,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
                     &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->gdesc, &ctx->gstate, &ctx->tl, &ctx->ptl,
-                    &ctx->tl_flag, &ctx->tl_rank, &ctx->tl_temp, &ctx->pf_a, &ctx->pf_b})
+                    &ctx->tl_rank, &ctx->pf_a, &ctx->pf_b})
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
   free_batch(ctx->oneshot);

@@ -149,11 +149,11 @@ size_t tree_scan_temp_bytes(size_t n);
 size_t lb_bytes(uint32_t total);
 size_t lb_stride_words(uint32_t total);
 // centroid (center = 1) + frames in pd, centred points, root segments
-// matcher treelets of n_refs trees (rd[r].tl_off / tl_cap set by the host): flag, rank: cap + 1
-// words each; temp: tree_scan_temp_bytes(cap + 1); errors into ctl->error (bit 4)
+// matcher treelets of n_refs trees (rd[r].tl_off / tl_cap set by the host) of the build w (its
+// look-back words and control block; cap = 2 * its points + 2): rank: cap + 1 words; errors into
+// w.ctl->error (bit 4)
 hipError_t launch_treelets(hipStream_t s, int n_refs, uint32_t cap, const PairDesc* rd, const uint4* nodes,
-                           int bucket, uint32_t* flag, uint32_t* rank, void* temp, size_t temp_bytes, uint4* tl,
-                           uint2* link, TreeCtl* ctl);
+                           int bucket, uint32_t* rank, uint4* tl, uint2* link, const TreeWork& w);
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
                                int center, const TreeWork& w, float4* bpts, int bucket);
 // one level: nodes at depth `level` are split (their children get depth level + 1)

@@ -1819,10 +1819,6 @@ size_t tree_scan_temp_bytes(size_t n) {
   return bytes;
 }
 
-static hipError_t scan_u32(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, size_t n) {
-  size_t bytes = temp_bytes;
-  return rocprim::exclusive_scan(temp, bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), s);
-}
 
 // ---- treelets: the matcher tree in two-level, pointer-light records (Trav2C) ----------------
 // The nodes at even depth are treelet roots. Treelet T = a root v and its two children, in one
@@ -1853,17 +1849,21 @@ __device__ __forceinline__ bool tl_has_block(const uint4* __restrict__ nd, uint3
   return (L.y & 3u) != kLeaf || (R.y & 3u) != kLeaf;
 }
 
-__global__ __launch_bounds__(256) void k_tl_flag(int n_refs, uint32_t n, const PairDesc* __restrict__ rd,
-                                                 const uint4* __restrict__ nodes, uint32_t* __restrict__ flag) {
-  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  if (g >= n) return;
+// rank = exclusive scan over the node records [0, n) of "has a block of grandchild treelets"
+// (tl_has_block), the flag computed inside the single-pass look-back scan (one launch instead of
+// a flag kernel and rocprim's two)
+__global__ __launch_bounds__(kLbThreads) void k_tl_scan(int n_refs, uint32_t n, const PairDesc* __restrict__ rd,
+                                                       const uint4* __restrict__ nodes, uint32_t* __restrict__ rank,
+                                                       uint64_t* st, TreeCtl* ctl) {
   const uint32_t total = rd[n_refs - 1].node_off + rd[n_refs - 1].n_nodes;
-  if (g >= total) {
-    flag[g] = 0;
-    return;
-  }
-  const PairDesc& r = rd[ref_of_node(rd, n_refs, g)];
-  flag[g] = tl_has_block(nodes + r.node_off, g - r.node_off) ? 1u : 0u;
+  lookback_scan(
+      n,
+      [&](uint32_t g) -> uint32_t {
+        if (g >= total) return 0u;
+        const PairDesc& r = rd[ref_of_node(rd, n_refs, g)];
+        return tl_has_block(nodes + r.node_off, g - r.node_off) ? 1u : 0u;
+      },
+      rank, st, ctl);
 }
 
 __device__ __forceinline__ uint32_t tl_slot(const uint4& a) {
@@ -1925,12 +1925,14 @@ __global__ void k_tl_check(int n_refs, const PairDesc* __restrict__ rd, const ui
 }
 
 hipError_t launch_treelets(hipStream_t s, int n_refs, uint32_t cap, const PairDesc* rd, const uint4* nodes,
-                           int bucket, uint32_t* flag, uint32_t* rank, void* temp, size_t temp_bytes, uint4* tl,
-                           uint2* link, TreeCtl* ctl) {
+                           int bucket, uint32_t* rank, uint4* tl, uint2* link, const TreeWork& w) {
   if (n_refs <= 0 || cap == 0) return hipSuccess;
-  k_tl_flag<<<grid_of((size_t)cap + 1), 256, 0, s>>>(n_refs, cap + 1, rd, nodes, flag);
-  const hipError_t e = scan_u32(s, temp, temp_bytes, flag, rank, (size_t)cap + 1);
-  if (e != hipSuccess) return e;
+  TreeCtl* ctl = w.ctl;
+  // the scan's look-back words: the two strides after the build's own (lb_bytes), zeroed with
+  // them by launch_tree_prepare; cap + 1 = 2 * points + 3 records need at most two strides
+  if (lb_words(cap + 1) > 2 * w.lb_stride) return hipErrorInvalidValue;
+  uint64_t* st = w.lb + (size_t)(2 * kFarStack + 1) * w.lb_stride;
+  k_tl_scan<<<(cap + 1 + kLbTile - 1) / kLbTile, kLbThreads, 0, s>>>(n_refs, cap + 1, rd, nodes, rank, st, ctl);
   k_tl_build<<<grid_of(cap), 256, 0, s>>>(n_refs, cap, rd, nodes, rank, tl, link);
   k_tl_check<<<(n_refs + 63) / 64, 64, 0, s>>>(n_refs, rd, rank, bucket, ctl);
   return hipGetLastError();
@@ -1952,7 +1954,8 @@ void launch_pairs_degenerate_part(hipStream_t s, int n_pairs, const PairDesc* pd
   k_pairs_degenerate<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, st, rst, what);
 }
 
-// look-back words of every scan of a build: two per global level and the node count scan
+// look-back words of every scan of a build: two per global level, the node count scan and (two
+// strides) the matcher treelets' scan
 size_t lb_stride_words(uint32_t total) { return lb_words(total + 2); }
 uint32_t tree_mid_max() { return (uint32_t)kMidMax; }
 size_t tree_sum_tiles(size_t n) { return tiles_of(n); }
@@ -1963,7 +1966,7 @@ uint32_t tree_lvl_min() {
   const char* e = std::getenv("AICP_TREE_LVL_MIN");
   return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (1u << 22);
 }
-size_t lb_bytes(uint32_t total) { return (size_t)(2 * kFarStack + 1) * lb_stride_words(total) * 8; }
+size_t lb_bytes(uint32_t total) { return (size_t)(2 * kFarStack + 3) * lb_stride_words(total) * 8; }
 
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
                                int center, const TreeWork& w, float4* bpts, int bucket) {

@@ -179,7 +179,7 @@ struct SeqSlot {
   DevBuf read_raw, read_s, read_c, match, d2, touch, cand, slab, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, maps, bitmap,
       ovl, caps, sel_hist, sel_cnt, ctrs, active;
   // reference side
-  DevBuf ref_src, ref_raw, bpts, bnrm, nodes, tl, ptl, tl_flag, tl_rank, tl_temp, bpts_raw, nodes_raw, nrm_raw, nbids,
+  DevBuf ref_src, ref_raw, bpts, bnrm, nodes, tl, ptl, tl_rank, bpts_raw, nodes_raw, nrm_raw, nbids,
       inv, rd, tsrc,  // rd: rdesc, rdesc_raw, gdesc (PairDesc) + rstate, gstate (PairState); tsrc: source T
       wdesc, wstate, woutT, isync,  // the window's readings (committed to the sequence's arrays at its end)
       sp_par, sp_cnt, sp_off, sp_keys_r, sp_keys_g, sp_tmp_r, sp_tmp_g, sp_pc;  // sorted-key overlap (sparse windows)
@@ -218,7 +218,7 @@ void seq_state_free(SeqState* S) {
     for (DevBuf* b : {&sl.read_raw, &sl.read_s, &sl.read_c, &sl.match, &sl.d2, &sl.touch, &sl.cand, &sl.slab,
                       &sl.ord_k0, &sl.ord_k1, &sl.ord_v0, &sl.ord_v1, &sl.ord_tmp, &sl.maps, &sl.bitmap, &sl.ovl,
                       &sl.caps, &sl.sel_hist, &sl.sel_cnt, &sl.ctrs, &sl.active, &sl.ref_src, &sl.ref_raw, &sl.bpts,
-                      &sl.bnrm, &sl.nodes, &sl.tl, &sl.ptl, &sl.tl_flag, &sl.tl_rank, &sl.tl_temp, &sl.bpts_raw,
+                      &sl.bnrm, &sl.nodes, &sl.tl, &sl.ptl, &sl.tl_rank, &sl.bpts_raw,
                       &sl.nodes_raw, &sl.nrm_raw, &sl.nbids, &sl.inv, &sl.rd, &sl.tsrc, &sl.wdesc, &sl.wstate,
                       &sl.woutT, &sl.isync, &sl.sp_par, &sl.sp_cnt, &sl.sp_off, &sl.sp_keys_r,
                       &sl.sp_keys_g, &sl.sp_tmp_r, &sl.sp_tmp_g, &sl.sp_pc})
@@ -892,13 +892,10 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
                           sl.nodes, false);
   if (rc) return rc;
   const uint32_t ncap = 2 * n_ref + 2;
-  const size_t tlb = tree_scan_temp_bytes((size_t)ncap + 1);
   if (use_tl) {
     HIPC(ensure(sl.tl, tl_cap * 16));
     HIPC(ensure(sl.ptl, tl_cap * 8));
-    HIPC(ensure(sl.tl_flag, ((size_t)ncap + 1) * 4));
     HIPC(ensure(sl.tl_rank, ((size_t)ncap + 1) * 4));
-    HIPC(ensure(sl.tl_temp, tlb));
   }
   const int plan0 = plan_levels(n_ref, sl.tb[0]), plan1 = plan_levels(n_ref, sl.tb[1]);
   const bool capturable = plan0 > 0 && plan1 > 0;  // (a host-polled build cannot be captured)
@@ -933,9 +930,8 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
                          !capturable);
     if (r) return r;
     if (use_tl)
-      HIPC(launch_treelets(s3, 1, ncap, dRdesc, sl.nodes.as<uint4>(), bucket, sl.tl_flag.as<uint32_t>(),
-                           sl.tl_rank.as<uint32_t>(), sl.tl_temp.p, tlb, sl.tl.as<uint4>(), sl.ptl.as<uint2>(),
-                           sl.tb[1].tw.ctl));
+      HIPC(launch_treelets(s3, 1, ncap, dRdesc, sl.nodes.as<uint4>(), bucket, sl.tl_rank.as<uint32_t>(),
+                           sl.tl.as<uint4>(), sl.ptl.as<uint2>(), sl.tb[1].tw));
     HIPC(hipGetLastError());
     return AICP_OK;
   };
@@ -945,7 +941,7 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
       Key k;
       k << n_ref << plan1 << bucket << use_tl << tl_cap << dRdesc << sl.ref_raw.p << sl.bpts.p << sl.nodes.p
         << sl.tb[1].tw;
-      if (use_tl) k << sl.tl.p << sl.ptl.p << sl.tl_flag.p << sl.tl_rank.p << sl.tl_temp.p << tlb;
+      if (use_tl) k << sl.tl.p << sl.ptl.p << sl.tl_rank.p;
       r = graph_run(ctx, sl.g_match, s3, k, match_build);
     } else {
       r = match_build();
