@@ -249,7 +249,9 @@ hipError_t launch_ovl_keys_intersect(hipStream_t s, const OvlKeySide& rd, const 
 // gd->ref_origin = translation of fromMatrix4fToIsometry3d(T) * prior pose of src (1 thread);
 // T (src's correction, written by another stream's kernel) is copied to Tcopy for the transform
 // that follows on the same stream
-void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy);
+// the next reference: its origin into gd, Tcopy = T, out = T * in (k_transform's arithmetic)
+void launch_seq_ref_points(hipStream_t s, int n, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy,
+                           const float4* in, float4* out);
 // the window's descriptors, states and corrections into the sequence's arrays (np readings)
 void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState* st, const float* T, PairDesc* gd,
                        PairState* gst, float* gT);

@@ -176,7 +176,7 @@ __global__ void k_spo_counts(int n_groups, int n_pairs, const unsigned long long
 // (no read-back of the true count: the stream stays free of host synchronisation); the words
 // past the true total are padding (n_clouds << 48, sorted last, never counted).
 
-// a cloud's origin written on the device: the reference's by k_seq_next_ref, a debug-mode
+// a cloud's origin written on the device: the reference's by k_seq_ref_points, a debug-mode
 // reading's by k_debug_prep
 __global__ void k_spo_origin(OvlCloud* c, const double* __restrict__ o) {
   if (threadIdx.x < 3) c->origin[threadIdx.x] = o[threadIdx.x];

@@ -1,8 +1,8 @@
 // kernels_sequence.hip — the device side of App's frame-to-reference stream (sequence.cpp).
 //
 // The next reference is built from the last reading of a window without a host round trip:
-// k_seq_next_ref writes its sensor origin (the corrected pose's translation, app.cpp:375-391)
-// into the overlap group descriptor, k_transform (kernels_icp.hip) writes the corrected cloud,
+// k_seq_ref_points writes its sensor origin (the corrected pose's translation, app.cpp:375-391)
+// into the overlap group descriptor and the corrected cloud,
 // and the voxel maps of the overlap are sized on the device (k_ovl_size) inside a slot whose
 // capacity the host bounds from the source cloud's extent (a rigid motion keeps its diameter).
 #include <hip/hip_runtime.h>
@@ -15,16 +15,32 @@
 
 namespace aicp {
 
-// gd: the new window's overlap group; src: the reading that becomes the reference; T: its
-// correction (column-major, the finalize output)
-__global__ void k_seq_next_ref(PairDesc* gd, const PairDesc* __restrict__ src, const float* T, float* Tcopy) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// The new reference from the window's last reading in one launch (two kernels before, back to
+// back on the matcher stream's critical path). gd: the new window's overlap group; src: the
+// reading that becomes the reference; T: its correction (column-major, the finalize output).
+// Every workgroup reads T; workgroup 0 also writes its copy and the reference's sensor origin
+// (the corrected pose's translation, app.cpp:375-391), and each point is moved by apply4 exactly
+// as k_transform moves it (pcl::transformPointCloud's float order).
+__global__ __launch_bounds__(256) void k_seq_ref_points(int n, PairDesc* gd, const PairDesc* __restrict__ src,
+                                                        const float* T, float* Tcopy, const float4* __restrict__ in,
+                                                        float4* __restrict__ out) {
+  __shared__ float Ts[16];
+  if (threadIdx.x < 16) Ts[threadIdx.x] = __hip_atomic_load(T + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
   float Tl[16];
-  for (int k = 0; k < 16; ++k) Tl[k] = __hip_atomic_load(T + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  for (int k = 0; k < 16; ++k) Tcopy[k] = Tl[k];
-  double o[3];
-  corrected_origin(Tl, src->read_origin, o);
-  for (int k = 0; k < 3; ++k) gd->ref_origin[k] = o[k];
+  for (int k = 0; k < 16; ++k) Tl[k] = Ts[k];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (int k = 0; k < 16; ++k) Tcopy[k] = Tl[k];
+    double o[3];
+    corrected_origin(Tl, src->read_origin, o);
+    for (int k = 0; k < 3; ++k) gd->ref_origin[k] = o[k];
+  }
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  float q[3];
+  apply4(Tl, p.x, p.y, p.z, q);
+  out[i] = make_float4(q[0], q[1], q[2], 1.f);
 }
 
 // App's debug working mode (app.cpp:87-96): before reading d is registered, initT (initialT_) is
@@ -132,8 +148,9 @@ void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState
     k_seq_commit<<<1, 256, 0, s>>>(np, (const uint32_t*)d, (const uint32_t*)st, (const uint32_t*)T, (uint32_t*)gd,
                                    (uint32_t*)gst, (uint32_t*)gT);
 }
-void launch_seq_next_ref(hipStream_t s, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy) {
-  k_seq_next_ref<<<1, 64, 0, s>>>(gd, src, T, Tcopy);
+void launch_seq_ref_points(hipStream_t s, int n, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy,
+                           const float4* in, float4* out) {
+  k_seq_ref_points<<<(unsigned)std::max(1, (n + 255) / 256), 256, 0, s>>>(n, gd, src, T, Tcopy, in, out);
 }
 void launch_debug_prep(hipStream_t s, PairDesc* d, const float* initT, float* hist) {
   k_debug_prep<<<1, 64, 0, s>>>(d, initT, hist);

@@ -13,7 +13,7 @@
 //
 // Device design. Readings go in windows of F = reference_update_frequency: the readings of a
 // window are independent given its reference, so they run as one batch. Window w+1's reference
-// is the last reading of window w corrected by its own T: k_seq_next_ref + k_transform build it
+// is the last reading of window w corrected by its own T: k_seq_ref_points builds it
 // on the device right after window w's ICP, and the whole sequence is enqueued at once with no
 // host synchronisation between windows (the host packs and uploads window w+1 while the device
 // runs window w). That schedule predicts that every reading is accepted; the host checks the
@@ -25,7 +25,7 @@
 // streams beyond that run in submission order, so the sequence keeps to few):
 //   rd   H2D of the readings and descriptors (pinned staging, ring of K slots), then the
 //        reading side: state init, Morton order, reading voxel maps (independent of the reference)
-//   r3   next reference points (k_seq_next_ref, k_transform), centroid + matcher kd-tree
+//   r3   next reference points (k_seq_ref_points), centroid + matcher kd-tree
 //   r2   raw kd-tree + SurfaceNormal, normals into the matcher tree's order
 //   icp  reference voxel map, overlap counts, ratio, ICP loop, corrections
 // Window w's ICP loop is enqueued iteration by iteration; k_active_list (fused into the previous
@@ -875,8 +875,8 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     if (R.debug && w.index == 0)
       launch_transform(s3, (int)n_ref, S->initT.as<float>() + 16 * (1 + (size_t)w.src), src_pts,
                        const_cast<float4*>(src_pts));
-    launch_seq_next_ref(s3, dG, R.src_desc, R.src_T, sl.tsrc.as<float>());
-    launch_transform(s3, (int)n_ref, sl.tsrc.as<float>(), src_pts, sl.ref_raw.as<float4>());
+    launch_seq_ref_points(s3, (int)n_ref, dG, R.src_desc, R.src_T, sl.tsrc.as<float>(), src_pts,
+                          sl.ref_raw.as<float4>());
   } else {
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
     HIPC(hipMemcpyAsync(sl.ref_raw.p, src_pts, (size_t)n_ref * 16, hipMemcpyDeviceToDevice, s3));
