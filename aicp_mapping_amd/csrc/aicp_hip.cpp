@@ -557,7 +557,7 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
   if (rc) return rc;
   rc = device_trees_end(ctx->tb[1], err, s3, R, B->total_ref, dRdesc, bucket, ctx->bpts, ctx->nodes, plan);
   if (rc) return rc;
-  // treelet records of the matcher trees (Trav2C), then the control block again: k_tl_check
+  // treelet records of the matcher trees (Trav2C), then the control block again: the treelet check
   // reports into its error word, checked after the batch
   if (ctx->tl_total) {
     const uint32_t cap = (uint32_t)(2 * B->total_ref + 2);  // node records allotted

@@ -959,7 +959,7 @@ __device__ void subtree_build(const SubSeg& g, uint32_t total, float4* pts, PosT
       R.mn[k] = k == cd ? cut : nd.mn[k];
     }
     if (L.depth > maxd) maxd = L.depth;
-    if (sp >= kFarStack) break;  // deeper than the device stack: k_tr_desc reports it
+    if (sp >= kFarStack) break;  // deeper than the device stack: k_tr_emit reports it
     if (lane == 0) stk[sp] = R;
     ++sp;
     __syncthreads();
@@ -1714,11 +1714,20 @@ __global__ __launch_bounds__(64) void k_tr_subtree(uint32_t total, const TreeCtl
 }
 
 // ---- node records --------------------------------------------------------------------------
+// the node records from the events, and (threads < n_pairs, formerly k_tr_desc) each pair's node
+// range and depth in its descriptor: fields no event reads
 __global__ __launch_bounds__(256) void k_tr_emit(uint32_t total, const NodeEvent* __restrict__ ev,
                                                  const uint8_t* __restrict__ valid, const uint32_t* __restrict__ S,
-                                                 const PairDesc* __restrict__ pd, uint4* __restrict__ nodes,
-                                                 TreeCtl* ctl) {
+                                                 PairDesc* pd, uint4* __restrict__ nodes, TreeCtl* ctl, int n_pairs,
+                                                 const int32_t* __restrict__ pair_depth) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (uint32_t)n_pairs) {
+    PairDesc& d = pd[i];
+    d.node_off = S[d.ref_off + 1];
+    d.n_nodes = S[d.ref_off + d.n_ref + 1] - d.node_off;
+    d.tree_depth = pair_depth[i];
+    if (d.tree_depth >= kFarStack) atomicOr(&ctl->error, 1);
+  }
   if (i >= 2 * total || !valid[i]) return;
   const NodeEvent e = ev[i];
   const uint32_t ro = pd[e.pair].ref_off;
@@ -1737,17 +1746,6 @@ __global__ __launch_bounds__(256) void k_tr_emit(uint32_t total, const NodeEvent
     return;
   }
   nodes[pre] = r;
-}
-
-__global__ void k_tr_desc(int n_pairs, PairDesc* pd, const uint32_t* __restrict__ S,
-                          const int32_t* __restrict__ pair_depth, TreeCtl* ctl) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n_pairs) return;
-  PairDesc& d = pd[p];
-  d.node_off = S[d.ref_off + 1];
-  d.n_nodes = S[d.ref_off + d.n_ref + 1] - d.node_off;
-  d.tree_depth = pair_depth[p];
-  if (d.tree_depth >= kFarStack) atomicOr(&ctl->error, 1);
 }
 
 // Pairs sharing a reference cloud share its centroid, kd-tree and normals (built once per
@@ -1870,10 +1868,15 @@ __device__ __forceinline__ uint32_t tl_slot(const uint4& a) {
   return (a.y & 3u) == kLeaf ? (a.x << 28) | (a.y >> 2) : a.x;
 }
 
+__device__ __forceinline__ void tl_check_ref(const PairDesc& r, const uint32_t* __restrict__ rank, int bucket,
+                                             TreeCtl* ctl);
+// the records; threads < n_refs also run k_tl_check's test for reference g
 __global__ __launch_bounds__(256) void k_tl_build(int n_refs, uint32_t cap, const PairDesc* __restrict__ rd,
                                                   const uint4* __restrict__ nodes, const uint32_t* __restrict__ rank,
-                                                  uint4* __restrict__ tl, uint2* __restrict__ link) {
+                                                  uint4* __restrict__ tl, uint2* __restrict__ link, int bucket,
+                                                  TreeCtl* ctl) {
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g < (uint32_t)n_refs) tl_check_ref(rd[g], rank, bucket, ctl);
   const uint32_t total = rd[n_refs - 1].node_off + rd[n_refs - 1].n_nodes;
   if (g >= total || g >= cap) return;
   const PairDesc& r = rd[ref_of_node(rd, n_refs, g)];
@@ -1891,7 +1894,7 @@ __global__ __launch_bounds__(256) void k_tl_build(int n_refs, uint32_t cap, cons
     return base_of(gp) + 2u * (p != gp + 1 ? 1u : 0u) + (u != p + 1 ? 1u : 0u);
   };
   const uint32_t id = id_of(v);
-  if (id >= r.tl_cap) return;  // k_tl_check reports it
+  if (id >= r.tl_cap) return;  // tl_check_ref reports it
   // parent of a treelet root u as a node id: the grandparent's treelet, slot of the parent
   auto up_of = [&](uint32_t u) -> uint32_t {
     if (u == 0) return 0xffffffffu;
@@ -1915,11 +1918,8 @@ __global__ __launch_bounds__(256) void k_tl_build(int n_refs, uint32_t cap, cons
 
 // treelets used per reference within its allotment and addressable by the 26-bit base field;
 // leaf slots need count < 16 and bucket starts < 2^28
-__global__ void k_tl_check(int n_refs, const PairDesc* __restrict__ rd, const uint32_t* __restrict__ rank,
-                           int bucket, TreeCtl* ctl) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_refs) return;
-  const PairDesc& r = rd[i];
+__device__ __forceinline__ void tl_check_ref(const PairDesc& r, const uint32_t* __restrict__ rank, int bucket,
+                                             TreeCtl* ctl) {
   const uint32_t used = 1u + 4u * (rank[r.node_off + r.n_nodes] - rank[r.node_off]);
   if (used > r.tl_cap || used >= (1u << 26) || bucket > 15 || r.n_ref >= (1u << 28)) atomicOr(&ctl->error, 4);
 }
@@ -1933,8 +1933,8 @@ hipError_t launch_treelets(hipStream_t s, int n_refs, uint32_t cap, const PairDe
   if (lb_words(cap + 1) > 2 * w.lb_stride) return hipErrorInvalidValue;
   uint64_t* st = w.lb + (size_t)(2 * kFarStack + 1) * w.lb_stride;
   k_tl_scan<<<(cap + 1 + kLbTile - 1) / kLbTile, kLbThreads, 0, s>>>(n_refs, cap + 1, rd, nodes, rank, st, ctl);
-  k_tl_build<<<grid_of(cap), 256, 0, s>>>(n_refs, cap, rd, nodes, rank, tl, link);
-  k_tl_check<<<(n_refs + 63) / 64, 64, 0, s>>>(n_refs, rd, rank, bucket, ctl);
+  k_tl_build<<<std::max(grid_of(cap), grid_of((size_t)n_refs)), 256, 0, s>>>(n_refs, cap, rd, nodes, rank, tl, link,
+                                                                            bucket, ctl);
   return hipGetLastError();
 }
 void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd) {
@@ -2061,8 +2061,8 @@ hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDe
   // S[p] = #nodes with end < p  (exclusive scan over end positions 0..total+1)
   k_tr_scan_counts<<<lb_words(total + 2) - 1, kLbThreads, 0, s>>>(total + 2, w.ecnt, w.X1,
                                                                     w.lb + (size_t)(2 * kFarStack) * w.lb_stride, w.ctl);
-  k_tr_emit<<<grid_of(2 * (size_t)total), 256, 0, s>>>(total, w.ev, w.valid, w.X1, pd, nodes, w.ctl);
-  k_tr_desc<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, w.X1, w.pair_depth, w.ctl);
+  k_tr_emit<<<std::max(grid_of(2 * (size_t)total), grid_of((size_t)n_pairs)), 256, 0, s>>>(
+      total, w.ev, w.valid, w.X1, pd, nodes, w.ctl, n_pairs, w.pair_depth);
   return hipGetLastError();
 }
 
