@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <cstdio>
 
@@ -2587,14 +2588,26 @@ __global__ __launch_bounds__(64) void k_solve6(const double* A, const double* b,
 // ------------------------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------------------------
-static int persistent_grid(int n_items, int blocks_per_cu = 8) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
+// CU count of the calling thread's current device, cached per device (contexts of
+// aicp_hip_multi_* call this from several host threads at once, possibly on different GPU models)
+static int device_cus() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  if (dev >= 0 && dev < kMaxDev) {
+    const int c = cache[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
   }
+  int cus = 0;
+  if (dev < 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  if (dev >= 0 && dev < kMaxDev) cache[dev].store(cus, std::memory_order_relaxed);
+  return cus;
+}
+
+static int persistent_grid(int n_items, int blocks_per_cu = 8) {
+  const int cus = device_cus();
   // every work group (blockIdx % kXcdGroups) needs at least one block: a multiple of 8
   int want = (n_items + 255) / 256;
   if (want > cus * blocks_per_cu) want = cus * blocks_per_cu;

@@ -367,6 +367,12 @@ uint64_t key_bound(WorkerPool& pool, const aicp_cloud& c, const double* org, dou
   return s;
 }
 
+// the error message of work run on a host thread of its own (copied into ctx->err after the join,
+// so two threads never write that string at once)
+struct ErrSink {
+  std::string err;
+};
+
 struct Win {
   size_t p0, np;
   int src;  // -1: the first cloud; else the reading whose corrected cloud is the reference
@@ -446,7 +452,9 @@ static int graph_run(aicp_hip_ctx* ctx, GraphCache& gc, hipStream_t s, const Key
 
 // The host parts: pack + upload the readings (and the reference source when it is not
 // resident), descriptors, block maps, map capacities; then the reading side (stream rd).
-static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+// (C: aicp_hip_ctx, or ErrSink on the upload thread: only ctx->err is used)
+template <class C>
+static int win_upload(C* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
                       const aicp_cloud* first, const aicp_cloud* rd, const float4* src_resident,
                       std::vector<Box>& rbox, WinRun& R) {
   const Win& w = R.w;
@@ -798,7 +806,8 @@ static int win_upload(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg
 // The reading side of the window on stream rd (independent of the reference): state init, Morton
 // order, the readings' voxel maps. Enqueued after the window's reference, so that it fills the
 // CUs the kd-tree builds leave idle instead of competing with the previous window's ICP loop.
-static int win_read_side(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+template <class C>
+static int win_read_side(C* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
                          WinRun& R) {
   WIN_REFS;
   (void)ctx;
@@ -1347,7 +1356,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       }
       for (size_t k = 0; k < plan.size(); ++k) runs[k].tev = S->tev.data() + 10 * k;
     }
-    auto upload = [&](size_t k) {
+    auto upload = [&](auto* ec, size_t k) {
       const Win& w = plan[k];
       runs[k].w = w;
       runs[k].ctl_w = ctl + 2 * k;
@@ -1369,7 +1378,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         for (size_t i = pw.p0; i < (size_t)w.src; ++i) off += readings[i].n;
         resident = S->slot[pw.slot].read_raw.as<float4>() + off;
       }
-      return win_upload(ctx, S, cfg, prm, first, readings, resident, rbox, runs[k]);
+      return win_upload(ec, S, cfg, prm, first, readings, resident, rbox, runs[k]);
     };
     const bool prof = seq_prof();
     double hp[5] = {0, 0, 0, 0, 0};  // upload (its thread), reference trees, icp loop, join, reference icp
@@ -1382,7 +1391,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     // The reading side of window k + 1 (Morton order, voxel maps) is enqueued with its upload,
     // during window k's loop. (Enqueued with the next reference instead, to keep it off the loop's
     // CUs, it slowed the kd-tree builds on the critical path: 2.29 against 2.20 ms per window.)
-    auto read_side = [&](size_t k) { return win_read_side(ctx, S, cfg, prm, runs[k]); };
+    auto read_side = [&](auto* ec, size_t k) { return win_read_side(ec, S, cfg, prm, runs[k]); };
     std::vector<IcpLoop> loops(plan.size());
     std::vector<uint8_t> done_enq(plan.size(), 0);  // the window's ev_done recorded
     // enqueue iterations while the host is less than one iteration ahead of the oldest poll, read
@@ -1425,8 +1434,8 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       else
         HIPC(hipMemcpyAsync(S->initT.p, S->initT.as<float>() + 16 * (1 + p), 64, hipMemcpyDeviceToDevice, S->s_icp));
     }
-    rc = timed(0, [&] { return upload(0); });
-    if (!rc) rc = timed(0, [&] { return read_side(0); });
+    rc = timed(0, [&] { return upload(ctx, 0); });
+    if (!rc) rc = timed(0, [&] { return read_side(ctx, 0); });
     if (!rc) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[0]); });
     if (!rc) rc = timed(4, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[0]); });
     for (size_t k = 0; k < plan.size() && !rc; ++k) {
@@ -1438,16 +1447,18 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       // smoothLength + 1, and the device waited ~0.25 ms per window for it (r04 trace).
       std::thread up_thr;
       int up_rc = AICP_OK;
+      ErrSink up_err;  // the upload thread's error message (ctx->err belongs to this thread)
       auto try_upload = [&]() -> int {
         if (uploaded || !can_upload(k)) return AICP_OK;
         uploaded = true;
         up_thr = std::thread([&, k] {
           if (hipSetDevice(S->device) != hipSuccess) {
+            up_err.err = "hipSetDevice on the upload thread";
             up_rc = AICP_ERR_HIP;
             return;
           }
-          int r = timed(0, [&] { return upload(k + 1); });
-          if (!r) r = timed(0, [&] { return read_side(k + 1); });
+          int r = timed(0, [&] { return upload(&up_err, k + 1); });
+          if (!r) r = timed(0, [&] { return read_side(&up_err, k + 1); });
           up_rc = r;
         });
         return AICP_OK;
@@ -1484,7 +1495,10 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       }
       {
         const int ur = timed(3, join_upload);  // (before any return: the thread uses this scope)
-        if (!rc) rc = ur;
+        if (!rc && ur) {  // the first error wins: the upload's message only if this thread had none
+          rc = ur;
+          ctx->err = up_err.err;
+        }
       }
       if (!rc && next) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
       if (!rc && next) rc = timed(4, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });

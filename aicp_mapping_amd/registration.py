@@ -203,6 +203,48 @@ def create_overlapper(parameters: OverlapParams, ctx: Context | None = None):
     return None
 
 
+def isometry_from_matrix4f(T) -> np.ndarray:
+    """fromMatrix4fToIsometry3d (aicp_core/src/utils/common.cpp:4-23): Eigen's Quaternionf of the
+    float rotation block (trace branch, else the largest-diagonal branch), cast to double and
+    expanded by toRotationMatrix in double; the translation is the float column widened. 4x4
+    float64."""
+    f = np.float32
+    m = np.asarray(T, np.float32).reshape(4, 4)
+    q = [f(0)] * 4  # x, y, z, w
+    t = f(f(m[0, 0] + m[1, 1]) + m[2, 2])
+    if t > f(0):
+        t = f(np.sqrt(f(t + f(1))))
+        q[3] = f(f(0.5) * t)
+        t = f(f(0.5) / t)
+        q[0] = f(f(m[2, 1] - m[1, 2]) * t)
+        q[1] = f(f(m[0, 2] - m[2, 0]) * t)
+        q[2] = f(f(m[1, 0] - m[0, 1]) * t)
+    else:
+        i = 0
+        if m[1, 1] > m[0, 0]:
+            i = 1
+        if m[2, 2] > m[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        t = f(np.sqrt(f(f(f(m[i, i] - m[j, j]) - m[k, k]) + f(1))))
+        q[i] = f(f(0.5) * t)
+        t = f(f(0.5) / t)
+        q[3] = f(f(m[k, j] - m[j, k]) * t)
+        q[j] = f(f(m[j, i] + m[i, j]) * t)
+        q[k] = f(f(m[k, i] + m[i, k]) * t)
+    x, y, z, w = (float(v) for v in q)
+    tx, ty, tz = 2.0 * x, 2.0 * y, 2.0 * z
+    twx, twy, twz = tx * w, ty * w, tz * w
+    txx, txy, txz = tx * x, ty * x, tz * x
+    tyy, tyz, tzz = ty * y, tz * y, tz * z
+    out = np.eye(4)
+    out[:3, :3] = [[1.0 - (tyy + tzz), txy - twz, txz + twy],
+                   [txy + twz, 1.0 - (txx + tzz), tyz - twx],
+                   [txz - twy, tyz + twx, 1.0 - (txx + tyy)]]
+    out[:3, 3] = m[:3, 3].astype(np.float64)
+    return out
+
+
 class AicpPipeline:
     """The registration hot path of App (app.cpp:112-141, 187-247) for one pair:
     computeOverlap -> ratio auto-tune (clamp + YAML text rewrite) -> registerClouds."""
@@ -218,6 +260,24 @@ class AicpPipeline:
             tempfile.gettempdir(), "aicp_hip_icp_autotuned.yaml")
         self.localize_against_prior_map = localize_against_prior_map
         self.octree_overlap_ = -1.0
+
+    def setAndFilterReading(self, raw_reading, prior_pose, working_mode="robot", initialT=None):
+        """App::setAndFilterReading (app.cpp:77-99): in "debug" mode the RAW reading is moved by
+        initialT_ (pcl::transformPointCloud, float; aicp_hip_transform) and its prior pose becomes
+        initialT_ * prior pose, and only then pre-filtered (regionGrowingUniformPlaneSegmentation-
+        Filter, aicp_hip_prefilter); "robot" mode pre-filters the reading as given. This is App's
+        filter order in debug mode, which aicp_hip_sequence_run (pre-filtered clouds in) does not
+        reproduce: the 0.08 m VoxelGrid is world-aligned. Returns (filtered cloud, pose)."""
+        from . import filtering
+
+        pose = np.asarray(prior_pose, np.float64)
+        cloud = _lib.as_points(raw_reading)[:, :3]
+        ctx = self.registr_.ctx if self.registr_ is not None else default_context()
+        if working_mode != "robot":
+            T = np.eye(4, dtype=np.float32) if initialT is None else np.asarray(initialT, np.float32)
+            cloud = ctx.transform(T, cloud)
+            pose = isometry_from_matrix4f(T) @ pose  # fromMatrix4fToIsometry3d(initialT_) * reading_pose
+        return filtering.regionGrowingUniformPlaneSegmentationFilter(cloud, ctx=ctx), pose
 
     def computeOverlap(self, ref, read, ref_pose, read_pose):
         if self.localize_against_prior_map:

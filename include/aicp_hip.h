@@ -276,7 +276,14 @@ int aicp_hip_last_phase_ms(const aicp_hip_ctx* ctx, double out_ms[5]);
  * initialT_ * prior pose (app.cpp:87-96); after each accepted reading initialT_ = correction *
  * initialT_ (app.cpp:414; identity at the start). The readings then depend on each other one by
  * one, so the device registers them one after the other (the reference trees are still built
- * once per window). Without the flag: "robot" mode, the node's default (aicp_ros_node.cpp:14). */
+ * once per window). Without the flag: "robot" mode, the node's default (aicp_ros_node.cpp:14).
+ * Filter order: this entry point takes pre-filtered clouds in both modes and moves them by
+ * initialT_ afterwards. App moves the RAW reading first and pre-filters the moved cloud
+ * (setAndFilterReading, app.cpp:87-99); the 0.08 m VoxelGrid is aligned to the world frame, so the
+ * two orders keep different points unless initialT_ is the identity. For App's exact debug order
+ * the caller runs aicp_hip_prefilter on initialT_ * raw reading itself (one reading at a time:
+ * initialT_ then depends on the previous correction), as registration.AicpPipeline's debug mode
+ * does; the stream is the robot-mode fast path. */
 #define AICP_SEQ_DEBUG 8
 
 typedef struct {

@@ -55,6 +55,38 @@ def test_c3_full_size_pair(ctx, oracle, L):
     assert (st[0]["nn_points_touched"], st[0]["nn_nodes_touched"]) == (st1.nn_points_touched, st1.nn_nodes_touched)
 
 
+def _c3_reading(a):
+    seed, i, n = a
+    return sy.stream_reading(seed, i, n)
+
+
+def test_c3_stream_windowed(ctx, oracle, L):
+    """C3 as App runs it (app.cpp:282-414): the first cloud plus 6 KITTI-sized readings of
+    600 000 points through aicp_hip_sequence_run, a reference every 5 accepted readings, so
+    reading 5 is registered against corrected reading 4 built on the device (app.cpp:383-391).
+    Against the oracle's replay of the same chain: key counts exact, ratios equal, T within
+    1e-6 rad / 1e-5 m, the same decisions, references and iteration counts."""
+    n, k = 600000, 6
+    first, o0 = sy.stream_first(3, n)
+    with ProcessPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        rd = list(ex.map(_c3_reading, [(3, i, n) for i in range(k)]))
+    reads, origins = [r[0] for r in rd], [r[1] for r in rd]
+    T, out, done, rc = ctx.sequence_run(first, o0, reads, origins)
+    assert rc == 0 and done == k
+    assert ctx.last_sequence_timing()["windows"] == 2
+    ref = oracle.sequence(first, o0, reads, origins, reference_update_frequency=5, resolution=RES)
+    assert [o["reference"] for o in out] == [r["reference"] for r in ref] == [-1] * 5 + [4]
+    for i, (o, r) in enumerate(zip(out, ref)):
+        assert o["status"] == r["status"] == 0, i
+        assert (o["accepted"], o["is_reference"]) == (r["accepted"], r["is_reference"]), i
+        assert o["icp"]["overlap_keys"] == [int(c) for c in r["counts"]], i
+        assert o["icp"]["trimmed_ratio"] == np.float32(r["ratio"]), i
+        assert o["icp"]["iterations"] == r["stats"].iterations, i
+        rr, tt = sy.rot_err(r["T"], T[i])
+        assert rr < 1e-6 and tt < 1e-5, (i, rr, tt)
+        np.testing.assert_allclose(o["corrected_origin"], r["corrected_origin"], rtol=0, atol=1e-9)
+
+
 def _c4_map(seed, n_map):
     scene = sy.make_scene(seed)
     rng = np.random.default_rng(seed * 7919 + 77)

@@ -261,3 +261,20 @@ def test_xyzrgbnormal_register_is_reference_noop():
     assert out is T and np.array_equal(T, np.arange(16, dtype=np.float32).reshape(4, 4))
     assert reg.registerClouds(pts, pts) is None
     assert reg._ctx is None
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_isometry_from_matrix4f_matches_oracle(oracle, seed):
+    """registration.isometry_from_matrix4f (fromMatrix4fToIsometry3d, common.cpp:4-23) moves a
+    prior origin like the oracle's corrected_origin, across the quaternion's trace and
+    largest-diagonal branches (seeds 2, 3: rotations near pi)."""
+    from aicp_mapping_amd import registration as R
+    from aicp_mapping_amd import synthetic as sy
+
+    rng = np.random.default_rng(seed)
+    yaw = [10.0, -35.0, 179.0, -178.5][seed]
+    T = sy.make_T(yaw_deg=yaw, pitch_deg=rng.uniform(-5, 5), roll_deg=rng.uniform(-5, 5),
+                  t=rng.uniform(-3, 3, 3)).astype(np.float32)
+    o = rng.uniform(-20, 20, 3)
+    got = (R.isometry_from_matrix4f(T) @ np.r_[o, 1.0])[:3]
+    np.testing.assert_allclose(got, oracle.corrected_origin(T, o), rtol=0, atol=1e-12)

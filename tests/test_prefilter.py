@@ -208,6 +208,27 @@ def _check_same(g, r):
 
 
 @pytest.mark.gpu
+def test_gpu_debug_order_transform_then_filter(ctx, oracle):
+    """App's debug working mode moves the RAW reading by initialT_ and pre-filters the moved
+    cloud (setAndFilterReading, app.cpp:87-99): AicpPipeline.setAndFilterReading does that on
+    the device and equals the oracle's pcl::transformPointCloud followed by its pre-filter; the
+    prior pose becomes fromMatrix4fToIsometry3d(initialT_) * pose."""
+    from aicp_mapping_amd import registration as R
+    from aicp_mapping_amd import synthetic as sy
+
+    P = scene_cloud(seed=5, half=8.0)
+    T = sy.make_T(yaw_deg=7.0, pitch_deg=1.0, roll_deg=-2.0, t=(0.4, -0.3, 0.05)).astype(np.float32)
+    pose = sy.make_T(yaw_deg=3.0, pitch_deg=0.0, roll_deg=0.0, t=(1.0, 2.0, 0.7))
+    pipe = R.AicpPipeline(R.RegistrationParams(type="HIP"), R.OverlapParams(type="OctreeBased"), ctx=ctx)
+    got, gpose = pipe.setAndFilterReading(P, pose, "debug", T)
+    want = oracle.prefilter(oracle.transform_cloud(T, P))["out"]
+    assert np.array_equal(got, want)
+    np.testing.assert_allclose(gpose[:3, 3], oracle.corrected_origin(T, pose[:3, 3]), rtol=0, atol=1e-12)
+    robot, rpose = pipe.setAndFilterReading(P, pose)
+    assert np.array_equal(robot, oracle.prefilter(P)["out"]) and np.array_equal(rpose, pose)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed,half", [(7, 5.0), (5, 8.0), (11, 12.0)])
 def test_gpu_prefilter_matches_oracle(ctx, oracle, seed, half):
     import aicp_mapping_amd._lib as L
