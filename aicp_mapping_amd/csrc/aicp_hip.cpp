@@ -807,6 +807,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     uint32_t reads = 0;
     for (size_t i = 0; i < P; ++i) reads += B->desc[i].n_read;
     ActiveList* al = ctx->active.as<ActiveList>();
+    const int sel_ff = sel_fused_from();
     for (int it = 0; it < cfg->max_iter; ++it) {
       if (it == 0) launch_active_list(s, (int)P, dDesc, dState, al, dCtr);
       prm.prof_slot = nn_launches;
@@ -822,8 +823,12 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       y.st = dState;
       y.al = al;
       y.ctr = dCtr;
-      launch_icp_select_f(s, B->m_sel, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
-                          ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), y);
+      if (sel_ff > 0 && it >= sel_ff)
+        launch_icp_select_fused(s, B->m_sel, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
+                                ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), y);
+      else
+        launch_icp_select_f(s, B->m_sel, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
+                            ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), y);
       launch_icp_reduce_f(s, B->m_red, dDesc, dState, readc, ctx->match.as<int32_t>(), ctx->d2.as<float>(),
                           ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>(), prm, y);
     }

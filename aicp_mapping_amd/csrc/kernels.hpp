@@ -70,6 +70,12 @@ inline size_t icp_sync_words(size_t n_pairs) { return 3 * n_pairs + 2; }
 IcpIterSync icp_sync_layout(uint32_t* words, size_t n_pairs, int group);
 void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
                          uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y);
+// from the second iteration on: the select in one launch, its compaction on the previous
+// iteration's digit-1 bin (same limit; a missed guess is compacted again by the pair's last
+// workgroup, counted in PairState::sel_miss)
+void launch_icp_select_fused(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
+                             uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y);
+int sel_fused_from();
 void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float4* read_c,
                          const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
                          const float4* bnrm, double* slab, const IcpParams& prm, const IcpIterSync& y);

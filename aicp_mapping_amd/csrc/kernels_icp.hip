@@ -1047,6 +1047,9 @@ __global__ void k_init_state(int n_pairs, const PairDesc* __restrict__ pd, PairS
   s.touched_nodes = 0;
   for (int i = 0; i < 3; ++i) s.ovl_counts[i] = 0;
   s.ovl_err = 0;
+  s.sel_b1 = 0;
+  s.sel_r1 = 0;
+  s.sel_miss = 0;
   quat_from_T(s.T, s.qh[0]);
   s.th[0][0] = s.th[0][1] = s.th[0][2] = 0.0;
 }
@@ -1878,7 +1881,10 @@ __global__ __launch_bounds__(256) void k_sel_compact(BlockMap m, const PairDesc*
 // trip), so up to kFinalLds of them are read once, eight loads in flight per thread, into LDS and
 // both passes run there (the passes over global memory took ~11 us of a C2 iteration, r03).
 constexpr uint32_t kFinalLds = 8192;
-__device__ void sel_final_body(PairState& s, const uint32_t* __restrict__ cv, uint32_t* cand_cnt) {
+// b1 / r1: digit 1's bin and the rank in it (s.sel_b1 / sel_r1; passed in, since in k_sel_fused
+// they were just written by another thread of the workgroup)
+__device__ void sel_final_body(PairState& s, uint32_t b1, uint32_t r1, const uint32_t* __restrict__ cv,
+                               uint32_t* cand_cnt) {
   __shared__ uint32_t h[kHistBins];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t res[2];
@@ -1906,12 +1912,12 @@ __device__ void sel_final_body(PairState& s, const uint32_t* __restrict__ cv, ui
   __syncthreads();
   for (uint32_t i = t; i < c; i += nt) atomicAdd(&h[(src[i] >> 10) & 2047u], 1u);
   __syncthreads();
-  block_find_rank(h, kHistBins, s.sel_r1, res, wsum);
+  block_find_rank(h, kHistBins, r1, res, wsum);
   const uint32_t b2 = res[0], r2 = res[1];
   __syncthreads();
   for (int i = t; i < kHistBins; i += nt) h[i] = 0;
   __syncthreads();
-  const uint32_t hi21 = (s.sel_b1 << 11) | b2;
+  const uint32_t hi21 = (b1 << 11) | b2;
   for (uint32_t i = t; i < c; i += nt) {
     const uint32_t v = src[i];
     if ((v >> 10) == hi21) atomicAdd(&h[v & 1023u], 1u);
@@ -1929,7 +1935,7 @@ __global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__
   const int pair = blockIdx.x;
   PairState& s = st[pair];
   if (!s.active) return;
-  sel_final_body(s, cand + pd[pair].read_off, cand_cnt + pair);
+  sel_final_body(s, s.sel_b1, s.sel_r1, cand + pd[pair].read_off, cand_cnt + pair);
 }
 
 // k_sel_compact + (last workgroup of the pair) k_sel_final. kT threads per workgroup over the
@@ -1986,9 +1992,122 @@ __global__ __launch_bounds__(kT) void k_sel_compact_f(BlockMap m, const PairDesc
   AICP_IP_BODY(1);
   if (!last_arrival(&y.sel2[pair], nblk)) return;
   AICP_IP_TAIL0;
-  sel_final_body(s, cand + d.read_off, cand_cnt + pair);
+  sel_final_body(s, s.sel_b1, s.sel_r1, cand + d.read_off, cand_cnt + pair);
   AICP_IP_TAIL(1);
 }
+// the values of v[0, kPer) (one block-map entry of the pair, kT threads) whose digit 1 is b into
+// the pair's candidate list: per-wave ballot counts, one atomic per workgroup on cand_cnt
+template <int kT, int kPer>
+__device__ __forceinline__ void sel_compact_bin(const uint32_t (&v)[kPer], uint32_t b, uint32_t* __restrict__ cv,
+                                                uint32_t* cnt) {
+  constexpr int kW = kT / 64;
+  __shared__ uint32_t wcount[kW];
+  __shared__ uint32_t base;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t mine = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) mine += (uint32_t)__popcll(__ballot(v[u] != kInfBits && (v[u] >> 21) == b));
+  if (lane == 0) wcount[w] = mine;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < kW; ++k) tot += wcount[k];
+    base = tot ? atomicAdd(cnt, tot) : 0u;
+  }
+  __syncthreads();
+  if (wcount[w]) {
+    uint32_t o = base;
+    for (int k = 0; k < w; ++k) o += wcount[k];
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const bool hit = v[u] != kInfBits && (v[u] >> 21) == b;
+      const uint64_t mk = __ballot(hit);
+      if (hit) cv[o + (uint32_t)__popcll(mk & below)] = v[u];
+      o += (uint32_t)__popcll(mk);
+    }
+  }
+  __syncthreads();  // (wcount / base are rewritten by the next call)
+}
+
+// The whole select in one launch from the second ICP iteration on: k_sel_hist_f's histogram, and
+// in the same pass the compaction of k_sel_compact_f for a guessed digit-1 bin, the pair's bin of
+// the previous iteration (the trimmed limit moves little between iterations). The last workgroup
+// of the pair runs find1; when the guess was the bin of the k-th value the candidates are already
+// compacted and it runs the final select at once, otherwise it compacts that bin from the pair's
+// distances itself first (slower, same candidates: the select is order-independent), so the
+// limit is k_sel_hist_f + k_sel_compact_f's bit for bit either way.
+template <int kT>
+__global__ __launch_bounds__(kT) void k_sel_fused(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
+                                                  const float* __restrict__ d2, uint32_t* __restrict__ hist1,
+                                                  uint32_t* __restrict__ cand, uint32_t* __restrict__ cand_cnt,
+                                                  IcpIterSync y) {
+  constexpr int kPer = kNNBlock * kSelPerThread / kT;
+  const int pair = m.pair[blockIdx.x];
+  PairState& s = st[pair];
+  if (!s.active) return;
+  __shared__ uint32_t h[2][kHistBins];  // one sub-histogram per half workgroup (LDS atomic conflicts)
+  const int t = threadIdx.x;
+  for (int i = t; i < 2 * kHistBins; i += kT) (&h[0][0])[i] = 0;
+  const PairDesc& d = pd[pair];
+  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
+  const uint32_t j0 = m.start[blockIdx.x];
+  const uint32_t guess = s.sel_b1;  // the previous iteration's bin (find1 rewrites it after every block arrived)
+  uint32_t v[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const uint32_t j = j0 + t + (uint32_t)kT * u;
+    v[u] = j < d.n_read ? bits[j] : kInfBits;
+  }
+  __syncthreads();
+  uint32_t* mine = h[t / (kT / 2)];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u)
+    if (v[u] != kInfBits) atomicAdd(&mine[v[u] >> 21], 1u);
+  __syncthreads();
+  uint32_t* g = hist1 + (size_t)pair * kHistBins;
+  for (int b = t; b < kHistBins; b += kT) {
+    const uint32_t c = h[0][b] + h[1][b];
+    if (c) atomicAdd(&g[b], c);
+  }
+  uint32_t* cv = cand + d.read_off;
+  sel_compact_bin<kT, kPer>(v, guess, cv, cand_cnt + pair);
+  const uint32_t nblk = (d.n_read + 256u * kSelPerThread - 1) / (256u * kSelPerThread);
+  if (!last_arrival(&y.sel1[pair], nblk)) return;
+  if (!sel_find1_body(s, g)) {  // no finite distance: the pair stops (ConvergenceError)
+    if (t == 0) cand_cnt[pair] = 0;
+    pair_done(y);
+    return;
+  }
+  // find1's bin and rank, written by thread 0: passed on through LDS (a global load of them
+  // by another wave could hit a stale L1 line from the guess's load above)
+  __shared__ uint32_t s_sel[2];
+  if (t == 0) {
+    s_sel[0] = s.sel_b1;
+    s_sel[1] = s.sel_r1;
+  }
+  __syncthreads();
+  const uint32_t b1 = s_sel[0], r1 = s_sel[1];
+  if (b1 != guess) {  // missed: the candidates of bin b1 from all of the pair's distances
+    if (t == 0) __hip_atomic_store(cand_cnt + pair, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    for (uint32_t jb = 0; jb < d.n_read; jb += (uint32_t)kT * kPer) {
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const uint32_t j = jb + t + (uint32_t)kT * u;
+        v[u] = j < d.n_read ? bits[j] : kInfBits;
+      }
+      sel_compact_bin<kT, kPer>(v, b1, cv, cand_cnt + pair);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __threadfence();
+    __syncthreads();
+    if (t == 0) atomicAdd(&s.sel_miss, 1u);
+  }
+  sel_final_body(s, b1, r1, cv, cand_cnt + pair);
+}
+
 #ifndef AICP_SEL_COMPACT_THREADS
 #define AICP_SEL_COMPACT_THREADS 1024
 #endif
@@ -2784,6 +2903,15 @@ void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairStat
   if (!m.n_blocks) return;
   k_sel_hist_f<kSelHistThreads><<<m.n_blocks, kSelHistThreads, 0, s>>>(m, pd, st, d2, hist1, y);
   k_sel_compact_f<kSelCompactThreads><<<m.n_blocks, kSelCompactThreads, 0, s>>>(m, pd, st, d2, cand, cand_cnt, y);
+}
+void launch_icp_select_fused(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
+                             uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y) {
+  if (!m.n_blocks) return;
+  k_sel_fused<256><<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, hist1, cand, cand_cnt, y);
+}
+int sel_fused_from() {  // AICP_SEL_FUSED=k: the fused select from iteration k on (0: never)
+  const char* e = std::getenv("AICP_SEL_FUSED");
+  return e ? std::atoi(e) : 3;  // (iterations 1-2 missed the guess on C2 2 times in 3, 3+ never: r05 log)
 }
 void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float4* read_c,
                          const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,

@@ -1125,8 +1125,13 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   y.al = al;
   y.ctr = ctr;
   y.host_n = hn_next;
-  launch_icp_select_f(st, msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(), sl.cand.as<uint32_t>(),
-                      sl.sel_cnt.as<uint32_t>(), y);
+  const int ff = sel_fused_from();
+  if (ff > 0 && it >= ff)  // (iteration 0 has no previous bin to guess)
+    launch_icp_select_fused(st, msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
+                            sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), y);
+  else
+    launch_icp_select_f(st, msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(), sl.cand.as<uint32_t>(),
+                        sl.sel_cnt.as<uint32_t>(), y);
   if (it == 0) {  // the reduce gathers the reference normals (stream r2, scattered into matcher order)
     HIPC(hipStreamWaitEvent(st, sl.ev_s2, 0));
     launch_pairs_degenerate_part(st, np_l, gd, gs, dRst, 1);
@@ -1633,6 +1638,15 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     o.nn_points_touched = st.touched_pts;
     o.nn_nodes_touched = st.touched_nodes;
     for (int k = 0; k < 3; ++k) o.overlap_keys[k] = st.ovl_counts[k];
+  }
+  if (seq_prof()) {  // guessed bins of the fused select that missed, against its launches
+    uint64_t miss = 0, fused = 0;
+    for (size_t i = 0; i < *n_done; ++i) {
+      miss += hs[i].sel_miss;
+      fused += hs[i].iters > 1 ? (uint64_t)(hs[i].iters - 1) : 0;
+    }
+    std::fprintf(stderr, "[aicp seq] fused select: %llu of %llu guessed bins missed\n", (unsigned long long)miss,
+                 (unsigned long long)fused);
   }
   // timing
   ctx->last_nn_launches = timeNN ? nn_launches : 0;
