@@ -103,7 +103,7 @@ struct PairState {
   int32_t ovl_bbox[6];  // kmin[3], kmax[3] (union of both clouds)
   int32_t ovl_err;
   uint32_t sel_b1, sel_r1;  // trimmed select: digit-1 bin of the k-th value and its rank in it
-  int32_t pad_;
+  uint32_t sel_miss;    // fused selects whose guessed bin was not the k-th value's (k_sel_fused)
   double qh[kHistRing][4];
   double th[kHistRing][3];
   // per history entry i >= 1: |angdist(q_i, q_i-1)| and |t_i - t_i-1|, computed once when entry
@@ -165,6 +165,7 @@ struct TreeCtl {
   uint32_t n_mid;                // mid-size segments (k_tr_mid)
   uint32_t n_big;                // of which above kSubMax points (planned build too shallow)
   int32_t error;
+  uint32_t arrive[kFarStack + 2];  // tiles done: [0] centring (roots in its last tile), [1 + level] pass-2 scan
 };
 
 struct IcpParams {
