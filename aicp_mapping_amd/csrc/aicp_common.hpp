@@ -165,7 +165,6 @@ struct TreeCtl {
   uint32_t n_mid;                // mid-size segments (k_tr_mid)
   uint32_t n_big;                // of which above kSubMax points (planned build too shallow)
   int32_t error;
-  uint32_t arrive[kFarStack + 2];  // tiles done: [0] centring (roots in its last tile), [1 + level] pass-2 scan
 };
 
 struct IcpParams {
