@@ -38,6 +38,7 @@ EXPORTS = [
     "aicp_hip_default_sequence_params", "aicp_hip_sequence_run", "aicp_hip_last_sequence_timing",
     "aicp_hip_map_register_batch", "aicp_hip_multi_create", "aicp_hip_multi_destroy", "aicp_hip_multi_size",
     "aicp_hip_multi_context", "aicp_hip_multi_last_error", "aicp_hip_multi_align_batch",
+    "aicp_hip_reference_cache_stats",
 ]
 
 
@@ -232,6 +233,7 @@ def _load():
     L.aicp_hip_last_sequence_timing.argtypes = [vp, C.POINTER(SequenceTiming)]
     L.aicp_hip_map_register_batch.argtypes = [vp, cfgp, vp, C.c_float, C.c_float, C.POINTER(Cloud), fp, sz, C.c_int,
                                               fp, stp]
+    L.aicp_hip_reference_cache_stats.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.aicp_hip_multi_create.argtypes = [ip, C.c_int, C.POINTER(vp)]
     L.aicp_hip_multi_destroy.argtypes = [vp]
     L.aicp_hip_multi_destroy.restype = None
@@ -417,6 +419,20 @@ class Context:
         st = IcpStats()
         self.check(lib.aicp_hip_register(self.h, C.byref(cfg), C.byref(p), _fptr(outT), C.byref(st)))
         return outT.reshape(4, 4).T.copy(), st.as_dict()
+
+    def overlap(self, ref, read, ref_origin=(0, 0, 0), read_origin=(0, 0, 0), resolution=0.2):
+        """aicp_hip_overlap (computeOverlap + getOverlap for one pair): the overlap in percent."""
+        p, keep = make_pair(ref, read, ref_origin, read_origin)
+        out = np.zeros(1, np.float32)
+        self.check(lib.aicp_hip_overlap(self.h, C.byref(p), float(resolution), _fptr(out)))
+        return float(out[0])
+
+    def reference_cache_stats(self):
+        """aicp_hip_reference_cache_stats: tree hits / builds, overlap-map hits / builds of the
+        one-shot calls' resident reference."""
+        a = (C.c_uint64 * 4)()
+        self.check(lib.aicp_hip_reference_cache_stats(self.h, a))
+        return dict(tree_hits=a[0], tree_builds=a[1], ovl_hits=a[2], ovl_builds=a[3])
 
     def upload(self, pairs):
         return ResidentBatch(self, pairs)

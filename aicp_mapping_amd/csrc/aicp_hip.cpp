@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <deque>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -72,7 +74,7 @@ void pack_xyz(const float* src, uint64_t n, uint64_t stride_bytes, float* dst3) 
 }
 // Strided xyz -> float4 for many clouds at once, split into equal point ranges over host
 // threads (the packing, not the DMA, bounded the host-buffer path: one thread moves ~5 GB/s)
-void pack_many(const std::vector<PackSeg>& segs) {
+void pack_many(const std::vector<PackSeg>& segs, WorkerPool* pool) {
   uint64_t total = 0;
   for (const PackSeg& g : segs) total += g.n;
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -93,10 +95,19 @@ void pack_many(const std::vector<PackSeg>& segs) {
       if (base >= hi) break;
     }
   };
+  if (pool) {  // the context's threads
+    pool->run(nt, [&](size_t t) { work(total * t / nt, total * (t + 1) / nt); });
+    return;
+  }
   std::vector<std::thread> th;
   for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, total * t / nt, total * (t + 1) / nt);
   work(0, total / nt);
   for (auto& x : th) x.join();
+}
+
+WorkerPool* ctx_pool(aicp_hip_ctx* ctx) {
+  if (!ctx->pool) ctx->pool = new WorkerPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+  return ctx->pool;
 }
 
 void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4) {
@@ -129,7 +140,12 @@ int check_cfg(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, int flags) {
 // refs_on_device: every pair has a reference of its own (n_ref points) that the caller writes
 // into B->ref_raw at rdesc[i].ref_off afterwards (the localization batch's map crops); the
 // pairs' ref pointers are then not read.
-int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_batch* B, bool refs_on_device) {
+// skip_refs: the reference points are not needed on the device (the context's cached reference
+// serves every reading of the call): not packed, not uploaded.
+// nosync: the caller synchronises the stream before the pinned staging is written again (a one-shot
+// call does, at its end); otherwise this returns once the copies are done
+int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_batch* B, bool refs_on_device,
+                 bool skip_refs = false, bool skip_reads = false, bool nosync = false) {
   if (!pairs || n == 0) FAIL(AICP_ERR_INVALID, "no pairs");
   B->P = n;
   B->desc.assign(n, PairDesc{});
@@ -215,31 +231,34 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   // raw clouds as float4
   HIPC(ensure(B->ref_raw, ro * 16));
   HIPC(ensure(B->read_raw, wo * 16));
-  HIPC(ensure(ctx->pin_io, ((refs_on_device ? 0 : ro) + wo) * 16));  // references, then readings: the readings are
+  const bool pack_refs = !refs_on_device && !skip_refs;
+  HIPC(ensure(ctx->pin_io, ((pack_refs ? ro : 0) + wo) * 16));  // references, then readings: the readings are
   float* st = ctx->pin_io.as<float>();          // packed while the references' DMA runs
   std::vector<PackSeg> segs;
-  if (!refs_on_device) {
+  if (pack_refs) {
     for (size_t r = 0; r < rep.size(); ++r) {
       const PairDesc& d = B->rdesc[r];
       segs.push_back(PackSeg{pairs[rep[r]].ref, d.n_ref, pairs[rep[r]].ref_stride, st + 4ull * d.ref_off});
     }
-    pack_many(segs);
+    pack_many(segs, ctx_pool(ctx));
     HIPC(hipMemcpyAsync(B->ref_raw.p, st, ro * 16, hipMemcpyHostToDevice, ctx->stream));
   }
-  float* sw = refs_on_device ? st : st + 4ull * ro;
+  float* sw = pack_refs ? st + 4ull * ro : st;
   segs.clear();
   for (size_t i = 0; i < n; ++i) {
     const PairDesc& d = B->desc[i];
     segs.push_back(PackSeg{pairs[i].read, d.n_read, pairs[i].read_stride, sw + 4ull * d.read_off});
   }
-  pack_many(segs);
-  HIPC(hipMemcpyAsync(B->read_raw.p, sw, wo * 16, hipMemcpyHostToDevice, ctx->stream));
+  if (!skip_reads) {  // (skip_reads: the previous call's reading, still on the device)
+    pack_many(segs, ctx_pool(ctx));
+    HIPC(hipMemcpyAsync(B->read_raw.p, sw, wo * 16, hipMemcpyHostToDevice, ctx->stream));
+  }
   // block maps: [read pair][read start][ref pair][ref start][red pair][red start]
   const size_t nr = mr.pair.size(), nf = mf.pair.size(), nd = md.pair.size(), ns = ms.pair.size();
   const size_t words = 2 * (nr + nf + nd + ns);
   HIPC(ensure(B->maps, words * 4));
-  HIPC(hipStreamSynchronize(ctx->stream));
-  uint32_t* mp = ctx->pin_io.as<uint32_t>();
+  HIPC(ensure(ctx->pin_maps, words * 4));  // (staged apart from pin_io, whose copy may still run)
+  uint32_t* mp = ctx->pin_maps.as<uint32_t>();
   size_t o = 0;
   auto put = [&](const Maps& m, BlockMap& bm) {
     const size_t cnt = m.pair.size();
@@ -250,14 +269,12 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     bm.n_blocks = (uint32_t)cnt;
     o += 2 * cnt;
   };
-  HIPC(ensure(ctx->pin_io, words * 4));
-  mp = ctx->pin_io.as<uint32_t>();
   put(mr, B->m_read);
   put(mf, B->m_gref);
   put(md, B->m_red);
   put(ms, B->m_sel);
   HIPC(hipMemcpyAsync(B->maps.p, mp, words * 4, hipMemcpyHostToDevice, ctx->stream));
-  HIPC(hipStreamSynchronize(ctx->stream));
+  if (!nosync) HIPC(hipStreamSynchronize(ctx->stream));
   return AICP_OK;
 }
 
@@ -488,6 +505,7 @@ int overlap_sparse(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, Pai
 // dense voxel maps of one batch beyond this size take the sorted-key path instead (a 60 x 60 x 6 m
 // scene at 0.2 m is ~2.7 MB per map; 8 GiB covers thousands of such clouds)
 constexpr uint64_t kDenseMapBudget = uint64_t(8) << 30;
+constexpr unsigned long long kReadOrderMin = 200000;
 
 bool force_sparse_overlap() {  // AICP_OVL_SPARSE=1: the sorted-key path for every batch (tests)
   const char* e = std::getenv("AICP_OVL_SPARSE");
@@ -499,9 +517,15 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
   hipStream_t s = ctx->stream;
   TCHK(hipSetDevice(ctx->device));
   TCHK(hipEventSynchronize(ctx->ev[1]));
-  if (force_sparse_overlap()) return overlap_sparse(ctx, B, P, G, dDesc, dState, dGst, readS, res, set_ratio, err);
+  RefCache& rc = ctx->refc;
+  const bool hit = rc.hit_ovl;  // the one group's map is the cached reference's (ctx->bitmap[0, rc.od.bytes))
+  if (force_sparse_overlap()) {
+    rc.ovl = false;
+    return overlap_sparse(ctx, B, P, G, dDesc, dState, dGst, readS, res, set_ratio, err);
+  }
   // one map per overlap group (reference side) and one per pair (reading side), each over
-  // the padded key box of that cloud's keys and origin
+  // the padded key box of that cloud's keys and origin; the groups' maps first, so a cached
+  // reference's map keeps its place at offset 0
   uint64_t bm_bytes = 0;
   TCHK(ensure(ctx->pin_ovl, (P + G) * sizeof(OvlDesc)));
   TCHK(ensure(ctx->ovl, (P + G) * sizeof(OvlDesc)));
@@ -521,23 +545,62 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
     return vox <= (1ull << 34);
   };
   bool fits = true;
+  if (hit) {
+    ho[P] = rc.od;
+    bm_bytes = rc.od.bytes;
+  } else {
+    for (size_t g = 0; g < G; ++g) fits &= size_map(ctx->pin_gstate.as<PairState>()[g], ho[P + g]);
+  }
+  const uint64_t ref_bytes = bm_bytes;
   for (size_t i = 0; i < P; ++i) fits &= size_map(ctx->pin_state.as<PairState>()[i], ho[i]);
-  for (size_t g = 0; g < G; ++g) fits &= size_map(ctx->pin_gstate.as<PairState>()[g], ho[P + g]);
   // all maps of the batch at once within half the free device memory (beyond what the arena
   // already holds); otherwise (far outlier points: key boxes of 10^9+ voxels) the sorted-key path
   size_t free_b = 0, total_b = 0;
   TCHK(hipMemGetInfo(&free_b, &total_b));
   const uint64_t limit = std::min<uint64_t>(ctx->bitmap.cap + free_b / 2, kDenseMapBudget);
-  if (!fits || bm_bytes > limit) return overlap_sparse(ctx, B, P, G, dDesc, dState, dGst, readS, res, set_ratio, err);
+  if (!fits || bm_bytes > limit) {  // (a cached group state is in dGst; the sparse path recounts |A|)
+    rc.ovl = false;
+    return overlap_sparse(ctx, B, P, G, dDesc, dState, dGst, readS, res, set_ratio, err);
+  }
+  if (hit && bm_bytes > ctx->bitmap.cap) {  // grow, keeping the cached map
+    DevBuf nb;
+    TCHK(ensure(nb, bm_bytes));
+    TCHK(hipMemcpyAsync(nb.p, ctx->bitmap.p, ref_bytes, hipMemcpyDeviceToDevice, s));
+    TCHK(hipStreamSynchronize(s));
+    release(ctx->bitmap);
+    ctx->bitmap = nb;
+  }
   TCHK(ensure(ctx->bitmap, bm_bytes));
   TCHK(hipMemcpyAsync(ctx->ovl.p, ho, (P + G) * sizeof(OvlDesc), hipMemcpyHostToDevice, s));
   TCHK(hipEventRecord(ctx->ev[6], s));
   uint8_t* bm = ctx->bitmap.as<uint8_t>();
   const OvlDesc* dOvl = ctx->ovl.as<OvlDesc>();
-  TCHK(hipMemsetAsync(bm, 0, bm_bytes, s));
-  launch_ovl_mark(s, B->m_gref, dG, dOvl + P, dGst, B->ref_raw.as<float4>(), 0, res, bm, true);
-  launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm, true);
-  launch_ovl_count(s, (int)P, (int)G, dDesc, dOvl, dOvl + P, dState, dGst, bm);
+  // the marks' LDS cache of stored voxels pays off where many rays share the maps (C5: 66 against
+  // 111 GB written per dispatch); a few clouds mark faster with plain stores (the
+  // stream's measurement)
+  const bool filter = P + G > 8;
+  if (hit) {  // the readings' maps only: the reference's map and |A| are the cached ones
+    TCHK(hipMemsetAsync(bm + ref_bytes, 0, bm_bytes - ref_bytes, s));
+    launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm, filter);
+    launch_ovl_popcount(s, (int)P, dOvl, dState, 1, bm);
+    launch_ovl_intersect(s, (int)P, dDesc, dOvl, dOvl + P, dState, bm);
+    ++rc.ovl_hits;
+  } else {
+    TCHK(hipMemsetAsync(bm, 0, bm_bytes, s));
+    launch_ovl_mark(s, B->m_gref, dG, dOvl + P, dGst, B->ref_raw.as<float4>(), 0, res, bm, filter);
+    launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm, filter);
+    launch_ovl_count(s, (int)P, (int)G, dDesc, dOvl, dOvl + P, dState, dGst, bm);
+    rc.ovl = false;
+    if (rc.use && G == 1) {  // keep the reference's map (offset 0) and its group state for the next call
+      TCHK(ensure(rc.gst, sizeof(PairState)));
+      TCHK(hipMemcpyAsync(rc.gst.p, dGst, sizeof(PairState), hipMemcpyDeviceToDevice, s));
+      rc.ovl = true;
+      rc.od = ho[P];
+      rc.res = res;
+      for (int k = 0; k < 3; ++k) rc.origin[k] = B->gdesc[0].ref_origin[k];
+      ++rc.ovl_builds;
+    }
+  }
   launch_ovl_finish(s, (int)P, dDesc, dState, dGst, set_ratio ? 1 : 0);
   TCHK(hipGetLastError());
   return AICP_OK;
@@ -588,6 +651,12 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   const bool doOvl = flags & AICP_RUN_OVERLAP, doIcp = flags & AICP_RUN_ICP;
   if (doOvl && !(res > 0)) FAIL(AICP_ERR_INVALID, "resolution");
   const size_t P = B->P;
+  RefCache& rcache = ctx->refc;
+  if (!rcache.use) rcache.invalidate();  // (this run rewrites the buffers a cached reference lives in)
+  const bool read_hit = ctx->rdc.hit;
+  if (!read_hit) ctx->rdc.valid = false;  // (read_s is rewritten below; oneshot() re-validates)
+  const bool hit_trees = rcache.use && rcache.hit_trees && doIcp;
+  const bool hit_ovl = rcache.use && rcache.hit_ovl && doOvl;
   hipStream_t s = ctx->stream;
   for (auto& e : ctx->ev)
     if (!e) HIPC(hipEventCreate(&e));
@@ -626,7 +695,17 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   // readings in Morton order inside each pair's range (kernels_order.hip): the overlap and
   // the ICP loop both visit the sorted copy
   const float4* readS = B->read_raw.as<float4>();
-  {
+  // Morton order from kReadOrderMin reading points on (AICP_READ_ORDER_MIN overrides): a single C2
+  // reading's NN launches gain less than its sort costs (the app bench, r05: 1.18-1.25 ms per
+  // overlap + registerClouds without, 1.29-1.37 with)
+  const char* rom = std::getenv("AICP_READ_ORDER_MIN");
+  const bool order = B->total_read >= (rom ? std::strtoull(rom, nullptr, 10) : kReadOrderMin);
+  if (read_hit) {  // the previous one-shot call's reading: its Morton-ordered copy is in read_s
+    if (ctx->rdc.sorted) readS = ctx->read_s.as<float4>();
+  } else if (!order) {
+    ctx->rdc.sorted = false;
+  } else {
+    ctx->rdc.sorted = true;
     const size_t n = B->total_read;
     const size_t tb = read_order_temp_bytes(n, (int)P);
     HIPC(ensure(ctx->read_s, n * 16));
@@ -654,8 +733,12 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     std::memcpy(ctx->pin_gdesc.p, B->gdesc.data(), G * sizeof(PairDesc));
     HIPC(hipMemcpyAsync(dG, ctx->pin_gdesc.p, G * sizeof(PairDesc), hipMemcpyHostToDevice, s));
     launch_ovl_init(s, (int)P, dDesc, dState, res, 2);
-    launch_ovl_init(s, (int)G, dG, dGst, res, 1);
-    launch_ovl_bbox(s, B->m_gref, dG, dGst, B->ref_raw.as<float4>(), 0, res);
+    if (hit_ovl) {  // the cached reference's group state (|A|, key box): its map is kept too
+      HIPC(hipMemcpyAsync(dGst, rcache.gst.p, sizeof(PairState), hipMemcpyDeviceToDevice, s));
+    } else {
+      launch_ovl_init(s, (int)G, dG, dGst, res, 1);
+      launch_ovl_bbox(s, B->m_gref, dG, dGst, B->ref_raw.as<float4>(), 0, res);
+    }
     launch_ovl_bbox(s, B->m_read, dDesc, dState, readS, 1, res);
     HIPC(hipMemcpyAsync(ctx->pin_state.p, dState, P * sizeof(PairState), hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(ctx->pin_gstate.p, dGst, G * sizeof(PairState), hipMemcpyDeviceToHost, s));
@@ -699,7 +782,15 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   };
   if (doOvl && doIcp)
     ovl_thread = std::thread([&] { orc = overlap_maps(ctx, B, P, G, dDesc, dState, dG, dGst, readS, res, true, oerr); });
-  if (doIcp) {
+  if (doIcp && hit_trees) {
+    // the cached reference's centroid, trees, treelets and normals (ctx->rdesc / rstate / bpts /
+    // bnrm / nodes / tl / ptl) serve this call: only the pairs' frames are new (below)
+    ctx->tl_total = rcache.tl_total;
+    dRdesc = ctx->rdesc.as<PairDesc>();
+    dRstate = ctx->rstate.as<PairState>();
+    for (int e : {8, 10, 12, 3}) HIPC(hipEventRecord(ctx->ev[e], s2));
+    ++rcache.tree_hits;
+  } else if (doIcp) {
     HIPC(ensure(ctx->rdesc, R * sizeof(PairDesc)));
     HIPC(ensure(ctx->rstate, R * sizeof(PairState)));
     HIPC(ensure(ctx->pin_rdesc, R * sizeof(PairDesc)));
@@ -786,11 +877,14 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     float4* readc = ctx->read_c.as<float4>();
     const uint4* nodes = ctx->nodes.as<uint4>();
     HIPC(hipStreamWaitEvent(s2, ctx->ev[11], 0));
+    if (hit_trees) launch_pairs_from_refs(s2, (int)P, dDesc, dRdesc);  // (the matcher worker's step)
     launch_prepare_read(s2, B->m_read, dDesc, readS, readc);
-    // normals from the raw tree's bucket order into the matcher tree's bucket order
+    // normals from the raw tree's bucket order into the matcher tree's bucket order (a cached
+    // reference's are there already)
     HIPC(ensure(ctx->inv, B->total_ref * 4));
-    launch_normals_to_matcher(s2, (int)R, (uint32_t)B->total_ref, dRdesc, bpts, ctx->bpts_raw.as<float4>(),
-                              ctx->nrm_raw.as<float4>(), ctx->inv.as<uint32_t>(), bnrm);
+    if (!hit_trees)
+      launch_normals_to_matcher(s2, (int)R, (uint32_t)B->total_ref, dRdesc, bpts, ctx->bpts_raw.as<float4>(),
+                                ctx->nrm_raw.as<float4>(), ctx->inv.as<uint32_t>(), bnrm);
     launch_pairs_degenerate(s2, (int)P, dDesc, dState, dRstate);
     HIPC(hipEventRecord(ctx->ev[4], s2));
     HIPC(hipStreamWaitEvent(s, ctx->ev[4], 0));
@@ -808,7 +902,37 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     for (size_t i = 0; i < P; ++i) reads += B->desc[i].n_read;
     ActiveList* al = ctx->active.as<ActiveList>();
     const int sel_ff = sel_fused_from();
-    for (int it = 0; it < cfg->max_iter; ++it) {
+    // Polled loop (the sequence's, sequence.cpp): from iteration smoothLength on the update of
+    // the last pair writes the next active count into mapped host memory; the host stays one
+    // iteration ahead and stops enqueueing once it reads 0, instead of maxIterationCount launches
+    // of which the ones after convergence are no-ops (~25 us each).
+    if (!ctx->poll_host) {
+      HIPC(hipHostMalloc((void**)&ctx->poll_host, kBatchPolls * 4, hipHostMallocMapped));
+      HIPC(hipHostGetDevicePointer((void**)&ctx->poll_dev, ctx->poll_host, 0));
+    }
+    const char* nee = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
+    const bool early = !(nee && nee[0] == '1');
+    auto polled = [&](int k) { return early && k >= cfg->smooth_length && k < kBatchPolls && k < cfg->max_iter; };
+    std::deque<int> pending;
+    bool stop = false;
+    for (int it = 0; it < cfg->max_iter && !stop; ++it) {
+      // every poll slot before this iteration read: its active count was not 0
+      while (!pending.empty() && pending.front() < it && !stop) {
+        volatile uint32_t* w = ctx->poll_host + pending.front();
+        while (*w == 0xffffffffu) {
+          const hipError_t q = hipStreamQuery(s);
+          if (q == hipErrorNotReady) {
+            std::this_thread::yield();
+            continue;
+          }
+          HIPC(q);
+          std::atomic_thread_fence(std::memory_order_seq_cst);
+          break;  // the stream drained without writing it: the launch that would have had no active pair
+        }
+        stop = *w == 0u || *w == 0xffffffffu;
+        pending.pop_front();
+      }
+      if (stop) break;
       if (it == 0) launch_active_list(s, (int)P, dDesc, dState, al, dCtr);
       prm.prof_slot = nn_launches;
       launch_icp_nn(s, (int)reads, dDesc, dState, al, readc, nodes, ctx->tl_total ? ctx->tl.as<uint4>() : nullptr,
@@ -823,6 +947,11 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       y.st = dState;
       y.al = al;
       y.ctr = dCtr;
+      if (polled(it + 1)) {
+        ctx->poll_host[it + 1] = 0xffffffffu;  // (before the launch that writes it)
+        y.host_n = ctx->poll_dev + it + 1;
+        pending.push_back(it + 1);
+      }
       if (sel_ff > 0 && it >= sel_ff)
         launch_icp_select_fused(s, B->m_sel, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
                                 ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), y);
@@ -851,12 +980,20 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   if (doIcp) HIPC(hipMemcpyAsync(ctx->pin_out.p, ctx->outT.p, P * 64, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(pdC, dDesc, P * sizeof(PairDesc), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
-  if (doIcp) {  // planned tree builds: errors recorded on the device
+  if (doIcp && !hit_trees) {  // planned tree builds: errors recorded on the device
+    rcache.trees = false;
     rc = device_trees_check(ctx->tb[0], ctx->err);
     if (!rc) rc = device_trees_check(ctx->tb[1], ctx->err);
     if (rc) return rc;
     if (ctx->tl_total && (ctx->tb[1].pin_ctl.as<TreeCtl>()->error & 4))
       FAIL(AICP_ERR_HIP, "matcher treelets exceed their allotment");
+    if (rcache.use && R == 1) {  // kept for the next call against the same reference
+      rcache.trees = true;
+      rcache.bucket = cfg->bucket_size;
+      rcache.knn = cfg->knn_normals;
+      rcache.tl_total = ctx->tl_total;
+      ++rcache.tree_builds;
+    }
   }
   // results
   const PairState* hs = ctx->pin_state.as<PairState>();
@@ -919,6 +1056,7 @@ void free_batch(aicp_hip_batch* B) {
 // single-cloud kd-tree on the points as given (no centring) for the kernel-level entry points
 int upload_tree(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t stride, PairDesc& d) {
   hipStream_t s = ctx->stream;
+  ctx->refc.invalidate();  // (ctx->bpts / nodes / bnrm are rewritten)
   HIPC(ensure(ctx->ref1, n * 16));
   HIPC(ensure(ctx->pin_io, n * 16));
   pack_xyz4(pts, n, stride, ctx->pin_io.as<float>());
@@ -991,6 +1129,9 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   release(ctx->ovl_keys);
   release(ctx->isync);
   release(ctx->pin_crop);
+  release(ctx->pin_maps);
+  if (ctx->poll_host) (void)hipHostFree(ctx->poll_host);
+  delete ctx->pool;
   seq_state_free(ctx->seq);
   for (PinBuf* b : {&ctx->pin_desc, &ctx->pin_state, &ctx->pin_out, &ctx->pin_io, &ctx->pin_ovl,
                     &ctx->pin_rdesc, &ctx->pin_gdesc, &ctx->pin_gstate, &ctx->pin_pf})
@@ -1037,22 +1178,127 @@ int aicp_hip_batch_run(aicp_hip_ctx* ctx, aicp_hip_batch* batch, const aicp_icp_
 
 constexpr size_t kOneshotKeepBytes = size_t(1) << 30;
 
-int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
-                         double resolution, int flags, float* out_T, aicp_icp_stats* stats) {
+namespace {
+
+// x, y, z of n points at a byte stride == packed[3 n], byte for byte; split over host threads for
+// large clouds (a C2 reference is ~2 MB to read on every call)
+bool same_points(WorkerPool* pool, const float* pts, uint64_t n, uint64_t stride, const float* packed) {
+  auto cmp = [&](uint64_t a, uint64_t b) {
+    const char* src = reinterpret_cast<const char*>(pts);
+    for (uint64_t i = a; i < b; ++i)
+      if (std::memcmp(src + i * stride, packed + 3 * i, 12) != 0) return false;
+    return true;
+  };
+  const unsigned nt = n < (1u << 16) ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  if (nt == 1) return cmp(0, n);
+  std::vector<char> ok(nt, 1);
+  pool->run(nt, [&](size_t t) { ok[t] = cmp(n * t / nt, n * (t + 1) / nt); });
+  for (char v : ok)
+    if (!v) return false;
+  return true;
+}
+
+// packed[3 n] = x, y, z of n points at a byte stride (the caches' host copies), over the pool
+void copy_points(WorkerPool* pool, const float* pts, uint64_t n, uint64_t stride, float* packed) {
+  auto cp = [&](uint64_t a, uint64_t b) {
+    const char* src = reinterpret_cast<const char*>(pts);
+    for (uint64_t i = a; i < b; ++i) std::memcpy(packed + 3 * i, src + i * stride, 12);
+  };
+  const unsigned nt = n < (1u << 16) ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  if (nt == 1) return cp(0, n);
+  pool->run(nt, [&](size_t t) { cp(n * t / nt, n * (t + 1) / nt); });
+}
+
+// The reference cache's check at the start of a one-shot call (runtime.hpp: RefCache): every pair
+// must pass the same reference array; it is the cached one when (pointer, count, stride) match
+// and its points are byte-identical to the cached copy. Sets what the call reuses; returns
+// whether the reference points need no upload (everything reference-side is cached; the
+// one-shot batch's ref_raw still holds them for a sparse-overlap fallback).
+bool refcache_begin(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n, double res,
+                    int flags) {
+  RefCache& c = ctx->refc;
+  c.use = c.hit_trees = c.hit_ovl = false;
+  if (!pairs || n == 0 || !valid_pair(pairs[0])) return false;
+  const aicp_pair& p = pairs[0];
+  bool one_origin = true;
+  for (size_t i = 1; i < n; ++i) {
+    const aicp_pair& q = pairs[i];
+    if (q.ref != p.ref || q.n_ref != p.n_ref || q.ref_stride != p.ref_stride) {
+      c.invalidate();
+      return false;
+    }
+    for (int k = 0; k < 3; ++k) one_origin &= q.ref_origin[k] == p.ref_origin[k];
+  }
+  const bool same = (c.trees || c.ovl) && c.ptr == p.ref && c.n == p.n_ref && c.stride == p.ref_stride &&
+                    c.pts.size() == 3 * (size_t)p.n_ref && same_points(ctx_pool(ctx), p.ref, p.n_ref, p.ref_stride, c.pts.data());
+  if (!same) {  // a new reference (or the cached one changed in place): rebuilt and kept by this call
+    c.invalidate();
+    c.ptr = p.ref;
+    c.n = p.n_ref;
+    c.stride = p.ref_stride;
+    c.pts.resize(3 * (size_t)p.n_ref);
+    copy_points(ctx_pool(ctx), p.ref, p.n_ref, p.ref_stride, c.pts.data());
+  }
+  c.use = true;
+  const bool icp = flags & AICP_RUN_ICP, ovl = flags & AICP_RUN_OVERLAP;
+  if (same) {
+    c.hit_trees = icp && c.trees && cfg && c.bucket == cfg->bucket_size && c.knn == cfg->knn_normals;
+    c.hit_ovl = ovl && c.ovl && one_origin && c.res == res && c.origin[0] == p.ref_origin[0] &&
+                c.origin[1] == p.ref_origin[1] && c.origin[2] == p.ref_origin[2];
+  }
+  return (!icp || c.hit_trees) && (!ovl || c.hit_ovl);
+}
+
+// register / overlap / align_batch: one-shot batches reuse the context's batch buffers (no device
+// allocation per call) and its reference cache
+int oneshot(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs, double resolution,
+            int flags, float* out_T, aicp_icp_stats* stats, float* out_overlap) {
   if (!ctx) return AICP_ERR_INVALID;
   HIPC(hipSetDevice(ctx->device));
-  // one-shot batches reuse the context's batch buffers (no device allocation per call)
+  if (!(flags & (AICP_RUN_ICP | AICP_RUN_OVERLAP))) FAIL(AICP_ERR_INVALID, "nothing to run");
   if (!ctx->oneshot) ctx->oneshot = new aicp_hip_batch();
   aicp_hip_batch* B = ctx->oneshot;
-  int rc = upload_pairs(ctx, pairs, n_pairs, B, false);
-  if (!rc) rc = aicp_hip_batch_run(ctx, B, cfg, resolution, flags, out_T, stats);
+  const bool skip_refs = refcache_begin(ctx, cfg, pairs, n_pairs, resolution, flags);
+  // the reading of the previous call again (computeOverlap, then registerClouds)?
+  ReadCache& rd = ctx->rdc;
+  const aicp_pair* p0 = n_pairs == 1 && pairs && valid_pair(pairs[0]) ? pairs : nullptr;
+  rd.hit = p0 && rd.valid && rd.ptr == p0->read && rd.n == p0->n_read && rd.stride == p0->read_stride &&
+           rd.pts.size() == 3 * (size_t)p0->n_read &&
+           same_points(ctx_pool(ctx), p0->read, p0->n_read, p0->read_stride, rd.pts.data());
+  int rc = upload_pairs(ctx, pairs, n_pairs, B, false, skip_refs, rd.hit, true);
+  if (!rc) rc = run_batch(ctx, B, cfg, resolution, flags, out_T, stats, out_overlap);
+  ctx->refc.use = false;
+  const bool was_hit = rd.hit;
+  rd.hit = false;
+  if (was_hit) ++rd.hits;
+  if (rc) {
+    ctx->refc.invalidate();  // (an error may leave the reference side half written)
+    (void)hipStreamSynchronize(ctx->stream);  // (the staging copies of upload_pairs are not awaited there)
+  }
+  rd.valid = !rc && p0;
+  if (rd.valid && !was_hit) {  // the reading this call uploaded: its copy for the next call's compare
+    rd.ptr = p0->read;
+    rd.n = p0->n_read;
+    rd.stride = p0->read_stride;
+    rd.pts.resize(3 * (size_t)p0->n_read);
+    copy_points(ctx_pool(ctx), p0->read, p0->n_read, p0->read_stride, rd.pts.data());
+  }
   // the input copies of a very large one-shot batch are not kept for the next call
   if (B->ref_raw.cap + B->read_raw.cap > kOneshotKeepBytes) {
     (void)hipStreamSynchronize(ctx->stream);
     release(B->ref_raw);
     release(B->read_raw);
+    ctx->refc.invalidate();
+    rd.valid = false;
   }
   return rc;
+}
+
+}  // namespace
+
+int aicp_hip_align_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
+                         double resolution, int flags, float* out_T, aicp_icp_stats* stats) {
+  return oneshot(ctx, cfg, pairs, n_pairs, resolution, flags, out_T, stats, nullptr);
 }
 
 int aicp_hip_register_batch(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pairs, size_t n_pairs,
@@ -1067,15 +1313,18 @@ int aicp_hip_register(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_
 
 int aicp_hip_overlap_batch(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs, double resolution,
                            float* out_overlap_percent, aicp_icp_stats* stats) {
-  if (!ctx) return AICP_ERR_INVALID;
-  aicp_hip_batch* B = nullptr;
-  int rc = aicp_hip_batch_upload(ctx, pairs, n_pairs, &B);
-  if (rc) return rc;
   aicp_icp_config cfg;
   aicp_hip_default_config(&cfg);
-  rc = run_batch(ctx, B, &cfg, resolution, AICP_RUN_OVERLAP, nullptr, stats, out_overlap_percent);
-  aicp_hip_batch_free(ctx, B);
-  return rc;
+  return oneshot(ctx, &cfg, pairs, n_pairs, resolution, AICP_RUN_OVERLAP, nullptr, stats, out_overlap_percent);
+}
+
+int aicp_hip_reference_cache_stats(const aicp_hip_ctx* ctx, uint64_t out[4]) {
+  if (!ctx || !out) return AICP_ERR_INVALID;
+  out[0] = ctx->refc.tree_hits;
+  out[1] = ctx->refc.tree_builds;
+  out[2] = ctx->refc.ovl_hits;
+  out[3] = ctx->refc.ovl_builds;
+  return AICP_OK;
 }
 
 int aicp_hip_overlap(aicp_hip_ctx* ctx, const aicp_pair* pair, double resolution, float* out) {
@@ -1399,6 +1648,7 @@ static int pf_layout(aicp_hip_ctx* ctx, size_t n, PfLayout* L) {
 
 // the whole chain on n points already in the layout's pts4 (enqueued on ctx->stream)
 static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n, const PfLayout& Lo, PfRun* o) {
+  ctx->refc.invalidate();  // (the sampled cloud's tree goes to ctx->bpts / nodes)
   hipStream_t s = ctx->stream;
   const int K = prm->normal_k, NB = prm->neighbours;
   for (auto& e : ctx->pf_ev)

@@ -15,6 +15,8 @@
 // (tools/experiments/microbench.hip: with 16 distinct pairs, check+atomicOr bitmaps ran 11x slower.)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "aicp_common.hpp"
 #include "icp_math.hpp"
 #include "kernels.hpp"
@@ -231,19 +233,21 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
   if (err) atomicOr(&st[pair].ovl_err, 1);
 }
 
-// popcounts: |A|, |B|, |A & B| (64 workgroups per pair, integer atomics -> deterministic)
-constexpr int kCountBlocksPerMap = 64;
+// popcounts: |A|, |B|, |A & B| (bpm workgroups per map, integer atomics -> deterministic).
+// count_bpm: 64 per map for batches, more for a few maps (a single reading's ~3 MB map with 64
+// workgroups took 57 us for the intersection, each thread walking 12 words of random lookups)
+inline int count_bpm(int n_maps) { return std::max(64, std::min(512, 2048 / std::max(1, n_maps))); }
 
 // |S| of every map in od[]: byte sums (bytes are 0 or 1; maps 16-byte aligned and padded)
 __global__ __launch_bounds__(256) void k_ovl_popcount(const OvlDesc* __restrict__ od, PairState* st, int slot,
-                                                      const uint8_t* __restrict__ maps) {
-  const int m = blockIdx.x / kCountBlocksPerMap;
-  const int sub = blockIdx.x % kCountBlocksPerMap;
+                                                      const uint8_t* __restrict__ maps, int bpm) {
+  const int m = blockIdx.x / bpm;
+  const int sub = blockIdx.x % bpm;
   const OvlDesc& ov = od[m];
   const uint4* A = (const uint4*)(maps + ov.off);
   const uint64_t n16 = ov.bytes / 16;
   unsigned long long c = 0;
-  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)kCountBlocksPerMap * 256) {
+  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)bpm * 256) {
     const uint4 a = A[w];
     c += __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w);
   }
@@ -256,9 +260,9 @@ __global__ __launch_bounds__(256) void k_ovl_popcount(const OvlDesc* __restrict_
 __global__ __launch_bounds__(256) void k_ovl_intersect(const PairDesc* __restrict__ pd,
                                                        const OvlDesc* __restrict__ od_read,
                                                        const OvlDesc* __restrict__ od_ref, PairState* st,
-                                                       const uint8_t* __restrict__ maps) {
-  const int p = blockIdx.x / kCountBlocksPerMap;
-  const int sub = blockIdx.x % kCountBlocksPerMap;
+                                                       const uint8_t* __restrict__ maps, int bpm) {
+  const int p = blockIdx.x / bpm;
+  const int sub = blockIdx.x % bpm;
   const OvlDesc& rb = od_read[p];
   const OvlDesc& ra = od_ref[pd[p].ogroup];
   const uint4* B = (const uint4*)(maps + rb.off);
@@ -268,7 +272,7 @@ __global__ __launch_bounds__(256) void k_ovl_intersect(const PairDesc* __restric
   const uint32_t d1 = (uint32_t)rb.dim[1], d2 = (uint32_t)rb.dim[2];
   const int o0 = rb.min[0] - ra.min[0], o1 = rb.min[1] - ra.min[1], o2 = rb.min[2] - ra.min[2];
   unsigned long long c = 0;
-  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)kCountBlocksPerMap * 256) {
+  for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)bpm * 256) {
     const uint4 b = B[w];
     if ((b.x | b.y | b.z | b.w) == 0) continue;
     const uint32_t words[4] = {b.x, b.y, b.z, b.w};
@@ -334,16 +338,17 @@ void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDes
 }
 void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
                       const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps) {
-  k_ovl_popcount<<<n_groups * kCountBlocksPerMap, 256, 0, s>>>(od_ref, gst, 0, maps);
-  k_ovl_popcount<<<n_pairs * kCountBlocksPerMap, 256, 0, s>>>(od_read, st, 1, maps);
-  k_ovl_intersect<<<n_pairs * kCountBlocksPerMap, 256, 0, s>>>(pd, od_read, od_ref, st, maps);
+  const int bg = count_bpm(n_groups), bp = count_bpm(n_pairs);
+  k_ovl_popcount<<<n_groups * bg, 256, 0, s>>>(od_ref, gst, 0, maps, bg);
+  k_ovl_popcount<<<n_pairs * bp, 256, 0, s>>>(od_read, st, 1, maps, bp);
+  k_ovl_intersect<<<n_pairs * bp, 256, 0, s>>>(pd, od_read, od_ref, st, maps, bp);
 }
 void launch_ovl_popcount(hipStream_t s, int n, const OvlDesc* od, PairState* st, int slot, const uint8_t* maps) {
-  if (n) k_ovl_popcount<<<n * kCountBlocksPerMap, 256, 0, s>>>(od, st, slot, maps);
+  if (n) k_ovl_popcount<<<n * count_bpm(n), 256, 0, s>>>(od, st, slot, maps, count_bpm(n));
 }
 void launch_ovl_intersect(hipStream_t s, int n_pairs, const PairDesc* pd, const OvlDesc* od_read, const OvlDesc* od_ref,
                           PairState* st, const uint8_t* maps) {
-  if (n_pairs) k_ovl_intersect<<<n_pairs * kCountBlocksPerMap, 256, 0, s>>>(pd, od_read, od_ref, st, maps);
+  if (n_pairs) k_ovl_intersect<<<n_pairs * count_bpm(n_pairs), 256, 0, s>>>(pd, od_read, od_ref, st, maps, count_bpm(n_pairs));
 }
 void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
                        int set_ratio) {

@@ -4,7 +4,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/aicp_hip.h"
@@ -63,6 +68,76 @@ inline void release(PinBuf& b) {
   b.cap = 0;
 }
 
+// A fixed pool of host threads for packing (spawning 16 threads per call costs more than the
+// packing of a C2 cloud: the stream's windows and the one-shot calls of a context share one).
+class WorkerPool {
+ public:
+  explicit WorkerPool(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // fn(task) for task in [0, n), on the pool and the calling thread; returns when all are done
+  // and no worker is inside the task loop any more (so the next run() may reset the counter)
+  void run(size_t n, const std::function<void(size_t)>& fn) {
+    if (n == 0) return;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(mu_);
+    done_cv_.wait(l, [&] { return done_ == n_ && active_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const size_t i = next_.fetch_add(1);
+      if (i >= n_) return;
+      (*fn_)(i);
+      std::lock_guard<std::mutex> l(mu_);
+      if (++done_ == n_) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || (gen_ != seen && fn_ != nullptr); });
+        if (stop_) return;
+        seen = gen_;
+        ++active_;
+      }
+      work();
+      std::lock_guard<std::mutex> l(mu_);
+      if (--active_ == 0 && done_ == n_) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  size_t n_ = 0, done_ = 0;
+  int active_ = 0;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 // Work space of one kd-tree construction (kernels_tree.hip). Two sets: the raw-coordinate
 // tree (SurfaceNormal) and the centred matcher tree are built concurrently on two streams.
 struct TreeBufs {
@@ -105,7 +180,7 @@ struct PackSeg {
 };
 // Strided xyz -> float4 (w = 1) for many clouds at once, split into equal point ranges over
 // up to 16 host threads
-void pack_many(const std::vector<PackSeg>& segs);
+void pack_many(const std::vector<PackSeg>& segs, WorkerPool* pool = nullptr);
 void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4);
 bool valid_pair(const aicp_pair& p);
 double ev_ms(hipEvent_t a, hipEvent_t b);
@@ -128,6 +203,51 @@ int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err);
 int device_trees_check(TreeBufs& T, std::string& err);
 int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean = false);
 int check_cfg(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, int flags);
+
+// The drop-in path's reference cache. App registers reading after reading against one reference
+// (app.cpp:72-73, a new one every reference_update_frequency readings, app.cpp:383-391) and calls
+// computeOverlap + registerClouds per reading (app.cpp:132-135, 205-210): the reference side of a
+// one-shot call (aicp_hip_register / _overlap / _align_batch with one reference array) stays
+// resident in the context and is reused while the next call passes the same reference.
+struct RefCache {
+  // identity: the caller's array (pointer, count, stride), and its points, packed, compared byte
+  // for byte on every call (the caller may rewrite the array in place)
+  const float* ptr = nullptr;
+  uint64_t n = 0, stride = 0;
+  std::vector<float> pts;
+  // ctx->bpts, bnrm, nodes, tl, ptl, rdesc, rstate hold its matcher tree, treelets and normals
+  bool trees = false;
+  int bucket = 0, knn = 0;
+  uint64_t tl_total = 0;
+  // ctx->bitmap[0, od.bytes) holds its voxel map for (origin, res); gst its group state (|A|, key box)
+  bool ovl = false;
+  double origin[3] = {0, 0, 0};
+  double res = 0;
+  OvlDesc od{};
+  DevBuf gst;
+  // this call
+  bool use = false;  // the call may reuse / record (one reference array, a one-shot call)
+  bool hit_trees = false, hit_ovl = false;
+  uint64_t tree_hits = 0, tree_builds = 0, ovl_hits = 0, ovl_builds = 0;
+  void invalidate() {
+    trees = ovl = false;
+    hit_trees = hit_ovl = use = false;
+  }
+};
+
+// The reading of the last one-shot call (one pair): App passes the same reading to
+// computeOverlap and then to registerClouds (app.cpp:132-135, 205-210), so the second call reuses
+// its upload and Morton order (the one-shot batch's read_raw, ctx->read_s) when the array is the
+// same and its points are byte-identical.
+struct ReadCache {
+  const float* ptr = nullptr;
+  uint64_t n = 0, stride = 0;
+  std::vector<float> pts;
+  bool valid = false;
+  bool sorted = false;  // its Morton order is in read_s (else the one-shot batch's read_raw serves)
+  bool hit = false;  // this call
+  uint64_t hits = 0;
+};
 
 struct SeqState;  // sequence.cpp
 void seq_state_free(SeqState* s);
@@ -180,7 +300,14 @@ struct aicp_hip_ctx {
   aicp::rt::DevBuf ovl_sp, ovl_keys;   // sparse overlap: clouds, counts, offsets / key words
   aicp::rt::DevBuf isync;              // fused ICP iteration: arrival counters (icp_sync_words)
   aicp::rt::PinBuf pin_crop;
+  aicp::rt::PinBuf pin_maps;  // upload_pairs' block maps
+  aicp::rt::RefCache refc;  // the drop-in path's resident reference (runtime.hpp)
+  aicp::rt::ReadCache rdc;  // and its last reading
+  aicp::rt::WorkerPool* pool = nullptr;  // host threads of the one-shot calls (packing, the reference compare)
+  uint32_t* poll_host = nullptr;  // the batch loop's active counts (hipHostMalloc, mapped), kBatchPolls words
+  uint32_t* poll_dev = nullptr;
 };
+constexpr int kBatchPolls = 64;
 
 #define HIPC(x)                                                                   \
   do {                                                                            \

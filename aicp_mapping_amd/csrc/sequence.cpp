@@ -67,76 +67,6 @@ using namespace aicp::rt;
 namespace aicp {
 namespace rt {
 
-// A fixed pool of host threads for packing (spawning 16 threads per window costs more than the
-// packing of a window's readings).
-class WorkerPool {
- public:
-  explicit WorkerPool(unsigned n) {
-    for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
-  }
-  ~WorkerPool() {
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  // fn(task) for task in [0, n), on the pool and the calling thread; returns when all are done
-  // and no worker is inside the task loop any more (so the next run() may reset the counter)
-  void run(size_t n, const std::function<void(size_t)>& fn) {
-    if (n == 0) return;
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      fn_ = &fn;
-      n_ = n;
-      next_.store(0);
-      done_ = 0;
-      ++gen_;
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> l(mu_);
-    done_cv_.wait(l, [&] { return done_ == n_ && active_ == 0; });
-    fn_ = nullptr;
-  }
-
- private:
-  void work() {
-    for (;;) {
-      const size_t i = next_.fetch_add(1);
-      if (i >= n_) return;
-      (*fn_)(i);
-      std::lock_guard<std::mutex> l(mu_);
-      if (++done_ == n_) done_cv_.notify_all();
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> l(mu_);
-        cv_.wait(l, [&] { return stop_ || (gen_ != seen && fn_ != nullptr); });
-        if (stop_) return;
-        seen = gen_;
-        ++active_;
-      }
-      work();
-      std::lock_guard<std::mutex> l(mu_);
-      if (--active_ == 0 && done_ == n_) done_cv_.notify_all();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(size_t)>* fn_ = nullptr;
-  size_t n_ = 0, done_ = 0;
-  int active_ = 0;
-  std::atomic<size_t> next_{0};
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
-
 // A captured launch sequence (hipGraph) replayed while its key -- every argument and buffer
 // address it was captured with -- stays the same: one graph launch instead of ~100 kernel
 // launches per kd-tree build, ~160 per ICP loop (the host cost of those launches, ~5 us each,

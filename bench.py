@@ -9,13 +9,14 @@ step = one aicp_hip_sequence_run over the 64 host clouds: H2D, every device phas
 of T are inside the timed region (§8(d): host xyz in -> T out). Each rank runs its own stream
 (weak scaling); RCCL all-gathers the per-reading {T, iterations, inlier ratio}.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|single|prefilter]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|single|app|prefilter]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Other configs: c3 (KITTI HDL-64 stream, N = 600 000), c4 (localization against a resident
 1 M-point map, device crops as references, r = 0.5), c5 (1024 independent pairs of 60 000 points
-sharded i mod G), single (one C2 pair through aicp_hip_register, latency), prefilter (§8(f)
-rank 2). The line carries the NN kernel's roofline (HIP events on its stream), the oracle as
+sharded i mod G), single (one C2 pair through aicp_hip_register, latency), app (the C2 readings
+through App's per-reading calls, overlap + registerClouds, with the reference cache), prefilter
+(§8(f) rank 2). The line carries the NN kernel's roofline (HIP events on its stream), the oracle as
 cpu_baseline (median of 5 bounded samples on this host) and parity against it.
 """
 from __future__ import annotations
@@ -750,12 +751,107 @@ def bench_single(args):
     ctx.close()
 
 
+def bench_app(args):
+    """The drop-in path as App drives it (app.cpp:282-414 robot mode, through the shim of
+    INTEGRATION.md): per reading computeOverlap (aicp_hip_overlap), the auto-tuned ratio
+    (app.cpp:197-205), registerClouds (aicp_hip_register), the max-correction drop
+    (app.cpp:366-373), and every 5th accepted reading, corrected by getOutputReading
+    (aicp_hip_transform), becomes the reference with its corrected pose as origin
+    (app.cpp:375-391). Host xyz in, T out, one call at a time: the reference side stays resident
+    between the calls of a window (aicp_hip_reference_cache_stats). Reports the per-reading latency
+    of window readings 2..5 (reference reused) and of the window's first reading (reference
+    built), and aligned clouds/s over the whole stream."""
+    import aicp_mapping_amd._lib as L
+    from aicp_mapping_amd import registration as R
+    from aicp_mapping_amd import synthetic as sy
+
+    n_read = args.pairs or 64
+    n_pts = args.points or 120000
+    st = make_stream(n_read, n_pts, seed=1)
+    ctx = L.Context(0)
+    res = float(np.float32(0.2))
+    max_corr = 1.0
+
+    split = []  # reused-reference readings: overlap call, register call, the register's phases
+
+    def run():
+        ref, ref_o = st.first, np.asarray(st.first_origin, np.float64)
+        acc = 0
+        lat, first_lat, Ts, its = [], [], [], []
+        for i, (r, o) in enumerate(zip(st.readings, st.origins)):
+            t = time.perf_counter()
+            ov = ctx.overlap(ref, r, ref_o, o, res)
+            t1 = time.perf_counter()
+            cfg = L.default_config(trimmed_ratio=L.autotune_ratio(ov))
+            T, s1 = ctx.register(ref, r, cfg)
+            t2 = time.perf_counter()
+            dt = t2 - t
+            (first_lat if acc == 0 else lat).append(dt)
+            if acc:
+                split.append((t1 - t, t2 - t1, ctx.last_phase_ms()))
+            Ts.append(T)
+            its.append(s1["iterations"])
+            if np.linalg.norm(T[:3, 3]) > max_corr:  # dropped (app.cpp:366-373)
+                continue
+            acc += 1
+            if acc == args.ref_every:  # the corrected reading becomes the reference (app.cpp:375-391)
+                ref = ctx.transform(T, r)
+                ref_o = (R.isometry_from_matrix4f(T) @ np.r_[np.asarray(o, np.float64), 1.0])[:3]
+                acc = 0
+        return lat, first_lat, Ts, its
+
+    for _ in range(args.warmup):
+        run()
+    c0 = ctx.reference_cache_stats()
+    t0 = time.perf_counter()
+    lat, first_lat = [], []
+    for _ in range(args.steps):
+        l, f, Ts, its = run()
+        lat += l
+        first_lat += f
+    elapsed = time.perf_counter() - t0
+    c1 = ctx.reference_cache_stats()
+    value = n_read * args.steps / elapsed
+    line = base_line(args, 1, METRIC + " -- drop-in call path (overlap + registerClouds per reading)", value,
+                     "aligned clouds/s", 1e3 * elapsed / args.steps, DTYPE, DATA,
+                     {"workload": "C2 readings through App's per-reading calls (aicp_hip_overlap + aicp_hip_register, "
+                                  "reference = every %dth accepted reading corrected by aicp_hip_transform), N=M=%d, "
+                                  "%d readings" % (args.ref_every, n_pts, n_read),
+                      "chain": CHAIN, "timed_region": "host xyz -> overlap -> ratio -> registerClouds -> T, per call"},
+                     scaling="strong")
+    line.update({
+        "reading_ms_reference_reused": {"median": round(1e3 * float(np.median(lat)), 3),
+                                        "p90": round(1e3 * float(np.percentile(lat, 90)), 3), "n": len(lat)},
+        "reading_ms_reference_built": {"median": round(1e3 * float(np.median(first_lat)), 3), "n": len(first_lat)},
+        "reference_cache": {k: int(c1[k] - c0[k]) for k in c1},
+        "reused_split_ms": {"overlap_call": round(1e3 * float(np.median([x[0] for x in split])), 3),
+                            "register_call": round(1e3 * float(np.median([x[1] for x in split])), 3),
+                            "register_icp_loop_device": round(float(np.median([x[2]["icp_loop"] for x in split])), 3)},
+        "mean_iterations": float(np.mean(its)),
+    })
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as po
+
+        po.lib()
+        k = min(6, n_read)
+        ref = po.sequence(st.first, st.first_origin, st.readings[:k], st.origins[:k], reference_update_frequency=
+                          args.ref_every, resolution=res)
+        pe = [sy.rot_err(x["T"], Ts[i]) for i, x in enumerate(ref)]
+        line["parity_vs_oracle"] = {"readings": k, "max_rot_rad": max(e[0] for e in pe),
+                                    "max_trans_m": max(e[1] for e in pe),
+                                    "iterations_equal": all(x["stats"].iterations == its[i] for i, x in enumerate(ref)),
+                                    "tol": [1e-6, 1e-5]}
+    print(json.dumps(line))
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "single", "prefilter"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "single", "app", "prefilter"], default="c2",
                     help="BASELINE.json workload (default c2: the metric's configuration)")
     ap.add_argument("--pairs", type=int, default=None, help="readings (pairs) per step per GPU")
     ap.add_argument("--ref-every", type=int, default=5, help="reference_update_frequency")
@@ -777,6 +873,8 @@ def main():
         return bench_c4(args)
     if args.config == "c5":
         return bench_c5(args)
+    if args.config == "app":
+        return bench_app(args)
     return bench_single(args)
 
 

@@ -132,6 +132,18 @@ int aicp_hip_overlap(aicp_hip_ctx* ctx, const aicp_pair* pair, double resolution
 int aicp_hip_overlap_batch(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n_pairs,
                            double resolution, float* out_overlap_percent /* n */,
                            aicp_icp_stats* stats /* n, nullable: overlap_keys */);
+/* Reference cache of the one-shot calls above (register*, overlap*, align_batch). App registers
+ * reading after reading against one reference (app.cpp:72-73; a new one every
+ * reference_update_frequency readings, app.cpp:383-391) and calls computeOverlap then
+ * registerClouds per reading (app.cpp:132-135, 205-210). When every pair of a call passes the same
+ * reference array as the previous call -- (pointer, count, stride) equal and the points
+ * byte-identical to a copy the context keeps -- the reference's centroid, kd-trees, treelets and
+ * normals (ICP), and its voxel map for the same origin and resolution (overlap), stay resident in
+ * the context and are reused; the reference is not uploaded again. Any other call that rewrites
+ * those buffers (a batch with several references, the kernel-level entry points, the
+ * pre-filter) drops the cache. Results are the same as without it.
+ * out: tree hits, tree builds, overlap-map hits, overlap-map builds since the context's creation. */
+int aicp_hip_reference_cache_stats(const aicp_hip_ctx* ctx, uint64_t out[4]);
 /* App::runAicpPipeline hot path (app.cpp:218-247): overlap -> auto-tuned ratio -> ICP,
  * all on device, one launch sequence for the whole batch. cfg->trimmed_ratio is ignored
  * when flags has AICP_RUN_OVERLAP. */
