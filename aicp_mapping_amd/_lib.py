@@ -42,6 +42,9 @@ EXPORTS = [
 ]
 
 
+_NEWEST = {"aicp_hip_reference_cache_stats"}  # added in r05
+
+
 class IcpConfig(C.Structure):
     _fields_ = [
         ("knn_normals", C.c_int32),
@@ -172,7 +175,8 @@ def _load():
             "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
     L = C.CDLL(LIB_PATH)
     for name in EXPORTS:
-        if not hasattr(L, name):
+        # (an AICP_HIP_LIB override may be an older build in an A/B run: the newest entry points only)
+        if not hasattr(L, name) and not (os.environ.get("AICP_HIP_LIB") and name in _NEWEST):
             raise ImportError(f"{LIB_PATH} does not export {name}")
     vp = C.c_void_p
     fp = C.POINTER(C.c_float)
@@ -233,7 +237,8 @@ def _load():
     L.aicp_hip_last_sequence_timing.argtypes = [vp, C.POINTER(SequenceTiming)]
     L.aicp_hip_map_register_batch.argtypes = [vp, cfgp, vp, C.c_float, C.c_float, C.POINTER(Cloud), fp, sz, C.c_int,
                                               fp, stp]
-    L.aicp_hip_reference_cache_stats.argtypes = [vp, C.POINTER(C.c_uint64)]
+    if hasattr(L, "aicp_hip_reference_cache_stats"):
+        L.aicp_hip_reference_cache_stats.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.aicp_hip_multi_create.argtypes = [ip, C.c_int, C.POINTER(vp)]
     L.aicp_hip_multi_destroy.argtypes = [vp]
     L.aicp_hip_multi_destroy.restype = None

@@ -399,6 +399,12 @@ int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err) {
   while (used < kFarStack + 1 && hctl->nseg[used]) ++used;
   // oversized segments at the last planned level: plan deeper next time
   T.needed = hctl->n_big ? std::min(kFarStack - 3, T.planned + 2) : used;
+  if (prof_enabled()) {
+    std::fprintf(stderr, "[aicp tree] planned %d used %d next %d: n_big %u n_mid %u n_small %u segments/level", T.planned,
+                 used, T.needed, hctl->n_big, hctl->n_mid, hctl->n_small);
+    for (int l = 0; l < used; ++l) std::fprintf(stderr, " %u", hctl->nseg[l]);
+    std::fprintf(stderr, "\n");
+  }
   if (hctl->error & 1) TFAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
   if (hctl->error & ~4) TFAIL(AICP_ERR_HIP, "kd-tree construction overflow " + std::to_string(hctl->error));
   return AICP_OK;
@@ -582,8 +588,8 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
   if (hit) {  // the readings' maps only: the reference's map and |A| are the cached ones
     TCHK(hipMemsetAsync(bm + ref_bytes, 0, bm_bytes - ref_bytes, s));
     launch_ovl_mark(s, B->m_read, dDesc, dOvl, dState, readS, 1, res, bm, filter);
-    launch_ovl_popcount(s, (int)P, dOvl, dState, 1, bm);
-    launch_ovl_intersect(s, (int)P, dDesc, dOvl, dOvl + P, dState, bm);
+    launch_ovl_popcount(s, (int)P, dOvl, dState, 1, bm, P == 1);
+    launch_ovl_intersect(s, (int)P, dDesc, dOvl, dOvl + P, dState, bm, P == 1);
     ++rc.ovl_hits;
   } else {
     TCHK(hipMemsetAsync(bm, 0, bm_bytes, s));

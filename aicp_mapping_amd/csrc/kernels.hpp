@@ -200,9 +200,11 @@ void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDes
 void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
                       const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps);
 // the parts of launch_ovl_count: |S| of n maps into st[i].ovl_counts[slot]; |A∩B| per pair
-void launch_ovl_popcount(hipStream_t s, int n, const OvlDesc* od, PairState* st, int slot, const uint8_t* maps);
+// wide: many workgroups per map (the one-shot call of a single pair)
+void launch_ovl_popcount(hipStream_t s, int n, const OvlDesc* od, PairState* st, int slot, const uint8_t* maps,
+                         bool wide = false);
 void launch_ovl_intersect(hipStream_t s, int n_pairs, const PairDesc* pd, const OvlDesc* od_read, const OvlDesc* od_ref,
-                          PairState* st, const uint8_t* maps);
+                          PairState* st, const uint8_t* maps, bool wide = false);
 void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
                        int set_ratio);
 

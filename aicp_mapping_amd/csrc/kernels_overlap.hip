@@ -236,7 +236,12 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
 // popcounts: |A|, |B|, |A & B| (bpm workgroups per map, integer atomics -> deterministic).
 // count_bpm: 64 per map for batches, more for a few maps (a single reading's ~3 MB map with 64
 // workgroups took 57 us for the intersection, each thread walking 12 words of random lookups)
-inline int count_bpm(int n_maps) { return std::max(64, std::min(512, 2048 / std::max(1, n_maps))); }
+// Only the one-shot call of a single pair takes the wide form (wide = true): on the stream the
+// counts run beside the window's kd-tree builds, and 409 workgroups per map there slowed the
+// critical normals chain (ref -> normals 0.79-0.82 against 0.77 ms, r05 same-box A/B).
+inline int count_bpm(int n_maps, bool wide) {
+  return wide ? std::max(64, std::min(512, 2048 / std::max(1, n_maps))) : 64;
+}
 
 // |S| of every map in od[]: byte sums (bytes are 0 or 1; maps 16-byte aligned and padded)
 __global__ __launch_bounds__(256) void k_ovl_popcount(const OvlDesc* __restrict__ od, PairState* st, int slot,
@@ -338,17 +343,21 @@ void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDes
 }
 void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
                       const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps) {
-  const int bg = count_bpm(n_groups), bp = count_bpm(n_pairs);
+  const bool wide = n_pairs + n_groups <= 2;  // (the one-shot call of one pair)
+  const int bg = count_bpm(n_groups, wide), bp = count_bpm(n_pairs, wide);
   k_ovl_popcount<<<n_groups * bg, 256, 0, s>>>(od_ref, gst, 0, maps, bg);
   k_ovl_popcount<<<n_pairs * bp, 256, 0, s>>>(od_read, st, 1, maps, bp);
   k_ovl_intersect<<<n_pairs * bp, 256, 0, s>>>(pd, od_read, od_ref, st, maps, bp);
 }
-void launch_ovl_popcount(hipStream_t s, int n, const OvlDesc* od, PairState* st, int slot, const uint8_t* maps) {
-  if (n) k_ovl_popcount<<<n * count_bpm(n), 256, 0, s>>>(od, st, slot, maps, count_bpm(n));
+void launch_ovl_popcount(hipStream_t s, int n, const OvlDesc* od, PairState* st, int slot, const uint8_t* maps,
+                         bool wide) {
+  if (n) k_ovl_popcount<<<n * count_bpm(n, wide), 256, 0, s>>>(od, st, slot, maps, count_bpm(n, wide));
 }
 void launch_ovl_intersect(hipStream_t s, int n_pairs, const PairDesc* pd, const OvlDesc* od_read, const OvlDesc* od_ref,
-                          PairState* st, const uint8_t* maps) {
-  if (n_pairs) k_ovl_intersect<<<n_pairs * count_bpm(n_pairs), 256, 0, s>>>(pd, od_read, od_ref, st, maps, count_bpm(n_pairs));
+                          PairState* st, const uint8_t* maps, bool wide) {
+  if (n_pairs)
+    k_ovl_intersect<<<n_pairs * count_bpm(n_pairs, wide), 256, 0, s>>>(pd, od_read, od_ref, st, maps,
+                                                                      count_bpm(n_pairs, wide));
 }
 void launch_ovl_finish(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const PairState* gst,
                        int set_ratio) {
