@@ -69,11 +69,35 @@ struct PairDesc {
 // Kept apart from PairDesc so the overlap (its own stream) never rewrites descriptors the
 // kd-tree stream is filling in.
 struct OvlDesc {
-  int32_t min[3];   // key of voxel (0,0,0)
-  int32_t dim[3];   // box extent in voxels
+  int32_t min[3];   // key of voxel (0,0,0), a multiple of the brick extent on each axis
+  int32_t dim[3];   // box extent in voxels, a multiple of the brick extent on each axis
   uint64_t off;     // byte offset of this cloud's map in the map arena
-  uint64_t bytes;   // map bytes (multiple of 16)
+  uint64_t bytes;   // map bytes (multiple of 128)
 };
+
+// Maps are bricked: 8 x 8 x 2 voxels (key axes 0, 1, 2) per 128-byte brick, bricks in (0, 1, 2)
+// row-major order, voxels inside a brick at ((a & 7) << 4) | ((b & 7) << 1) | (c & 1). A ray
+// crosses a brick in several steps, so its marks land on ~1/8 of the 128-byte lines a linear
+// layout (a new line for every step along axis 0 or 1) has them on, and the lines of a scan's
+// near-sensor voxels are shared by more rays. Boxes start on brick boundaries of the key lattice,
+// so the 16-byte word s of a brick holds the same voxels (a & 7 = s) in every map.
+constexpr int kOvlBrick0 = 8, kOvlBrick1 = 8, kOvlBrick2 = 2, kOvlBrickBytes = 128;
+// the padded box of keys [lo, hi] (lo > hi: empty) on one axis of brick extent b
+__host__ __device__ inline void ovl_axis(int lo, int hi, int b, int32_t& mn, int32_t& dim) {
+  if (lo > hi) lo = hi = 0;  // nothing inside the key range
+  const int l = lo - 2, h = hi + 3;  // two voxels of padding below, two above (exclusive end + 1)
+  mn = (int32_t)((l >= 0 ? l / b : -((-l + b - 1) / b)) * b);
+  dim = (int32_t)(((h - mn) + b - 1) / b * b);
+}
+// map bytes of a box (the bricks cover it exactly)
+__host__ __device__ inline uint64_t ovl_bytes(const int32_t dim[3]) {
+  return (uint64_t)dim[0] * (uint64_t)dim[1] * (uint64_t)dim[2];
+}
+// byte of the voxel at box coordinates (a, b, c), 0 <= a < dim[0] ...
+__host__ __device__ inline uint64_t ovl_index(uint32_t a, uint32_t b, uint32_t c, uint32_t dim1, uint32_t dim2) {
+  const uint64_t brick = ((uint64_t)(a >> 3) * (dim1 >> 3) + (b >> 3)) * (dim2 >> 1) + (c >> 1);
+  return brick * kOvlBrickBytes + (((a & 7u) << 4) | ((b & 7u) << 1) | (c & 1u));
+}
 
 // One cloud of the sparse overlap path (kernels_overlap_sparse.hip): an overlap group's reference
 // (side 0, points in ref_raw) or a pair's reading (side 1, points in the sorted readings).

@@ -348,9 +348,11 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
 // `plan` global levels without any host read-back (the whole build is asynchronous) plus an
 // async copy of the control block, checked after the batch by device_trees_check; plan = 0:
 // the host polls the next level's segment count from level 4 on (fallback when a planned
-// build turned out too shallow).
+// build turned out too shallow). levels_done (optional) is recorded after the global levels and
+// the mid-size segments, before the subtree kernels.
 int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst, bool copy_ctl) {
+                     int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst, bool copy_ctl,
+                     hipEvent_t levels_done) {
   const size_t n = (size_t)total;
   const TreeWork& w = T.tw;
   float4* bpts = bpts_out.as<float4>();
@@ -361,6 +363,7 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
     for (int level = 0; level < plan; ++level)
       TCHK(launch_tree_level(s, level, (uint32_t)n, w, bpts, bucket, level == plan - 1));
     TCHK(launch_tree_mid(s, (uint32_t)n, w, bpts, bucket));
+    if (levels_done) TCHK(hipEventRecord(levels_done, s));
     TCHK(launch_tree_subtrees(s, (uint32_t)n, w, bpts, bucket));
     TCHK(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
     if (copy_ctl) TCHK(hipMemcpyAsync(hctl, w.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s));
@@ -378,6 +381,7 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
   }
   if (!done) TFAIL(AICP_ERR_UNSUPPORTED, "kd-tree deeper than the device stack (48 levels)");
   TCHK(launch_tree_mid(s, (uint32_t)n, w, bpts, bucket));
+  if (levels_done) TCHK(hipEventRecord(levels_done, s));
   TCHK(launch_tree_subtrees(s, (uint32_t)n, w, bpts, bucket));
   TCHK(launch_tree_finish(s, (int)P, (uint32_t)n, dDesc, w, nodes_out.as<uint4>()));
   TCHK(hipMemcpyAsync(&hctl->error, &w.ctl->error, 4, hipMemcpyDeviceToHost, s));
@@ -537,15 +541,10 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
   TCHK(ensure(ctx->ovl, (P + G) * sizeof(OvlDesc)));
   OvlDesc* ho = ctx->pin_ovl.as<OvlDesc>();
   auto size_map = [&](const PairState& hs, OvlDesc& o) -> bool {
-    uint64_t vox = 1;
-    for (int k = 0; k < 3; ++k) {
-      int lo = hs.ovl_bbox[k], hi = hs.ovl_bbox[3 + k];
-      if (lo > hi) lo = hi = 0;  // nothing inside the key range
-      o.min[k] = lo - 2;
-      o.dim[k] = (hi - lo) + 5;
-      vox *= (uint64_t)o.dim[k];
-    }
-    o.bytes = (vox + 15) / 16 * 16;
+    const int br[3] = {kOvlBrick0, kOvlBrick1, kOvlBrick2};
+    for (int k = 0; k < 3; ++k) ovl_axis(hs.ovl_bbox[k], hs.ovl_bbox[3 + k], br[k], o.min[k], o.dim[k]);
+    const uint64_t vox = ovl_bytes(o.dim);
+    o.bytes = vox;
     o.off = bm_bytes;
     bm_bytes += o.bytes;
     return vox <= (1ull << 34);
@@ -614,13 +613,14 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
 
 // the centred reference's matcher tree and the pairs' frames, on stream3 (worker thread)
 int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dDesc, PairDesc* dRdesc,
-                  int plan, std::string& err) {
+                  int plan, std::string& err, hipEvent_t after = nullptr) {
   hipStream_t s3 = ctx->stream3;
   const size_t R = B->rdesc.size();
   TCHK(hipSetDevice(ctx->device));  // the current device is per host thread
   TCHK(hipStreamWaitEvent(s3, ctx->ev[7], 0));
   TCHK(hipEventRecord(ctx->ev[12], s3));
   TCHK(hipMemcpyAsync(dRdesc, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s3));
+  if (after) TCHK(hipStreamWaitEvent(s3, after, 0));  // the raw tree first (raw_tree_first())
   int rc = device_trees_begin(ctx->tb[1], err, s3, R, B->total_ref, dRdesc, B->ref_raw.as<float4>(), 1, bucket,
                               ctx->bpts, ctx->nodes);
   if (rc) return rc;
@@ -641,6 +641,32 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
   launch_pairs_from_refs(s3, (int)B->P, dDesc, dRdesc);
   TCHK(hipEventRecord(ctx->ev[3], s3));
   return AICP_OK;
+}
+
+// AICP_RAW_FIRST=0/1 forces the order; by default batches of >= 4 M reference points build the
+// raw tree first
+bool raw_tree_first(uint64_t total_ref) {
+  static const int v = [] {
+    const char* e = std::getenv("AICP_RAW_FIRST");
+    return e ? std::atoi(e) : -1;
+  }();
+  return v >= 0 ? v > 0 : total_ref >= (4ull << 20);
+}
+
+// With the raw tree first, the matcher tree starts when the raw tree's global levels and mid-size
+// segments are done (2, default: its bandwidth-bound levels beside the raw tree's latency-bound
+// subtree kernel) or when the whole raw tree is (AICP_RAW_FIRST_AT=1: the normals' kNN, launched
+// at the same time, then holds every wave slot and the matcher kernels wait behind it). C5, same
+// box, alternating: 3578 / 3494 (2) against 3409 / 3265 (1) and 3244 / 3352 clouds/s (both trees
+// together). Also measured: the normals' kNN waiting for the matcher tree's mid-size segments
+// (k_tr_mid needs most of a CU's LDS per workgroup and starves behind the persistent kNN):
+// 3420 / 3368 against 3495 / 3433.
+int raw_first_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("AICP_RAW_FIRST_AT");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
 }
 
 double ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -829,7 +855,13 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     // s3 (worker thread; it still polls its levels in a polled redo): centroid, centred
     // reference, matcher tree, pair frames
     const int plan1 = plan_levels(n_ref_max, ctx->tb[1]);
-    worker = std::thread([&, plan1] { wrc = matcher_trees(ctx, B, cfg->bucket_size, dDesc, dRdesc, plan1, werr); });
+    // Large batches build the raw tree first and the matcher tree beside the normals' kNN
+    // (raw_tree_first()): the raw tree gates the kNN, which gates the loop, while the matcher
+    // tree is needed only by the loop; built together, the two trees' latency-bound subtree
+    // kernels share the CUs' wave slots and both finish late.
+    const bool raw_first = raw_tree_first(B->total_ref);
+    if (!raw_first)
+      worker = std::thread([&, plan1] { wrc = matcher_trees(ctx, B, cfg->bucket_size, dDesc, dRdesc, plan1, werr); });
     // SurfaceNormal runs on the reference as given, before the centring (ICP::compute,
     // SURVEY A.1 steps 1-2): its own libnabo tree over the raw coordinates first
     rc = device_trees_begin(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(),
@@ -837,9 +869,16 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     if (rc) return join_worker(rc);
     // s2: raw tree levels + subtrees, SurfaceNormal, all enqueued before the host waits for
     // the overlap's key boxes
+    const int rf = raw_first_mode();
     rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), kNormalsBucket,
-                          ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0], true));
+                          ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0], true), nullptr, true,
+                          raw_first && rf == 2 ? ctx->ev[13] : nullptr);
     if (rc) return join_worker(rc);
+    if (raw_first) {
+      if (rf != 2) HIPC(hipEventRecord(ctx->ev[13], s2));
+      worker = std::thread(
+          [&, plan1] { wrc = matcher_trees(ctx, B, cfg->bucket_size, dDesc, dRdesc, plan1, werr, ctx->ev[13]); });
+    }
     // normals on the raw tree (bucket order of that tree)
     HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
@@ -968,9 +1007,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
                           ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>(), prm, y);
     }
     launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
-    if (prof_enabled()) {  // diagnostic builds' counters (AICP_XCD_PROF / AICP_NN_PROF)
+    if (prof_enabled()) {  // diagnostic builds' counters (AICP_XCD_PROF / AICP_NN_PROF / AICP_ITER_PROF)
       HIPC(hipStreamSynchronize(s));
       nn_prof_dump();
+      tree_prof_dump();
     }
   } else {
     HIPC(hipEventRecord(ctx->ev[8], s));

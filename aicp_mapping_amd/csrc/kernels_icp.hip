@@ -823,6 +823,14 @@ __device__ __forceinline__ void coop_bucket(Eng& t, bool act, const float4* __re
 #if AICP_XCD_PROF
 __device__ unsigned long long g_xcd_prof[64 * kXcdGroups * 2];
 #endif
+#ifndef AICP_QLAT_PROF
+#define AICP_QLAT_PROF 0  // diagnostic builds: per-query NN latency / completion-time histograms
+#endif
+#if AICP_QLAT_PROF
+// [0, 256): query latency (pick-up to result, 1 us bins); [256, 512): completion time of the
+// query after its wave's start (1 us bins); last bin of each half = overflow
+__device__ unsigned long long g_qlat[512];
+#endif
 #ifndef AICP_NN_PROF
 #define AICP_NN_PROF 0  // diagnostic builds: per-phase s_memtime cycles of the persistent waves
 #endif
@@ -1577,8 +1585,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
                                                 uint32_t* ctr, IcpParams prm) {
   const uint32_t total = al->total;
   if (total == 0) return;
-#if AICP_XCD_PROF
+#if AICP_XCD_PROF || AICP_QLAT_PROF
   const uint64_t xt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+#if AICP_QLAT_PROF
+  uint32_t qt0 = 0;
+  __shared__ uint32_t qh[512];  // block-local histograms, flushed once at the end
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) qh[i] = 0;
+  __syncthreads();
 #endif
   // chunk context: wave-uniform (scalar registers)
   uint32_t c_lo = 0, c_n = 0, c_read = 0, c_node = 0, c_ref = 0;
@@ -1614,13 +1628,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
         float q0, q1, q2;
         apply_cols(Tp[0], Tp[1], Tp[2], Tp[3], r.x, r.y, r.z, q0, q1, q2);
         t.reset(q0, q1, q2);
+#if AICP_QLAT_PROF
+        qt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
         return true;
       },
       [&](uint32_t, Eng& t) {
         match[qidx] = t.res_id();
         d2out[qidx] = t.res_d2();
         touched[qidx] = (min(t.tn, 65535u) << 16) | min(t.tp, 65535u);
+#if AICP_QLAT_PROF
+        const uint32_t qt1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        atomicAdd(&qh[min((qt1 - qt0) / 100, 255u)], 1u);
+        atomicAdd(&qh[256 + min((qt1 - (uint32_t)xt0) / 100, 255u)], 1u);
+#endif
       });
+#if AICP_QLAT_PROF
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += blockDim.x)
+    if (qh[i]) atomicAdd(&g_qlat[i], (unsigned long long)qh[i]);
+#endif
 #if AICP_XCD_PROF
   // per launch slot and XCD group: earliest wave start, latest wave end (100 MHz clock)
   const uint64_t xt1 = __builtin_amdgcn_s_memrealtime();
@@ -2879,6 +2906,37 @@ void nn_prof_dump() {
   }
   unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_nn_prof), z, sizeof(z));
+#endif
+#if AICP_QLAT_PROF
+  static unsigned long long q[512];
+  if (hipMemcpyFromSymbol(q, HIP_SYMBOL(g_qlat), sizeof(q)) == hipSuccess) {
+    const char* nm[2] = {"query latency", "completion after wave start"};
+    for (int k = 0; k < 2; ++k) {
+      const unsigned long long* h = q + 256 * k;
+      unsigned long long n = 0, acc = 0;
+      double mean = 0;
+      for (int b = 0; b < 256; ++b) n += h[b], mean += (b + 0.5) * h[b];
+      if (!n) continue;
+      fprintf(stderr, "qlat %s: n %llu mean %.1f us |", nm[k], n, mean / n);
+      const double ps[6] = {0.5, 0.9, 0.99, 0.999, 0.9999, 1.0};
+      int p = 0;
+      for (int b = 0; b < 256 && p < 6; ++b) {
+        acc += h[b];
+        while (p < 6 && acc >= (unsigned long long)(ps[p] * n)) {
+          fprintf(stderr, " p%g %d", ps[p] * 100, b + 1);
+          ++p;
+        }
+      }
+      fprintf(stderr, " us\nqlat %s histogram (2 us bins):", nm[k]);
+      for (int b = 0; b < 256; b += 2) {
+        const unsigned long long c = h[b] + h[b + 1];
+        if (c) fprintf(stderr, " %d:%llu", b, c);
+      }
+      fprintf(stderr, "\n");
+    }
+  }
+  for (auto& v : q) v = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_qlat), q, sizeof(q));
 #endif
 }
 

@@ -5,8 +5,8 @@
 // float direction, double tMax) plus every endpoint key; overlap% = min(|A∩B|/|A|,
 // |A∩B|/|B|) * 100. octomap stores S in an octree, prunes and expands it; only the set matters.
 //
-// Device form: one byte per voxel of a padded key box per cloud. Every ray key is a plain
-// byte store of 1 -- concurrent writers store the same value, so no atomics and no
+// Device form: one byte per voxel of a padded key box per cloud, in 8 x 8 x 2 bricks of 128 B
+// (aicp_common.hpp: ovl_index). Every ray key is a plain byte store of 1 -- concurrent writers store the same value, so no atomics and no
 // read-before-write are needed. A reference cloud seen from one origin has one voxel set
 // whatever reading it is paired with, so its map is built once per (reference, origin)
 // group and shared by the pairs of a reference window; |A| is counted once per group, |B|
@@ -156,8 +156,7 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
       err = true;
       return;
     }
-    const uint64_t idx = ((uint64_t)a * (uint64_t)dm1 + (uint64_t)b) * (uint64_t)dm2 + (uint64_t)c;
-    put((int64_t)idx);
+    put((int64_t)ovl_index((uint32_t)a, (uint32_t)b, (uint32_t)c, (uint32_t)dm1, (uint32_t)dm2));
   };
   const double* org = side ? d.read_origin : d.ref_origin;
   const float o[3] = {(float)org[0], (float)org[1], (float)org[2]};
@@ -191,12 +190,10 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
       }
     }
     const double len = (double)length;
-    // the linear map index follows the walk: one add per step, one bounds test on the axis
-    // that moved (the other two are unchanged)
-    const int64_t stride[3] = {(int64_t)dm1 * dm2, (int64_t)dm2, 1};
+    // the box coordinates follow the walk (one bounds test on the axis that moved: the other two
+    // are unchanged); the brick index is formed from them per step
     int rel[3] = {cur[0] - mn0, cur[1] - mn1, cur[2] - mn2};
     const int dims[3] = {dm0, dm1, dm2}, mins[3] = {mn0, mn1, mn2};
-    int64_t idx = (int64_t)rel[0] * stride[0] + (int64_t)rel[1] * stride[1] + rel[2];
     // one step of the walk: false once it has ended (endpoint key, past the length, or bad)
     auto walk = [&](int64_t& out) -> bool {
       int dim;
@@ -212,7 +209,6 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
           cur[i] = (cur[i] + step[i]) & 0xFFFF;
           tMax[i] += tDelta[i];
           rel[i] += step[i];
-          idx += step[i] * stride[i];
           // a key wrap (0xFFFF) or a walk leaving the padded box is reported, never stored
           bad = (cur[i] - mins[i]) != rel[i] || (unsigned)rel[i] >= (unsigned)dims[i];
         }
@@ -223,7 +219,7 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
         err = true;
         return false;
       }
-      out = idx;
+      out = (int64_t)ovl_index((uint32_t)rel[0], (uint32_t)rel[1], (uint32_t)rel[2], (uint32_t)dm1, (uint32_t)dm2);
       return true;
     };
     int64_t g;
@@ -261,7 +257,9 @@ __global__ __launch_bounds__(256) void k_ovl_popcount(const OvlDesc* __restrict_
   if ((threadIdx.x & 63) == 0 && c) atomicAdd((unsigned long long*)&st[m].ovl_counts[slot], c);
 }
 
-// |A ∩ B|: every set voxel of a reading's map looked up in its group's reference map
+// |A ∩ B|: every 16-byte word of a reading's map against the word holding the same voxels in its
+// group's reference map (both boxes start on brick boundaries of the key lattice, so the word s of
+// a brick covers the same keys in both); bytes are 0 or 1, so the popcount of the AND counts them
 __global__ __launch_bounds__(256) void k_ovl_intersect(const PairDesc* __restrict__ pd,
                                                        const OvlDesc* __restrict__ od_read,
                                                        const OvlDesc* __restrict__ od_ref, PairState* st,
@@ -271,39 +269,28 @@ __global__ __launch_bounds__(256) void k_ovl_intersect(const PairDesc* __restric
   const OvlDesc& rb = od_read[p];
   const OvlDesc& ra = od_ref[pd[p].ogroup];
   const uint4* B = (const uint4*)(maps + rb.off);
-  const uint8_t* A = maps + ra.off;
+  const uint4* A = (const uint4*)(maps + ra.off);
   const uint64_t n16 = rb.bytes / 16;
-  const uint64_t vox = (uint64_t)rb.dim[0] * rb.dim[1] * rb.dim[2];
-  const uint32_t d1 = (uint32_t)rb.dim[1], d2 = (uint32_t)rb.dim[2];
-  const int o0 = rb.min[0] - ra.min[0], o1 = rb.min[1] - ra.min[1], o2 = rb.min[2] - ra.min[2];
+  const uint32_t b1 = (uint32_t)rb.dim[1] / kOvlBrick1, b2 = (uint32_t)rb.dim[2] / kOvlBrick2;
+  const uint32_t a0 = (uint32_t)ra.dim[0] / kOvlBrick0, a1 = (uint32_t)ra.dim[1] / kOvlBrick1,
+                 a2 = (uint32_t)ra.dim[2] / kOvlBrick2;
+  // the reading box's brick (0, 0, 0) in the reference box's bricks
+  const int o0 = (rb.min[0] - ra.min[0]) / kOvlBrick0, o1 = (rb.min[1] - ra.min[1]) / kOvlBrick1,
+            o2 = (rb.min[2] - ra.min[2]) / kOvlBrick2;
+  constexpr uint32_t kWords = kOvlBrickBytes / 16;
   unsigned long long c = 0;
   for (uint64_t w = (uint64_t)sub * 256 + threadIdx.x; w < n16; w += (uint64_t)bpm * 256) {
     const uint4 b = B[w];
     if ((b.x | b.y | b.z | b.w) == 0) continue;
-    const uint32_t words[4] = {b.x, b.y, b.z, b.w};
-    uint64_t i0 = w * 16;
-    // (a, bb, cc) of the word's first voxel, then step along the fastest axis
-    uint32_t a = (uint32_t)(i0 / ((uint64_t)d1 * d2));
-    const uint64_t rem = i0 - (uint64_t)a * d1 * d2;
-    uint32_t bb = (uint32_t)(rem / d2), cc = (uint32_t)(rem - (uint64_t)bb * d2);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const bool set = ((words[k >> 2] >> ((k & 3) * 8)) & 0xFFu) != 0u;
-      if (set && i0 + k < vox) {
-        const int x = (int)a + o0, y = (int)bb + o1, z = (int)cc + o2;
-        if ((unsigned)x < (unsigned)ra.dim[0] && (unsigned)y < (unsigned)ra.dim[1] && (unsigned)z < (unsigned)ra.dim[2]) {
-          const uint64_t j = ((uint64_t)x * (uint64_t)ra.dim[1] + (uint64_t)y) * (uint64_t)ra.dim[2] + (uint64_t)z;
-          c += A[j];
-        }
-      }
-      if (++cc == d2) {
-        cc = 0;
-        if (++bb == d1) {
-          bb = 0;
-          ++a;
-        }
-      }
-    }
+    const uint64_t brick = w / kWords;
+    const uint32_t s = (uint32_t)(w % kWords);
+    const uint32_t z = (uint32_t)(brick % b2);
+    const uint64_t r = brick / b2;
+    const uint32_t y = (uint32_t)(r % b1), x = (uint32_t)(r / b1);
+    const int gx = (int)x + o0, gy = (int)y + o1, gz = (int)z + o2;
+    if ((unsigned)gx >= a0 || (unsigned)gy >= a1 || (unsigned)gz >= a2) continue;
+    const uint4 a = A[(((uint64_t)gx * a1 + (uint64_t)gy) * a2 + (uint64_t)gz) * kWords + s];
+    c += __popc(a.x & b.x) + __popc(a.y & b.y) + __popc(a.z & b.z) + __popc(a.w & b.w);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);

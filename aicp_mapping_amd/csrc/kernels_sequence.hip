@@ -84,15 +84,9 @@ __global__ void k_ovl_size(int n, PairState* st, OvlDesc* od, const uint64_t* __
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   OvlDesc& o = od[i];
-  uint64_t vox = 1;
-  for (int k = 0; k < 3; ++k) {
-    int lo = st[i].ovl_bbox[k], hi = st[i].ovl_bbox[3 + k];
-    if (lo > hi) lo = hi = 0;  // nothing inside the key range
-    o.min[k] = lo - 2;
-    o.dim[k] = (hi - lo) + 5;
-    vox *= (uint64_t)o.dim[k];
-  }
-  o.bytes = (vox + 15) / 16 * 16;
+  const int br[3] = {kOvlBrick0, kOvlBrick1, kOvlBrick2};
+  for (int k = 0; k < 3; ++k) ovl_axis(st[i].ovl_bbox[k], st[i].ovl_bbox[3 + k], br[k], o.min[k], o.dim[k]);
+  o.bytes = ovl_bytes(o.dim);
   if (o.bytes > cap[i]) {
     for (int k = 0; k < 3; ++k) o.dim[k] = 0;
     o.bytes = 0;

@@ -1204,6 +1204,27 @@ __device__ __forceinline__ void lvl_scan(const uint32_t* fl, uint32_t* X, uint32
   if (t == 0) X[n] = base;
 }
 
+#ifndef AICP_ITER_PROF
+#define AICP_ITER_PROF 0
+#endif
+#if AICP_ITER_PROF
+// diagnostic builds: k_tr_subtree_lvl's phases summed over segments (thread 0, s_memrealtime
+// ticks at 100 MHz): [0] load, [1] min/max, [2] counts, [3] Hoare passes, [4] nodes + events,
+// [5] child map, [6] store, [7] levels, [8] segments, [9] points, [10] slowest segment
+__device__ unsigned long long g_lvl_prof[12];
+#define AICP_LP(k)                                                  \
+  do {                                                              \
+    if (threadIdx.x == 0) {                                         \
+      const uint64_t now_ = __builtin_amdgcn_s_memrealtime();       \
+      lp[k] += now_ - lp_t;                                         \
+      lp_t = now_;                                                  \
+    }                                                               \
+  } while (0)
+#else
+#define AICP_LP(k) \
+  do {             \
+  } while (0)
+#endif
 __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t total, const TreeCtl* __restrict__ ctl,
                                                                 const SubSeg* __restrict__ subs,
                                                                 const float4* __restrict__ W, float4* __restrict__ bpts,
@@ -1222,11 +1243,21 @@ __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t tota
   __shared__ uint32_t n_next, any_eq;
   const int t = threadIdx.x;
   const uint32_t n_small = ctl->n_small;
+#if AICP_ITER_PROF
+  uint64_t lp[12] = {}, lp_t = __builtin_amdgcn_s_memrealtime(), lp_seg0 = 0;
+#endif
   for (uint32_t si = blockIdx.x; si < n_small; si += gridDim.x) {
     __syncthreads();  // the previous segment's last LDS reads precede this one's loads
     const SubSeg g = subs[si];
     if (g.c > (uint32_t)kSubMax) continue;  // oversized: k_tr_subtree's global path
     const uint32_t gf = g.f, n = g.c;
+#if AICP_ITER_PROF
+    if (t == 0) {
+      lp_t = lp_seg0 = __builtin_amdgcn_s_memrealtime();
+      lp[8] += 1;
+      lp[9] += n;
+    }
+#endif
     for (uint32_t j = t; j < n; j += kLvlThreads) {
       pts[j] = W[gf + j];
       nid[j] = 0;
@@ -1267,6 +1298,7 @@ __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t tota
         any_eq = 0;
       }
       __syncthreads();
+      AICP_LP(0);
       // the cut dimension's min / max per node
       int key[kLvlPer];
       float v[kLvlPer];
@@ -1283,6 +1315,7 @@ __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t tota
         }
       }
       __syncthreads();
+      AICP_LP(1);
       // the partition counts (v < cut, v == cut) per node
       float cut[kLvlPer];
 #pragma unroll
@@ -1300,6 +1333,7 @@ __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t tota
         }
       }
       __syncthreads();
+      AICP_LP(2);
       // Hoare pass 1 over each node on (v < cut) with boundary nl, then (if a node has ties)
       // pass 2 over [nl, count) on (v == cut) with boundary nl + ne
       for (int pass = 0; pass < 2; ++pass) {
@@ -1340,6 +1374,7 @@ __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t tota
           }
         __syncthreads();
       }
+      AICP_LP(3);
       // per node: the left count, its event, the children (leaf events or next-level nodes)
       if ((uint32_t)t < nn) {
         const uint32_t count = N.c[t], nl = ncnt[t] & 0xFFFFu, ne = ncnt[t] >> 16;
@@ -1387,6 +1422,7 @@ __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t tota
         }
       }
       __syncthreads();
+      AICP_LP(4);
       // positions to their child nodes
 #pragma unroll
       for (int u = 0; u < kLvlPer; ++u)
@@ -1397,13 +1433,27 @@ __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t tota
       maxd = depth + 1;
       nn = n_next;
       __syncthreads();
+      AICP_LP(5);
+#if AICP_ITER_PROF
+      if (t == 0) lp[7] += 1;
+#endif
       if (nn == 0) break;
       cur ^= 1;
       ++depth;
     }
     for (uint32_t j = t; j < n; j += kLvlThreads) bpts[gf + j] = pts[j];
     if (t == 0 && pair_depth[g.pair] < maxd) atomicMax(&pair_depth[g.pair], maxd);
+#if AICP_ITER_PROF
+    AICP_LP(6);
+    if (t == 0) lp[10] = max(lp[10], (unsigned long long)(lp_t - lp_seg0));
+#endif
   }
+#if AICP_ITER_PROF
+  if (t == 0) {
+    for (int k = 0; k < 10; ++k) atomicAdd(&g_lvl_prof[k], (unsigned long long)lp[k]);
+    atomicMax(&g_lvl_prof[10], (unsigned long long)lp[10]);
+  }
+#endif
 }
 
 // ---- mid-size builder: one workgroup splits a segment of <= kMidMax points in LDS ----------------
@@ -1419,9 +1469,6 @@ constexpr int kMidOut = 64;  // pieces of <= kSubMax points per mid segment (2 p
 
 static_assert(kMidMax < 65536, "k_tr_mid packs two counts of a node into one word");
 
-#ifndef AICP_ITER_PROF
-#define AICP_ITER_PROF 0
-#endif
 #if AICP_ITER_PROF
 // diagnostic builds: k_tr_mid's phases per segment (s_memrealtime ticks, 100 MHz): load, nodes,
 // store, node count, segments, and the slowest segment's total
@@ -2053,6 +2100,17 @@ void tree_prof_dump() {
             "slowest segment %.2f us, most nodes %llu, segments %llu\n",
             h[0] / 100.0 / h[4], h[1] / 100.0 / h[4], (double)h[3] / h[4], h[2] / 100.0 / h[4], h[5] / 100.0, h[6],
             h[4]);
+  unsigned long long l[12];
+  if (hipMemcpyFromSymbol(l, HIP_SYMBOL(g_lvl_prof), sizeof(l)) == hipSuccess && l[8]) {
+    fprintf(stderr,
+            "[tree prof] k_tr_subtree_lvl per segment (%llu segments, %.1f points, %.2f levels): load %.2f, "
+            "minmax %.2f, counts %.2f, passes %.2f, nodes %.2f, child map %.2f, store %.2f us; slowest %.2f us\n",
+            l[8], (double)l[9] / l[8], (double)l[7] / l[8], l[0] / 100.0 / l[8], l[1] / 100.0 / l[8],
+            l[2] / 100.0 / l[8], l[3] / 100.0 / l[8], l[4] / 100.0 / l[8], l[5] / 100.0 / l[8],
+            l[6] / 100.0 / l[8], l[10] / 100.0);
+    unsigned long long z[12] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lvl_prof), z, sizeof(z));
+  }
 #endif
 }
 

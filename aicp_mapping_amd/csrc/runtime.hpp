@@ -197,7 +197,7 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
 // ctl_dst (default T.pin_ctl) at the end of the build unless copy_ctl is false
 int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
                      int bucket, DevBuf& bpts_out, DevBuf& nodes_out, int plan, TreeCtl* ctl_dst = nullptr,
-                     bool copy_ctl = true);
+                     bool copy_ctl = true, hipEvent_t levels_done = nullptr);
 // errors of a planned build whose control block is in hctl (after its stream completed)
 int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err);
 int device_trees_check(TreeBufs& T, std::string& err);

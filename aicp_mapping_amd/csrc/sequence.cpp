@@ -236,7 +236,8 @@ void pack_clouds(WorkerPool& pool, const std::vector<PackSeg>& segs, std::vector
 // voxel-map capacity (bytes) of a cloud with AABB b plus origin o at resolution res: `rigid`
 // allows any rotation (a rigid motion keeps the diameter; the device sizes the box after the
 // transform), otherwise the axis extents. Both include the 2 + 2 voxels of padding, one more
-// for the floor of each end, and the rounding of the corrected origin.
+// for the floor of each end, the rounding of the corrected origin, and the brick alignment of
+// both box ends (ovl_axis: up to 2 x 7 voxels).
 uint64_t map_cap(const Box& b0, const double* o, double res, bool rigid) {
   Box b = b0;
   b.add((float)o[0], (float)o[1], (float)o[2]);
@@ -248,9 +249,9 @@ uint64_t map_cap(const Box& b0, const double* o, double res, bool rigid) {
   uint64_t vox = 1;
   for (int k = 0; k < 3; ++k) {
     const double e = rigid ? std::sqrt(d2) : ext[k];
-    vox *= (uint64_t)std::ceil(e / res) + 8;
+    vox *= (uint64_t)std::ceil(e / res) + 8 + 2 * (kOvlBrick0 - 1);
   }
-  return (vox + 15) / 16 * 16;
+  return (vox + kOvlBrickBytes - 1) / kOvlBrickBytes * kOvlBrickBytes;
 }
 
 // A window's voxel maps beyond this many bytes (all of them together) take the sorted-key path
@@ -1577,6 +1578,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     }
     std::fprintf(stderr, "[aicp seq] fused select: %llu of %llu guessed bins missed\n", (unsigned long long)miss,
                  (unsigned long long)fused);
+    nn_prof_dump();  // diagnostic builds' counters (AICP_QLAT_PROF / AICP_XCD_PROF / AICP_NN_PROF)
   }
   // timing
   ctx->last_nn_launches = timeNN ? nn_launches : 0;
