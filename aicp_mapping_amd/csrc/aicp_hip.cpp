@@ -235,13 +235,37 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   HIPC(ensure(ctx->pin_io, ((pack_refs ? ro : 0) + wo) * 16));  // references, then readings: the readings are
   float* st = ctx->pin_io.as<float>();          // packed while the references' DMA runs
   std::vector<PackSeg> segs;
+  // pack and copy in chunks of >= kPackChunk points, so each chunk's DMA runs while the next one
+  // is packed (C5: 983 MB of references per side took ~15 ms to pack before the first byte moved)
+  constexpr uint64_t kPackChunk = 4u << 20;
+  auto pack_copy = [&](const std::vector<PackSeg>& all, const float* host0, void* dev0) -> int {
+    size_t a = 0;
+    while (a < all.size()) {
+      size_t b = a;
+      uint64_t pts = 0;
+      while (b < all.size() && (pts < kPackChunk || b == a)) pts += all[b++].n;
+      std::vector<PackSeg> part(all.begin() + a, all.begin() + b);
+      pack_many(part, ctx_pool(ctx));
+      const uint64_t off = (uint64_t)(all[a].dst4 - host0) / 4;  // first point of the chunk
+      HIPC(hipMemcpyAsync(static_cast<char*>(dev0) + off * 16, all[a].dst4, pts * 16, hipMemcpyHostToDevice,
+                          ctx->stream));
+      a = b;
+    }
+    return AICP_OK;
+  };
   if (pack_refs) {
     for (size_t r = 0; r < rep.size(); ++r) {
       const PairDesc& d = B->rdesc[r];
       segs.push_back(PackSeg{pairs[rep[r]].ref, d.n_ref, pairs[rep[r]].ref_stride, st + 4ull * d.ref_off});
     }
-    pack_many(segs, ctx_pool(ctx));
-    HIPC(hipMemcpyAsync(B->ref_raw.p, st, ro * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (int rc = pack_copy(segs, st, B->ref_raw.p)) return rc;
+  }
+  // the reference side (trees, normals) waits for this event only, so its kernels run while the
+  // readings are packed and copied (references written on the device later record it in run_batch)
+  B->refs_event = pack_refs;
+  if (pack_refs) {
+    if (!ctx->ev[14]) HIPC(hipEventCreate(&ctx->ev[14]));
+    HIPC(hipEventRecord(ctx->ev[14], ctx->stream));
   }
   float* sw = pack_refs ? st + 4ull * ro : st;
   segs.clear();
@@ -250,8 +274,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
     segs.push_back(PackSeg{pairs[i].read, d.n_read, pairs[i].read_stride, sw + 4ull * d.read_off});
   }
   if (!skip_reads) {  // (skip_reads: the previous call's reading, still on the device)
-    pack_many(segs, ctx_pool(ctx));
-    HIPC(hipMemcpyAsync(B->read_raw.p, sw, wo * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (int rc = pack_copy(segs, sw, B->read_raw.p)) return rc;
   }
   // block maps: [read pair][read start][ref pair][ref start][red pair][red start]
   const size_t nr = mr.pair.size(), nf = mf.pair.size(), nd = md.pair.size(), ns = ms.pair.size();
@@ -617,7 +640,7 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
   hipStream_t s3 = ctx->stream3;
   const size_t R = B->rdesc.size();
   TCHK(hipSetDevice(ctx->device));  // the current device is per host thread
-  TCHK(hipStreamWaitEvent(s3, ctx->ev[7], 0));
+  TCHK(hipStreamWaitEvent(s3, ctx->ev[14], 0));  // the reference points are on the device
   TCHK(hipEventRecord(ctx->ev[12], s3));
   TCHK(hipMemcpyAsync(dRdesc, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s3));
   if (after) TCHK(hipStreamWaitEvent(s3, after, 0));  // the raw tree first (raw_tree_first())
@@ -638,6 +661,7 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
                          ctx->tl.as<uint4>(), ctx->ptl.as<uint2>(), T.tw));
     TCHK(hipMemcpyAsync(T.pin_ctl.p, T.tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
   }
+  TCHK(hipStreamWaitEvent(s3, ctx->ev[7], 0));  // the pairs' descriptors are on the device
   launch_pairs_from_refs(s3, (int)B->P, dDesc, dRdesc);
   TCHK(hipEventRecord(ctx->ev[3], s3));
   return AICP_OK;
@@ -724,6 +748,8 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   HIPC(hipMemcpyAsync(dDesc, pdA, P * sizeof(PairDesc), hipMemcpyHostToDevice, s));
   launch_init_state(s, (int)P, dDesc, dState);
   HIPC(hipEventRecord(ctx->ev[7], s));
+  if (!B->refs_event) HIPC(hipEventRecord(ctx->ev[14], s));
+  B->refs_event = false;  // (a later run of the same batch records it here)
   // readings in Morton order inside each pair's range (kernels_order.hip): the overlap and
   // the ICP loop both visit the sorted copy
   const float4* readS = B->read_raw.as<float4>();
@@ -846,7 +872,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       if (force_trav1()) ctx->tl_total = 0;
     }
     HIPC(ensure(ctx->rdesc_raw, R * sizeof(PairDesc)));
-    HIPC(hipStreamWaitEvent(s2, ctx->ev[7], 0));
+    HIPC(hipStreamWaitEvent(s2, ctx->ev[14], 0));  // the reference points (not the readings) are on the device
     HIPC(hipEventRecord(ctx->ev[8], s2));
     HIPC(hipMemcpyAsync(ctx->rdesc_raw.p, ctx->pin_rdesc.p, R * sizeof(PairDesc), hipMemcpyHostToDevice, s2));
     launch_init_state(s2, (int)R, ctx->rdesc_raw.as<PairDesc>(), dRstate);
@@ -1222,7 +1248,7 @@ int aicp_hip_batch_run(aicp_hip_ctx* ctx, aicp_hip_batch* batch, const aicp_icp_
   return run_batch(ctx, batch, cfg, resolution, flags, out_T, stats, nullptr);
 }
 
-constexpr size_t kOneshotKeepBytes = size_t(1) << 30;
+constexpr size_t kOneshotKeepBytes = size_t(16) << 30;
 
 namespace {
 

@@ -264,6 +264,7 @@ struct aicp_hip_batch {
   uint32_t n_red_total = 0;
   aicp::rt::DevBuf ref_raw, read_raw, maps;
   aicp::BlockMap m_read{}, m_gref{}, m_red{}, m_sel{};
+  bool refs_event = false;  // upload_pairs recorded ctx->ev[14] after the references' copy
 };
 
 struct aicp_hip_map {  // a device-resident point cloud (float4, w = 1)
