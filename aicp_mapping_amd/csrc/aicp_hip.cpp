@@ -969,10 +969,14 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     prm.knn_normals = cfg->knn_normals;
     // The ICP loop on s: per iteration the NN, then select + reduce with the per-pair steps and
     // the next active list inside (launch_icp_select_f / _reduce_f)
-    uint32_t reads = 0;
-    for (size_t i = 0; i < P; ++i) reads += B->desc[i].n_read;
+    uint32_t reads = 0, max_read = 0;
+    for (size_t i = 0; i < P; ++i) {
+      reads += B->desc[i].n_read;
+      max_read = std::max(max_read, B->desc[i].n_read);
+    }
     ActiveList* al = ctx->active.as<ActiveList>();
     const int sel_ff = sel_fused_from();
+    const bool sel_pair = sel_pair_fits(P, max_read);
     // Polled loop (the sequence's, sequence.cpp): from iteration smoothLength on the update of
     // the last pair writes the next active count into mapped host memory; the host stays one
     // iteration ahead and stops enqueueing once it reads 0, instead of maxIterationCount launches
@@ -1023,7 +1027,9 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
         y.host_n = ctx->poll_dev + it + 1;
         pending.push_back(it + 1);
       }
-      if (sel_ff > 0 && it >= sel_ff)
+      if (sel_pair)
+        launch_icp_select_pair(s, (int)P, dDesc, dState, ctx->d2.as<float>(), ctx->sel_cand.as<uint32_t>(), y);
+      else if (sel_ff > 0 && it >= sel_ff)
         launch_icp_select_fused(s, B->m_sel, dDesc, dState, ctx->d2.as<float>(), ctx->sel_hist.as<uint32_t>(),
                                 ctx->sel_cand.as<uint32_t>(), ctx->sel_cnt.as<uint32_t>(), y);
       else

@@ -73,6 +73,10 @@ void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairStat
 // from the second iteration on: the select in one launch, its compaction on the previous
 // iteration's digit-1 bin (same limit; a missed guess is compacted again by the pair's last
 // workgroup, counted in PairState::sel_miss)
+// the whole select of each pair in one workgroup (batches of many pairs of <= 65536 readings)
+void launch_icp_select_pair(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const float* d2,
+                            uint32_t* cand, const IcpIterSync& y);
+bool sel_pair_fits(size_t n_pairs, uint64_t max_read);
 void launch_icp_select_fused(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
                              uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y);
 int sel_fused_from();

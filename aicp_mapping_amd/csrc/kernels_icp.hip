@@ -1737,10 +1737,21 @@ __global__ __launch_bounds__(256) void k_sel_hist(BlockMap m, const PairDesc* __
 // per pair (one workgroup, any size): n = #finite, k, bin b1 holding rank k, rank r1 inside it;
 // the global histogram is read (atomics wrote it; agent-scope loads) and zeroed for the next
 // iteration. Returns false when the pair stopped (no finite distance).
-__device__ bool sel_find1_body(PairState& s, uint32_t* __restrict__ g) {
-  __shared__ uint32_t h[kHistBins];
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t res[2];
+// LDS scratch of the select's serial tails, passed in by the kernel so that one allocation serves
+// every phase (separate __shared__ arrays in each inlined body added up: k_sel_fused had 65.8 KB
+// per workgroup and ran at 2 waves per SIMD)
+struct SelLds {
+  uint32_t* h;     // kHistBins
+  uint32_t* wsum;  // 16
+  uint32_t* res;   // 2
+  uint32_t* cl;    // cl_cap candidates (the final select's LDS copy)
+  uint32_t cl_cap;
+};
+
+__device__ bool sel_find1_body(PairState& s, uint32_t* __restrict__ g, const SelLds& L) {
+  uint32_t* h = L.h;
+  uint32_t* wsum = L.wsum;
+  uint32_t* res = L.res;
   const int t = threadIdx.x, lane = t & 63, nt = (int)blockDim.x;
   uint32_t v = 0;
   // eight agent-scope loads in flight per thread (each is a fabric round trip), then the stores
@@ -1802,7 +1813,8 @@ __global__ __launch_bounds__(1024) void k_sel_find1(PairState* st, uint32_t* __r
   const int pair = blockIdx.x;
   PairState& s = st[pair];
   if (!s.active) return;
-  (void)sel_find1_body(s, hist1 + (size_t)pair * kHistBins);
+  __shared__ uint32_t h[kHistBins], wsum[16], res[2];
+  (void)sel_find1_body(s, hist1 + (size_t)pair * kHistBins, SelLds{h, wsum, res, nullptr, 0});
 }
 
 // a pair is done with this iteration; the group's last one builds the next active list
@@ -1825,6 +1837,7 @@ __global__ __launch_bounds__(kT) void k_sel_hist_f(BlockMap m, const PairDesc* _
   const int pair = m.pair[blockIdx.x];
   if (!st[pair].active) return;
   __shared__ uint32_t h[2][kHistBins];  // one sub-histogram per half workgroup (LDS atomic conflicts)
+  __shared__ uint32_t wsum[16], res[2];
   const int t = threadIdx.x;
   for (int i = t; i < 2 * kHistBins; i += kT) (&h[0][0])[i] = 0;
   const PairDesc& d = pd[pair];
@@ -1851,7 +1864,8 @@ __global__ __launch_bounds__(kT) void k_sel_hist_f(BlockMap m, const PairDesc* _
   AICP_IP_BODY(0);
   if (!last_arrival(&y.sel1[pair], nblk)) return;
   AICP_IP_TAIL0;
-  if (!sel_find1_body(st[pair], g)) pair_done(y);
+  __syncthreads();  // (every thread's reads of the sub-histograms precede find1's writes to h[0])
+  if (!sel_find1_body(st[pair], g, SelLds{h[0], wsum, res, nullptr, 0})) pair_done(y);
   AICP_IP_TAIL(0);
 }
 #ifndef AICP_SEL_HIST_THREADS
@@ -1911,14 +1925,14 @@ constexpr uint32_t kFinalLds = 8192;
 // b1 / r1: digit 1's bin and the rank in it (s.sel_b1 / sel_r1; passed in, since in k_sel_fused
 // they were just written by another thread of the workgroup)
 __device__ void sel_final_body(PairState& s, uint32_t b1, uint32_t r1, const uint32_t* __restrict__ cv,
-                               uint32_t* cand_cnt) {
-  __shared__ uint32_t h[kHistBins];
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t res[2];
-  __shared__ uint32_t cl[kFinalLds];
+                               uint32_t* cand_cnt, const SelLds& L) {
+  uint32_t* h = L.h;
+  uint32_t* wsum = L.wsum;
+  uint32_t* res = L.res;
+  uint32_t* cl = L.cl;
   const int t = threadIdx.x, nt = (int)blockDim.x;
   const uint32_t c = __hip_atomic_load(cand_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const bool lds = c <= kFinalLds;
+  const bool lds = c <= L.cl_cap;
   const uint32_t* src = lds ? cl : cv;
   if (lds) {
     for (uint32_t i0 = 0; i0 < c; i0 += 8u * (uint32_t)nt) {
@@ -1962,7 +1976,9 @@ __global__ __launch_bounds__(1024) void k_sel_final(const PairDesc* __restrict__
   const int pair = blockIdx.x;
   PairState& s = st[pair];
   if (!s.active) return;
-  sel_final_body(s, s.sel_b1, s.sel_r1, cand + pd[pair].read_off, cand_cnt + pair);
+  __shared__ uint32_t h[kHistBins], wsum[16], res[2], cl[kFinalLds];
+  sel_final_body(s, s.sel_b1, s.sel_r1, cand + pd[pair].read_off, cand_cnt + pair,
+                 SelLds{h, wsum, res, cl, kFinalLds});
 }
 
 // k_sel_compact + (last workgroup of the pair) k_sel_final. kT threads per workgroup over the
@@ -2019,7 +2035,8 @@ __global__ __launch_bounds__(kT) void k_sel_compact_f(BlockMap m, const PairDesc
   AICP_IP_BODY(1);
   if (!last_arrival(&y.sel2[pair], nblk)) return;
   AICP_IP_TAIL0;
-  sel_final_body(s, s.sel_b1, s.sel_r1, cand + d.read_off, cand_cnt + pair);
+  __shared__ uint32_t h[kHistBins], wsum[16], res[2], cl[kFinalLds];
+  sel_final_body(s, s.sel_b1, s.sel_r1, cand + d.read_off, cand_cnt + pair, SelLds{h, wsum, res, cl, kFinalLds});
   AICP_IP_TAIL(1);
 }
 // the values of v[0, kPer) (one block-map entry of the pair, kT threads) whose digit 1 is b into
@@ -2065,16 +2082,23 @@ __device__ __forceinline__ void sel_compact_bin(const uint32_t (&v)[kPer], uint3
 // compacted and it runs the final select at once, otherwise it compacts that bin from the pair's
 // distances itself first (slower, same candidates: the select is order-independent), so the
 // limit is k_sel_hist_f + k_sel_compact_f's bit for bit either way.
-template <int kT>
+// kCl: candidates the final select copies into LDS (beyond them it reads them from global memory).
+// Launches of many workgroups (C5: 15k) take kCl = kHistBins: 16 KB of LDS per workgroup, the
+// sub-histograms' space reused by both tails, 8 waves per SIMD; a few workgroups (the stream's
+// window) take kFinalLds, whose tail then loads all of a pair's ~6k candidates into LDS once.
+template <int kT, int kCl>
 __global__ __launch_bounds__(kT) void k_sel_fused(BlockMap m, const PairDesc* __restrict__ pd, PairState* st,
                                                   const float* __restrict__ d2, uint32_t* __restrict__ hist1,
                                                   uint32_t* __restrict__ cand, uint32_t* __restrict__ cand_cnt,
                                                   IcpIterSync y) {
   constexpr int kPer = kNNBlock * kSelPerThread / kT;
+  static_assert(kCl >= kHistBins, "the final select's histogram and candidates share the LDS");
   const int pair = m.pair[blockIdx.x];
   PairState& s = st[pair];
   if (!s.active) return;
-  __shared__ uint32_t h[2][kHistBins];  // one sub-histogram per half workgroup (LDS atomic conflicts)
+  __shared__ uint32_t lds[kHistBins + kCl];  // sub-histograms (2 x kHistBins), then the tails' scratch
+  __shared__ uint32_t wsum[16], res[2];
+  uint32_t(*h)[kHistBins] = reinterpret_cast<uint32_t(*)[kHistBins]>(lds);
   const int t = threadIdx.x;
   for (int i = t; i < 2 * kHistBins; i += kT) (&h[0][0])[i] = 0;
   const PairDesc& d = pd[pair];
@@ -2102,7 +2126,9 @@ __global__ __launch_bounds__(kT) void k_sel_fused(BlockMap m, const PairDesc* __
   sel_compact_bin<kT, kPer>(v, guess, cv, cand_cnt + pair);
   const uint32_t nblk = (d.n_read + 256u * kSelPerThread - 1) / (256u * kSelPerThread);
   if (!last_arrival(&y.sel1[pair], nblk)) return;
-  if (!sel_find1_body(s, g)) {  // no finite distance: the pair stops (ConvergenceError)
+  __syncthreads();  // (every thread's reads of the sub-histograms precede the tails' writes)
+  const SelLds L{lds, wsum, res, lds + kHistBins, (uint32_t)kCl};
+  if (!sel_find1_body(s, g, L)) {  // no finite distance: the pair stops (ConvergenceError)
     if (t == 0) cand_cnt[pair] = 0;
     pair_done(y);
     return;
@@ -2132,7 +2158,125 @@ __global__ __launch_bounds__(kT) void k_sel_fused(BlockMap m, const PairDesc* __
     __syncthreads();
     if (t == 0) atomicAdd(&s.sel_miss, 1u);
   }
-  sel_final_body(s, b1, r1, cv, cand_cnt + pair);
+  sel_final_body(s, b1, r1, cv, cand_cnt + pair, L);
+}
+
+// The whole select of a pair in one workgroup, for batches of many pairs of at most kSelPairMax
+// readings each (C5: 1024 pairs of ~60k): the pair's distances stay in registers, the digit-1
+// histogram, find1, the compaction of the k-th value's bin and digits 2 and 3 all run in LDS. No
+// global histogram atomics (C5's multi-workgroup select flushed up to 2048 bins per workgroup into
+// the pair's global histogram at the memory side: 600-730 us per launch for 245 MB of distances)
+// and no hand-off between workgroups. Same limit bit for bit (the k-th smallest value is unique).
+constexpr int kSelPairThreads = 1024, kSelPairPer = 64;
+constexpr uint32_t kSelPairMax = (uint32_t)kSelPairThreads * kSelPairPer;
+constexpr uint32_t kSelPairCand = 12288;  // candidates kept in LDS (beyond: the pair's global slice)
+__global__ __launch_bounds__(kSelPairThreads) void k_sel_pair(const PairDesc* __restrict__ pd, PairState* st,
+                                                              const float* __restrict__ d2,
+                                                              uint32_t* __restrict__ cand, IcpIterSync y) {
+  const int pair = blockIdx.x;
+  PairState& s = st[pair];
+  if (!s.active) return;
+  constexpr int kT = kSelPairThreads;
+  __shared__ uint32_t h[2][kHistBins];
+  __shared__ uint32_t cl[kSelPairCand];
+  __shared__ uint32_t wsum[16], res[2];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const PairDesc& d = pd[pair];
+  const uint32_t n_read = d.n_read;
+  const uint32_t* bits = (const uint32_t*)(d2 + d.read_off);
+  for (int i = t; i < 2 * kHistBins; i += kT) (&h[0][0])[i] = 0;
+  uint32_t v[kSelPairPer];
+#pragma unroll
+  for (int u = 0; u < kSelPairPer; ++u) {
+    const uint32_t j = (uint32_t)t + (uint32_t)kT * u;
+    v[u] = j < n_read ? bits[j] : kInfBits;
+  }
+  __syncthreads();
+  uint32_t* mine = h[t / (kT / 2)];
+#pragma unroll
+  for (int u = 0; u < kSelPairPer; ++u)
+    if (v[u] != kInfBits) atomicAdd(&mine[v[u] >> 21], 1u);
+  __syncthreads();
+  uint32_t cnt = 0;
+  for (int b = t; b < kHistBins; b += kT) {
+    const uint32_t c = h[0][b] + h[1][b];
+    h[0][b] = c;
+    cnt += c;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+  if (lane == 0) wsum[w] = cnt;
+  __syncthreads();
+  uint32_t n = 0;
+  for (int k = 0; k < kT / 64; ++k) n += wsum[k];
+  __syncthreads();  // (wsum is reused by block_find_rank)
+  if (n == 0) {  // ConvergenceError("no outlier to filter"), as sel_find1_body
+    if (t == 0) {
+      s.status = 1;
+      s.active = 0;
+    }
+    pair_done(y);
+    return;
+  }
+  const float ratio = s.ratio;
+  uint32_t k;
+  if (ratio == 1.0f) {
+    k = n - 1;
+  } else {
+    const float kf = (float)n * ratio;
+    k = (uint32_t)kf;
+    if (k >= n) k = n - 1;
+  }
+  block_find_rank(h[0], kHistBins, k, res, wsum);
+  const uint32_t b1 = res[0], r1 = res[1];
+  if (t == 0) {
+    s.sel_b1 = b1;
+    s.sel_r1 = r1;
+    s.n_finite = (int32_t)n;
+  }
+  // the values of bin b1: counted per wave, then placed (LDS, or the pair's global slice when
+  // more than kSelPairCand)
+  uint32_t mine_n = 0;
+#pragma unroll
+  for (int u = 0; u < kSelPairPer; ++u) mine_n += (uint32_t)__popcll(__ballot(v[u] != kInfBits && (v[u] >> 21) == b1));
+  __syncthreads();  // (block_find_rank's last reads of wsum / res precede the writes below)
+  if (lane == 0) wsum[w] = mine_n;
+  __syncthreads();
+  uint32_t c = 0, o = 0;
+  for (int q = 0; q < kT / 64; ++q) {
+    if (q < w) o += wsum[q];
+    c += wsum[q];
+  }
+  const bool lds = c <= kSelPairCand;
+  uint32_t* dst = lds ? cl : cand + d.read_off;
+  const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int u = 0; u < kSelPairPer; ++u) {
+    const bool hit = v[u] != kInfBits && (v[u] >> 21) == b1;
+    const uint64_t mk = __ballot(hit);
+    if (hit) dst[o + (uint32_t)__popcll(mk & below)] = v[u];
+    o += (uint32_t)__popcll(mk);
+  }
+  if (!lds) __threadfence_block();
+  __syncthreads();
+  // digits 2 (bits 20..10) and 3 (bits 9..0) over the candidates
+  for (int i = t; i < kHistBins; i += kT) h[0][i] = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < c; i += kT) atomicAdd(&h[0][(dst[i] >> 10) & 2047u], 1u);
+  __syncthreads();
+  block_find_rank(h[0], kHistBins, r1, res, wsum);
+  const uint32_t b2 = res[0], r2 = res[1];
+  __syncthreads();
+  for (int i = t; i < kHistBins; i += kT) h[0][i] = 0;
+  __syncthreads();
+  const uint32_t hi21 = (b1 << 11) | b2;
+  for (uint32_t i = t; i < c; i += kT) {
+    const uint32_t x = dst[i];
+    if ((x >> 10) == hi21) atomicAdd(&h[0][x & 1023u], 1u);
+  }
+  __syncthreads();
+  block_find_rank(h[0], kHist3Bins, r2, res, wsum);
+  if (t == 0) s.limit = __uint_as_float((hi21 << 10) | res[0]);
 }
 
 #ifndef AICP_SEL_COMPACT_THREADS
@@ -2965,7 +3109,20 @@ void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairStat
 void launch_icp_select_fused(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
                              uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y) {
   if (!m.n_blocks) return;
-  k_sel_fused<256><<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, hist1, cand, cand_cnt, y);
+  if (m.n_blocks > 2048)  // more workgroups than fit the chip at once: occupancy over the tail's LDS copy
+    k_sel_fused<256, kHistBins><<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, hist1, cand, cand_cnt, y);
+  else
+    k_sel_fused<256, kFinalLds><<<m.n_blocks, 256, 0, s>>>(m, pd, st, d2, hist1, cand, cand_cnt, y);
+}
+void launch_icp_select_pair(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const float* d2,
+                            uint32_t* cand, const IcpIterSync& y) {
+  if (n_pairs > 0) k_sel_pair<<<n_pairs, kSelPairThreads, 0, s>>>(pd, st, d2, cand, y);
+}
+bool sel_pair_fits(size_t n_pairs, uint64_t max_read) {  // AICP_SEL_PAIR=0/1 forces it off / on
+  const char* e = std::getenv("AICP_SEL_PAIR");
+  if (max_read > kSelPairMax) return false;
+  if (e) return e[0] == '1';
+  return n_pairs >= 256;
 }
 int sel_fused_from() {  // AICP_SEL_FUSED=k: the fused select from iteration k on (0: never)
   const char* e = std::getenv("AICP_SEL_FUSED");

@@ -373,6 +373,30 @@ def test_batch_deterministic_and_order_independent(ctx, L):
     np.testing.assert_array_equal(Ta[1], Tc[0])
 
 
+def test_select_one_workgroup_per_pair_equals_chip_wide(ctx, L, monkeypatch):
+    """k_sel_pair (the whole TrimmedDist select of a pair in one workgroup; batches of >= 256 pairs
+    take it) gives the chip-wide select's limits: same transforms and statistics bit for bit, on
+    ordinary pairs and on one whose distances all fall into one digit-1 bin (more candidates than
+    the kernel keeps in LDS: its global-memory path)."""
+    prs = [sy.make_pair(9000 + 1500 * i, 12000 - 1000 * i, seed=70 + i) for i in range(4)]
+    pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
+    g = np.random.default_rng(7)
+    plane = np.zeros((20000, 3), np.float32)
+    plane[:, :2] = g.uniform(-10, 10, (20000, 2)).astype(np.float32)
+    lifted = plane.copy()
+    lifted[:, 2] = np.float32(0.1)  # every nearest distance^2 is 0.01: one bin, 20000 candidates
+    pairs.append(dict(ref=plane, read=lifted, ref_origin=np.zeros(3), read_origin=np.zeros(3)))
+    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("AICP_SEL_PAIR", v)
+        out[v] = ctx.align_batch(pairs, flags=flags, resolution=RES)
+    (T0, s0, rc0), (T1, s1, rc1) = out["0"], out["1"]
+    assert rc0 == rc1
+    np.testing.assert_array_equal(T0, T1)
+    assert s0 == s1
+
+
 def test_concurrent_contexts_identical(ctx, L):
     """Two contexts on one device driven by two host threads at once (bench.py --lanes): each
     batch's transforms and touch counts equal a lone run's (no shared device state)."""
