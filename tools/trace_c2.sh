@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel trace of the default C2 stream (no batched leg, no CPU leg) for timelines
-# (tools/timeline_seq.py) and per-kernel stats; output under gpurun_out/trace_$1.
+# (tools/timeline.py) and per-kernel stats; output under gpurun_out/trace_$1.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 R=${1:-x}
