@@ -377,7 +377,8 @@ def test_select_one_workgroup_per_pair_equals_chip_wide(ctx, L, monkeypatch):
     """k_sel_pair (the whole TrimmedDist select of a pair in one workgroup; batches of >= 256 pairs
     take it) gives the chip-wide select's limits: same transforms and statistics bit for bit, on
     ordinary pairs and on one whose distances all fall into one digit-1 bin (more candidates than
-    the kernel keeps in LDS: its global-memory path)."""
+    the kernel keeps in LDS: its global-memory path). raw_tree_first's order (batches of >= 4 M
+    reference points) changes nothing either."""
     prs = [sy.make_pair(9000 + 1500 * i, 12000 - 1000 * i, seed=70 + i) for i in range(4)]
     pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
     g = np.random.default_rng(7)
@@ -388,13 +389,18 @@ def test_select_one_workgroup_per_pair_equals_chip_wide(ctx, L, monkeypatch):
     pairs.append(dict(ref=plane, read=lifted, ref_origin=np.zeros(3), read_origin=np.zeros(3)))
     flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
     out = {}
-    for v in ("0", "1"):
+    # also the batch path's stream order for large batches (the raw tree first, the matcher tree
+    # from the raw tree's global levels on), forced on this small batch: same results
+    for v, raw in (("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")):
         monkeypatch.setenv("AICP_SEL_PAIR", v)
-        out[v] = ctx.align_batch(pairs, flags=flags, resolution=RES)
-    (T0, s0, rc0), (T1, s1, rc1) = out["0"], out["1"]
-    assert rc0 == rc1
-    np.testing.assert_array_equal(T0, T1)
-    assert s0 == s1
+        monkeypatch.setenv("AICP_RAW_FIRST", raw)
+        out[v + raw] = ctx.align_batch(pairs, flags=flags, resolution=RES)
+    T0, s0, rc0 = out["00"]
+    for k in ("10", "01", "11"):
+        T1, s1, rc1 = out[k]
+        assert rc0 == rc1, k
+        np.testing.assert_array_equal(T0, T1)
+        assert s0 == s1, k
 
 
 def test_concurrent_contexts_identical(ctx, L):
