@@ -1261,11 +1261,19 @@ namespace {
 // x, y, z of n points at a byte stride == packed[3 n], byte for byte; split over host threads for
 // large clouds (a C2 reference is ~2 MB to read on every call)
 bool same_points(WorkerPool* pool, const float* pts, uint64_t n, uint64_t stride, const float* packed) {
+  // bitwise equality (NaN payloads included): one memcmp of the range for packed xyz rows, else the
+  // XOR of the three words of every row OR-ed together (no branch per point: vectorised)
   auto cmp = [&](uint64_t a, uint64_t b) {
     const char* src = reinterpret_cast<const char*>(pts);
-    for (uint64_t i = a; i < b; ++i)
-      if (std::memcmp(src + i * stride, packed + 3 * i, 12) != 0) return false;
-    return true;
+    if (stride == 12) return std::memcmp(src + a * 12, packed + 3 * a, (b - a) * 12) == 0;
+    uint32_t diff = 0;
+    for (uint64_t i = a; i < b; ++i) {
+      uint32_t x[3], y[3];
+      std::memcpy(x, src + i * stride, 12);
+      std::memcpy(y, packed + 3 * i, 12);
+      diff |= (x[0] ^ y[0]) | (x[1] ^ y[1]) | (x[2] ^ y[2]);
+    }
+    return diff == 0;
   };
   const unsigned nt = n < (1u << 16) ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   if (nt == 1) return cmp(0, n);
@@ -1280,6 +1288,10 @@ bool same_points(WorkerPool* pool, const float* pts, uint64_t n, uint64_t stride
 void copy_points(WorkerPool* pool, const float* pts, uint64_t n, uint64_t stride, float* packed) {
   auto cp = [&](uint64_t a, uint64_t b) {
     const char* src = reinterpret_cast<const char*>(pts);
+    if (stride == 12) {
+      std::memcpy(packed + 3 * a, src + a * 12, (b - a) * 12);
+      return;
+    }
     for (uint64_t i = a; i < b; ++i) std::memcpy(packed + 3 * i, src + i * stride, 12);
   };
   const unsigned nt = n < (1u << 16) ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
@@ -1336,15 +1348,27 @@ int oneshot(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pair
   if (!(flags & (AICP_RUN_ICP | AICP_RUN_OVERLAP))) FAIL(AICP_ERR_INVALID, "nothing to run");
   if (!ctx->oneshot) ctx->oneshot = new aicp_hip_batch();
   aicp_hip_batch* B = ctx->oneshot;
+  using clk = std::chrono::steady_clock;
+  const auto h0 = clk::now();
   const bool skip_refs = refcache_begin(ctx, cfg, pairs, n_pairs, resolution, flags);
+  const auto h1 = clk::now();
   // the reading of the previous call again (computeOverlap, then registerClouds)?
   ReadCache& rd = ctx->rdc;
   const aicp_pair* p0 = n_pairs == 1 && pairs && valid_pair(pairs[0]) ? pairs : nullptr;
   rd.hit = p0 && rd.valid && rd.ptr == p0->read && rd.n == p0->n_read && rd.stride == p0->read_stride &&
            rd.pts.size() == 3 * (size_t)p0->n_read &&
            same_points(ctx_pool(ctx), p0->read, p0->n_read, p0->read_stride, rd.pts.data());
+  const auto h2 = clk::now();
   int rc = upload_pairs(ctx, pairs, n_pairs, B, false, skip_refs, rd.hit, true);
+  const auto h3 = clk::now();
   if (!rc) rc = run_batch(ctx, B, cfg, resolution, flags, out_T, stats, out_overlap);
+  if (prof_enabled()) {  // host time per part of a one-shot call (us)
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    const auto h4 = clk::now();
+    std::fprintf(stderr, "[aicp oneshot] flags %d pairs %zu: reference compare %.0f, reading compare %.0f, upload %.0f, run %.0f us%s%s\n",
+                 flags, n_pairs, us(h0, h1), us(h1, h2), us(h2, h3), us(h3, h4), skip_refs ? " (reference resident)" : "",
+                 rd.hit ? " (reading resident)" : "");
+  }
   ctx->refc.use = false;
   const bool was_hit = rd.hit;
   rd.hit = false;

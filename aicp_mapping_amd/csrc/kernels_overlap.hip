@@ -239,6 +239,20 @@ inline int count_bpm(int n_maps, bool wide) {
   return wide ? std::max(64, std::min(512, 2048 / std::max(1, n_maps))) : 64;
 }
 
+// the workgroup's sum of c added to *dst by one atomic (the counts of a map share one address:
+// one atomic per wave was 2048 same-address atomics per map for the wide grid, ~20 us)
+__device__ __forceinline__ void block_add_u64(unsigned long long c, unsigned long long* dst) {
+  __shared__ unsigned long long wsum[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (t) atomicAdd(dst, t);
+  }
+}
+
 // |S| of every map in od[]: byte sums (bytes are 0 or 1; maps 16-byte aligned and padded)
 __global__ __launch_bounds__(256) void k_ovl_popcount(const OvlDesc* __restrict__ od, PairState* st, int slot,
                                                       const uint8_t* __restrict__ maps, int bpm) {
@@ -252,9 +266,7 @@ __global__ __launch_bounds__(256) void k_ovl_popcount(const OvlDesc* __restrict_
     const uint4 a = A[w];
     c += __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd((unsigned long long*)&st[m].ovl_counts[slot], c);
+  block_add_u64(c, (unsigned long long*)&st[m].ovl_counts[slot]);
 }
 
 // |A ∩ B|: every 16-byte word of a reading's map against the word holding the same voxels in its
@@ -292,9 +304,7 @@ __global__ __launch_bounds__(256) void k_ovl_intersect(const PairDesc* __restric
     const uint4 a = A[(((uint64_t)gx * a1 + (uint64_t)gy) * a2 + (uint64_t)gz) * kWords + s];
     c += __popc(a.x & b.x) + __popc(a.y & b.y) + __popc(a.z & b.z) + __popc(a.w & b.w);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd((unsigned long long*)&st[p].ovl_counts[2], c);
+  block_add_u64(c, (unsigned long long*)&st[p].ovl_counts[2]);
 }
 
 __global__ void k_ovl_finish(int n_pairs, const PairDesc* __restrict__ pd, PairState* st,
