@@ -822,6 +822,7 @@ __device__ __forceinline__ void coop_bucket(Eng& t, bool act, const float4* __re
 #endif
 #if AICP_XCD_PROF
 __device__ unsigned long long g_xcd_prof[64 * kXcdGroups * 2];
+__device__ unsigned long long g_xcd_cost[64 * kXcdGroups];  // per launch slot and group: queries << 40 | sum tn + tp
 #endif
 #ifndef AICP_QLAT_PROF
 #define AICP_QLAT_PROF 0  // diagnostic builds: per-query NN latency / completion-time histograms
@@ -1598,6 +1599,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
   uint32_t c_lo = 0, c_n = 0, c_read = 0, c_node = 0, c_ref = 0;
   int c_pair = 0;
   uint32_t qidx = 0;
+#if AICP_XCD_PROF
+  uint64_t xc_cost = 0;  // this lane's queries and their inner nodes + bucket points
+#endif
   persistent_xcd<Eng>(
       total, ctr, prm.maxE2, prm.maxR2, nodes, bpts,
       [&](uint32_t base, Eng& t) {
@@ -1637,6 +1641,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
         match[qidx] = t.res_id();
         d2out[qidx] = t.res_d2();
         touched[qidx] = (min(t.tn, 65535u) << 16) | min(t.tp, 65535u);
+#if AICP_XCD_PROF
+        xc_cost += (1ull << 40) + t.tn + t.tp;
+#endif
 #if AICP_QLAT_PROF
         const uint32_t qt1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
         atomicAdd(&qh[min((qt1 - qt0) / 100, 255u)], 1u);
@@ -1655,6 +1662,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
     unsigned long long* r = g_xcd_prof + (prm.prof_slot * kXcdGroups + blockIdx.x % kXcdGroups) * 2;
     atomicMin(&r[0], (unsigned long long)xt0);
     atomicMax(&r[1], (unsigned long long)xt1);
+  }
+  {  // the block's query count and cost, one add per block
+    __shared__ unsigned long long xc_sum;
+    if (threadIdx.x == 0) xc_sum = 0;
+    __syncthreads();
+    atomicAdd(&xc_sum, (unsigned long long)xc_cost);
+    __syncthreads();
+    if (threadIdx.x == 0 && prm.prof_slot < 64)
+      atomicAdd(&g_xcd_cost[prm.prof_slot * kXcdGroups + blockIdx.x % kXcdGroups], xc_sum);
   }
 #endif
 }
@@ -3024,13 +3040,20 @@ void nn_prof_dump() {
     for (int l = 0; l < 64; ++l) {
       unsigned long long t0 = ~0ull, t1 = 0;
       for (int g = 0; g < kXcdGroups; ++g) {
-        t0 = std::min(t0, h[(l * kXcdGroups + g) * 2]);
+        if (h[(l * kXcdGroups + g) * 2]) t0 = std::min(t0, h[(l * kXcdGroups + g) * 2]);  // (0: not reset yet)
         t1 = std::max(t1, h[(l * kXcdGroups + g) * 2 + 1]);
       }
       if (t1 == 0) continue;
-      fprintf(stderr, "xcd launch %2d: %6.1f us |", l, (t1 - t0) / 100.0);
-      for (int g = 0; g < kXcdGroups; ++g)
-        fprintf(stderr, " %6.1f", (h[(l * kXcdGroups + g) * 2 + 1] - t0) / 100.0);
+      unsigned long long c[kXcdGroups];
+      (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(g_xcd_cost), sizeof(c), sizeof(c) * l);
+      fprintf(stderr, "xcd launch %2d: %6.1f us | per group: start end (us), queries, mean tn+tp:", l,
+              (t1 - t0) / 100.0);
+      for (int g = 0; g < kXcdGroups; ++g) {
+        const unsigned long long q = c[g] >> 40, w = c[g] & ((1ull << 40) - 1);
+        const unsigned long long s0 = h[(l * kXcdGroups + g) * 2];
+        fprintf(stderr, " [%.1f %.1f %llu %.1f]", s0 ? (s0 - t0) / 100.0 : -1.0,
+                (h[(l * kXcdGroups + g) * 2 + 1] - t0) / 100.0, q, q ? (double)w / q : 0.0);
+      }
       fprintf(stderr, "\n");
     }
   }
@@ -3039,6 +3062,8 @@ void nn_prof_dump() {
     h[2 * i + 1] = 0;
   }
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_prof), h, sizeof(h));
+  static unsigned long long zc[64 * kXcdGroups] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_cost), zc, sizeof(zc));
 #endif
 #if AICP_NN_PROF
   unsigned long long h[8];
