@@ -1474,7 +1474,10 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         a[1] += ev_ms(t[0], t[2]);
         a[2] += ev_ms(t[0], t[3]);
         a[3] += ev_ms(t[3], t[4]);
-        a[4] += ev_ms(runs[k - 1].tev[0], t[0]);
+        // the period from window 1 on: window 0's reference side starts the call with nothing
+        // prepared ahead of it, and counting its period made the average ~0.09 ms longer than the
+        // sum of the steady windows' phases (C2, r05)
+        if (k >= 2) a[4] += ev_ms(runs[k - 1].tev[0], t[0]);
         const hipEvent_t* u = runs[k - 1].tev;  // the hand-off from window k - 1's commit
         b[0] += ev_ms(u[4], u[5]);
         b[1] += ev_ms(u[5], t[6]);
@@ -1496,7 +1499,16 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       std::fprintf(stderr,
                    "[aicp seq] device ms/window: ref->matcher %.3f ref->normals %.3f ref->icp start %.3f icp %.3f "
                    "period %.3f\n",
-                   a[0] / m, a[1] / m, a[2] / m, a[3] / m, a[4] / m);
+                   a[0] / m, a[1] / m, a[2] / m, a[3] / m, a[4] / (m - 1));
+      // the pass's ends: from its first device work to window 0's reference start (window 0's
+      // upload, which nothing runs beside), and from the last window's commit to the read-back
+      std::fprintf(stderr,
+                   "[aicp seq] pass ms: begin->window 0 reference %.3f, window 0 ref->next ref %.3f (ref->matcher %.3f "
+                   "ref->normals %.3f ref->icp start %.3f icp %.3f), last commit->end %.3f, total %.3f over %zu windows\n",
+                   ev_ms(S->ev_begin, runs[0].tev[0]), ev_ms(runs[0].tev[0], runs[1].tev[0]),
+                   ev_ms(runs[0].tev[0], runs[0].tev[1]), ev_ms(runs[0].tev[0], runs[0].tev[2]),
+                   ev_ms(runs[0].tev[0], runs[0].tev[3]), ev_ms(runs[0].tev[3], runs[0].tev[4]),
+                   ev_ms(runs[plan.size() - 1].tev[5], S->ev_end), ev_ms(S->ev_begin, S->ev_end), plan.size());
     }
     for (size_t k = 0; k < plan.size(); ++k) {
       for (int t = 0; t < 2; ++t) {
