@@ -57,8 +57,30 @@ __device__ __forceinline__ void best_init(Best<K>& b) {
   }
 }
 
+#ifndef AICP_BEST_NOCHAIN
+#define AICP_BEST_NOCHAIN 1
+#endif
 template <int K>
 __device__ __forceinline__ void best_replace(Best<K>& b, int32_t id, float val) {
+#if AICP_BEST_NOCHAIN
+  // the same insertion without the serial `placed` chain: with c(i) = v[i-1] > val (the list is
+  // ascending, so c(i) implies c(i+1)), slot i takes v[i-1] when c(i), val when c(i+1) alone and
+  // keeps v[i] otherwise -- equal values stay ahead of the new one, as in the loop below. Each
+  // compare reads a slot not yet written (slots go downwards).
+  bool cn = true;  // c(i+1); the last slot takes val unless shifted into
+#pragma unroll
+  for (int i = K - 1; i > 0; --i) {
+    const bool ci = b.v[i - 1] > val;
+    b.v[i] = ci ? b.v[i - 1] : (cn ? val : b.v[i]);
+    b.id[i] = ci ? b.id[i - 1] : (cn ? id : b.id[i]);
+    cn = ci;
+  }
+  if (cn) {
+    b.v[0] = val;
+    b.id[0] = id;
+  }
+  return;
+#endif
   bool placed = false;
 #pragma unroll
   for (int i = K - 1; i > 0; --i) {
