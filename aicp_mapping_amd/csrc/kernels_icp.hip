@@ -71,7 +71,9 @@ __device__ __forceinline__ void best_replace(Best<K>& b, int32_t id, float val) 
 #pragma unroll
   for (int i = K - 1; i > 0; --i) {
     const bool ci = b.v[i - 1] > val;
-    b.v[i] = ci ? b.v[i - 1] : (cn ? val : b.v[i]);
+    // v[i-1] <= v[i]: their median with val is v[i-1] below it, val between, v[i] above (the
+    // caller passes val < v[K-1], finite)
+    b.v[i] = __builtin_amdgcn_fmed3f(b.v[i - 1], b.v[i], val);
     b.id[i] = ci ? b.id[i - 1] : (cn ? id : b.id[i]);
     cn = ci;
   }
