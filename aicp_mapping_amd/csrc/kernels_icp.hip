@@ -135,6 +135,17 @@ struct NnLdsFrame {
   int32_t start;
   float mnf;
 };
+// Trav2C's frames past its LDS ones, in scratch in the same 20-byte layout (5 dwords per push
+// and pop where FarFrame moves 8; scratch lines are written back to HBM through L2)
+struct NnFarStack {
+  NnLdsFrame f[kFarStack];
+};
+__device__ __forceinline__ void put_far(NnFarStack& fs, int32_t sp, const NnLdsFrame& g, const FarFrame&) {
+  fs.f[sp] = g;
+}
+__device__ __forceinline__ void put_far(FarStack& fs, int32_t sp, const NnLdsFrame&, const FarFrame& f) {
+  fs.f[sp] = f;
+}
 
 constexpr int kLeafBatch = 8;  // = libnabo's default bucket size
 #ifndef AICP_NN_COOP
@@ -169,6 +180,7 @@ constexpr int kKnnLdsFrames = AICP_KNN_LDS_FRAMES;
 
 template <int K>
 struct Trav {
+  using Stack = FarStack;
   const uint4* nodes;
   const float4* pts;
   float q0, q1, q2;
@@ -363,6 +375,11 @@ __device__ __forceinline__ uint8_t& pmb_at(int d) { return g_pmb[d * kNNBlock + 
 #endif
 
 struct Trav2C {
+#if AICP_NN_CLIMB2 && !AICP_NN_CLIMB4
+  using Stack = NnFarStack;
+#else
+  using Stack = FarStack;
+#endif
   const uint4* tlb;      // the batch's treelets (uniform: set per chunk)
   const uint2* ptlb;     // the batch's treelet links {parent of the root, parent of the parent treelet's root}
   uint32_t tlo;          // the pair's first treelet: one VGPR instead of two 64-bit pointers
@@ -504,7 +521,7 @@ struct Trav2C {
   // far test of node p (slot s of record r, parent pp); on a pass: push the frame, start the far
   // descent and return true
   // dp: depth of p (AICP_NN_POPCHK: kept in the frame, the far descent starts at dp + 1)
-  __device__ __forceinline__ bool far_push(FarStack& fs, const uint4& r, int32_t p, uint32_t s, int32_t pp,
+  __device__ __forceinline__ bool far_push(Stack& fs, const uint4& r, int32_t p, uint32_t s, int32_t pp,
                                            float maxE2, float maxR2, int32_t dp = 0) {
     const uint32_t T = (uint32_t)p >> 2;
     const uint32_t w = slot_word(r, s), cd = (r.w >> (2 * s)) & 3u;
@@ -521,10 +538,10 @@ struct Trav2C {
 #else
     const int32_t sdp = start;
 #endif
-    if (sp < AICP_NN_LDS_FRAMES)
-      lf[sp * kNNBlock] = NnLdsFrame{(int32_t)(((uint32_t)pp & 0x3fffffffu) | (cd << 30)), rd, oc, sdp,
-                                     __int_as_float(max(__float_as_int(minFar), 0) | (p == start ? (int32_t)0x80000000 : 0))};
-    else fs.f[sp] = FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, dp};
+    const NnLdsFrame frame{(int32_t)(((uint32_t)pp & 0x3fffffffu) | (cd << 30)), rd, oc, sdp,
+                           __int_as_float(max(__float_as_int(minFar), 0) | (p == start ? (int32_t)0x80000000 : 0))};
+    if (sp < AICP_NN_LDS_FRAMES) lf[sp * kNNBlock] = frame;
+    else put_far(fs, sp, frame, FarFrame{(int32_t)((uint32_t)far | (cd << 30)), rd, oc, minFar, start, p, pp, dp});
     ++sp;
     const float nn = -no * no;
     if (cd == 0) noc0 = nn;
@@ -625,7 +642,7 @@ struct Trav2C {
   // by the deeper far descents since) decides at once whether any level left to climb can pass.
   // The far tests it skips are ones the climb would have made and failed, so the visit order,
   // counts and result are unchanged.
-  __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
+  __device__ __forceinline__ bool climb(Stack& fs, float maxE2, float maxR2) {
     int32_t c = n, pc = pl;
     if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
     for (;;) {
@@ -633,9 +650,12 @@ struct Trav2C {
         if (sp == 0) return true;
         --sp;
         FarFrame f;
-        if (sp < AICP_NN_LDS_FRAMES) {
+        {
+          // the innermost frames from LDS, the deeper ones from scratch, both in one layout.
           // P only matters through P == start (the sign bit of mn); any other id != start will do
-          const NnLdsFrame g = lf[sp * kNNBlock];
+          NnLdsFrame g;
+          if (sp < AICP_NN_LDS_FRAMES) g = lf[sp * kNNBlock];
+          else g = fs.f[sp];
           const int32_t mi = __float_as_int(g.mnf);
 #if AICP_NN_POPCHK
           const int32_t gs = g.start & ((1 << kStartBits) - 1);
@@ -645,8 +665,6 @@ struct Trav2C {
           f = FarFrame{g.PPcd, g.rd, g.old, __int_as_float(mi & 0x7fffffff), g.start, mi < 0 ? g.start : -2,
                        g.PPcd & 0x3fffffff, 0};
 #endif
-        } else {
-          f = fs.f[sp];
         }
         const uint32_t pcd = (uint32_t)f.F >> 30;
         rd = f.rd;
@@ -689,89 +707,7 @@ struct Trav2C {
   }
 #endif  // AICP_NN_CLIMB4
 #else
-  __device__ __forceinline__ bool climb(FarStack& fs, float maxE2, float maxR2) {
-    int32_t c = n, pc = pl;
-    uint32_t cT = 0xffffffffu;  // treelet whose record cr (and root parent cpp) is held
-    uint4 cr;
-    int32_t cpp = -1;
-    if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
-    for (;;) {
-      if (c == start) {
-        if (sp == 0) return true;
-        --sp;
-        const uint32_t pcd = (uint32_t)fs.f[sp].F >> 30;
-        rd = fs.f[sp].rd;
-        const float old = fs.f[sp].old;
-        if (pcd == 0) noc0 = old;
-        else if (pcd == 1) noc1 = old;
-        else noc2 = old;
-        minFar = fs.f[sp].mn;
-        start = fs.f[sp].start;
-        c = fs.f[sp].P;
-        pc = fs.f[sp].PP;
-#if AICP_NN_PREFMIN
-        dep = (int32_t)((uint32_t)fs.f[sp].F & 0x3fffffffu);
-#endif
-        if (!(minFar <= maxR2 && minFar * maxE2 < best.v[0])) c = start;
-        continue;
-      }
-      const int32_t p = pc;
-#if AICP_NN_PREFMIN
-      const int32_t dp = dep - 1;  // depth of p
-      if (dp < kPmDepth) {
-        const float bnd = __uint_as_float((uint32_t)pm[dp * kNNBlock] << 16);
-        if (!(bnd <= maxR2 && bnd * maxE2 < best.v[0])) {  // no level from start to p can pass
-          c = start;
-          continue;
-        }
-      }
-#endif
-      const uint32_t T = (uint32_t)p >> 2, s = (uint32_t)p & 3u;
-      if (T != cT) {  // the record and its root's parent, one round trip per treelet
-        cT = T;
-        cr = ld_rec_up(tl + T, ptl + T, cpp);
-      }
-      const uint4 r = cr;
-      const int32_t pp = s != 0 ? (int32_t)(T << 2) : cpp;  // parent of p
-      const uint32_t w = slot_word(r, s), cd = (r.w >> (2 * s)) & 3u;
-      const float no = sel3(cd, q0, q1, q2) - __uint_as_float(w);
-      const float oc = sel3(cd, noc0, noc1, noc2);
-      const float rdf = rd + (oc + no * no);
-      if (rdf <= maxR2 && rdf * maxE2 < best.v[0]) {
-        // far child = the left one when the query is right of the cut
-        const uint32_t fr = no > 0.f ? 0u : 1u;
-        const int32_t far = s == 0 ? (int32_t)(T << 2 | (1u + fr))
-                                   : (int32_t)(((r.w >> 6) + 2 * (s - 1) + fr) << 2);
-#if AICP_NN_PREFMIN
-        fs.f[sp].F = (int32_t)((uint32_t)dp | (cd << 30));  // the far child is n; keep p's depth
-        dep = dp + 1;
-#else
-        fs.f[sp].F = (int32_t)((uint32_t)far | (cd << 30));
-#endif
-        fs.f[sp].rd = rd;
-        fs.f[sp].old = oc;
-        fs.f[sp].mn = minFar;
-        fs.f[sp].start = start;
-        fs.f[sp].P = p;
-        fs.f[sp].PP = pp;
-        ++sp;
-        const float nn = -no * no;
-        if (cd == 0) noc0 = nn;
-        else if (cd == 1) noc1 = nn;
-        else noc2 = nn;
-        rd = rdf;
-        n = far;
-        start = far;
-        pl = p;
-        return false;
-      }
-      c = p;
-      pc = pp;
-#if AICP_NN_PREFMIN
-      dep = dp;
-#endif
-    }
-  }
+#error "AICP_NN_CLIMB2=0: the one-node-per-step climb was removed in r05 (it no longer built)"
 #endif
 };
 
@@ -923,7 +859,7 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
   const uint32_t hi = g + 1 == kXcdGroups ? total : (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups) & ~63u;
   uint32_t* gctr = ctr + g * kCtrStride;
   Eng t;
-  FarStack fs;
+  typename Eng::Stack fs;
   bool has = false;
   uint32_t pool = 0, pool_end = 0, my = 0;
   bool exhausted = false;
