@@ -1256,15 +1256,17 @@ __device__ __forceinline__ void oct_insert(OctBest<K, G>& b, bool first_lane, fl
   if (first_lane) pv = -__builtin_inff();
   float nv[M];
   int32_t ni[M];
+  bool sh = pv > val;  // slot i's predecessor above val; pl of slot i is sh of slot i + 1
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     const float a = i == 0 ? pv : b.v[i - 1];
     const int32_t ai = i == 0 ? pid : b.id[i - 1];
-    const bool sh = a > val, pl = b.v[i] > val;
+    const bool pl = b.v[i] > val;
     // a <= b.v[i] (ascending): the median of (a, b.v[i], val) is a if val < a, val if it lies
     // between, b.v[i] above (val is finite and not NaN: the caller filtered with `< head`)
     nv[i] = __builtin_amdgcn_fmed3f(a, b.v[i], val);
     ni[i] = sh ? ai : (pl ? vid : b.id[i]);
+    sh = pl;
   }
 #pragma unroll
   for (int i = 0; i < M; ++i) {
