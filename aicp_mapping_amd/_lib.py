@@ -38,11 +38,13 @@ EXPORTS = [
     "aicp_hip_default_sequence_params", "aicp_hip_sequence_run", "aicp_hip_last_sequence_timing",
     "aicp_hip_map_register_batch", "aicp_hip_multi_create", "aicp_hip_multi_destroy", "aicp_hip_multi_size",
     "aicp_hip_multi_context", "aicp_hip_multi_last_error", "aicp_hip_multi_align_batch",
-    "aicp_hip_reference_cache_stats",
+    "aicp_hip_reference_cache_stats", "aicp_hip_default_options", "aicp_hip_set_options", "aicp_hip_get_options",
+    "aicp_hip_test_force_scan_stall",
 ]
 
 
-_NEWEST = {"aicp_hip_reference_cache_stats"}  # added in r05
+_NEWEST = {"aicp_hip_reference_cache_stats", "aicp_hip_default_options", "aicp_hip_set_options",
+           "aicp_hip_get_options", "aicp_hip_test_force_scan_stall"}  # added in r05 / r06
 
 
 class IcpConfig(C.Structure):
@@ -159,6 +161,29 @@ class SequenceResult(C.Structure):
         return d
 
 
+class Options(C.Structure):
+    """aicp_hip_options (include/aicp_hip.h): a context's engine and schedule switches."""
+    _fields_ = [
+        ("profile", C.c_int32),
+        ("nn_engine", C.c_int32),
+        ("overlap_path", C.c_int32),
+        ("normals_knn_engine", C.c_int32),
+        ("select_pair", C.c_int32),
+        ("select_fused_from", C.c_int32),
+        ("raw_tree_first", C.c_int32),
+        ("raw_first_at", C.c_int32),
+        ("no_early_exit", C.c_int32),
+        ("tree_plan", C.c_int32),
+        ("tree_lvl_min", C.c_uint32),
+        ("reference_cache", C.c_int32),
+        ("oneshot_keep_mib", C.c_uint32),
+        ("read_order_min", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class SequenceTiming(C.Structure):
     _fields_ = [
         ("windows", C.c_int32),
@@ -239,6 +264,12 @@ def _load():
                                               fp, stp]
     if hasattr(L, "aicp_hip_reference_cache_stats"):
         L.aicp_hip_reference_cache_stats.argtypes = [vp, C.POINTER(C.c_uint64)]
+    if hasattr(L, "aicp_hip_set_options"):
+        L.aicp_hip_default_options.argtypes = [C.POINTER(Options)]
+        L.aicp_hip_default_options.restype = None
+        L.aicp_hip_set_options.argtypes = [vp, C.POINTER(Options)]
+        L.aicp_hip_get_options.argtypes = [vp, C.POINTER(Options)]
+        L.aicp_hip_test_force_scan_stall.argtypes = [C.c_int]
     L.aicp_hip_multi_create.argtypes = [ip, C.c_int, C.POINTER(vp)]
     L.aicp_hip_multi_destroy.argtypes = [vp]
     L.aicp_hip_multi_destroy.restype = None
@@ -267,6 +298,22 @@ class ConvergenceError(AicpError):
 class TransformationError(AicpError):
     """Maps PM::TransformationError: RigidTransformation::checkParameters rejected a transform
     applied to the reading (|1 - det R| > 0.001)."""
+
+
+def default_options(**kw) -> Options:
+    """aicp_hip_default_options (the product path) with keyword overrides."""
+    o = Options()
+    lib.aicp_hip_default_options(C.byref(o))
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise AttributeError(f"aicp_hip_options has no field {k}")
+        setattr(o, k, v)
+    return o
+
+
+def test_force_scan_stall(on: bool) -> int:
+    """aicp_hip_test_force_scan_stall (test hook, the calling thread's device)."""
+    return lib.aicp_hip_test_force_scan_stall(1 if on else 0)
 
 
 def default_config(**kw) -> IcpConfig:
@@ -364,6 +411,11 @@ def default_prefilter(**kw) -> PrefilterParams:
     return p
 
 
+# aicp_hip_options overrides every new Context starts with (bench.py --opt k=v); empty: the
+# library's defaults
+CONTEXT_OPTIONS: dict = {}
+
+
 class Context:
     """One aicp_hip_ctx: a HIP stream + device arena on one GPU."""
 
@@ -374,6 +426,8 @@ class Context:
             raise AicpError(rc, f"aicp_hip_create(device={device}) failed (no HIP device?)")
         self.h = h
         self.device = device
+        if CONTEXT_OPTIONS:
+            self.set_options(**CONTEXT_OPTIONS)
 
     def close(self):
         if getattr(self, "h", None):
@@ -385,6 +439,38 @@ class Context:
 
     def last_error(self) -> str:
         return lib.aicp_hip_last_error(self.h).decode()
+
+    def get_options(self) -> Options:
+        o = Options()
+        self.check(lib.aicp_hip_get_options(self.h, C.byref(o)))
+        return o
+
+    def set_options(self, opt: Options = None, **kw) -> Options:
+        """aicp_hip_set_options: `opt` (default: the context's current options) with keyword
+        overrides. Returns the options in force before the call."""
+        old = self.get_options()
+        new = Options.from_buffer_copy(opt if opt is not None else old)
+        for k, v in kw.items():
+            if not hasattr(new, k):
+                raise AttributeError(f"aicp_hip_options has no field {k}")
+            setattr(new, k, v)
+        self.check(lib.aicp_hip_set_options(self.h, C.byref(new)))
+        return old
+
+    def options(self, **kw):
+        """with ctx.options(overlap_path=1): ... -- the overrides for the block only."""
+        ctx = self
+
+        class _Scope:
+            def __enter__(self):
+                self.old = ctx.set_options(**kw)
+                return ctx
+
+            def __exit__(self, *exc):
+                ctx.set_options(self.old)
+                return False
+
+        return _Scope()
 
     def check(self, rc):
         if rc == AICP_ERR_CONVERGENCE:

@@ -36,17 +36,51 @@ constexpr int kHistRing = 32;       // differential checker history ring
 constexpr uint32_t kLeaf = 3;
 constexpr int kMaxPairs = 4096;     // pairs per batch
 constexpr int kXcdGroups = 8;       // work groups of the persistent kernels (one per XCD)
-constexpr int kCtrStride = 16;      // words between the per-group work counters (64 B)
-constexpr int kCtrWords = 3 * kXcdGroups * kCtrStride;  // ICP NN counters, normals kNN, ICP group 1 NN
+constexpr int kCtrStride = 16;      // words between work counters (64 B: one counter per line)
+// A persistent kernel's work counters: per XCD group kHeads heads (the group's slot range cut
+// into kHeads contiguous parts, so that no more than ~1/kHeads of the group's waves pull from
+// one word: a word serves ~88 returning atomics per us, MI355X_MICROARCH.md "dequeue") and one
+// word of exhausted-head bits.
+constexpr int kHeads = 4;
+constexpr int kGroupCtrs = kHeads + 1;
+constexpr int kPersistCtrWords = kXcdGroups * kGroupCtrs * kCtrStride;  // one persistent kernel's counters
+constexpr int kKnnCtrOff = kPersistCtrWords;                            // the normals kNN's, after the ICP NN's
+constexpr int kCtrWords = 2 * kPersistCtrWords;                         // ICP NN counters, normals kNN
+
+// One entry of the active list: what a wave of the NN kernel holds in scalar registers while it
+// serves a 64-slot chunk of the entry's pair (32 bytes: one scalar load).
+struct NnEntry {
+  uint32_t off;                // first slot of the pair in the work space
+  uint32_t n_read, read_off;   // the pair's readings
+  uint32_t tl_off, node_off;   // its matcher tree (treelets / node records)
+  uint32_t ref_off;            // its reference points
+  int32_t pair;
+  uint32_t pad;
+};
 
 // Compacted list of the pairs still iterating (k_active_list), consumed by the persistent
-// NN kernel: slot s of the work space belongs to pair[e] with off[e] <= s < off[e+1].
+// NN kernel: slot s of the work space belongs to pair[e] with off[e] <= s < off[e+1]. The
+// chunk table that follows the struct in the same allocation (al_chunks) names the entry of
+// every 64-slot chunk, so a wave finds its chunk's context with two dependent scalar loads
+// (chunk table, entry) instead of a binary search over off[] plus a PairDesc load.
 struct ActiveList {
   uint32_t n;
   uint32_t total;
+  uint32_t pad[6];
+  NnEntry ent[kMaxPairs];
   uint32_t off[kMaxPairs + 1];
   int32_t pair[kMaxPairs];
 };
+// the u16 chunk table behind the active list: entry of chunk c (slots [64 c, 64 c + 64))
+__host__ __device__ inline uint16_t* al_chunks(ActiveList* al) { return reinterpret_cast<uint16_t*>(al + 1); }
+__host__ __device__ inline const uint16_t* al_chunks(const ActiveList* al) {
+  return reinterpret_cast<const uint16_t*>(al + 1);
+}
+// bytes of an active list whose work space holds n_read readings in n_pairs pairs (each pair's
+// range padded to a multiple of 64 slots)
+inline size_t active_list_bytes(uint64_t n_read, uint64_t n_pairs) {
+  return sizeof(ActiveList) + 2 * (size_t)(n_read / 64 + n_pairs + 1) + 4;
+}
 
 struct PairDesc {
   uint32_t ref_off, n_ref;      // into ref arrays (ref_raw, bpts, bnrm)

@@ -38,22 +38,9 @@ using namespace aicp::rt;
 namespace aicp {
 namespace rt {
 
-// Test-only: AICP_FORCE_TRAV1=1 runs the ICP NN on node records (Trav<1>), the engine used when
-// treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records); read per
-// call so a test can switch it.
-// AICP_PROF=1: diagnostic output to stderr (the stream's phase times; the counters of the
-// diagnostic builds -DAICP_ITER_PROF / AICP_NN_PROF / AICP_XCD_PROF); never changes results
-bool prof_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("AICP_PROF");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-bool force_trav1() {
-  const char* e = std::getenv("AICP_FORCE_TRAV1");
-  return e && e[0] == '1';
+void tree_opts(TreeBufs& T, const aicp_hip_options& o) {
+  T.lvl_min = o.tree_lvl_min;
+  T.prof = o.profile != 0;
 }
 
 bool valid_pair(const aicp_pair& p) {
@@ -353,6 +340,7 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
   w.lb = T.lb.as<uint64_t>();
   w.lb_stride = lb_stride_words((uint32_t)n);
   w.mid_max = tree_mid_max();
+  w.lvl_min = T.lvl_min;
   w.n_pairs = (int)P;
   w.ecnt = T.ecnt.as<uint32_t>();
   w.sums = T.sums.as<uint64_t>();
@@ -426,7 +414,7 @@ int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err) {
   while (used < kFarStack + 1 && hctl->nseg[used]) ++used;
   // oversized segments at the last planned level: plan deeper next time
   T.needed = hctl->n_big ? std::min(kFarStack - 3, T.planned + 2) : used;
-  if (prof_enabled()) {
+  if (T.prof) {
     std::fprintf(stderr, "[aicp tree] planned %d used %d next %d: n_big %u n_mid %u n_small %u segments/level", T.planned,
                  used, T.needed, hctl->n_big, hctl->n_mid, hctl->n_small);
     for (int l = 0; l < used; ++l) std::fprintf(stderr, " %u", hctl->nseg[l]);
@@ -442,13 +430,11 @@ int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err) {
 // first plan keeps a margin, and later plans follow what the previous build of this tree used
 // (every planned level costs its launches and two full-length scans even when no segment is
 // left: C2 with 8 instead of 11 levels, +2 %).
-// AICP_TREE_PLAN=k forces k levels (tests: a too-shallow plan); AICP_TREE_PLAN=0 selects the
+// force (aicp_hip_options::tree_plan): k > 0 forces k levels (tests: a too-shallow plan), -1 the
 // host-polled build (A/B measurements).
-int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean) {
-  if (const char* e = std::getenv("AICP_TREE_PLAN")) {
-    const int v = std::atoi(e);
-    return v > 0 ? std::min(kFarStack - 2, v) : 0;
-  }
+int plan_levels(uint64_t n_max, const TreeBufs& T, int force, bool lean) {
+  if (force > 0) return std::min(kFarStack - 2, force);
+  if (force < 0) return 0;
   int l = 0;
   while (((uint64_t)tree_mid_max() << l) < n_max) ++l;
   // lean: the balanced estimate + 1, whatever the previous build used; the few segments still
@@ -540,10 +526,6 @@ int overlap_sparse(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, Pai
 constexpr uint64_t kDenseMapBudget = uint64_t(8) << 30;
 constexpr unsigned long long kReadOrderMin = 200000;
 
-bool force_sparse_overlap() {  // AICP_OVL_SPARSE=1: the sorted-key path for every batch (tests)
-  const char* e = std::getenv("AICP_OVL_SPARSE");
-  return e && e[0] == '1';
-}
 
 int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairDesc* dDesc, PairState* dState,
                  PairDesc* dG, PairState* dGst, const float4* readS, double res, bool set_ratio, std::string& err) {
@@ -552,7 +534,7 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
   TCHK(hipEventSynchronize(ctx->ev[1]));
   RefCache& rc = ctx->refc;
   const bool hit = rc.hit_ovl;  // the one group's map is the cached reference's (ctx->bitmap[0, rc.od.bytes))
-  if (force_sparse_overlap()) {
+  if (ctx->opt.overlap_path == 1) {  // the sorted-key path for every batch (tests)
     rc.ovl = false;
     return overlap_sparse(ctx, B, P, G, dDesc, dState, dGst, readS, res, set_ratio, err);
   }
@@ -592,9 +574,11 @@ int overlap_maps(aicp_hip_ctx* ctx, aicp_hip_batch* B, size_t P, size_t G, PairD
   }
   if (hit && bm_bytes > ctx->bitmap.cap) {  // grow, keeping the cached map
     DevBuf nb;
-    TCHK(ensure(nb, bm_bytes));
-    TCHK(hipMemcpyAsync(nb.p, ctx->bitmap.p, ref_bytes, hipMemcpyDeviceToDevice, s));
-    TCHK(hipStreamSynchronize(s));
+    hipError_t e = ensure(nb, bm_bytes);
+    if (e == hipSuccess) e = hipMemcpyAsync(nb.p, ctx->bitmap.p, ref_bytes, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) release(nb);  // (a DevBuf is not released by its destructor)
+    TCHK(e);
     release(ctx->bitmap);
     ctx->bitmap = nb;
   }
@@ -667,31 +651,20 @@ int matcher_trees(aicp_hip_ctx* ctx, aicp_hip_batch* B, int bucket, PairDesc* dD
   return AICP_OK;
 }
 
-// AICP_RAW_FIRST=0/1 forces the order; by default batches of >= 4 M reference points build the
-// raw tree first
-bool raw_tree_first(uint64_t total_ref) {
-  static const int v = [] {
-    const char* e = std::getenv("AICP_RAW_FIRST");
-    return e ? std::atoi(e) : -1;
-  }();
-  return v >= 0 ? v > 0 : total_ref >= (4ull << 20);
+// aicp_hip_options::raw_tree_first 0/1 forces the order; by default batches of >= 4 M reference
+// points build the raw tree first
+bool raw_tree_first(uint64_t total_ref, const aicp_hip_options& o) {
+  return o.raw_tree_first >= 0 ? o.raw_tree_first > 0 : total_ref >= (4ull << 20);
 }
 
 // With the raw tree first, the matcher tree starts when the raw tree's global levels and mid-size
 // segments are done (2, default: its bandwidth-bound levels beside the raw tree's latency-bound
-// subtree kernel) or when the whole raw tree is (AICP_RAW_FIRST_AT=1: the normals' kNN, launched
+// subtree kernel) or when the whole raw tree is (raw_first_at = 1: the normals' kNN, launched
 // at the same time, then holds every wave slot and the matcher kernels wait behind it). C5, same
 // box, alternating: 3578 / 3494 (2) against 3409 / 3265 (1) and 3244 / 3352 clouds/s (both trees
 // together). Also measured: the normals' kNN waiting for the matcher tree's mid-size segments
 // (k_tr_mid needs most of a CU's LDS per workgroup and starves behind the persistent kNN):
 // 3420 / 3368 against 3495 / 3433.
-int raw_first_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("AICP_RAW_FIRST_AT");
-    return e ? std::atoi(e) : 2;
-  }();
-  return v;
-}
 
 double ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
@@ -728,7 +701,11 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   HIPC(ensure(ctx->desc, P * sizeof(PairDesc)));
   HIPC(ensure(ctx->state, P * sizeof(PairState)));
   if (P > (size_t)kMaxPairs) FAIL(AICP_ERR_UNSUPPORTED, "more than 4096 pairs in one batch");
-  HIPC(ensure(ctx->active, 2 * sizeof(ActiveList)));
+  {
+    uint64_t nr = 0;
+    for (const PairDesc& d : desc) nr += d.n_read;
+    HIPC(ensure(ctx->active, active_list_bytes(nr, P)));
+  }
   HIPC(ensure(ctx->ctrs, kCtrWords * 4));
   HIPC(ensure(ctx->pin_desc, 3 * P * sizeof(PairDesc)));
   HIPC(ensure(ctx->pin_state, P * sizeof(PairState)));
@@ -753,11 +730,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   // readings in Morton order inside each pair's range (kernels_order.hip): the overlap and
   // the ICP loop both visit the sorted copy
   const float4* readS = B->read_raw.as<float4>();
-  // Morton order from kReadOrderMin reading points on (AICP_READ_ORDER_MIN overrides): a single C2
-  // reading's NN launches gain less than its sort costs (the app bench, r05: 1.18-1.25 ms per
-  // overlap + registerClouds without, 1.29-1.37 with)
-  const char* rom = std::getenv("AICP_READ_ORDER_MIN");
-  const bool order = B->total_read >= (rom ? std::strtoull(rom, nullptr, 10) : kReadOrderMin);
+  // Morton order from read_order_min (200000) reading points on: a single C2 reading's NN launches
+  // gain less than its sort costs (the app bench, r05: 1.18-1.25 ms per overlap + registerClouds
+  // without, 1.29-1.37 with)
+  const bool order = B->total_read >= ctx->opt.read_order_min;
   if (read_hit) {  // the previous one-shot call's reading: its Morton-ordered copy is in read_s
     if (ctx->rdc.sorted) readS = ctx->read_s.as<float4>();
   } else if (!order) {
@@ -869,7 +845,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       // the NN kernel's LDS frames keep a node id (< 16 * (n_ref + 1)) in 26 bits
       for (size_t r = 0; r < R; ++r)
         if (ctx->pin_rdesc.as<PairDesc>()[r].n_ref > 4000000u) ctx->tl_total = 0;
-      if (force_trav1()) ctx->tl_total = 0;
+      if (ctx->opt.nn_engine == 1) ctx->tl_total = 0;
     }
     HIPC(ensure(ctx->rdesc_raw, R * sizeof(PairDesc)));
     HIPC(hipStreamWaitEvent(s2, ctx->ev[14], 0));  // the reference points (not the readings) are on the device
@@ -880,12 +856,12 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     for (const PairDesc& r : B->rdesc) n_ref_max = std::max<uint64_t>(n_ref_max, r.n_ref);
     // s3 (worker thread; it still polls its levels in a polled redo): centroid, centred
     // reference, matcher tree, pair frames
-    const int plan1 = plan_levels(n_ref_max, ctx->tb[1]);
+    const int plan1 = plan_levels(n_ref_max, ctx->tb[1], ctx->opt.tree_plan);
     // Large batches build the raw tree first and the matcher tree beside the normals' kNN
     // (raw_tree_first()): the raw tree gates the kNN, which gates the loop, while the matcher
     // tree is needed only by the loop; built together, the two trees' latency-bound subtree
     // kernels share the CUs' wave slots and both finish late.
-    const bool raw_first = raw_tree_first(B->total_ref);
+    const bool raw_first = raw_tree_first(B->total_ref, ctx->opt);
     if (!raw_first)
       worker = std::thread([&, plan1] { wrc = matcher_trees(ctx, B, cfg->bucket_size, dDesc, dRdesc, plan1, werr); });
     // SurfaceNormal runs on the reference as given, before the centring (ICP::compute,
@@ -895,9 +871,9 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     if (rc) return join_worker(rc);
     // s2: raw tree levels + subtrees, SurfaceNormal, all enqueued before the host waits for
     // the overlap's key boxes
-    const int rf = raw_first_mode();
+    const int rf = ctx->opt.raw_first_at;
     rc = device_trees_end(ctx->tb[0], ctx->err, s2, R, B->total_ref, ctx->rdesc_raw.as<PairDesc>(), kNormalsBucket,
-                          ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0], true), nullptr, true,
+                          ctx->bpts_raw, ctx->nodes_raw, plan_levels(n_ref_max, ctx->tb[0], ctx->opt.tree_plan, true), nullptr, true,
                           raw_first && rf == 2 ? ctx->ev[13] : nullptr);
     if (rc) return join_worker(rc);
     if (raw_first) {
@@ -908,11 +884,11 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     // normals on the raw tree (bucket order of that tree)
     HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
-    uint32_t* nCtr = dCtr + kXcdGroups * kCtrStride;
-    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
+    uint32_t* nCtr = dCtr + kKnnCtrOff;
+    HIPC(hipMemsetAsync(nCtr, 0, kPersistCtrWords * 4, s2));
     if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, ctx->rdesc_raw.as<PairDesc>(), dRstate,
                         ctx->nodes_raw.as<uint4>(), nullptr, ctx->bpts_raw.as<float4>(), ctx->nrm_raw.as<float4>(),
-                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr))
+                        cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr, ctx->opt.normals_knn_engine))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
     HIPC(hipEventRecord(ctx->ev[10], s2));
   }
@@ -975,8 +951,8 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       max_read = std::max(max_read, B->desc[i].n_read);
     }
     ActiveList* al = ctx->active.as<ActiveList>();
-    const int sel_ff = sel_fused_from();
-    const bool sel_pair = sel_pair_fits(P, max_read);
+    const int sel_ff = ctx->opt.select_fused_from;
+    const bool sel_pair = sel_pair_fits(P, max_read, ctx->opt.select_pair);
     // Polled loop (the sequence's, sequence.cpp): from iteration smoothLength on the update of
     // the last pair writes the next active count into mapped host memory; the host stays one
     // iteration ahead and stops enqueueing once it reads 0, instead of maxIterationCount launches
@@ -985,8 +961,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       HIPC(hipHostMalloc((void**)&ctx->poll_host, kBatchPolls * 4, hipHostMallocMapped));
       HIPC(hipHostGetDevicePointer((void**)&ctx->poll_dev, ctx->poll_host, 0));
     }
-    const char* nee = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
-    const bool early = !(nee && nee[0] == '1');
+    const bool early = !ctx->opt.no_early_exit;
     auto polled = [&](int k) { return early && k >= cfg->smooth_length && k < kBatchPolls && k < cfg->max_iter; };
     std::deque<int> pending;
     bool stop = false;
@@ -1039,7 +1014,7 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
                           ctx->touch.as<uint32_t>(), bpts, bnrm, ctx->slab.as<double>(), prm, y);
     }
     launch_finalize(s, (int)P, dDesc, dState, ctx->outT.as<float>());
-    if (prof_enabled()) {  // diagnostic builds' counters (AICP_XCD_PROF / AICP_NN_PROF / AICP_ITER_PROF)
+    if (ctx->opt.profile) {  // the diagnostic build's counters (-DAICP_DIAG=1)
       HIPC(hipStreamSynchronize(s));
       nn_prof_dump();
       tree_prof_dump();
@@ -1162,6 +1137,42 @@ extern "C" {
 
 const char* aicp_hip_version(void) { return "aicp_hip 0.1 (gfx950)"; }
 
+void aicp_hip_default_options(aicp_hip_options* o) {
+  if (!o) return;
+  *o = aicp_hip_options{};
+  o->select_pair = -1;
+  o->select_fused_from = 3;  // (iterations 1-2 missed the guessed bin on C2 2 times in 3, 3+ never: r05)
+  o->raw_tree_first = -1;
+  o->raw_first_at = 2;
+  o->tree_lvl_min = 1u << 22;
+  o->reference_cache = 1;
+  o->oneshot_keep_mib = 4096;
+  o->read_order_min = kReadOrderMin;
+}
+
+int aicp_hip_set_options(aicp_hip_ctx* ctx, const aicp_hip_options* o) {
+  if (!ctx || !o) return AICP_ERR_INVALID;
+  if (o->nn_engine < 0 || o->nn_engine > 1 || o->overlap_path < 0 || o->overlap_path > 1 ||
+      o->normals_knn_engine < 0 || o->normals_knn_engine > 2 || o->select_pair < -1 || o->select_pair > 1 ||
+      o->select_fused_from < 0 || o->raw_tree_first < -1 || o->raw_tree_first > 1 || o->raw_first_at < 1 ||
+      o->raw_first_at > 2 || o->tree_plan < -1 || o->reference_cache < 0 || o->reference_cache > 1)
+    FAIL(AICP_ERR_INVALID, "aicp_hip_set_options: value out of range");
+  // the reference cache was built under the previous options (engine, tree plan): drop it
+  ctx->refc.invalidate();
+  ctx->rdc.valid = false;
+  ctx->opt = *o;
+  for (auto& t : ctx->tb) tree_opts(t, ctx->opt);
+  return AICP_OK;
+}
+
+int aicp_hip_get_options(const aicp_hip_ctx* ctx, aicp_hip_options* out) {
+  if (!ctx || !out) return AICP_ERR_INVALID;
+  *out = ctx->opt;
+  return AICP_OK;
+}
+
+int aicp_hip_test_force_scan_stall(int on) { return set_lb_force_stall(on) == hipSuccess ? AICP_OK : AICP_ERR_HIP; }
+
 int aicp_hip_create(int device, aicp_hip_ctx** out) {
   if (!out) return AICP_ERR_INVALID;
   *out = nullptr;
@@ -1171,6 +1182,8 @@ int aicp_hip_create(int device, aicp_hip_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return AICP_ERR_HIP;
   aicp_hip_ctx* c = new aicp_hip_ctx();
   c->device = device;
+  aicp_hip_default_options(&c->opt);
+  for (auto& t : c->tb) tree_opts(t, c->opt);
   // the overlap (stream) yields the CUs to the kd-tree streams, whose chains of short
   // level kernels are the critical path before the ICP loop
   int prio_lo = 0, prio_hi = 0;
@@ -1206,6 +1219,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
   release(ctx->ovl_sp);
   release(ctx->ovl_keys);
   release(ctx->isync);
+  release(ctx->refc.gst);
   release(ctx->pin_crop);
   release(ctx->pin_maps);
   if (ctx->poll_host) (void)hipHostFree(ctx->poll_host);
@@ -1254,7 +1268,6 @@ int aicp_hip_batch_run(aicp_hip_ctx* ctx, aicp_hip_batch* batch, const aicp_icp_
   return run_batch(ctx, batch, cfg, resolution, flags, out_T, stats, nullptr);
 }
 
-constexpr size_t kOneshotKeepBytes = size_t(16) << 30;
 
 namespace {
 
@@ -1308,6 +1321,10 @@ bool refcache_begin(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pa
                     int flags) {
   RefCache& c = ctx->refc;
   c.use = c.hit_trees = c.hit_ovl = false;
+  if (!ctx->opt.reference_cache) {  // (aicp_hip_options: nothing kept, copied or compared)
+    c.invalidate();
+    return false;
+  }
   if (!pairs || n == 0 || !valid_pair(pairs[0])) return false;
   const aicp_pair& p = pairs[0];
   bool one_origin = true;
@@ -1362,7 +1379,7 @@ int oneshot(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pair
   int rc = upload_pairs(ctx, pairs, n_pairs, B, false, skip_refs, rd.hit, true);
   const auto h3 = clk::now();
   if (!rc) rc = run_batch(ctx, B, cfg, resolution, flags, out_T, stats, out_overlap);
-  if (prof_enabled()) {  // host time per part of a one-shot call (us)
+  if (ctx->opt.profile) {  // host time per part of a one-shot call (us)
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     const auto h4 = clk::now();
     std::fprintf(stderr, "[aicp oneshot] flags %d pairs %zu: reference compare %.0f, reading compare %.0f, upload %.0f, run %.0f us%s%s\n",
@@ -1377,7 +1394,7 @@ int oneshot(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pair
     ctx->refc.invalidate();  // (an error may leave the reference side half written)
     (void)hipStreamSynchronize(ctx->stream);  // (the staging copies of upload_pairs are not awaited there)
   }
-  rd.valid = !rc && p0;
+  rd.valid = !rc && p0 && ctx->opt.reference_cache;
   if (rd.valid && !was_hit) {  // the reading this call uploaded: its copy for the next call's compare
     rd.ptr = p0->read;
     rd.n = p0->n_read;
@@ -1386,7 +1403,7 @@ int oneshot(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_pair* pair
     copy_points(ctx_pool(ctx), p0->read, p0->n_read, p0->read_stride, rd.pts.data());
   }
   // the input copies of a very large one-shot batch are not kept for the next call
-  if (B->ref_raw.cap + B->read_raw.cap > kOneshotKeepBytes) {
+  if (B->ref_raw.cap + B->read_raw.cap > ((size_t)ctx->opt.oneshot_keep_mib << 20)) {
     (void)hipStreamSynchronize(ctx->stream);
     release(B->ref_raw);
     release(B->read_raw);
@@ -1611,7 +1628,8 @@ int aicp_hip_normals(aicp_hip_ctx* ctx, const float* pts, size_t n, size_t strid
   launch_init_state(st_, 1, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>());
   if (!launch_normals(st_, 1, (uint32_t)n, ctx->desc.as<PairDesc>(), ctx->state.as<PairState>(),
                       ctx->nodes.as<uint4>(), nullptr, ctx->bpts.as<float4>(),
-                      ctx->bnrm.as<float4>(), knn, ctx->nbids.as<int32_t>(), ctx->ctrs.as<uint32_t>()))
+                      ctx->bnrm.as<float4>(), knn, ctx->nbids.as<int32_t>(), ctx->ctrs.as<uint32_t>(),
+                      ctx->opt.normals_knn_engine))
     FAIL(AICP_ERR_UNSUPPORTED, "knn must be 10, 20 or 30");
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(st_));
@@ -1798,7 +1816,7 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   unsigned long long* dtouch = (unsigned long long*)(ctx->ctrs.as<uint32_t>() + kCtrWords);
   HIPC(hipEventRecord(E[2], s));
   if (!launch_knn_ids(s, 1, V, ctx->desc.as<PairDesc>(), ctx->nodes.as<uint4>(), bpts, K, ctx->match.as<int32_t>(),
-                      ctx->ctrs.as<uint32_t>(), dtouch))
+                      ctx->ctrs.as<uint32_t>(), dtouch, ctx->opt.normals_knn_engine))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(E[3], s));

@@ -27,15 +27,17 @@ void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const floa
                        const int32_t* perm, float4* bpts);
 void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st);
 // SurfaceNormal of the reference points (bucket order); ids: scratch of total_ref * knn;
-// ctr: zeroed work counter. Returns false if knn is unsupported.
+// ctr: zeroed work counters (kPersistCtrWords). engine: aicp_hip_options::normals_knn_engine.
+// Returns false if knn is unsupported.
 bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
-                    int32_t* ids, uint32_t* ctr);
+                    int32_t* ids, uint32_t* ctr, int engine);
 // the kNN of every reference point in its own tree (bucket order in and out: ids are bucket
 // positions of the pair's tree, -1 past the cloud size); eps 0, self included. touched
 // (nullable, zeroed): += touched points, inner nodes
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
-                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched);
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
+                    int engine);
 // host_n (nullable): device pointer of mapped host memory that receives the active count;
 // done_sig (nullable, signal memory): once no pair is active, the final corrections go to outT
 // and *ticket is stored to done_sig (the sequence's next reference waits on it)
@@ -76,10 +78,10 @@ void launch_icp_select_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairStat
 // the whole select of each pair in one workgroup (batches of many pairs of <= 65536 readings)
 void launch_icp_select_pair(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st, const float* d2,
                             uint32_t* cand, const IcpIterSync& y);
-bool sel_pair_fits(size_t n_pairs, uint64_t max_read);
+// force: aicp_hip_options::select_pair (-1 auto, 0 off, 1 on)
+bool sel_pair_fits(size_t n_pairs, uint64_t max_read, int force);
 void launch_icp_select_fused(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float* d2,
                              uint32_t* hist1, uint32_t* cand, uint32_t* cand_cnt, const IcpIterSync& y);
-int sel_fused_from();
 void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float4* read_c,
                          const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,
                          const float4* bnrm, double* slab, const IcpParams& prm, const IcpIterSync& y);
@@ -152,8 +154,10 @@ struct TreeWork {
   uint64_t* lb;          // look-back words of the build's scans (lb_bytes), zeroed by launch_tree_prepare
   size_t lb_stride;      // words per scan
   uint32_t mid_max;      // segments up to this size leave the global levels (kMidMax; kSubMax: no mid builder)
+  uint32_t lvl_min;      // the level-synchronous subtree builder from this many points (aicp_hip_options)
 };
 uint32_t tree_mid_max();
+hipError_t set_lb_force_stall(int on);  // aicp_hip_test_force_scan_stall
 size_t tree_sum_tiles(size_t n);  // k_tr_sum's tiles over n points
 size_t tree_scan_temp_bytes(size_t n);
 size_t lb_bytes(uint32_t total);

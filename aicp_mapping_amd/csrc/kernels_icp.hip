@@ -841,12 +841,23 @@ __device__ unsigned long long g_iter_prof[16];
 // blockIdx % 8 == g, which the dispatcher places on one XCD (MI355X_MICROARCH.md, workgroup
 // dispatch: speed only, never correctness -- any placement still processes every slot exactly
 // once). Consecutive slots belong to the same pair, so each XCD's 4 MiB L2 holds the trees of
-// ~P/8 pairs instead of all P. Each group has its own counter (64-byte stride); a wave takes
-// 64-slot chunks (one atomic each) and hands their slots to the lanes that need work in lane
-// order, so a lane starts a new query as soon as its previous one completes.
+// ~P/8 pairs instead of all P. A wave takes 64-slot chunks (one returning atomic each) and hands
+// their slots to the lanes that need work in lane order, so a lane starts a new query as soon as
+// its previous one completes.
+// r06: a group's range is cut into kHeads contiguous parts with a head each (one 64-byte line
+// apiece). One head served all ~1024 waves of a group: a word takes ~88 returning atomics per us
+// (MI355X_MICROARCH.md, "dequeue"), so the last wave of a full-chip launch got its first chunk
+// ~12 us after the first. A wave starts at head (its index in the group) mod kHeads and, when
+// that part is exhausted, moves to a part of the same group still open (the exhausted parts are
+// bits of one more word): the work stays on the group's XCD and every chunk is still served
+// exactly once.
 //   on_chunk(base)      wave-uniform, once per chunk, before its slots are handed out
 //   fetch(slot, eng)    initialises a lane's query; false: the slot has no work
 //   done(slot, eng)     consumes the result
+// ctr: kGroupCtrs * kXcdGroups counters at kCtrStride words, zero at the launch
+__device__ __forceinline__ uint32_t head_lo(uint32_t lo, uint32_t hi, uint32_t h) {
+  return h >= (uint32_t)kHeads ? hi : lo + ((uint32_t)(((uint64_t)(hi - lo) * h) / kHeads) & ~63u);
+}
 template <class Eng, class OnChunk, class Fetch, class Done>
 __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, float maxE2, float maxR2,
                                                const uint4* __restrict__ nodes, const float4* __restrict__ pts,
@@ -857,7 +868,10 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
   // round-robin instead measured equal on C2 windows, r03.)
   const uint32_t lo = (uint32_t)(((uint64_t)total * g) / kXcdGroups) & ~63u;
   const uint32_t hi = g + 1 == kXcdGroups ? total : (uint32_t)(((uint64_t)total * (g + 1)) / kXcdGroups) & ~63u;
-  uint32_t* gctr = ctr + g * kCtrStride;
+  uint32_t* gctr = ctr + g * kGroupCtrs * kCtrStride;
+  // this wave's head: consecutive waves of the group on different heads
+  uint32_t h = ((blockIdx.x / kXcdGroups) * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kHeads;
+  h = __builtin_amdgcn_readfirstlane(h);
   Eng t;
   typename Eng::Stack fs;
   bool has = false;
@@ -882,16 +896,27 @@ __device__ __forceinline__ void persistent_xcd(uint32_t total, uint32_t* ctr, fl
       const uint64_t needm = __ballot(!has);
       if (needm == 0 || exhausted) break;
       if (pool >= pool_end) {
-        uint32_t base = 0;
-        if (lane == 0)
-          base = lo + atomicAdd(gctr, 64u);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (base >= hi) {
-          exhausted = true;
-          break;
+        uint32_t base = 0, end = 0;
+        for (;;) {
+          const uint32_t hl = head_lo(lo, hi, h);
+          end = head_lo(lo, hi, h + 1);
+          uint32_t b = 0;
+          if (lane == 0) b = atomicAdd(gctr + h * kCtrStride, 64u);
+          base = hl + __builtin_amdgcn_readfirstlane(b);
+          if (base < end) break;
+          // part h is exhausted: mark it, go on with the next part still open
+          uint32_t m = 0;
+          if (lane == 0) m = atomicOr(gctr + kHeads * kCtrStride, 1u << h);
+          m = __builtin_amdgcn_readfirstlane(m) | (1u << h);
+          if (m == (1u << kHeads) - 1u) {
+            exhausted = true;
+            break;
+          }
+          h = (uint32_t)__builtin_ctz(~m & ((1u << kHeads) - 1u));
         }
+        if (exhausted) break;
         pool = base;
-        pool_end = min(base + 64u, hi);
+        pool_end = min(base + 64u, end);
         if constexpr (std::is_invocable_v<OnChunk, uint32_t, Eng&>) on_chunk(base, t);  // may set uniform engine state
         else on_chunk(base);
       }
@@ -1031,9 +1056,11 @@ __device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, c
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t wcnt[16];
   __shared__ uint32_t carry_off, carry_cnt;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = (int)blockDim.x;
+  __shared__ uint32_t r_off[1024];  // first slot of each entry of the current round
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = (int)blockDim.x, nw = nt >> 6;
+  uint16_t* chunk = al_chunks(al);
   if (t == 0) carry_off = carry_cnt = 0;
-  if (t < kXcdGroups) ctr[t * kCtrStride] = 0;
+  if (t < kXcdGroups * kGroupCtrs) ctr[t * kCtrStride] = 0;
   __syncthreads();
   for (int base = 0; base < n_pairs; base += nt) {
     const int p = base + t;
@@ -1058,17 +1085,31 @@ __device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, c
       wcnt[wave] = c;
     }
     __syncthreads();
-    uint32_t bo = carry_off, bc = carry_cnt;
+    const uint32_t e0 = carry_cnt, o0 = carry_off;  // this round's first entry and slot
+    uint32_t bo = o0, bc = e0;
     for (int w = 0; w < wave; ++w) {
       bo += wsum[w];
       bc += wcnt[w];
     }
+    uint32_t rn = 0, rs = 0;  // entries and slots of the whole round
+    for (int w = 0; w < nw; ++w) {
+      rn += wcnt[w];
+      rs += wsum[w];
+    }
     if (a) {
-      const uint32_t e = bc + c - 1;
+      const uint32_t e = bc + c - 1, o = bo + x - v;
       al->pair[e] = p;
-      al->off[e] = bo + x - v;
+      al->off[e] = o;
+      const PairDesc& d = pd[p];
+      al->ent[e] = NnEntry{o, d.n_read, d.read_off, d.tl_off, d.node_off, d.ref_off, p, 0u};
+      r_off[e - e0] = o;
     }
     __syncthreads();
+    // the chunk table of this round's entries: wave w fills entries w, w + nw, ...
+    for (uint32_t i = (uint32_t)wave; i < rn; i += (uint32_t)nw) {
+      const uint32_t c0 = r_off[i] >> 6, c1 = (i + 1 < rn ? r_off[i + 1] : o0 + rs) >> 6;
+      for (uint32_t j = c0 + (uint32_t)lane; j < c1; j += 64) chunk[j] = (uint16_t)(e0 + i);
+    }
     if (t == nt - 1) {
       carry_off = bo + x;
       carry_cnt = bc + c;
@@ -1568,20 +1609,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AICP_NN_WAV
       total, ctr, prm.maxE2, prm.maxR2, nodes, bpts,
       [&](uint32_t base, Eng& t) {
         if constexpr (std::is_same<Eng, Trav2C>::value) t.bind_batch(nodes, ptl);
-        int lo = 0, hi = (int)al->n - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (al->off[mid] <= base) lo = mid;
-          else hi = mid - 1;
-        }
-        c_pair = __builtin_amdgcn_readfirstlane(al->pair[lo]);
-        c_lo = __builtin_amdgcn_readfirstlane(al->off[lo]);
-        const PairDesc& d = pd[c_pair];
-        c_n = __builtin_amdgcn_readfirstlane(d.n_read);
-        c_read = __builtin_amdgcn_readfirstlane(d.read_off);
-        if constexpr (is_coop<Eng>::value) c_node = __builtin_amdgcn_readfirstlane(d.tl_off);
-        else c_node = __builtin_amdgcn_readfirstlane(d.node_off);
-        c_ref = __builtin_amdgcn_readfirstlane(d.ref_off);
+        // the chunk's entry (u16 table, read as its aligned dword), then the entry: two
+        // dependent scalar loads
+        const uint32_t c = base >> 6;
+        const uint32_t w2 = reinterpret_cast<const uint32_t*>(al_chunks(al))[c >> 1];
+        const uint32_t e = __builtin_amdgcn_readfirstlane((w2 >> ((c & 1u) << 4)) & 0xffffu);
+        const NnEntry& en = al->ent[e];
+        c_pair = __builtin_amdgcn_readfirstlane(en.pair);
+        c_lo = __builtin_amdgcn_readfirstlane(en.off);
+        c_n = __builtin_amdgcn_readfirstlane(en.n_read);
+        c_read = __builtin_amdgcn_readfirstlane(en.read_off);
+        if constexpr (is_coop<Eng>::value) c_node = __builtin_amdgcn_readfirstlane(en.tl_off);
+        else c_node = __builtin_amdgcn_readfirstlane(en.node_off);
+        c_ref = __builtin_amdgcn_readfirstlane(en.ref_off);
       },
       [&](uint32_t s, Eng& t) {
         const uint32_t j = s - c_lo;
@@ -2894,9 +2934,9 @@ void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState
 }
 bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,
-                    int32_t* ids, uint32_t* ctr) {
+                    int32_t* ids, uint32_t* ctr, int engine) {
   if (!total_ref) return true;
-  if (!launch_knn_ids(s, n_pairs, total_ref, pd, nodes, bpts, knn, ids, ctr, nullptr)) return false;
+  if (!launch_knn_ids(s, n_pairs, total_ref, pd, nodes, bpts, knn, ids, ctr, nullptr, engine)) return false;
   const int gu = (int)((total_ref + 255) / 256);
   switch (knn) {
     case 10: k_normals_from_ids<10><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm); break;
@@ -2906,24 +2946,22 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   }
   return true;
 }
-// k_knn_oct for launches of at most kKnnOctMax queries (AICP_KNN_OCT=0: never, =1: always --
-// tests compare the engines): with eight lanes per query it issues ~2.3x the VALU instructions of
+// k_knn_oct for launches of at most kKnnOctMax queries (engine 2: never, 1: always -- tests
+// compare the engines): with eight lanes per query it issues ~2.3x the VALU instructions of
 // the per-lane engine, which pays only while the per-lane launch leaves the chip short of waves
 // (the C2 stream's single 120k-point reference: 377 -> 245 us); on C5's 61 M queries it ran
 // 91.7 ms per launch against the per-lane engine's throughput (C5 3962 -> 3097 clouds/s, r03c).
 // (Quads, 4 lanes per query, measured equal to octets on C2, r03.)
 constexpr uint32_t kKnnOctMax = 300000;
-static bool knn_oct_enabled(uint32_t n_queries) {  // (the environment is read per launch: tests switch engines)
-  const char* e = std::getenv("AICP_KNN_OCT");
-  if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
-  return n_queries <= kKnnOctMax;
+static bool knn_oct_enabled(uint32_t n_queries, int engine) {
+  return engine == 0 ? n_queries <= kKnnOctMax : engine == 1;
 }
 
 bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, const uint4* nodes,
-                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched) {
+                    const float4* bpts, int knn, int32_t* ids, uint32_t* ctr, unsigned long long* touched,
+                    int engine) {
   if (!total_ref) return true;
-  if (knn_oct_enabled(total_ref)) {
+  if (knn_oct_enabled(total_ref, engine)) {
     const unsigned go = (unsigned)(((uint64_t)total_ref * 8 + 255) / 256);
     switch (knn) {
       case 10: k_knn_oct<10, 8><<<go, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, bpts, ids, touched); break;
@@ -3105,15 +3143,10 @@ void launch_icp_select_pair(hipStream_t s, int n_pairs, const PairDesc* pd, Pair
                             uint32_t* cand, const IcpIterSync& y) {
   if (n_pairs > 0) k_sel_pair<<<n_pairs, kSelPairThreads, 0, s>>>(pd, st, d2, cand, y);
 }
-bool sel_pair_fits(size_t n_pairs, uint64_t max_read) {  // AICP_SEL_PAIR=0/1 forces it off / on
-  const char* e = std::getenv("AICP_SEL_PAIR");
+bool sel_pair_fits(size_t n_pairs, uint64_t max_read, int force) {
   if (max_read > kSelPairMax) return false;
-  if (e) return e[0] == '1';
+  if (force >= 0) return force == 1;
   return n_pairs >= 256;
-}
-int sel_fused_from() {  // AICP_SEL_FUSED=k: the fused select from iteration k on (0: never)
-  const char* e = std::getenv("AICP_SEL_FUSED");
-  return e ? std::atoi(e) : 3;  // (iterations 1-2 missed the guess on C2 2 times in 3, 3+ never: r05 log)
 }
 void launch_icp_reduce_f(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st, const float4* read_c,
                          const int32_t* match, const float* d2, const uint32_t* touched, const float4* bpts,

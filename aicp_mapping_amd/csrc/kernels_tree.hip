@@ -193,8 +193,16 @@ __device__ __forceinline__ float seg_cut(const TreeSeg& s) {
 // have started), its aggregate published at once, its inclusive prefix once the look-back over
 // the predecessors' words (flag << 32 | value, one 64-bit word each) reaches an inclusive one.
 // The counts are computed inside (a predicate: no flag array, no separate flag kernel). `st` holds the
-// ticket and one word per tile, zeroed before the launch; a stalled look-back (impossible while
-// tiles only wait on earlier tickets) gives up after a bounded spin and reports ctl->error 16.
+// ticket and one word per tile, zeroed before the launch.
+// A stalled look-back (impossible while tiles only wait on earlier tickets) gives up after a
+// bounded spin, reports ctl->error 16 (the host then fails the call with AICP_ERR_HIP) and takes
+// the slow path: the tile's wave 0 sums the predicate over every position before the tile itself
+// (val is a pure function of inputs the scan does not write), so the prefix it writes and
+// publishes is the exact one and no later kernel of the build indexes with a partial prefix.
+// (r05 lost a box to the pattern "time out, then go on with what was there": a grid barrier that
+// timed out and left garbage indices behind.) g_lb_force_stall (test hook,
+// aicp_hip_test_force_scan_stall) sends every tile but the first down the slow path.
+__device__ int g_lb_force_stall;
 constexpr int kLbThreads = 256;
 constexpr int kLbItems = 8;
 constexpr uint32_t kLbTile = kLbThreads * kLbItems;
@@ -244,7 +252,8 @@ __device__ __forceinline__ void lookback_scan(uint32_t n, Val val, uint32_t* __r
       if (lane == 0) __hip_atomic_store(&tw[tile], kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int64_t top = (int64_t)tile - 1;  // the nearest predecessor not summed yet
       uint32_t spins = 0;
-      for (;;) {
+      bool stalled = __hip_atomic_load(&g_lb_force_stall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      while (!stalled) {
         const int64_t idx = top - lane;
         const uint64_t w = idx >= 0 ? __hip_atomic_load(&tw[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                     : kLbIncl;
@@ -254,7 +263,7 @@ __device__ __forceinline__ void lookback_scan(uint32_t n, Val val, uint32_t* __r
         const uint64_t need = first == 64 ? ~0ull : ((2ull << first) - 1ull);
         if (zero & need) {  // a predecessor up to there has not published yet
           if (++spins > (1u << 22)) {
-            if (lane == 0) atomicOr(&ctl->error, 16);
+            stalled = true;
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -266,6 +275,15 @@ __device__ __forceinline__ void lookback_scan(uint32_t n, Val val, uint32_t* __r
         excl += part;
         if (first < 64) break;
         top -= 64;
+      }
+      if (stalled) {  // the exact prefix the slow way (see above)
+        if (lane == 0) atomicOr(&ctl->error, 16);
+        uint32_t part = 0;
+        const uint32_t end = min(tile * kLbTile, n);
+        for (uint32_t i = (uint32_t)lane; i < end; i += 64) part += val(i);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+        excl = part;
       }
       if (lane == 0) __hip_atomic_store(&tw[tile], kLbIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2008,10 +2026,11 @@ uint32_t tree_mid_max() { return (uint32_t)kMidMax; }
 size_t tree_sum_tiles(size_t n) { return tiles_of(n); }
 // k_tr_subtree_lvl from this many points of a build (C5: 61 M); smaller builds are latency-bound
 // and keep k_tr_subtree_blk (r04: C2 2620 against 2479 clouds/s with the level builder).
-// AICP_TREE_LVL_MIN overrides it (the equivalence test builds small trees both ways).
-uint32_t tree_lvl_min() {
-  const char* e = std::getenv("AICP_TREE_LVL_MIN");
-  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (1u << 22);
+// aicp_hip_options::tree_lvl_min sets it (TreeWork::lvl_min; the equivalence test builds small
+// trees both ways).
+hipError_t set_lb_force_stall(int on) {
+  const int v = on ? 1 : 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_lb_force_stall), &v, sizeof(v));
 }
 size_t lb_bytes(uint32_t total) { return (size_t)(2 * kFarStack + 3) * lb_stride_words(total) * 8; }
 
@@ -2065,7 +2084,7 @@ hipError_t launch_tree_level(hipStream_t s, int level, uint32_t total, const Tre
 hipError_t launch_tree_subtrees(hipStream_t s, uint32_t total, const TreeWork& w, float4* bpts, int bucket) {
   const size_t bound = std::min<size_t>(w.max_seg, (size_t)total / (size_t)(bucket + 1) + (size_t)w.n_pairs + 1);
   const bool blk = bucket >= 4;  // level widths fit kSubLevelCap
-  if (bucket >= 8 && total >= tree_lvl_min()) {  // level widths fit kLvlCap
+  if (bucket >= 8 && total >= w.lvl_min) {  // level widths fit kLvlCap
     const unsigned gl = (unsigned)std::max<size_t>(1, std::min<size_t>(bound, 2048));
     k_tr_subtree_lvl<<<gl, kLvlThreads, 0, s>>>(total, w.ctl, w.subs, w.W[0], bpts, w.ev, w.valid, w.ecnt,
                                                  w.pair_depth, bucket);

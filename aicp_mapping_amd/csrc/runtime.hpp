@@ -147,6 +147,8 @@ struct TreeBufs {
   TreeWork tw{};    // device_trees_begin -> device_trees_end
   int planned = 0;  // global levels enqueued without host polling (0: polled build)
   int needed = 0;   // global levels the last planned build actually used
+  uint32_t lvl_min = 1u << 22;  // aicp_hip_options::tree_lvl_min of the owning context
+  bool prof = false;            // aicp_hip_options::profile
   void release_all() {
     for (DevBuf* b : {&W0, &W1, &segof0, &segof1, &seg0, &seg1, &flag, &X1, &X2, &posL, &posR, &ev, &valid, &subs,
                       &mids, &ecnt, &lb, &sums, &pdepth, &ctl, &scan})
@@ -184,9 +186,8 @@ void pack_many(const std::vector<PackSeg>& segs, WorkerPool* pool = nullptr);
 void pack_xyz4(const float* src, uint64_t n, uint64_t stride_bytes, float* dst4);
 bool valid_pair(const aicp_pair& p);
 double ev_ms(hipEvent_t a, hipEvent_t b);
-bool force_trav1();
-bool force_sparse_overlap();  // AICP_OVL_SPARSE=1: every overlap on the sorted-key path (tests)
-bool prof_enabled();  // AICP_PROF=1: diagnostic output (stderr) only
+// the context options a tree buffer set follows (tree_lvl_min, profile)
+void tree_opts(TreeBufs& T, const aicp_hip_options& o);
 
 // Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device (kernels_tree.hip).
 // launch = false: allocate the work space only (nothing enqueued; before a stream capture)
@@ -201,7 +202,8 @@ int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uin
 // errors of a planned build whose control block is in hctl (after its stream completed)
 int device_trees_check_ctl(TreeBufs& T, const TreeCtl* hctl, std::string& err);
 int device_trees_check(TreeBufs& T, std::string& err);
-int plan_levels(uint64_t n_max, const TreeBufs& T, bool lean = false);
+// force: aicp_hip_options::tree_plan
+int plan_levels(uint64_t n_max, const TreeBufs& T, int force, bool lean = false);
 int check_cfg(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, int flags);
 
 // The drop-in path's reference cache. App registers reading after reading against one reference
@@ -307,6 +309,7 @@ struct aicp_hip_ctx {
   aicp::rt::WorkerPool* pool = nullptr;  // host threads of the one-shot calls (packing, the reference compare)
   uint32_t* poll_host = nullptr;  // the batch loop's active counts (hipHostMalloc, mapped), kBatchPolls words
   uint32_t* poll_dev = nullptr;
+  aicp_hip_options opt{};  // aicp_hip_set_options (read by the calls; nothing reads the environment)
 };
 constexpr int kBatchPolls = 64;
 

@@ -82,7 +82,6 @@ struct GraphCache {
   }
 };
 
-bool seq_prof() { return prof_enabled(); }  // AICP_PROF=1: host time per part and device phase times (stderr)
 
 struct Key {
   std::vector<uint64_t> v;
@@ -99,10 +98,6 @@ struct Key {
 constexpr int kSlots = 3;  // window slots in flight (>= 2: a window reads the previous slot's reading)
 constexpr int kMaxPolls = 64;  // ICP iterations that can end a window's loop early
 
-bool early_exit_disabled() {  // AICP_SEQ_NO_EARLY_EXIT=1: every window runs maxIterationCount launches (tests)
-  const char* e = std::getenv("AICP_SEQ_NO_EARLY_EXIT");
-  return e && e[0] == '1';
-}
 
 struct SeqSlot {
   // reading side (window-local offsets)
@@ -127,14 +122,15 @@ struct SeqSlot {
 
 struct SeqState {
   hipStream_t s_up = nullptr, s_rd = nullptr, s_r2 = nullptr, s_r3 = nullptr, s_icp = nullptr;
-  hipStream_t s_probe = nullptr;  // seq_prof(): an idle stream whose markers time the host's enqueue
+  hipStream_t s_probe = nullptr;  // opt.profile: an idle stream whose markers time the host's enqueue
   SeqSlot slot[kSlots];
   DevBuf desc, state, outT;
   DevBuf initT;  // debug working mode: initialT_ (16 floats), then its value before each reading
   PinBuf pin_state, pin_out, pin_ctl, pin_desc;
   std::vector<hipEvent_t> nn_ev;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;
-  std::vector<hipEvent_t> tev;  // seq_prof(): 10 timing events per window
+  std::vector<hipEvent_t> tev;  // opt.profile: 10 timing events per window
+  aicp_hip_options opt{};        // the context's options at the start of the running call
   WorkerPool pool{std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1};
   aicp_sequence_timing last{};
   int device = 0;
@@ -334,7 +330,7 @@ struct WinRun {
   TreeCtl* ctl_w = nullptr;
   const PairDesc* src_desc = nullptr;   // the reference source's descriptor and correction
   const float* src_T = nullptr;
-  // seq_prof(): ref start, matcher done, normals done, ICP start, ICP done, commit done, host at the
+  // S->opt.profile: ref start, matcher done, normals done, ICP start, ICP done, commit done, host at the
   // next reference's enqueue (a marker on an idle stream), its upload ready on r3, reading side
   // start and end
   hipEvent_t* tev = nullptr;
@@ -400,7 +396,7 @@ static int win_upload(C* ctx, SeqState* S, const aicp_icp_config* cfg, const aic
   for (size_t i = 0; i < np; ++i) nread += rd[w.p0 + i].n;
   // slot buffers (sizes grow to the largest window seen)
   const size_t tl_cap = 4 * (size_t)n_ref + 4;
-  const bool use_tl = cfg->bucket_size <= 15 && n_ref <= 4000000u && tl_cap < (1ull << 28) && !force_trav1();
+  const bool use_tl = cfg->bucket_size <= 15 && n_ref <= 4000000u && tl_cap < (1ull << 28) && S->opt.nn_engine != 1;
   constexpr uint32_t kRedBlk = kNNBlock * kReducePerThread * kReduceChunks;
   if (sl.used) {
     // the slot's previous window (w - K) must be done before its buffers are rewritten, and so
@@ -422,7 +418,7 @@ static int win_upload(C* ctx, SeqState* S, const aicp_icp_config* cfg, const aic
   HIPC(ensure(sl.sel_hist, np * kHistBins * 4));
   HIPC(ensure(sl.sel_cnt, np * 4));
   HIPC(ensure(sl.ctrs, kCtrWords * 4));
-  HIPC(ensure(sl.active, sizeof(ActiveList)));
+  HIPC(ensure(sl.active, active_list_bytes(nread, np)));
   HIPC(ensure(sl.ref_raw, (size_t)n_ref * 16));
   HIPC(ensure(sl.bpts, (size_t)n_ref * 16));
   HIPC(ensure(sl.bnrm, (size_t)n_ref * 16));
@@ -511,7 +507,7 @@ static int win_upload(C* ctx, SeqState* S, const aicp_icp_config* cfg, const aic
   // a window whose maps do not fit the budget runs its overlap on sorted key lists: sized by host
   // bounds of the rays' keys (readings from their own points; the reference for any rigid
   // motion of its source), so the stream needs no read-back
-  const bool sparse = doOvl && (force_sparse_overlap() || bm > kSeqMapBudget);
+  const bool sparse = doOvl && (S->opt.overlap_path == 1 || bm > kSeqMapBudget);
   std::vector<OvlCloud> scl;
   std::vector<uint32_t> sbc, sbs;
   uint64_t cap_r = 0, cap_g = 0;
@@ -837,12 +833,12 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     HIPC(ensure(sl.ptl, tl_cap * 8));
     HIPC(ensure(sl.tl_rank, ((size_t)ncap + 1) * 4));
   }
-  const int plan0 = plan_levels(n_ref, sl.tb[0]), plan1 = plan_levels(n_ref, sl.tb[1]);
+  const int plan0 = plan_levels(n_ref, sl.tb[0], S->opt.tree_plan), plan1 = plan_levels(n_ref, sl.tb[1], S->opt.tree_plan);
   const bool capturable = plan0 > 0 && plan1 > 0;  // (a host-polled build cannot be captured)
   // ---- r2: raw-coordinate tree + SurfaceNormal (reference as given)
   hipStream_t s2 = S->s_r2;
   HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
-  uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kXcdGroups * kCtrStride;
+  uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kKnnCtrOff;
   auto raw_build = [&]() -> int {
     launch_init_state(s2, 1, dRraw, dRst);
     int r = device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
@@ -851,9 +847,10 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     r = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw, plan0,
                          ctl_w, !capturable);
     if (r) return r;
-    HIPC(hipMemsetAsync(nCtr, 0, kXcdGroups * kCtrStride * 4, s2));
+    HIPC(hipMemsetAsync(nCtr, 0, kPersistCtrWords * 4, s2));
     if (!launch_normals(s2, 1, n_ref, dRraw, dRst, sl.nodes_raw.as<uint4>(), nullptr, sl.bpts_raw.as<float4>(),
-                        sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr))
+                        sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr,
+                        S->opt.normals_knn_engine))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
     HIPC(hipGetLastError());
     return AICP_OK;
@@ -1020,7 +1017,7 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   IcpParams ip = icp_params(cfg);
   ip.prof_slot = nn_launches;
   auto polled = [&](int k) {
-    return !early_exit_disabled() && k >= cfg->smooth_length && k < kMaxPolls && k < cfg->max_iter;
+    return !S->opt.no_early_exit && k >= cfg->smooth_length && k < kMaxPolls && k < cfg->max_iter;
   };
   // poll slot k holds the active count at the start of iteration k, written by the launch that
   // builds that iteration's active list (k_active_list at it = 0, else the previous update)
@@ -1056,7 +1053,7 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
   y.al = al;
   y.ctr = ctr;
   y.host_n = hn_next;
-  const int ff = sel_fused_from();
+  const int ff = S->opt.select_fused_from;
   if (ff > 0 && it >= ff)  // (iteration 0 has no previous bin to guess)
     launch_icp_select_fused(st, msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
                             sl.cand.as<uint32_t>(), sl.sel_cnt.as<uint32_t>(), y);
@@ -1192,7 +1189,11 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     (void)hipGetLastError();
   }
   SeqState* S = ctx->seq;
-  for (SeqSlot& sl : S->slot) sl.used = false;
+  S->opt = ctx->opt;
+  for (SeqSlot& sl : S->slot) {
+    sl.used = false;
+    for (auto& t : sl.tb) tree_opts(t, S->opt);
+  }
   HIPC(ensure(S->desc, n * sizeof(PairDesc)));
   HIPC(ensure(S->state, n * sizeof(PairState)));
   HIPC(ensure(S->outT, n * 64));
@@ -1283,7 +1284,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     TreeCtl* ctl = S->pin_ctl.as<TreeCtl>();
     std::memset(ctl, 0, plan.size() * 2 * sizeof(TreeCtl));
     std::vector<WinRun> runs(plan.size());
-    if (seq_prof()) {
+    if (S->opt.profile) {
       if (!S->s_probe) HIPC(hipStreamCreateWithFlags(&S->s_probe, hipStreamNonBlocking));
       while (S->tev.size() < 10 * plan.size()) {
         hipEvent_t e;
@@ -1316,7 +1317,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       }
       return win_upload(ec, S, cfg, prm, first, readings, resident, rbox, runs[k]);
     };
-    const bool prof = seq_prof();
+    const bool prof = S->opt.profile;
     double hp[5] = {0, 0, 0, 0, 0};  // upload (its thread), reference trees, icp loop, join, reference icp
     auto timed = [&](int slot, const std::function<int()>& f) {
       const auto a = std::chrono::steady_clock::now();
@@ -1582,7 +1583,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     o.nn_nodes_touched = st.touched_nodes;
     for (int k = 0; k < 3; ++k) o.overlap_keys[k] = st.ovl_counts[k];
   }
-  if (seq_prof()) {  // guessed bins of the fused select that missed, against its launches
+  if (S->opt.profile) {  // guessed bins of the fused select that missed, against its launches
     uint64_t miss = 0, fused = 0;
     for (size_t i = 0; i < *n_done; ++i) {
       miss += hs[i].sel_miss;

@@ -896,7 +896,16 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=5, help="repetitions of the bounded CPU sample (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-batched", action="store_true", help="skip the batched-independent extra figure")
+    ap.add_argument("--opt", action="append", default=[], metavar="K=V",
+                    help="context option (aicp_hip_options, include/aicp_hip.h) for every context, e.g. profile=1")
     args = ap.parse_args()
+    if args.opt:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import aicp_mapping_amd._lib as L
+
+        for kv in args.opt:
+            k, _, v = kv.partition("=")
+            L.CONTEXT_OPTIONS[k.strip()] = int(v)
     if args.config == "prefilter":
         return bench_prefilter(args)
     if args.config in ("c2", "c3"):

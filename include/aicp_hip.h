@@ -110,6 +110,52 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx);
 const char* aicp_hip_last_error(const aicp_hip_ctx* ctx);
 const char* aicp_hip_version(void);
 
+/* Context options: the engine and schedule switches the tests and A/B measurements use. The
+ * library reads no environment variable; a context starts with aicp_hip_default_options' values
+ * (the product path) and keeps what aicp_hip_set_options gives it until the next call. No option
+ * changes a result: every engine and schedule gives the same transforms, statistics and counts
+ * (the tests compare them). Replaces nothing in the reference. */
+typedef struct {
+  int32_t profile;            /* 1: host and device phase times (and the counters of the diagnostic
+                                 build, -DAICP_DIAG=1) on stderr; the timing events it records
+                                 shift the schedule slightly */
+  int32_t nn_engine;          /* 0: treelet records where they fit (bucketSize <= 15, <= 4 M
+                                 reference points); 1: node records (Trav<1>) always */
+  int32_t overlap_path;       /* 0: voxel maps within their memory budget, sorted key lists above;
+                                 1: sorted key lists always */
+  int32_t normals_knn_engine; /* SurfaceNormal kNN: 0: one octet of lanes per query up to 300 000
+                                 queries, one lane above; 1: octets always; 2: one lane always */
+  int32_t select_pair;        /* trimmed select: -1: one workgroup per pair from 256 pairs on
+                                 (readings <= 65536 each); 0: never; 1: whenever it fits */
+  int32_t select_fused_from;  /* ICP iteration from which the chip-wide select runs as one launch
+                                 (0: never); 3 */
+  int32_t raw_tree_first;     /* batch path: -1: the raw-coordinate tree before the matcher tree
+                                 from 4 M reference points on; 0: never; 1: always */
+  int32_t raw_first_at;       /* with the raw tree first, the matcher tree starts after the raw
+                                 tree's global levels (2) or after the whole raw tree (1); 2 */
+  int32_t no_early_exit;      /* 1: every ICP loop enqueues maxIterationCount iterations (tests:
+                                 the polled early exit must not change results) */
+  int32_t tree_plan;          /* kd-tree global levels: 0: planned from the cloud size; k > 0: k
+                                 levels (tests: a too-shallow plan); -1: host-polled build */
+  uint32_t tree_lvl_min;      /* the level-synchronous subtree builder from this many points of a
+                                 build on; 4194304 */
+  int32_t reference_cache;    /* 1: the one-shot calls keep their reference (and last reading)
+                                 resident for the next call, identified by a byte compare against a
+                                 host copy (aicp_hip_reference_cache_stats); 0: nothing is kept,
+                                 copied or compared between calls */
+  uint32_t oneshot_keep_mib;  /* device copies of a one-shot call's inputs are kept for the next
+                                 call up to this size (MiB), released above it; 4096 */
+  uint64_t read_order_min;    /* Morton order of a batch's readings from this many points on;
+                                 200000 */
+} aicp_hip_options;
+void aicp_hip_default_options(aicp_hip_options* out);
+int aicp_hip_set_options(aicp_hip_ctx* ctx, const aicp_hip_options* opt);
+int aicp_hip_get_options(const aicp_hip_ctx* ctx, aicp_hip_options* out);
+/* Test hook, process-wide on the calling thread's device: on != 0 sends every tile but the first
+ * of the kd-tree builds' single-pass scans down the path a stalled look-back takes (the exact
+ * prefix recomputed, error 16 reported: the call returns AICP_ERR_HIP and nothing faults). */
+int aicp_hip_test_force_scan_stall(int on);
+
 /* ---- configuration (host-only; the reference re-parses the chain per call) -------------- */
 void aicp_hip_default_config(aicp_icp_config* out);
 /* Parses the libpointmatcher chain subset (pointmatcher_registration.cpp:59-66).

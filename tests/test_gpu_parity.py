@@ -83,18 +83,18 @@ def test_normals_match_oracle(ctx, oracle):
     assert np.mean(np.all(n_gpu == n_cpu, axis=1)) > 0.99  # same tree, same neighbours, same solver
 
 
-@pytest.mark.parametrize("engine", ["1", "0"])
-def test_normals_knn_engines_identical(ctx, oracle, monkeypatch, engine):
+@pytest.mark.parametrize("engine", [1, 2])
+def test_normals_knn_engines_identical(ctx, oracle, engine):
     """The SurfaceNormal kNN engines (one query per octet of lanes, k_knn_oct; one per lane,
     k_knn_ids) keep libnabo's visit order and replaceHead semantics, ties included: on a scene
     with a block of duplicate points their normals are bit-identical to each other and to the
     oracle's."""
     P = sy.make_pair(15000, 10, seed=3).ref.copy()
     P[2000:2040] = P[2000]  # 40 duplicates: exact distance ties in the k-best lists
-    monkeypatch.setenv("AICP_KNN_OCT", engine)
-    n_gpu, deg_gpu = ctx.normals(P, knn=20)
-    monkeypatch.setenv("AICP_KNN_OCT", "0")
-    n_lane, deg_lane = ctx.normals(P, knn=20)
+    with ctx.options(normals_knn_engine=engine):
+        n_gpu, deg_gpu = ctx.normals(P, knn=20)
+    with ctx.options(normals_knn_engine=2):
+        n_lane, deg_lane = ctx.normals(P, knn=20)
     assert deg_gpu == deg_lane
     np.testing.assert_array_equal(n_gpu, n_lane)
     n_cpu, _, deg_cpu = oracle.surface_normals(P, knn=20)
@@ -185,16 +185,15 @@ def test_overlap_extreme_outlier_sparse_path(ctx, oracle, L):
     assert st[0]["overlap_percent"] == np.float32(ov)
 
 
-def test_overlap_sparse_path_equals_dense(ctx, oracle, L, monkeypatch):
-    """AICP_OVL_SPARSE=1 forces the sorted-key path on an ordinary ragged batch with a shared
+def test_overlap_sparse_path_equals_dense(ctx, oracle, L):
+    """The option overlap_path = 1 forces the sorted-key path on an ordinary ragged batch with a shared
     reference: every pair's three counts and ratio equal the voxel-map path's and the oracle's."""
     seq = sy.make_sequence(n_readings=4, ref_every=2, n_points=6000, seed=5, half=20.0)
     pairs = [dict(ref=p.ref, read=p.read[: 4000 + 500 * i], ref_origin=p.ref_origin, read_origin=p.read_origin)
              for i, p in enumerate(seq)]
     T0, s0, rc0 = ctx.align_batch(pairs, flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP, resolution=RES)
-    monkeypatch.setenv("AICP_OVL_SPARSE", "1")
-    T1, s1, rc1 = ctx.align_batch(pairs, flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP, resolution=RES)
-    monkeypatch.delenv("AICP_OVL_SPARSE")
+    with ctx.options(overlap_path=1):
+        T1, s1, rc1 = ctx.align_batch(pairs, flags=L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP, resolution=RES)
     assert rc0 == rc1 == 0
     np.testing.assert_array_equal(T0, T1)
     for a, b, p in zip(s0, s1, pairs):
@@ -230,18 +229,17 @@ def test_icp_matches_oracle(ctx, oracle, seed, n, ratio):
     assert rg < 2e-3 and tg < 2e-2
 
 
-@pytest.mark.parametrize("bucket,force", [(16, "0"), (8, "1"), (3, "0")])
-def test_node_record_engine_matches_oracle(ctx, oracle, L, monkeypatch, bucket, force):
+@pytest.mark.parametrize("bucket,force", [(16, 0), (8, 1), (3, 0)])
+def test_node_record_engine_matches_oracle(ctx, oracle, L, bucket, force):
     """The NN engine over node records (Trav<1>) serves chains with KDTreeMatcher bucketSize
     above 15 (treelet leaf slots hold 4-bit counts), references above 4 M points and batches
-    past 2^28 treelet records; AICP_FORCE_TRAV1=1 selects it on a normal cloud. Both paths give
+    past 2^28 treelet records; the option nn_engine = 1 selects it on a normal cloud. Both paths give
     the oracle's transform, iteration count and libnabo touch counts; SurfaceNormal keeps its own
     bucket-8 tree whatever the matcher's bucketSize."""
     pr = sy.make_pair(20000, 20000, seed=61)
-    monkeypatch.setenv("AICP_FORCE_TRAV1", force)
     cfg = L.default_config(trimmed_ratio=0.6, bucket_size=bucket)
-    T, st, rc = ctx.align_batch([dict(ref=pr.ref, read=pr.read)], cfg, flags=L.AICP_RUN_ICP)
-    monkeypatch.delenv("AICP_FORCE_TRAV1")
+    with ctx.options(nn_engine=force):
+        T, st, rc = ctx.align_batch([dict(ref=pr.ref, read=pr.read)], cfg, flags=L.AICP_RUN_ICP)
     rc1, T1, st1 = oracle.icp(pr.ref, pr.read, oracle.default_config(trimmed_ratio=0.6, bucket_size=bucket))
     assert rc == 0 and rc1 == 0
     r, t = sy.rot_err(T1, T[0])
@@ -373,7 +371,7 @@ def test_batch_deterministic_and_order_independent(ctx, L):
     np.testing.assert_array_equal(Ta[1], Tc[0])
 
 
-def test_select_one_workgroup_per_pair_equals_chip_wide(ctx, L, monkeypatch):
+def test_select_one_workgroup_per_pair_equals_chip_wide(ctx, L):
     """k_sel_pair (the whole TrimmedDist select of a pair in one workgroup; batches of >= 256 pairs
     take it) gives the chip-wide select's limits: same transforms and statistics bit for bit, on
     ordinary pairs and on one whose distances all fall into one digit-1 bin (more candidates than
@@ -391,10 +389,9 @@ def test_select_one_workgroup_per_pair_equals_chip_wide(ctx, L, monkeypatch):
     out = {}
     # also the batch path's stream order for large batches (the raw tree first, the matcher tree
     # from the raw tree's global levels on), forced on this small batch: same results
-    for v, raw in (("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")):
-        monkeypatch.setenv("AICP_SEL_PAIR", v)
-        monkeypatch.setenv("AICP_RAW_FIRST", raw)
-        out[v + raw] = ctx.align_batch(pairs, flags=flags, resolution=RES)
+    for v, raw in ((0, 0), (1, 0), (0, 1), (1, 1)):
+        with ctx.options(select_pair=v, raw_tree_first=raw):
+            out[f"{v}{raw}"] = ctx.align_batch(pairs, flags=flags, resolution=RES)
     T0, s0, rc0 = out["00"]
     for k in ("10", "01", "11"):
         T1, s1, rc1 = out[k]
@@ -438,24 +435,46 @@ def test_concurrent_contexts_identical(ctx, L):
         c.close()
 
 
-@pytest.mark.parametrize("plan", ["1", "2", "0"])
-def test_planned_tree_build(ctx, L, monkeypatch, plan):
+@pytest.mark.parametrize("plan", [1, 2, -1])
+def test_planned_tree_build(ctx, L, plan):
     """The kd-trees are built with a planned number of global levels and no host read-back.
     A plan too shallow for the data (1 or 2 levels here) leaves segments above the wave-LDS
-    size, which the subtree kernel finishes in global memory; "0" is the host-polled build.
+    size, which the subtree kernel finishes in global memory; -1 is the host-polled build.
     Every variant must give the default build's transforms, depths and touch counts."""
     prs = [sy.make_pair(30000, 30000, seed=70 + i) for i in range(2)]
     pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
     flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
     Ta, sa, rca = ctx.align_batch(pairs, flags=flags, resolution=RES)
-    monkeypatch.setenv("AICP_TREE_PLAN", plan)
-    Tb, sb, rcb = ctx.align_batch(pairs, flags=flags, resolution=RES)
-    monkeypatch.delenv("AICP_TREE_PLAN")
+    with ctx.options(tree_plan=plan):
+        Tb, sb, rcb = ctx.align_batch(pairs, flags=flags, resolution=RES)
     assert rca == rcb == 0
     np.testing.assert_array_equal(Ta, Tb)
     for a, b in zip(sa, sb):
         assert (a["iterations"], a["tree_depth"], a["nn_points_touched"], a["nn_nodes_touched"]) == \
                (b["iterations"], b["tree_depth"], b["nn_points_touched"], b["nn_nodes_touched"])
+
+
+def test_tree_scan_stall_fails_safely(ctx, L):
+    """A kd-tree scan whose look-back gives up (kernels_tree.hip lookback_scan; never seen, the
+    pattern that cost r05 a box when a grid barrier timed out) recomputes its exact prefix, so no
+    later kernel indexes with a partial one, and reports error 16: forced through the test hook on
+    every tile but the first, the call returns AICP_ERR_HIP without a fault, and the context's next
+    call gives the results of the run before."""
+    prs = [sy.make_pair(30000, 30000, seed=40 + i) for i in range(2)]  # two references: no cache
+    pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
+    flags = L.AICP_RUN_OVERLAP | L.AICP_RUN_ICP
+    T0, s0, rc0 = ctx.align_batch(pairs, flags=flags, resolution=RES)
+    assert rc0 == 0
+    assert L.test_force_scan_stall(True) == L.AICP_OK
+    try:
+        _, _, rc1 = ctx.align_batch(pairs, flags=flags, resolution=RES, raise_on_error=False)
+    finally:
+        assert L.test_force_scan_stall(False) == L.AICP_OK
+    assert rc1 == L.AICP_ERR_HIP and "16" in ctx.last_error(), (rc1, ctx.last_error())
+    T2, s2, rc2 = ctx.align_batch(pairs, flags=flags, resolution=RES)
+    assert rc2 == 0
+    np.testing.assert_array_equal(T0, T2)
+    assert s0 == s2
 
 
 def test_block_subtree_builder_matches_oracle_trees(ctx, oracle, L):
@@ -475,17 +494,16 @@ def test_block_subtree_builder_matches_oracle_trees(ctx, oracle, L):
 
 
 @pytest.mark.parametrize("builder", ["level", "block", "block_b6"])
-def test_subtree_builders_match_oracle_trees(ctx, oracle, L, monkeypatch, builder):
+def test_subtree_builders_match_oracle_trees(ctx, oracle, L, builder):
     """The finishing builders below the global levels give libnabo's trees (touch counts, depth,
     normals): k_tr_subtree_lvl (all nodes of a level per pass; builds of >= 4 M points, forced
     here), k_tr_subtree_blk (a node per wave) with bucketSize 8 and 6."""
     bucket = 6 if builder == "block_b6" else 8
-    if builder == "level":
-        monkeypatch.setenv("AICP_TREE_LVL_MIN", "1")
     prs = [sy.make_pair(20000, 20000, seed=90 + i) for i in range(2)]
     pairs = [dict(ref=p.ref, read=p.read, ref_origin=p.ref_origin, read_origin=p.read_origin) for p in prs]
-    T, st, rc = ctx.align_batch(pairs, flags=L.AICP_RUN_ICP, cfg=L.default_config(trimmed_ratio=0.65, bucket_size=bucket))
-    monkeypatch.delenv("AICP_TREE_LVL_MIN", raising=False)
+    with ctx.options(tree_lvl_min=1 if builder == "level" else L.default_options().tree_lvl_min):
+        T, st, rc = ctx.align_batch(pairs, flags=L.AICP_RUN_ICP,
+                                    cfg=L.default_config(trimmed_ratio=0.65, bucket_size=bucket))
     assert rc == 0
     for i, p in enumerate(prs):
         rc1, T1, st1 = oracle.icp(p.ref, p.read, oracle.default_config(trimmed_ratio=0.65, bucket_size=bucket))

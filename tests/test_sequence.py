@@ -134,8 +134,11 @@ def test_sequence_repeatable_and_matches_batch_window0(ctx, L):
 
 def test_sequence_c2_full_size(ctx, oracle, L):
     """C2 at full size (64 readings of 120k points, a reference every 5): 13 windows, no
-    re-plan, all accepted, and reading 4 plus the first reading that depends on a device-built
-    reference (5: registered against corrected reading 4) equal the oracle's replay of that chain."""
+    re-plan, all accepted, and readings 0-10 equal the oracle's replay of App's chain
+    (app.cpp:375-391, 414): window 0 against the first cloud, window 1 against corrected reading 4
+    and reading 10 against corrected reading 9 -- two references built on the device -- with key
+    counts, ratios, iterations and decisions exact and T within 1e-6 rad / 1e-5 m. (~7 s of oracle
+    time at 1.66 clouds/s.)"""
     st = sy.make_stream(n_readings=64, n_points=120000, seed=1)
     T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins)
     assert rc == 0 and done == 64
@@ -148,32 +151,22 @@ def test_sequence_c2_full_size(ctx, oracle, L):
     for i, Tg in enumerate(st.T_gt):
         rg, tg = sy.rot_err(Tg, T[i])
         assert rg < 0.05 and tg < 0.25, (i, rg, tg)
-    # oracle: reading 4 against the first cloud, then readings 5 and 6 against corrected reading 4
-    sub_r = [st.readings[4], st.readings[5], st.readings[6]]
-    sub_o = [st.origins[4], st.origins[5], st.origins[6]]
-    ref = oracle.sequence(st.first, st.first_origin, sub_r, sub_o, reference_update_frequency=1, resolution=RES,
-                          stop=2)
-    # the chain: reading 4 closes window 0 (frequency 1 here makes it the next reference at once)
-    o4, o5 = out[4], out[5]
-    assert o4["icp"]["overlap_keys"] == [int(c) for c in ref[0]["counts"]]
-    assert o5["icp"]["overlap_keys"] == [int(c) for c in ref[1]["counts"]]
-    for k, i in ((0, 4), (1, 5)):
-        rr, tt = sy.rot_err(ref[k]["T"], T[i])
-        assert rr < 1e-6 and tt < 1e-5, (i, rr, tt)
-        assert out[i]["icp"]["iterations"] == ref[k]["stats"].iterations
+    # oracle: App's chain over readings 0-10 (two device-built references: corrected 4 and 9)
+    ref = oracle.sequence(st.first, st.first_origin, st.readings[:11], st.origins[:11], resolution=RES)
+    assert [r["reference"] for r in ref] == [-1] * 5 + [4] * 5 + [9]
+    _compare(out[:11], ref, T[:11])
 
 
 
-def test_sequence_polled_loop_identical(ctx, L, monkeypatch):
+def test_sequence_polled_loop_identical(ctx, L):
     """The polled loop (the host stops enqueueing a window's iterations once the update kernel
     reports no active reading) gives the corrections and statistics of the unpolled schedule,
-    which runs maxIterationCount launches per window (AICP_SEQ_NO_EARLY_EXIT=1), bit for bit,
+    which runs maxIterationCount launches per window (option no_early_exit = 1), bit for bit,
     across dropped readings and re-plans."""
     st = sy.make_stream(n_readings=12, n_points=5000, seed=8, half=18.0, jumps={2: (0.6, 0, 0), 6: (0, -0.6, 0)})
     prm = L.default_sequence_params(max_correction_magnitude=0.4)  # readings 2 and 6 drop
-    monkeypatch.setenv("AICP_SEQ_NO_EARLY_EXIT", "1")
-    T0, out0, done0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
-    monkeypatch.delenv("AICP_SEQ_NO_EARLY_EXIT")
+    with ctx.options(no_early_exit=1):
+        T0, out0, done0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
     T1, out1, done1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
     assert (rc0, done0) == (rc1, done1) == (0, 12)
     assert sum(1 - o["accepted"] for o in out1) == 2
@@ -203,15 +196,14 @@ def test_sequence_far_return_sparse_overlap(ctx, oracle, L):
     assert out[1]["icp"]["overlap_keys"][1] > out[0]["icp"]["overlap_keys"][1] + 20000
 
 
-def test_sequence_sparse_overlap_identical(ctx, L, monkeypatch):
-    """Every window on the sorted-key path (AICP_OVL_SPARSE=1) gives the dense maps' key counts
+def test_sequence_sparse_overlap_identical(ctx, L):
+    """Every window on the sorted-key path (option overlap_path = 1) gives the dense maps' key counts
     and corrections bit for bit, across dropped readings and re-plans."""
     st = sy.make_stream(n_readings=12, n_points=5000, seed=8, half=18.0, jumps={2: (0.6, 0, 0), 6: (0, -0.6, 0)})
     prm = L.default_sequence_params(max_correction_magnitude=0.4)
-    monkeypatch.delenv("AICP_OVL_SPARSE", raising=False)
     T0, out0, done0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
-    monkeypatch.setenv("AICP_OVL_SPARSE", "1")
-    T1, out1, done1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    with ctx.options(overlap_path=1):
+        T1, out1, done1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
     assert (rc0, done0) == (rc1, done1) == (0, 12)
     assert np.array_equal(T0, T1)
     for a, b in zip(out0, out1):
@@ -241,15 +233,14 @@ def test_sequence_debug_mode_matches_oracle(ctx, oracle, L, jumps):
             assert rr < 5e-3 and tt < 5e-2, (i, rr, tt)
 
 
-def test_sequence_debug_mode_sparse_overlap(ctx, oracle, L, monkeypatch):
+def test_sequence_debug_mode_sparse_overlap(ctx, oracle, L):
     """Debug mode with every overlap on the sorted-key path (one key side per reading, bounds for
     any rigid motion): the same results as the dense maps, and the oracle's."""
     st = sy.make_stream(n_readings=7, n_points=4000, seed=9, half=15.0)
     prm = L.default_sequence_params(flags=L.AICP_RUN_OVERLAP | L.AICP_SEQ_DEBUG)
-    monkeypatch.delenv("AICP_OVL_SPARSE", raising=False)
     T0, out0, _, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
-    monkeypatch.setenv("AICP_OVL_SPARSE", "1")
-    T1, out1, _, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    with ctx.options(overlap_path=1):
+        T1, out1, _, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
     assert rc0 == rc1 == 0
     assert np.array_equal(T0, T1)
     assert [o["icp"]["overlap_keys"] for o in out0] == [o["icp"]["overlap_keys"] for o in out1]
