@@ -19,6 +19,37 @@
 #pragma once
 #include <stdint.h>
 
+// ---- diagnostic builds ----------------------------------------------------------------------
+// The product library carries no counters. -DAICP_DIAG=1 builds a diagnostic library
+// (tools/variants.sh NAME "-DAICP_DIAG=1 -DAICP_QLAT_PROF=1"), whose counters are chosen with
+//   AICP_XCD_PROF   per-XCD-group first start / last end and query cost of each NN launch
+//   AICP_QLAT_PROF  per-query NN latency / completion-time histograms
+//   AICP_NN_PROF    per-phase s_memtime cycles of the NN's persistent waves
+//   AICP_ITER_PROF  bodies and serial tails of the ICP iteration kernels, k_tr_mid phases
+// and printed with the context option profile = 1. Without AICP_DIAG each is 0 whatever the
+// command line says.
+#ifndef AICP_DIAG
+#define AICP_DIAG 0
+#endif
+#if !AICP_DIAG
+#undef AICP_XCD_PROF
+#undef AICP_QLAT_PROF
+#undef AICP_NN_PROF
+#undef AICP_ITER_PROF
+#endif
+#ifndef AICP_XCD_PROF
+#define AICP_XCD_PROF 0
+#endif
+#ifndef AICP_QLAT_PROF
+#define AICP_QLAT_PROF 0
+#endif
+#ifndef AICP_NN_PROF
+#define AICP_NN_PROF 0
+#endif
+#ifndef AICP_ITER_PROF
+#define AICP_ITER_PROF 0
+#endif
+
 namespace aicp {
 
 constexpr int kHistBins = 2048;     // radix-select digit 1/2 (11 bits)
@@ -41,7 +72,10 @@ constexpr int kCtrStride = 16;      // words between work counters (64 B: one co
 // into kHeads contiguous parts, so that no more than ~1/kHeads of the group's waves pull from
 // one word: a word serves ~88 returning atomics per us, MI355X_MICROARCH.md "dequeue") and one
 // word of exhausted-head bits.
-constexpr int kHeads = 4;
+#ifndef AICP_NN_HEADS
+#define AICP_NN_HEADS 8  // (C2 NN per launch, rocprofv3: 2 heads 75.2, 4 heads 70.6, 8 heads 68.0-68.7 us)
+#endif
+constexpr int kHeads = AICP_NN_HEADS;
 constexpr int kGroupCtrs = kHeads + 1;
 constexpr int kPersistCtrWords = kXcdGroups * kGroupCtrs * kCtrStride;  // one persistent kernel's counters
 constexpr int kKnnCtrOff = kPersistCtrWords;                            // the normals kNN's, after the ICP NN's

@@ -777,29 +777,17 @@ __device__ __forceinline__ void coop_bucket(Eng& t, bool act, const float4* __re
   if (act && res_d < t.best.v[0]) best_replace<1>(t.best, (int32_t)(t.lb0 + res_i), res_d);
 }
 
-#ifndef AICP_XCD_PROF
-#define AICP_XCD_PROF 0  // diagnostic builds: per-XCD-group first start / last end of each NN launch
-#endif
 #if AICP_XCD_PROF
 __device__ unsigned long long g_xcd_prof[64 * kXcdGroups * 2];
 __device__ unsigned long long g_xcd_cost[64 * kXcdGroups];  // per launch slot and group: queries << 40 | sum tn + tp
-#endif
-#ifndef AICP_QLAT_PROF
-#define AICP_QLAT_PROF 0  // diagnostic builds: per-query NN latency / completion-time histograms
 #endif
 #if AICP_QLAT_PROF
 // [0, 256): query latency (pick-up to result, 1 us bins); [256, 512): completion time of the
 // query after its wave's start (1 us bins); last bin of each half = overflow
 __device__ unsigned long long g_qlat[512];
 #endif
-#ifndef AICP_NN_PROF
-#define AICP_NN_PROF 0  // diagnostic builds: per-phase s_memtime cycles of the persistent waves
-#endif
 #if AICP_NN_PROF
 __device__ unsigned long long g_nn_prof[8];
-#endif
-#ifndef AICP_ITER_PROF
-#define AICP_ITER_PROF 0  // diagnostic builds: time the ICP iteration kernels' bodies and serial tails
 #endif
 #if AICP_ITER_PROF
 // per kernel k (0 hist_f, 1 compact_f, 2 reduce, 3 update_f): [4k] body sum, [4k+1] bodies,
@@ -850,7 +838,9 @@ __device__ unsigned long long g_iter_prof[16];
 // ~12 us after the first. A wave starts at head (its index in the group) mod kHeads and, when
 // that part is exhausted, moves to a part of the same group still open (the exhausted parts are
 // bits of one more word): the work stays on the group's XCD and every chunk is still served
-// exactly once.
+// exactly once. (Measured and not kept: each wave's first chunk dealt by its index, the heads
+// serving only the rest -- 86.8 against 70.6 us per C2 launch: a wave that starts late, beside
+// another stream's kernel, holds its dealt chunk back; with heads the early waves take it.)
 //   on_chunk(base)      wave-uniform, once per chunk, before its slots are handed out
 //   fetch(slot, eng)    initialises a lane's query; false: the slot has no work
 //   done(slot, eng)     consumes the result
@@ -1138,7 +1128,7 @@ __device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, c
   }
 }
 
-__global__ __launch_bounds__(1024) void k_active_list(int n_pairs, const PairDesc* __restrict__ pd,
+__global__ __launch_bounds__(256) void k_active_list(int n_pairs, const PairDesc* __restrict__ pd,
                                                       const PairState* __restrict__ st,
                                                       ActiveList* al, uint32_t* ctr, uint32_t* host_n,
                                                       uint64_t* done_sig, const uint64_t* ticket, float* outT) {
@@ -2982,7 +2972,9 @@ bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
 }
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st, ActiveList* al,
                         uint32_t* ctr, uint32_t* host_n, uint64_t* done_sig, const uint64_t* ticket, float* outT) {
-  k_active_list<<<1, 1024, 0, s>>>(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT);
+  // 256 threads: the first iteration's list is launched while the normals' kNN fills the chip, and
+  // a 1024-thread workgroup waited for 16 free wave slots on one CU (C2 trace: 33 us median)
+  k_active_list<<<1, 256, 0, s>>>(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT);
 }
 // The ICP matcher's NN engine: Trav2C on the treelet records; Trav<1> on the node records where
 // treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records) or

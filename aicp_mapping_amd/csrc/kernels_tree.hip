@@ -1222,9 +1222,6 @@ __device__ __forceinline__ void lvl_scan(const uint32_t* fl, uint32_t* X, uint32
   if (t == 0) X[n] = base;
 }
 
-#ifndef AICP_ITER_PROF
-#define AICP_ITER_PROF 0
-#endif
 #if AICP_ITER_PROF
 // diagnostic builds: k_tr_subtree_lvl's phases summed over segments (thread 0, s_memrealtime
 // ticks at 100 MHz): [0] load, [1] min/max, [2] counts, [3] Hoare passes, [4] nodes + events,
