@@ -946,7 +946,7 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
   HIPC(hipStreamWaitEvent(si, sl.ev_s3, 0));
   launch_pairs_from_refs(si, (int)np, dDesc, dRdesc);
   launch_pairs_degenerate_part(si, (int)np, dDesc, dState, dRst, 2);
-  // the normals (ev_s2) are waited for by the first iteration's reduce (loop_iteration): the
+  // the normals (ev_s2) are waited for by the first iteration's reduce (loop_part): the
   // first NN and select need only the matcher tree, which is ready ~0.2 ms earlier on C2
   if (!R.debug) launch_prepare_read(si, R.m_read, dDesc, readS, sl.read_c.as<float4>());
   HIPC(hipGetLastError());
@@ -955,12 +955,15 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
 
 // The ICP loop of a window, polled: from iteration smoothLength on (no pair can stop earlier
 // except on an error) the update kernel of the last pair to finish an iteration writes the next
-// active count into mapped host memory (a system-scope store); the host, one iteration ahead,
-// reads the word itself and stops enqueueing once it reads 0 (the launch after the one that found
-// no active pair is a no-op that still holds the stream). (r03 recorded an event per poll and
-// queried it: each marker left a 5-10 us gap before the next NN launch, C2 2512 against 2620
-// clouds/s in r04.) The window's states and corrections are then committed to the sequence's arrays
-// (ev_done), which the next reference waits for.
+// active count into mapped host memory (a system-scope store), and the host reads the word
+// itself. An iteration is enqueued in two parts: its NN launch as soon as the previous iteration
+// is enqueued (so the device never waits for the host), the rest (select, reduce, update) once
+// the iteration's active count is known to be non-zero; when it reads 0 only the NN launch, a
+// no-op, was enqueued for nothing. (r05 enqueued whole iterations one ahead: the trailing no-op
+// iteration was four launches. r03 recorded an event per poll and queried it: each marker left a
+// 5-10 us gap before the next NN launch, C2 2512 against 2620 clouds/s in r04.) The window's
+// states and corrections are then committed to the sequence's arrays (ev_done), which the next
+// reference waits for.
 // (r03, measured and removed: the window's last reading -- the next reference's source -- in a
 // loop of its own with the others on a second stream: the one-reading loop took 0.99 against
 // 1.06 ms, but the others' NN launches beside the next reference's kd-trees slowed those from 0.88
@@ -969,9 +972,9 @@ struct IcpLoop {
   WinRun* R = nullptr;
   int sub = -1;   // debug mode: the one reading of the window this loop registers
   int area = 0;   // poll words / events used: [area * kMaxPolls, + kMaxPolls)
-  int it = 0;
+  int it = 0;      // iterations enqueued whole
+  int nn = 0;      // iterations whose NN launch is enqueued (it or it + 1)
   bool stop = false;
-  std::deque<int> pending;  // poll slots recorded, oldest first
 };
 
 // the blocks [off, off + cnt) of a block map
@@ -996,60 +999,74 @@ static IcpParams icp_params(const aicp_icp_config* cfg) {
   return ip;
 }
 
-// enqueue the loop's next iteration (and its poll slots)
-static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
-                          IcpLoop& q, bool timeNN, int& nn_launches) {
+// whether the active count at the start of iteration k is written to poll word k (from
+// smoothLength on: no pair can stop earlier except on an error)
+static bool loop_polled(const SeqState* S, const aicp_icp_config* cfg, int k) {
+  return !S->opt.no_early_exit && k >= cfg->smooth_length && k < kMaxPolls && k < cfg->max_iter;
+}
+
+// The pairs one loop iterates: the window's, or (debug mode) reading q.sub alone.
+struct LoopPairs {
+  int np_l;
+  PairDesc* gd;
+  PairState* gs;
+  uint64_t reads;
+};
+
+// one part of iteration q.it: part 0 its NN launch (with the first active list at iteration 0),
+// part 1 the rest (select, reduce, update)
+static int loop_part(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                     IcpLoop& q, int part, bool timeNN, int& nn_launches) {
   WinRun& R = *q.R;
   WIN_REFS;
   const int it = q.it;
   ActiveList* al = sl.active.as<ActiveList>();
   uint32_t* ctr = sl.ctrs.as<uint32_t>();
-  // the pairs this loop iterates: the window's, or (debug mode) reading q.sub alone
   const int r = q.sub;
-  const int np_l = r >= 0 ? 1 : (int)np;
-  PairDesc* gd = r >= 0 ? dDesc + r : dDesc;
-  PairState* gs = r >= 0 ? dState + r : dState;
-  const uint64_t reads = r >= 0 ? R.n_read[r] : R.nread;
-  const BlockMap msel = r >= 0 ? map_sub(R.m_sel, R.b_sel[r], R.b_sel[r + 1] - R.b_sel[r]) : R.m_sel;
-  const BlockMap mred = r >= 0 ? map_sub(R.m_red, R.b_red[r], R.b_red[r + 1] - R.b_red[r]) : R.m_red;
+  const LoopPairs lp{r >= 0 ? 1 : (int)np, r >= 0 ? dDesc + r : dDesc, r >= 0 ? dState + r : dState,
+                     r >= 0 ? R.n_read[r] : R.nread};
   uint32_t* poll_host = sl.poll_host + q.area * kMaxPolls;
   uint32_t* poll_dev = sl.poll_dev + q.area * kMaxPolls;
   IcpParams ip = icp_params(cfg);
   ip.prof_slot = nn_launches;
-  auto polled = [&](int k) {
-    return !S->opt.no_early_exit && k >= cfg->smooth_length && k < kMaxPolls && k < cfg->max_iter;
-  };
-  // poll slot k holds the active count at the start of iteration k, written by the launch that
-  // builds that iteration's active list (k_active_list at it = 0, else the previous update)
-  uint32_t* hn_this = nullptr;
-  uint32_t* hn_next = nullptr;
-  if (it == 0 && polled(it)) {
-    poll_host[it] = 0xffffffffu;  // before the launch that overwrites it
-    hn_this = poll_dev + it;
+  hipStream_t st = S->s_icp;
+  // poll word k holds the active count at the start of iteration k, written by the launch that
+  // builds that iteration's active list (k_active_list at it = 0, else the previous update); it
+  // is marked unwritten before that launch is enqueued
+  if (part == 0) {
+    uint32_t* hn_this = nullptr;
+    if (it == 0 && loop_polled(S, cfg, it)) {
+      poll_host[it] = 0xffffffffu;
+      hn_this = poll_dev + it;
+    }
+    if (timeNN)
+      while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
+        hipEvent_t e;
+        HIPC(hipEventCreate(&e));
+        S->nn_ev.push_back(e);
+      }
+    if (it == 0) launch_active_list(st, lp.np_l, lp.gd, lp.gs, al, ctr, hn_this);
+    launch_icp_nn(st, (int)lp.reads, lp.gd, lp.gs, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
+                  R.use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
+                  R.use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
+                  sl.touch.as<uint32_t>(), ctr, ip, timeNN ? S->nn_ev[2 * nn_launches] : nullptr,
+                  timeNN ? S->nn_ev[2 * nn_launches + 1] : nullptr);
+    HIPC(hipGetLastError());
+    ++nn_launches;
+    q.nn = it + 1;
+    return AICP_OK;
   }
-  if (polled(it + 1)) {
+  const BlockMap msel = r >= 0 ? map_sub(R.m_sel, R.b_sel[r], R.b_sel[r + 1] - R.b_sel[r]) : R.m_sel;
+  const BlockMap mred = r >= 0 ? map_sub(R.m_red, R.b_red[r], R.b_red[r + 1] - R.b_red[r]) : R.m_red;
+  uint32_t* hn_next = nullptr;
+  if (loop_polled(S, cfg, it + 1)) {
     poll_host[it + 1] = 0xffffffffu;
     hn_next = poll_dev + it + 1;
   }
-  if (timeNN)
-    while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
-      hipEvent_t e;
-      HIPC(hipEventCreate(&e));
-      S->nn_ev.push_back(e);
-    }
-  hipStream_t st = S->s_icp;
-  if (it == 0) launch_active_list(st, np_l, gd, gs, al, ctr, hn_this);
-  launch_icp_nn(st, (int)reads, gd, gs, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
-                R.use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
-                R.use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
-                sl.touch.as<uint32_t>(), ctr, ip, timeNN ? S->nn_ev[2 * nn_launches] : nullptr,
-                timeNN ? S->nn_ev[2 * nn_launches + 1] : nullptr);
-  HIPC(hipGetLastError());
-  ++nn_launches;
   IcpIterSync y = icp_sync_layout(sl.isync.as<uint32_t>(), np, 0);
-  y.np = np_l;
-  y.pd = gd;
-  y.st = gs;
+  y.np = lp.np_l;
+  y.pd = lp.gd;
+  y.st = lp.gs;
   y.al = al;
   y.ctr = ctr;
   y.host_n = hn_next;
@@ -1062,15 +1079,11 @@ static int loop_iteration(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config*
                         sl.sel_cnt.as<uint32_t>(), y);
   if (it == 0) {  // the reduce gathers the reference normals (stream r2, scattered into matcher order)
     HIPC(hipStreamWaitEvent(st, sl.ev_s2, 0));
-    launch_pairs_degenerate_part(st, np_l, gd, gs, dRst, 1);
+    launch_pairs_degenerate_part(st, lp.np_l, lp.gd, lp.gs, dRst, 1);
   }
   launch_icp_reduce_f(st, mred, dDesc, dState, sl.read_c.as<float4>(), sl.match.as<int32_t>(), sl.d2.as<float>(),
                       sl.touch.as<uint32_t>(), sl.bpts.as<float4>(), sl.bnrm.as<float4>(), sl.slab.as<double>(), ip, y);
   HIPC(hipGetLastError());
-  for (int k : {hn_this ? it : -1, hn_next ? it + 1 : -1})
-    if (k >= 0) {
-      q.pending.push_back(k);
-    }
   ++q.it;
   if (q.it >= cfg->max_iter) q.stop = true;
   return AICP_OK;
@@ -1091,12 +1104,11 @@ static int loop_finish(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_param
   return AICP_OK;
 }
 
-// the oldest poll of the loop (got: it was read; q.stop set when it read 0)
+// poll word q.it of the loop (got: known; q.stop set when it reads 0)
 static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool& got) {
   got = false;
   SeqSlot& sl = S->slot[q.R->w.slot];
-  const int k = q.pending.front();
-  volatile uint32_t* w = sl.poll_host + q.area * kMaxPolls + k;
+  volatile uint32_t* w = sl.poll_host + q.area * kMaxPolls + q.it;
   if (*w == 0xffffffffu) {
     // not written yet: still running, or the launch that writes it had no active pair (then
     // the stream drains and the word stays unwritten: the loop is over)
@@ -1105,13 +1117,11 @@ static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool& got) {
     HIPC(r);
     std::atomic_thread_fence(std::memory_order_seq_cst);
     if (*w == 0xffffffffu) {
-      q.pending.pop_front();
       got = true;
       q.stop = true;
       return AICP_OK;
     }
   }
-  q.pending.pop_front();
   got = true;
   if (*w == 0) q.stop = true;
   return AICP_OK;
@@ -1334,17 +1344,24 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
     // enqueue iterations while the host is less than one iteration ahead of the oldest poll, read
     // the polls that have completed, finish the loop once one reads 0
     auto advance = [&](IcpLoop& q, bool& progress) -> int {
-      for (;;) {
-        while (!q.stop && (q.pending.empty() || q.it - q.pending.front() < 1)) {
-          const int r = loop_iteration(ctx, S, cfg, prm, q, timeNN, nn_launches);
+      while (!q.stop) {
+        if (q.nn == q.it) {  // the next NN launch: enqueued before its active count is known
+          const int r = loop_part(ctx, S, cfg, prm, q, 0, timeNN, nn_launches);
           if (r) return r;
           progress = true;
+          continue;
         }
-        if (q.stop || q.pending.empty()) break;
-        bool got = false;
-        const int r = loop_poll(ctx, S, q, got);
+        // the rest of iteration q.it, once some pair is known to be active in it
+        if (loop_polled(S, cfg, q.it)) {
+          bool got = false;
+          const int r = loop_poll(ctx, S, q, got);
+          if (r) return r;
+          if (!got) break;
+          progress = true;
+          if (q.stop) break;
+        }
+        const int r = loop_part(ctx, S, cfg, prm, q, 1, timeNN, nn_launches);
         if (r) return r;
-        if (!got) break;
         progress = true;
       }
       if (q.stop && q.it >= 0) {
