@@ -57,6 +57,25 @@ def test_version_and_defaults(L):
     assert math.isinf(c.nn_max_dist)
 
 
+def test_context_options_defaults_and_layout(L):
+    """aicp_hip_options: the library's defaults are the product path, the ctypes mirror has the
+    header's layout (14 32-bit fields, then a uint64), and nothing in the package reads the
+    environment for them (r05 had 12 getenv switches in the library)."""
+    import ctypes
+
+    assert ctypes.sizeof(L.Options) == 64
+    o = L.default_options().as_dict()
+    assert o == dict(profile=0, nn_engine=0, overlap_path=0, normals_knn_engine=0, select_pair=-1,
+                     select_fused_from=3, raw_tree_first=-1, raw_first_at=2, no_early_exit=0, tree_plan=0,
+                     tree_lvl_min=1 << 22, reference_cache=1, oneshot_keep_mib=4096, read_order_min=200000)
+    with pytest.raises(AttributeError):
+        L.default_options(no_such_switch=1)
+    src = "".join(open(os.path.join(ROOT, "aicp_mapping_amd", "csrc", f)).read()
+                  for f in os.listdir(os.path.join(ROOT, "aicp_mapping_amd", "csrc"))
+                  if f.endswith((".cpp", ".hip", ".hpp")))
+    assert "getenv" not in src
+
+
 def test_parse_default_chain_fixture(L):
     rc, c = L.parse_pm_yaml(os.path.join(GOLDEN, "icp_autotuned_default.yaml"))
     assert rc == 0
