@@ -201,9 +201,11 @@ void launch_pairs_degenerate_part(hipStream_t s, int n_pairs, const PairDesc* pd
 void launch_ovl_init(hipStream_t s, int n, const PairDesc* pd, PairState* st, double res, int sides);
 void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* st,
                      const float4* pts, int side, double res);
-// od[i]: the map of entry i (group or pair) of the side being marked
+// od[i]: the map of entry i (group or pair) of the side being marked; max_blocks > 0: at most
+// that many workgroups, each marking every max_blocks-th block of the map
 void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDesc* od, PairState* st,
-                     const float4* pts, int side, double res, uint8_t* maps, bool filter);
+                     const float4* pts, int side, double res, uint8_t* maps, bool filter,
+                     unsigned max_blocks = 0);
 // |A| per group (gst.ovl_counts[0]), |B| and |A∩B| per pair (st.ovl_counts[1], [2])
 void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
                       const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps);

@@ -126,12 +126,15 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
     for (int i = threadIdx.x; i < kMarkCache; i += 256) cache[i] = 0xFFFFFFFFu;
     __syncthreads();
   }
-  const int pair = m.pair[blockIdx.x];
-  if (pair < 0) return;  // (padding block of an XCD-dealt map)
-  const uint32_t j = m.start[blockIdx.x] + threadIdx.x;
+  // grid-stride over the map's blocks (a launch may use fewer workgroups than blocks: the stream's
+  // reference-side marks run beside the critical kd-tree build, launch_ovl_mark's max_blocks)
+  for (uint32_t mb = blockIdx.x; mb < m.n_blocks; mb += gridDim.x) {
+  const int pair = m.pair[mb];
+  if (pair < 0) continue;  // (padding block of an XCD-dealt map)
+  const uint32_t j = m.start[mb] + threadIdx.x;
   const PairDesc& d = pd[pair];
   const uint32_t n = side ? d.n_read : d.n_ref;
-  if (j >= n) return;
+  if (j >= n) continue;
   const uint32_t off = side ? d.read_off : d.ref_off;
   const OvlDesc& ov = od[pair];
   uint8_t* bm = maps + ov.off;
@@ -227,6 +230,7 @@ __global__ __launch_bounds__(256) void k_ovl_mark(BlockMap m, const PairDesc* __
   }
   if (okE) mark(ke[0], ke[1], ke[2]);
   if (err) atomicOr(&st[pair].ovl_err, 1);
+  }
 }
 
 // popcounts: |A|, |B|, |A & B| (bpm workgroups per map, integer atomics -> deterministic).
@@ -331,12 +335,13 @@ void launch_ovl_bbox(hipStream_t s, BlockMap m, const PairDesc* pd, PairState* s
   if (m.n_blocks) k_ovl_bbox<<<m.n_blocks, 256, 0, s>>>(m, pd, st, pts, side, res);
 }
 void launch_ovl_mark(hipStream_t s, BlockMap m, const PairDesc* pd, const OvlDesc* od, PairState* st,
-                     const float4* pts, int side, double res, uint8_t* maps, bool filter) {
+                     const float4* pts, int side, double res, uint8_t* maps, bool filter, unsigned max_blocks) {
   if (!m.n_blocks) return;
+  const unsigned g = max_blocks ? std::min<unsigned>(m.n_blocks, max_blocks) : m.n_blocks;
   if (filter)
-    k_ovl_mark<true><<<m.n_blocks, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
+    k_ovl_mark<true><<<g, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
   else
-    k_ovl_mark<false><<<m.n_blocks, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
+    k_ovl_mark<false><<<g, 256, 0, s>>>(m, pd, od, st, pts, side, res, maps);
 }
 void launch_ovl_count(hipStream_t s, int n_pairs, int n_groups, const PairDesc* pd, const OvlDesc* od_read,
                       const OvlDesc* od_ref, PairState* st, PairState* gst, const uint8_t* maps) {
