@@ -929,7 +929,7 @@ static int win_ref_icp(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cf
     launch_ovl_bbox(si, R.m_gref, dG, dGst, sl.ref_raw.as<float4>(), 0, res);
     launch_ovl_size(si, 1, dGst, dOvl, dCap);
     launch_ovl_clear(si, 1, dOvl, bmp, R.cap[0]);
-    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp, false, S->opt.ref_mark_blocks);
+    launch_ovl_mark(si, R.m_gref, dG, dOvl, dGst, sl.ref_raw.as<float4>(), 0, res, bmp, false);
     launch_ovl_popcount(si, 1, dOvl, dGst, 0, bmp);
   }
   HIPC(hipStreamWaitEvent(si, sl.ev_rd, 0));  // (the slot's previous window is done: its upload waited)

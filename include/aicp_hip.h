@@ -145,8 +145,7 @@ typedef struct {
                                  copied or compared between calls */
   uint32_t oneshot_keep_mib;  /* device copies of a one-shot call's inputs are kept for the next
                                  call up to this size (MiB), released above it; 4096 */
-  uint32_t ref_mark_blocks;   /* stream: workgroups of the reference's voxel-map marks, which run
-                                 beside the window's matcher kd-tree build (0: one per 256 rays) */
+  uint32_t reserved;          /* 0 */
   uint64_t read_order_min;    /* Morton order of a batch's readings from this many points on;
                                  200000 */
 } aicp_hip_options;
