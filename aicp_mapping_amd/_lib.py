@@ -39,12 +39,13 @@ EXPORTS = [
     "aicp_hip_map_register_batch", "aicp_hip_multi_create", "aicp_hip_multi_destroy", "aicp_hip_multi_size",
     "aicp_hip_multi_context", "aicp_hip_multi_last_error", "aicp_hip_multi_align_batch",
     "aicp_hip_reference_cache_stats", "aicp_hip_default_options", "aicp_hip_set_options", "aicp_hip_get_options",
-    "aicp_hip_test_force_scan_stall",
+    "aicp_hip_test_force_scan_stall", "aicp_hip_sequence_run_raw",
 ]
 
 
 _NEWEST = {"aicp_hip_reference_cache_stats", "aicp_hip_default_options", "aicp_hip_set_options",
-           "aicp_hip_get_options", "aicp_hip_test_force_scan_stall"}  # added in r05 / r06
+           "aicp_hip_get_options", "aicp_hip_test_force_scan_stall",
+           "aicp_hip_sequence_run_raw"}  # added in r05 / r06
 
 
 class IcpConfig(C.Structure):
@@ -261,6 +262,10 @@ def _load():
     L.aicp_hip_sequence_run.argtypes = [vp, cfgp, C.POINTER(SequenceParams), C.POINTER(Cloud), C.POINTER(Cloud), sz,
                                         fp, C.POINTER(SequenceResult), C.POINTER(C.c_size_t)]
     L.aicp_hip_last_sequence_timing.argtypes = [vp, C.POINTER(SequenceTiming)]
+    if hasattr(L, "aicp_hip_sequence_run_raw"):
+        L.aicp_hip_sequence_run_raw.argtypes = [vp, cfgp, C.POINTER(SequenceParams), C.POINTER(PrefilterParams),
+                                                C.POINTER(Cloud), C.POINTER(Cloud), sz, fp, C.POINTER(SequenceResult),
+                                                C.POINTER(C.c_size_t)]
     L.aicp_hip_map_register_batch.argtypes = [vp, cfgp, vp, C.c_float, C.c_float, C.POINTER(Cloud), fp, sz, C.c_int,
                                               fp, stp]
     if hasattr(L, "aicp_hip_reference_cache_stats"):
@@ -529,13 +534,17 @@ class Context:
     def upload(self, pairs):
         return ResidentBatch(self, pairs)
 
-    def sequence_run(self, first, first_origin, readings, origins, cfg=None, params=None, raise_on_error=True):
+    def sequence_run(self, first, first_origin, readings, origins, cfg=None, params=None, raise_on_error=True,
+                     prefilter=None):
         """App's frame-to-reference stream (aicp_hip_sequence_run): the first cloud is the
         reference, readings[i] (prior-pose origin origins[i]) are registered in order with the
         windowed reference update and the max-correction drop. Returns (T[n, 4, 4] row-major
-        corrections, list of result dicts, n_done, rc)."""
+        corrections, list of result dicts, n_done, rc). prefilter (PrefilterParams, or True for
+        the defaults): the clouds are RAW and run in App's order (aicp_hip_sequence_run_raw)."""
         cfg = cfg or default_config()
         prm = params or default_sequence_params()
+        if prefilter is True:
+            prefilter = default_prefilter()
         n = len(readings)
         fc, keep0 = make_cloud(first, first_origin)
         arr = (Cloud * max(n, 1))()
@@ -547,8 +556,12 @@ class Context:
         outT = np.zeros((max(n, 1), 16), np.float32)
         res = (SequenceResult * max(n, 1))()
         done = C.c_size_t(0)
-        rc = lib.aicp_hip_sequence_run(self.h, C.byref(cfg), C.byref(prm), C.byref(fc), arr, n, _fptr(outT), res,
-                                       C.byref(done))
+        if prefilter is not None:
+            rc = lib.aicp_hip_sequence_run_raw(self.h, C.byref(cfg), C.byref(prm), C.byref(prefilter), C.byref(fc), arr,
+                                               n, _fptr(outT), res, C.byref(done))
+        else:
+            rc = lib.aicp_hip_sequence_run(self.h, C.byref(cfg), C.byref(prm), C.byref(fc), arr, n, _fptr(outT), res,
+                                           C.byref(done))
         if raise_on_error and rc != AICP_OK:
             self.check(rc)
         T = outT[:n].reshape(-1, 4, 4).transpose(0, 2, 1).copy()

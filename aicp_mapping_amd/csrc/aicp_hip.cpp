@@ -1210,7 +1210,7 @@ void aicp_hip_destroy(aicp_hip_ctx* ctx) {
                     &ctx->ctrs, &ctx->nbids, &ctx->ref1, &ctx->sel_hist, &ctx->sel_cand, &ctx->sel_cnt,
                     &ctx->qmap, &ctx->ovl, &ctx->rdesc, &ctx->rstate, &ctx->rdesc_raw, &ctx->bpts_raw,
                     &ctx->nodes_raw, &ctx->nrm_raw, &ctx->inv, &ctx->gdesc, &ctx->gstate, &ctx->tl, &ctx->ptl,
-                    &ctx->tl_rank, &ctx->pf_a, &ctx->pf_b})
+                    &ctx->tl_rank, &ctx->pf_a, &ctx->pf_b, &ctx->pf_bpts, &ctx->pf_nodes})
     release(*b);
   for (auto& t : ctx->tb) t.release_all();
   free_batch(ctx->oneshot);
@@ -1768,7 +1768,7 @@ static int pf_layout(aicp_hip_ctx* ctx, size_t n, PfLayout* L) {
 
 // the whole chain on n points already in the layout's pts4 (enqueued on ctx->stream)
 static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n, const PfLayout& Lo, PfRun* o) {
-  ctx->refc.invalidate();  // (the sampled cloud's tree goes to ctx->bpts / nodes)
+  // (the sampled cloud's tree goes to pf_bpts / pf_nodes: a cached reference stays resident)
   hipStream_t s = ctx->stream;
   const int K = prm->normal_k, NB = prm->neighbours;
   for (auto& e : ctx->pf_ev)
@@ -1805,17 +1805,17 @@ static int pf_core(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, size_t n
   HIPC(ensure(ctx->desc, sizeof(PairDesc)));
   HIPC(hipMemcpyAsync(ctx->desc.p, &d, sizeof(d), hipMemcpyHostToDevice, s));
   int rc = device_trees_begin(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), ctx->ref1.as<float4>(), 0, 8,
-                              ctx->bpts, ctx->nodes);
+                              ctx->pf_bpts, ctx->pf_nodes);
   if (rc) return rc;
-  rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), 8, ctx->bpts, ctx->nodes, 0);
+  rc = device_trees_end(ctx->tb[0], ctx->err, s, 1, V, ctx->desc.as<PairDesc>(), 8, ctx->pf_bpts, ctx->pf_nodes, 0);
   if (rc) return rc;
   HIPC(ensure(ctx->match, (size_t)V * K * 4));
   HIPC(ensure(ctx->ctrs, kCtrWords * 4 + 16));
   HIPC(hipMemsetAsync(ctx->ctrs.p, 0, kCtrWords * 4 + 16, s));
-  const float4* bpts = ctx->bpts.as<float4>();
+  const float4* bpts = ctx->pf_bpts.as<float4>();
   unsigned long long* dtouch = (unsigned long long*)(ctx->ctrs.as<uint32_t>() + kCtrWords);
   HIPC(hipEventRecord(E[2], s));
-  if (!launch_knn_ids(s, 1, V, ctx->desc.as<PairDesc>(), ctx->nodes.as<uint4>(), bpts, K, ctx->match.as<int32_t>(),
+  if (!launch_knn_ids(s, 1, V, ctx->desc.as<PairDesc>(), ctx->pf_nodes.as<uint4>(), bpts, K, ctx->match.as<int32_t>(),
                       ctx->ctrs.as<uint32_t>(), dtouch, ctx->opt.normals_knn_engine))
     FAIL(AICP_ERR_UNSUPPORTED, "normal_k must be 10, 20 or 30");
   HIPC(hipGetLastError());
@@ -2142,6 +2142,169 @@ int aicp_hip_map_prefilter(aicp_hip_ctx* ctx, aicp_hip_map* map, const aicp_pref
   map->n = o.V ? o.n_out : 0;
   ctx->last_pf.wall_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wall).count();
+  return AICP_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// One raw cloud through regionGrowingUniformPlaneSegmentationFilter on the device, moved first
+// by T when T is given (pcl::transformPointCloud in float, launch_transform: setAndFilterReading's
+// debug branch, app.cpp:90-99). The kept points come back packed xyz (clusters concatenated).
+int pf_cloud(aicp_hip_ctx* ctx, const aicp_prefilter_params* prm, const aicp_cloud& c, const float* T,
+             std::vector<float>& out) {
+  out.clear();
+  hipStream_t s = ctx->stream;
+  PfLayout Lo;
+  int rc = pf_layout(ctx, c.n, &Lo);
+  if (rc) return rc;
+  HIPC(hipStreamSynchronize(s));  // (pin_io and scratch are free)
+  HIPC(ensure(ctx->pin_io, c.n * 16 + 64));
+  float* h = ctx->pin_io.as<float>();
+  if (T) {
+    HIPC(ensure(ctx->scratch, 64 + c.n * 16));
+    std::memcpy(h, T, 64);
+    pack_xyz4(c.pts, c.n, c.stride, h + 16);
+    char* d = ctx->scratch.as<char>();
+    HIPC(hipMemcpyAsync(d, h, 64 + c.n * 16, hipMemcpyHostToDevice, s));
+    launch_transform(s, (int)c.n, (const float*)d, (const float4*)(d + 64), Lo.pts4);
+    HIPC(hipGetLastError());
+  } else {
+    pack_xyz4(c.pts, c.n, c.stride, h);
+    HIPC(hipMemcpyAsync(Lo.pts4, h, c.n * 16, hipMemcpyHostToDevice, s));
+  }
+  PfRun o;
+  rc = pf_core(ctx, prm, c.n, Lo, &o);  // (returns with the stream idle)
+  if (rc) return rc;
+  if (!o.V || !o.n_out) return AICP_OK;
+  HIPC(hipMemcpy(h, o.out4, (size_t)o.n_out * 16, hipMemcpyDeviceToHost));
+  out.resize(3 * (size_t)o.n_out);
+  for (size_t i = 0; i < o.n_out; ++i)
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = h[4 * i + k];
+  return AICP_OK;
+}
+
+aicp_cloud packed_cloud(const std::vector<float>& p, const double origin[3]) {
+  aicp_cloud c{};
+  c.pts = p.data();
+  c.n = p.size() / 3;
+  c.stride = 12;
+  for (int k = 0; k < 3; ++k) c.origin[k] = origin[k];
+  return c;
+}
+}  // namespace
+
+extern "C" {
+
+// App's stream from raw clouds in App's order (app.cpp:282-414 with setAndFilterReading,
+// app.cpp:77-100): see include/aicp_hip.h.
+int aicp_hip_sequence_run_raw(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                              const aicp_prefilter_params* pf, const aicp_cloud* first, const aicp_cloud* readings,
+                              size_t n, float* out_T, aicp_sequence_result* out, size_t* n_done) {
+  if (!ctx || !cfg || !prm || !pf || !first || (n && (!readings || !out_T || !out)) || !n_done) return AICP_ERR_INVALID;
+  *n_done = 0;
+  int rc = pf_check(ctx, pf);
+  if (rc) return rc;
+  const int F = prm->reference_update_frequency;
+  if (F < 1) FAIL(AICP_ERR_INVALID, "reference_update_frequency must be >= 1");
+  const bool doOvl = prm->flags & AICP_RUN_OVERLAP, debug = prm->flags & AICP_SEQ_DEBUG;
+  if (doOvl && !(prm->resolution > 0)) FAIL(AICP_ERR_INVALID, "resolution");
+  rc = check_cfg(ctx, cfg, AICP_RUN_ICP | (doOvl ? AICP_RUN_OVERLAP : 0));
+  if (rc) return rc;
+  auto valid = [](const aicp_cloud& c) {
+    return c.pts && c.n >= 1 && c.n < (1ull << 31) && c.stride >= 12 && c.stride % 4 == 0;
+  };
+  if (!valid(*first)) FAIL(AICP_ERR_INVALID, "invalid first cloud");
+  for (size_t i = 0; i < n; ++i)
+    if (!valid(readings[i])) FAIL(AICP_ERR_INVALID, "invalid reading " + std::to_string(i));
+  HIPC(hipSetDevice(ctx->device));
+  // the first cloud: pre-filtered as given (processCloud, app.cpp:293-297)
+  std::vector<float> ref;
+  rc = pf_cloud(ctx, pf, *first, nullptr, ref);
+  if (rc) return rc;
+  if (ref.empty()) FAIL(AICP_ERR_INVALID, "the first cloud keeps no point after the pre-filter");
+  // a reading the pre-filter empties fails its registration (libpointmatcher throws on an empty
+  // cloud), which ends the stream like any registration error (app.cpp:210)
+  auto empty_reading = [&](size_t i, int reference) {
+    out[i] = aicp_sequence_result{};
+    out[i].status = out[i].icp.status = AICP_ERR_INVALID;
+    out[i].reference = reference;
+    ident4(out_T + 16 * i);
+    *n_done = i + 1;
+    FAIL(AICP_ERR_INVALID, "reading " + std::to_string(i) + " keeps no point after the pre-filter");
+  };
+  if (!debug) {  // robot mode: each reading pre-filtered as given (app.cpp:87-88), then the stream
+    std::vector<std::vector<float>> kept(n);
+    std::vector<aicp_cloud> clouds(n);
+    size_t m = n;
+    for (size_t i = 0; i < n && m == n; ++i) {
+      rc = pf_cloud(ctx, pf, readings[i], nullptr, kept[i]);
+      if (rc) return rc;
+      if (kept[i].empty()) m = i;
+      clouds[i] = packed_cloud(kept[i], readings[i].origin);
+    }
+    const aicp_cloud c0 = packed_cloud(ref, first->origin);
+    rc = aicp_hip_sequence_run(ctx, cfg, prm, &c0, clouds.data(), m, out_T, out, n_done);
+    if (rc || m == n) return rc;
+    int reference = -1;
+    for (size_t i = 0; i < m; ++i)
+      if (out[i].is_reference) reference = (int)i;
+    return empty_reading(m, reference);
+  }
+  // debug mode: reading after reading (initialT_ carries every accepted correction)
+  float initT[16];
+  ident4(initT);
+  double ref_origin[3] = {first->origin[0], first->origin[1], first->origin[2]};
+  int ref_id = -1, acc = 0;
+  const int flags = AICP_RUN_ICP | (doOvl ? AICP_RUN_OVERLAP : 0) | (prm->flags & AICP_RUN_TIME_NN);
+  std::vector<float> rd;
+  for (size_t i = 0; i < n; ++i) {
+    // setAndFilterReading (app.cpp:90-99): the raw reading moved by initialT_, then pre-filtered;
+    // its prior pose becomes initialT_iso * prior pose
+    double o[3];
+    corrected_origin(initT, readings[i].origin, o);
+    rc = pf_cloud(ctx, pf, readings[i], initT, rd);
+    if (rc) return rc;
+    if (rd.empty()) return empty_reading(i, ref_id);
+    aicp_pair p{};
+    p.ref = ref.data();
+    p.n_ref = ref.size() / 3;
+    p.ref_stride = 12;
+    p.read = rd.data();
+    p.n_read = rd.size() / 3;
+    p.read_stride = 12;
+    for (int k = 0; k < 3; ++k) {
+      p.ref_origin[k] = ref_origin[k];
+      p.read_origin[k] = o[k];
+    }
+    aicp_sequence_result& r = out[i];
+    r = aicp_sequence_result{};
+    r.reference = ref_id;
+    float* T = out_T + 16 * i;
+    ident4(T);
+    // computeOverlap -> ratio -> registerClouds against the resident reference (app.cpp:218-247)
+    rc = oneshot(ctx, cfg, &p, 1, doOvl ? prm->resolution : 0.0, flags, T, &r.icp, nullptr);
+    if (!rc) rc = r.icp.status;
+    r.status = r.icp.status = rc;
+    *n_done = i + 1;
+    if (rc) {  // the worker ends here (app.cpp:210)
+      ctx->err = "reading " + std::to_string(i) + ": status " + std::to_string(rc) + ": " + ctx->err;
+      return rc;
+    }
+    if (correction_rejected(T, prm->max_correction_magnitude)) continue;  // app.cpp:366-373
+    r.accepted = 1;
+    corrected_origin(T, o, r.corrected_origin);
+    if (++acc == F) {  // the corrected reading is the next reference (app.cpp:375-391)
+      std::vector<float> next(rd.size());
+      for (size_t j = 0; j < rd.size(); j += 3) apply4(T, rd[j], rd[j + 1], rd[j + 2], &next[j]);
+      ref.swap(next);
+      for (int k = 0; k < 3; ++k) ref_origin[k] = r.corrected_origin[k];
+      ref_id = (int)i;
+      r.is_reference = 1;
+      acc = 0;
+    }
+    mul4(T, initT, initT);  // initialT_ = correction * initialT_ (app.cpp:414)
+  }
   return AICP_OK;
 }
 

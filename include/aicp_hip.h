@@ -339,10 +339,8 @@ int aicp_hip_last_phase_ms(const aicp_hip_ctx* ctx, double out_ms[5]);
  * Filter order: this entry point takes pre-filtered clouds in both modes and moves them by
  * initialT_ afterwards. App moves the RAW reading first and pre-filters the moved cloud
  * (setAndFilterReading, app.cpp:87-99); the 0.08 m VoxelGrid is aligned to the world frame, so the
- * two orders keep different points unless initialT_ is the identity. For App's exact debug order
- * the caller runs aicp_hip_prefilter on initialT_ * raw reading itself (one reading at a time:
- * initialT_ then depends on the previous correction), as registration.AicpPipeline's debug mode
- * does; the stream is the robot-mode fast path. */
+ * two orders keep different points unless initialT_ is the identity. App's exact order is
+ * aicp_hip_sequence_run_raw below; this entry point is the robot-mode fast path. */
 #define AICP_SEQ_DEBUG 8
 
 typedef struct {
@@ -377,6 +375,25 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
                           const aicp_cloud* first, const aicp_cloud* readings, size_t n_readings,
                           float* out_T /* 16*n */, aicp_sequence_result* out /* n */, size_t* n_done);
 int aicp_hip_last_sequence_timing(const aicp_hip_ctx* ctx, aicp_sequence_timing* out);
+
+/* App's stream from RAW clouds, in App's own order (processCloud, app.cpp:282-414 with
+ * setAndFilterReading, app.cpp:77-100): the first cloud is pre-filtered as given (app.cpp:293-297)
+ * and becomes the reference. Robot mode: every reading is pre-filtered as given on the device,
+ * then the kept points run through aicp_hip_sequence_run. Debug mode (prm->flags AICP_SEQ_DEBUG):
+ * reading after reading, the RAW reading is moved by initialT_ on the device
+ * (pcl::transformPointCloud, float), the moved cloud is pre-filtered there, its prior pose becomes
+ * initialT_ * prior pose, and it is registered against the current reference (overlap ->
+ * auto-tuned ratio -> ICP; the reference's trees stay resident across readings); then the drop
+ * test, the reference update and initialT_ = correction * initialT_ (app.cpp:362-414). The
+ * pre-filter's region growing is host-driven, so debug mode takes host round trips per reading.
+ * pf: the pre-filter (aicp_hip_default_prefilter). A reading the pre-filter empties ends the
+ * stream with AICP_ERR_INVALID as its status (libpointmatcher throws on an empty cloud).
+ * Results as aicp_hip_sequence_run (corrected_origin from initialT_ * prior pose in debug mode);
+ * aicp_hip_last_sequence_timing describes robot mode's inner aicp_hip_sequence_run only. */
+int aicp_hip_sequence_run_raw(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const aicp_sequence_params* prm,
+                              const aicp_prefilter_params* pf, const aicp_cloud* first, const aicp_cloud* readings,
+                              size_t n_readings, float* out_T /* 16*n */, aicp_sequence_result* out /* n */,
+                              size_t* n_done);
 
 /* ---- kernel-level entry points (parity tests and diagnostics) --------------------------- */
 /* kd-tree over pts (as given, no centring) + k-NN of queries: libnabo

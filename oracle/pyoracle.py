@@ -372,7 +372,8 @@ def mul4(A, B):
 
 
 def sequence(first, first_origin, readings, origins, cfg=None, reference_update_frequency=5,
-             max_correction_magnitude=1.0, resolution=0.2, overlap=True, stop=None, working_mode="robot"):
+             max_correction_magnitude=1.0, resolution=0.2, overlap=True, stop=None, working_mode="robot",
+             prefilter_with=None):
     """App::processCloud over a stream (app.cpp:282-414, robot mode): the first cloud is the
     reference; each reading: overlap -> ratio -> ICP against the current reference; dropped when
     some |T(i,3)| > max_correction_magnitude (float compare, app.cpp:366-373); an accepted reading
@@ -382,9 +383,17 @@ def sequence(first, first_origin, readings, origins, cfg=None, reference_update_
     working_mode "debug" (app.cpp:87-96, 414): each reading is first transformed by initialT_
     (float, transform_cloud) and its prior pose becomes initialT_ * prior pose; after an accepted
     reading initialT_ = correction * initialT_ (a dropped reading returns before that line).
+    prefilter_with (PrefilterParams, or True for the defaults): the clouds are RAW, in App's order:
+    the first cloud is pre-filtered as given (app.cpp:293-297); a reading is moved by initialT_
+    (debug mode) and then pre-filtered (setAndFilterReading, app.cpp:77-100). Each record then also
+    holds n_kept, the reading's point count after the pre-filter.
     Returns a list of dicts (status, T, stats, accepted, reference, is_reference,
     corrected_origin, overlap, counts, ratio, prior_origin)."""
     cfg = cfg or default_config()
+    pfp = None
+    if prefilter_with is not None:
+        pfp = prefilter_params() if prefilter_with is True else prefilter_with
+        first = prefilter(first, pfp)["out"]
     ref, ref_origin, ref_id = _pts(first), np.asarray(first_origin, np.float64), -1
     acc = 0
     out = []
@@ -396,8 +405,12 @@ def sequence(first, first_origin, readings, origins, cfg=None, reference_update_
         if working_mode == "debug":
             r = transform_cloud(initT, r)
             o = corrected_origin(initT, o)
+        if pfp is not None:
+            r = prefilter(r, pfp)["out"]
         rec = dict(reference=ref_id, is_reference=0, accepted=0, corrected_origin=None,
                    prior_origin=np.asarray(o, np.float64))
+        if pfp is not None:
+            rec["n_kept"] = len(r)
         if overlap:
             ov, cnt = globals()["overlap"](ref, ref_origin, r, o, resolution)
             ratio = autotune_ratio(ov)

@@ -246,3 +246,48 @@ def test_sequence_debug_mode_sparse_overlap(ctx, oracle, L):
     assert [o["icp"]["overlap_keys"] for o in out0] == [o["icp"]["overlap_keys"] for o in out1]
     ref = oracle.sequence(st.first, st.first_origin, st.readings, st.origins, resolution=RES, working_mode="debug")
     _compare(out1, ref, T1)
+
+
+@pytest.mark.parametrize("mode,jumps", [("debug", None), ("debug", {3: (0.6, 0, 0)}), ("robot", None)])
+def test_sequence_raw_clouds_in_app_order(ctx, oracle, L, mode, jumps):
+    """App's order from RAW clouds (aicp_hip_sequence_run_raw): the first cloud is pre-filtered as
+    given (app.cpp:293-297); in debug mode each raw reading is moved by initialT_ and then
+    pre-filtered (setAndFilterReading, app.cpp:77-100), in robot mode pre-filtered as given. The
+    oracle replays the same order (pcl::transformPointCloud, then its pre-filter restatement):
+    decisions, references, key counts, iterations and corrections agree, and the reference's
+    trees stay resident across the per-reading pre-filters."""
+    st = sy.make_stream(n_readings=10, n_points=20000, seed=8, half=12.0, jumps=jumps)
+    flags = L.AICP_RUN_OVERLAP | (L.AICP_SEQ_DEBUG if mode == "debug" else 0)
+    prm = L.default_sequence_params(max_correction_magnitude=0.4, flags=flags)
+    s0 = ctx.reference_cache_stats()
+    T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm,
+                                        prefilter=True)
+    s1 = ctx.reference_cache_stats()
+    assert rc == 0 and done == 10
+    ref = oracle.sequence(st.first, st.first_origin, st.readings, st.origins, max_correction_magnitude=0.4,
+                          resolution=RES, working_mode=mode, prefilter_with=True)
+    _compare(out, ref, T)
+    if jumps:
+        assert not out[3]["accepted"] and ref[3]["accepted"] == 0
+    if mode == "debug":  # one tree build per reference, every other reading reuses it
+        n_refs = len({o["reference"] for o in out})
+        assert s1["tree_builds"] - s0["tree_builds"] == n_refs
+        assert s1["tree_hits"] - s0["tree_hits"] == 10 - n_refs
+
+
+@pytest.mark.parametrize("mode", ["debug", "robot"])
+def test_sequence_raw_empty_after_prefilter_ends_stream(ctx, oracle, L, mode):
+    """A reading the pre-filter empties (30 scattered points: no region of 50) fails its
+    registration, which ends the stream there (app.cpp:210); the readings before it are App's."""
+    st = sy.make_stream(n_readings=5, n_points=20000, seed=3, half=12.0)
+    rng = np.random.default_rng(4)
+    reads = st.readings[:3] + [rng.uniform(-5, 5, size=(30, 3)).astype(np.float32)] + st.readings[4:]
+    flags = L.AICP_RUN_OVERLAP | (L.AICP_SEQ_DEBUG if mode == "debug" else 0)
+    prm = L.default_sequence_params(flags=flags)
+    T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, reads, st.origins, params=prm, prefilter=True,
+                                        raise_on_error=False)
+    assert rc == L.AICP_ERR_INVALID and done == 4
+    assert out[3]["status"] == L.AICP_ERR_INVALID and not out[3]["accepted"]
+    ref = oracle.sequence(st.first, st.first_origin, reads, st.origins, resolution=RES, working_mode=mode,
+                          prefilter_with=True, stop=3)
+    _compare(out[:3], ref, T[:3])
