@@ -372,7 +372,7 @@ def bench_stream(args):
 
     def step(timed=False):
         T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, cfg,
-                                            prm_t if timed else prm)
+                                            prm_t if timed else prm, prefilter=True if args.raw else None)
         if dist is not None:
             sh.gather_records(sh.pack_records(T.transpose(0, 2, 1).reshape(-1, 16),
                                               [o["icp"]["iterations"] for o in out],
@@ -437,8 +437,11 @@ def bench_stream(args):
                                   n_pts, n_read, args.ref_every, prm.max_correction_magnitude),
                   "readings_per_step_per_gpu": n_read, "windows_per_step": windows, "replans": replans,
                   "working_mode": args.working_mode,
+                  "raw_clouds": bool(args.raw),
                   "chain": CHAIN, "overlap": "octree-equivalent voxel sets at 0.2 m",
-                  "timed_region": "host clouds -> packing -> H2D -> device -> corrections (aicp_hip_sequence_run)",
+                  "timed_region": ("raw host clouds -> device pre-filter (App's order) -> stream -> corrections "
+                                   "(aicp_hip_sequence_run_raw)" if args.raw else
+                                   "host clouds -> packing -> H2D -> device -> corrections (aicp_hip_sequence_run)"),
                   "parallelism": "one stream per rank (replicas), RCCL all_gather of T"}
         out_line = base_line(args, world, METRIC, value, "aligned clouds/s", 1e3 * elapsed / args.steps, DTYPE, DATA,
                              config)
@@ -489,7 +492,7 @@ def cpu_stream(st, T, out, args):
         t = time.perf_counter()
         last["r"] = po.sequence(st.first, st.first_origin, st.readings[:k], st.origins[:k],
                                 reference_update_frequency=args.ref_every, resolution=res,
-                                working_mode=args.working_mode)
+                                working_mode=args.working_mode, prefilter_with=True if args.raw else None)
         return k, time.perf_counter() - t
 
     med, rates = median_rate(rep, args.cpu_reps)
@@ -497,9 +500,9 @@ def cpu_stream(st, T, out, args):
     same = all(r["is_reference"] == out[i]["is_reference"] and r["accepted"] == out[i]["accepted"] and
                r["stats"].iterations == out[i]["icp"]["iterations"] for i, r in enumerate(last["r"]))
     cb = {"value": med, "unit": "aligned_clouds/s", "cores": 1, "kind": "port",
-          "sample": "oracle replay of App's stream on readings 0..%d of the same workload (overlap + ratio + ICP, "
+          "sample": "oracle replay of App's stream on readings 0..%d of the same workload (%soverlap + ratio + ICP, "
                     "reference update after reading %d), N=%d, on 1 host core (%s, nproc %d); median of %d runs: %s "
-                    "clouds/s" % (k - 1, args.ref_every - 1, len(st.readings[0]), cpu_model(), os.cpu_count(),
+                    "clouds/s" % (k - 1, "pre-filter + " if args.raw else "", args.ref_every - 1, len(st.readings[0]), cpu_model(), os.cpu_count(),
                                   len(rates), ", ".join("%.3f" % r for r in rates))}
     par = {"readings": k, "max_rot_rad": max(e[0] for e in pe), "max_trans_m": max(e[1] for e in pe),
            "same_decisions_and_iterations": bool(same), "tol": [1e-4, 1e-3]}
@@ -889,6 +892,9 @@ def main():
     ap.add_argument("--ref-every", type=int, default=5, help="reference_update_frequency")
     ap.add_argument("--working-mode", choices=["robot", "debug"], default="robot",
                     help="App's working_mode for c2/c3 (debug: readings pre-transformed by initialT_, serial)")
+    ap.add_argument("--raw", action="store_true",
+                    help="c2/c3: the clouds are raw; App's pre-filter runs in App's order inside the timed "
+                         "region (aicp_hip_sequence_run_raw)")
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--data", default=None,
                     help="recorded directory (aicp_input_poses.csv + cloud_*.pcd) replayed as the stream")

@@ -248,7 +248,7 @@ def test_sequence_debug_mode_sparse_overlap(ctx, oracle, L):
     _compare(out1, ref, T1)
 
 
-@pytest.mark.parametrize("mode,jumps", [("debug", None), ("debug", {3: (0.6, 0, 0)}), ("robot", None)])
+@pytest.mark.parametrize("mode,jumps", [("debug", None), ("debug", {3: (0, -0.8, 0)}), ("robot", None)])
 def test_sequence_raw_clouds_in_app_order(ctx, oracle, L, mode, jumps):
     """App's order from RAW clouds (aicp_hip_sequence_run_raw): the first cloud is pre-filtered as
     given (app.cpp:293-297); in debug mode each raw reading is moved by initialT_ and then
