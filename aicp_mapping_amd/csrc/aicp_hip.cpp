@@ -963,27 +963,46 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     }
     const bool early = !ctx->opt.no_early_exit;
     auto polled = [&](int k) { return early && k >= cfg->smooth_length && k < kBatchPolls && k < cfg->max_iter; };
+    // every iteration's active count is written (not only the polled ones'), so the words written
+    // so far are a prefix and its last word tells whether more will come (see sequence.cpp, loop_poll)
+    auto written = [&](int k) { return early && k < kBatchPolls; };
     std::deque<int> pending;
     bool stop = false;
     for (int it = 0; it < cfg->max_iter && !stop; ++it) {
       // every poll slot before this iteration read: its active count was not 0
       while (!pending.empty() && pending.front() < it && !stop) {
-        volatile uint32_t* w = ctx->poll_host + pending.front();
-        while (*w == 0xffffffffu) {
-          const hipError_t q = hipStreamQuery(s);
-          if (q == hipErrorNotReady) {
-            std::this_thread::yield();
-            continue;
+        const int k = pending.front();
+        volatile uint32_t* w = ctx->poll_host;
+        const auto t0 = std::chrono::steady_clock::now();
+        while (w[k] == 0xffffffffu) {
+          // the last word written so far is 0: no launch after it had an active pair, so this one
+          // stays unwritten (no hipStreamQuery on the way: it enqueues a marker the next kernel
+          // waits behind)
+          int m = k - 1;
+          while (m >= 0 && w[m] == 0xffffffffu) --m;
+          if (m >= 0 && w[m] == 0u) break;
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
+            const hipError_t q = hipStreamQuery(s);  // (a stream that drained without writing it)
+            if (q != hipErrorNotReady) {
+              HIPC(q);
+              std::atomic_thread_fence(std::memory_order_seq_cst);
+              break;
+            }
           }
-          HIPC(q);
-          std::atomic_thread_fence(std::memory_order_seq_cst);
-          break;  // the stream drained without writing it: the launch that would have had no active pair
+          std::this_thread::yield();
         }
-        stop = *w == 0u || *w == 0xffffffffu;
+        stop = w[k] == 0u || w[k] == 0xffffffffu;
         pending.pop_front();
       }
       if (stop) break;
-      if (it == 0) launch_active_list(s, (int)P, dDesc, dState, al, dCtr);
+      if (it == 0) {
+        uint32_t* hn0 = nullptr;
+        if (written(0)) {
+          ctx->poll_host[0] = 0xffffffffu;
+          hn0 = ctx->poll_dev;
+        }
+        launch_active_list(s, (int)P, dDesc, dState, al, dCtr, hn0);
+      }
       prm.prof_slot = nn_launches;
       launch_icp_nn(s, (int)reads, dDesc, dState, al, readc, nodes, ctx->tl_total ? ctx->tl.as<uint4>() : nullptr,
                     nullptr, bpts, ctx->tl_total ? ctx->ptl.as<uint2>() : nullptr, ctx->match.as<int32_t>(),
@@ -997,10 +1016,10 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
       y.st = dState;
       y.al = al;
       y.ctr = dCtr;
-      if (polled(it + 1)) {
+      if (written(it + 1)) {
         ctx->poll_host[it + 1] = 0xffffffffu;  // (before the launch that writes it)
         y.host_n = ctx->poll_dev + it + 1;
-        pending.push_back(it + 1);
+        if (polled(it + 1)) pending.push_back(it + 1);
       }
       if (sel_pair)
         launch_icp_select_pair(s, (int)P, dDesc, dState, ctx->d2.as<float>(), ctx->sel_cand.as<uint32_t>(), y);

@@ -975,6 +975,8 @@ struct IcpLoop {
   int it = 0;      // iterations enqueued whole
   int nn = 0;      // iterations whose NN launch is enqueued (it or it + 1)
   bool stop = false;
+  int wait_it = -1;  // the poll word being waited for since wait_t0 (the drained-stream check)
+  std::chrono::steady_clock::time_point wait_t0;
 };
 
 // the blocks [off, off + cnt) of a block map
@@ -999,11 +1001,15 @@ static IcpParams icp_params(const aicp_icp_config* cfg) {
   return ip;
 }
 
-// whether the active count at the start of iteration k is written to poll word k (from
-// smoothLength on: no pair can stop earlier except on an error)
+// whether the host waits for poll word k, the active count at the start of iteration k, before
+// it enqueues the rest of that iteration (from smoothLength on: no pair can stop earlier except on
+// an error)
 static bool loop_polled(const SeqState* S, const aicp_icp_config* cfg, int k) {
   return !S->opt.no_early_exit && k >= cfg->smooth_length && k < kMaxPolls && k < cfg->max_iter;
 }
+// whether poll word k is written at all: every iteration's, so that the words written so far are a
+// prefix and the last of them tells whether more will come (loop_poll)
+static bool loop_written(const SeqState* S, int k) { return !S->opt.no_early_exit && k < kMaxPolls; }
 
 // The pairs one loop iterates: the window's, or (debug mode) reading q.sub alone.
 struct LoopPairs {
@@ -1035,7 +1041,7 @@ static int loop_part(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
   // is marked unwritten before that launch is enqueued
   if (part == 0) {
     uint32_t* hn_this = nullptr;
-    if (it == 0 && loop_polled(S, cfg, it)) {
+    if (it == 0 && loop_written(S, it)) {
       poll_host[it] = 0xffffffffu;
       hn_this = poll_dev + it;
     }
@@ -1059,7 +1065,7 @@ static int loop_part(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
   const BlockMap msel = r >= 0 ? map_sub(R.m_sel, R.b_sel[r], R.b_sel[r + 1] - R.b_sel[r]) : R.m_sel;
   const BlockMap mred = r >= 0 ? map_sub(R.m_red, R.b_red[r], R.b_red[r + 1] - R.b_red[r]) : R.m_red;
   uint32_t* hn_next = nullptr;
-  if (loop_polled(S, cfg, it + 1)) {
+  if (loop_written(S, it + 1)) {
     poll_host[it + 1] = 0xffffffffu;
     hn_next = poll_dev + it + 1;
   }
@@ -1108,22 +1114,42 @@ static int loop_finish(aicp_hip_ctx* ctx, SeqState* S, const aicp_sequence_param
 static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool& got) {
   got = false;
   SeqSlot& sl = S->slot[q.R->w.slot];
-  volatile uint32_t* w = sl.poll_host + q.area * kMaxPolls + q.it;
-  if (*w == 0xffffffffu) {
-    // not written yet: still running, or the launch that writes it had no active pair (then
-    // the stream drains and the word stays unwritten: the loop is over)
+  volatile uint32_t* w = sl.poll_host + q.area * kMaxPolls;
+  if (w[q.it] == 0xffffffffu) {
+    // Not written yet. Every iteration's word is written by the launch that builds its active
+    // list (loop_written; reset before that launch is enqueued), so the words written so far are a
+    // prefix: when the last of them is 0, no launch after it had an active pair and this one stays
+    // unwritten -- the loop is over. (r06: the drained-stream test by hipStreamQuery that this
+    // replaces enqueued a marker behind the NN launch, and the next iteration's select waited
+    // ~7.5 us behind it, C2 kernel trace.)
+    int m = q.it - 1;
+    while (m >= 0 && w[m] == 0xffffffffu) --m;
+    if (m >= 0 && w[m] == 0u) {
+      got = true;
+      q.stop = true;
+      return AICP_OK;
+    }
+    // a stream that drained without writing it (not expected: a kernel that returned early on an
+    // error): checked only after a long wait
+    const auto now = std::chrono::steady_clock::now();
+    if (q.wait_it != q.it) {
+      q.wait_it = q.it;
+      q.wait_t0 = now;
+      return AICP_OK;
+    }
+    if (now - q.wait_t0 < std::chrono::milliseconds(20)) return AICP_OK;
     const hipError_t r = hipStreamQuery(S->s_icp);
     if (r == hipErrorNotReady) return AICP_OK;
     HIPC(r);
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    if (*w == 0xffffffffu) {
+    if (w[q.it] == 0xffffffffu) {
       got = true;
       q.stop = true;
       return AICP_OK;
     }
   }
   got = true;
-  if (*w == 0) q.stop = true;
+  if (w[q.it] == 0) q.stop = true;
   return AICP_OK;
 }
 
