@@ -6,6 +6,7 @@ or does not export the declared entry points. There is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 
 import numpy as np
@@ -39,13 +40,13 @@ EXPORTS = [
     "aicp_hip_map_register_batch", "aicp_hip_multi_create", "aicp_hip_multi_destroy", "aicp_hip_multi_size",
     "aicp_hip_multi_context", "aicp_hip_multi_last_error", "aicp_hip_multi_align_batch",
     "aicp_hip_reference_cache_stats", "aicp_hip_default_options", "aicp_hip_set_options", "aicp_hip_get_options",
-    "aicp_hip_test_force_scan_stall", "aicp_hip_sequence_run_raw",
+    "aicp_hip_test_force_scan_stall", "aicp_hip_sequence_run_raw", "aicp_hip_build_info",
 ]
 
 
 _NEWEST = {"aicp_hip_reference_cache_stats", "aicp_hip_default_options", "aicp_hip_set_options",
            "aicp_hip_get_options", "aicp_hip_test_force_scan_stall",
-           "aicp_hip_sequence_run_raw"}  # added in r05 / r06
+           "aicp_hip_sequence_run_raw", "aicp_hip_build_info"}  # added in r05 / r06
 
 
 class IcpConfig(C.Structure):
@@ -220,6 +221,8 @@ def _load():
     L.aicp_hip_last_error.argtypes = [vp]
     L.aicp_hip_last_error.restype = C.c_char_p
     L.aicp_hip_version.restype = C.c_char_p
+    if hasattr(L, "aicp_hip_build_info"):
+        L.aicp_hip_build_info.restype = C.c_char_p
     L.aicp_hip_default_config.argtypes = [cfgp]
     L.aicp_hip_default_config.restype = None
     L.aicp_hip_parse_pm_yaml.argtypes = [C.c_char_p, cfgp]
@@ -289,6 +292,41 @@ def _load():
 
 
 lib = _load()
+
+
+def build_info() -> str:
+    """The loaded library's provenance line (aicp_hip_build_info): "src <hash> arch <gfx> extra
+    <flags>", or "" for a library older than the call."""
+    return lib.aicp_hip_build_info().decode() if hasattr(lib, "aicp_hip_build_info") else ""
+
+
+def source_hash(csrc: str = os.path.join(PKG_DIR, "csrc")) -> str:
+    """The hash the Makefile embeds: sha256 over its SRCS_HIP, SRCS_CPP and HDRS files and the
+    Makefile itself, in that order (first 16 hex digits)."""
+    mk = os.path.join(csrc, "Makefile")
+    lists = {}
+    text = open(mk).read().replace("\\\n", " ")
+    for line in text.splitlines():
+        for key in ("SRCS_HIP", "SRCS_CPP", "HDRS"):
+            if line.startswith(key + " ="):
+                lists[key] = line.split("=", 1)[1].split()
+    h = hashlib.sha256()
+    for f in lists["SRCS_HIP"] + lists["SRCS_CPP"] + lists["HDRS"] + ["Makefile"]:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def provenance() -> dict:
+    """Whether the loaded library was built from this tree's sources (bench lines carry it)."""
+    info = build_info()
+    src = info.split()[1] if info.startswith("src ") else ""
+    try:
+        tree = source_hash()
+    except OSError:
+        tree = ""
+    return {"library": os.path.abspath(LIB_PATH), "build_info": info, "tree_source_hash": tree,
+            "built_from_tree": bool(src) and src == tree}
 
 
 class AicpError(RuntimeError):

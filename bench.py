@@ -316,6 +316,8 @@ def add_traffic(rf, name):
 
 
 def base_line(args, world, metric, value, unit, ms_per_step, dtype, data, config, scaling="weak", hib=True):
+    import aicp_mapping_amd._lib as L
+
     return {
         "metric": metric,
         "value": round(value, 3),
@@ -330,6 +332,9 @@ def base_line(args, world, metric, value, unit, ms_per_step, dtype, data, config
         "dtype": dtype,
         "data": data,
         "config": config,
+        # the library this line measured and whether it was built from this tree's sources
+        # (aicp_hip_build_info against the sources' hash)
+        "build": L.provenance(),
     }
 
 

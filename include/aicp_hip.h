@@ -109,6 +109,10 @@ int aicp_hip_create(int device, aicp_hip_ctx** out);
 void aicp_hip_destroy(aicp_hip_ctx* ctx);
 const char* aicp_hip_last_error(const aicp_hip_ctx* ctx);
 const char* aicp_hip_version(void);
+/* Provenance of this binary: "src <sha256 prefix of its sources and Makefile> arch <gfx> extra
+ * <extra compile flags>" (aicp_mapping_amd/csrc/Makefile); aicp_mapping_amd._lib.source_hash()
+ * computes the same hash from a source tree. */
+const char* aicp_hip_build_info(void);
 
 /* Context options: the engine and schedule switches the tests and A/B measurements use. The
  * library reads no environment variable; a context starts with aicp_hip_default_options' values

@@ -46,6 +46,19 @@ def test_library_is_gfx950_code_object(L):
     assert b"k_icp_nn" in blob
 
 
+def test_library_built_from_this_tree(L):
+    """Provenance: the in-tree library's embedded source hash (aicp_hip_build_info, Makefile)
+    equals the hash of the sources it sits next to, and it is a plain build (no diagnostic flags),
+    so the binary that travels to the GPU box is the one these sources make."""
+    info = L.build_info()
+    assert info.startswith("src ") and " arch gfx950 " in info, info
+    if os.environ.get("AICP_HIP_LIB"):
+        pytest.skip("an A/B library override is loaded")
+    p = L.provenance()
+    assert p["built_from_tree"], p
+    assert info.rstrip().endswith("extra"), info  # no -DAICP_DIAG / diagnostic flags
+
+
 def test_version_and_defaults(L):
     assert L.lib.aicp_hip_version().decode().startswith("aicp_hip")
     c = L.default_config()
