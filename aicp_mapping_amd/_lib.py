@@ -179,12 +179,12 @@ class Options(C.Structure):
         ("tree_lvl_min", C.c_uint32),
         ("reference_cache", C.c_int32),
         ("oneshot_keep_mib", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("early_reference", C.c_int32),
         ("read_order_min", C.c_uint64),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class SequenceTiming(C.Structure):

@@ -1166,6 +1166,7 @@ void aicp_hip_default_options(aicp_hip_options* o) {
   o->tree_lvl_min = 1u << 22;
   o->reference_cache = 1;
   o->oneshot_keep_mib = 4096;
+  o->early_reference = 1;
   o->read_order_min = kReadOrderMin;
 }
 
@@ -1174,7 +1175,8 @@ int aicp_hip_set_options(aicp_hip_ctx* ctx, const aicp_hip_options* o) {
   if (o->nn_engine < 0 || o->nn_engine > 1 || o->overlap_path < 0 || o->overlap_path > 1 ||
       o->normals_knn_engine < 0 || o->normals_knn_engine > 2 || o->select_pair < -1 || o->select_pair > 1 ||
       o->select_fused_from < 0 || o->raw_tree_first < -1 || o->raw_tree_first > 1 || o->raw_first_at < 1 ||
-      o->raw_first_at > 2 || o->tree_plan < -1 || o->reference_cache < 0 || o->reference_cache > 1)
+      o->raw_first_at > 2 || o->tree_plan < -1 || o->reference_cache < 0 || o->reference_cache > 1 ||
+      o->early_reference < 0 || o->early_reference > 1)
     FAIL(AICP_ERR_INVALID, "aicp_hip_set_options: value out of range");
   // the reference cache was built under the previous options (engine, tree plan): drop it
   ctx->refc.invalidate();

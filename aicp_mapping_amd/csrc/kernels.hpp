@@ -43,7 +43,7 @@ bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
 // and *ticket is stored to done_sig (the sequence's next reference waits on it)
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st,
                         ActiveList* al, uint32_t* ctr, uint32_t* host_n = nullptr, uint64_t* done_sig = nullptr,
-                        const uint64_t* ticket = nullptr, float* outT = nullptr);
+                        const uint64_t* ticket = nullptr, float* outT = nullptr, int src_pair = -1);
 // Fused ICP iteration (AICP_ICP_FUSE=0 restores one launch per step): the last workgroup of a
 // pair to finish the histogram / compaction / reduction runs that pair's find1 / final select /
 // update, and the last pair of the group rebuilds the active list for the next iteration (and,
@@ -64,6 +64,7 @@ struct IcpIterSync {
   uint64_t* done_sig;  // nullable: see launch_active_list
   const uint64_t* ticket;
   float* outT;
+  int src_pair = -1;  // >= 0: bit 31 of host_n says whether this pair (of the group) is still active
 };
 void tree_prof_dump();  // diagnostic builds (AICP_ITER_PROF): k_tr_mid phase times to stderr
 void iter_prof_dump();  // diagnostic builds (AICP_ITER_PROF): per-kernel body / tail times to stderr
@@ -267,9 +268,10 @@ hipError_t launch_ovl_keys_intersect(hipStream_t s, const OvlKeySide& rd, const 
 // gd->ref_origin = translation of fromMatrix4fToIsometry3d(T) * prior pose of src (1 thread);
 // T (src's correction, written by another stream's kernel) is copied to Tcopy for the transform
 // that follows on the same stream
-// the next reference: its origin into gd, Tcopy = T, out = T * in (k_transform's arithmetic)
-void launch_seq_ref_points(hipStream_t s, int n, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy,
-                           const float4* in, float4* out);
+// the next reference: its origin into gd, Tcopy = T, out = T * in (k_transform's arithmetic);
+// src_st (nullable): T from the source's state and frames instead (k_finalize's product)
+void launch_seq_ref_points(hipStream_t s, int n, PairDesc* gd, const PairDesc* src, const PairState* src_st,
+                           const float* T, float* Tcopy, const float4* in, float4* out);
 // the window's descriptors, states and corrections into the sequence's arrays (np readings)
 void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState* st, const float* T, PairDesc* gd,
                        PairState* gst, float* gT);

@@ -1042,7 +1042,7 @@ __global__ void k_init_state(int n_pairs, const PairDesc* __restrict__ pd, PairS
 // work counter
 __device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, const PairState* __restrict__ st,
                                  ActiveList* al, uint32_t* ctr, uint32_t* host_n, uint64_t* done_sig,
-                                 const uint64_t* ticket, float* outT) {
+                                 const uint64_t* ticket, float* outT, int src_pair) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t wcnt[16];
   __shared__ uint32_t carry_off, carry_cnt;
@@ -1111,8 +1111,11 @@ __device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, c
     al->total = carry_off;
     al->off[carry_cnt] = carry_off;
     // mapped host memory: the sequence's early-exit poll, read by the host without an event
-    // (a system-scope store goes through to host memory; nothing else is published with it)
-    if (host_n) __hip_atomic_store(host_n, carry_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // (a system-scope store goes through to host memory; nothing else is published with it);
+    // bit 31: pair src_pair is still active (the stream starts the next reference once it is not)
+    const bool src_on = src_pair >= 0 && src_pair < n_pairs && st[src_pair].active;
+    if (host_n)
+      __hip_atomic_store(host_n, carry_cnt | (src_on ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // every pair has stopped: their corrections are final (k_finalize's arithmetic), and the
   // sequence's next reference, waiting on done_sig on another stream, may start now
@@ -1131,8 +1134,9 @@ __device__ void active_list_body(int n_pairs, const PairDesc* __restrict__ pd, c
 __global__ __launch_bounds__(256) void k_active_list(int n_pairs, const PairDesc* __restrict__ pd,
                                                       const PairState* __restrict__ st,
                                                       ActiveList* al, uint32_t* ctr, uint32_t* host_n,
-                                                      uint64_t* done_sig, const uint64_t* ticket, float* outT) {
-  active_list_body(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT);
+                                                      uint64_t* done_sig, const uint64_t* ticket, float* outT,
+                                                      int src_pair) {
+  active_list_body(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT, src_pair);
 }
 
 // The last workgroup to arrive at a per-pair (or per-group) counter runs the serial step that
@@ -1828,7 +1832,7 @@ __global__ __launch_bounds__(1024) void k_sel_find1(PairState* st, uint32_t* __r
 // a pair is done with this iteration; the group's last one builds the next active list
 __device__ void pair_done(const IcpIterSync& y) {
   if (!last_arrival(y.pairs, y.al->n)) return;
-  active_list_body(y.np, y.pd, y.st, y.al, y.ctr, y.host_n, y.done_sig, y.ticket, y.outT);
+  active_list_body(y.np, y.pd, y.st, y.al, y.ctr, y.host_n, y.done_sig, y.ticket, y.outT, y.src_pair);
 }
 
 // k_sel_hist + (last workgroup of the pair) k_sel_find1; a pair that stops here is done with
@@ -2971,10 +2975,11 @@ bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
   return true;
 }
 void launch_active_list(hipStream_t s, int n_pairs, const PairDesc* pd, const PairState* st, ActiveList* al,
-                        uint32_t* ctr, uint32_t* host_n, uint64_t* done_sig, const uint64_t* ticket, float* outT) {
+                        uint32_t* ctr, uint32_t* host_n, uint64_t* done_sig, const uint64_t* ticket, float* outT,
+                        int src_pair) {
   // 256 threads: the first iteration's list is launched while the normals' kNN fills the chip, and
   // a 1024-thread workgroup waited for 16 free wave slots on one CU (C2 trace: 33 us median)
-  k_active_list<<<1, 256, 0, s>>>(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT);
+  k_active_list<<<1, 256, 0, s>>>(n_pairs, pd, st, al, ctr, host_n, done_sig, ticket, outT, src_pair);
 }
 // The ICP matcher's NN engine: Trav2C on the treelet records; Trav<1> on the node records where
 // treelets do not fit (bucketSize > 15, references above 4 M points, 2^28 records) or

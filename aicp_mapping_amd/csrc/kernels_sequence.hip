@@ -21,11 +21,30 @@ namespace aicp {
 // Every workgroup reads T; workgroup 0 also writes its copy and the reference's sensor origin
 // (the corrected pose's translation, app.cpp:375-391), and each point is moved by apply4 exactly
 // as k_transform moves it (pcl::transformPointCloud's float order).
+// src_st (nullable): the source's state in the previous window, whose loop may still be running
+// (the source pair itself has stopped): its correction is k_finalize's product of the frames and
+// the ICP transform, computed here with the same operations instead of read from T.
 __global__ __launch_bounds__(256) void k_seq_ref_points(int n, PairDesc* gd, const PairDesc* __restrict__ src,
-                                                        const float* T, float* Tcopy, const float4* __restrict__ in,
+                                                        const PairState* __restrict__ src_st, const float* T,
+                                                        float* Tcopy, const float4* __restrict__ in,
                                                         float4* __restrict__ out) {
   __shared__ float Ts[16];
-  if (threadIdx.x < 16) Ts[threadIdx.x] = __hip_atomic_load(T + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (src_st) {
+    if (threadIdx.x == 0) {  // (system-scope loads, as for T: written by another stream's kernels)
+      auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+      float St[16], Tm[16], Ti[16], tmp[16], Tf[16];
+      for (int k = 0; k < 16; ++k) {
+        St[k] = ld(src_st->T + k);
+        Tm[k] = ld(src->Tmean + k);
+        Ti[k] = ld(src->Tinit + k);
+      }
+      mul4(Tm, St, tmp);
+      mul4(tmp, Ti, Tf);
+      for (int k = 0; k < 16; ++k) Ts[k] = Tf[k];
+    }
+  } else if (threadIdx.x < 16) {
+    Ts[threadIdx.x] = __hip_atomic_load(T + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __syncthreads();
   float Tl[16];
   for (int k = 0; k < 16; ++k) Tl[k] = Ts[k];
@@ -142,9 +161,9 @@ void launch_seq_commit(hipStream_t s, int np, const PairDesc* d, const PairState
     k_seq_commit<<<1, 256, 0, s>>>(np, (const uint32_t*)d, (const uint32_t*)st, (const uint32_t*)T, (uint32_t*)gd,
                                    (uint32_t*)gst, (uint32_t*)gT);
 }
-void launch_seq_ref_points(hipStream_t s, int n, PairDesc* gd, const PairDesc* src, const float* T, float* Tcopy,
-                           const float4* in, float4* out) {
-  k_seq_ref_points<<<(unsigned)std::max(1, (n + 255) / 256), 256, 0, s>>>(n, gd, src, T, Tcopy, in, out);
+void launch_seq_ref_points(hipStream_t s, int n, PairDesc* gd, const PairDesc* src, const PairState* src_st,
+                           const float* T, float* Tcopy, const float4* in, float4* out) {
+  k_seq_ref_points<<<(unsigned)std::max(1, (n + 255) / 256), 256, 0, s>>>(n, gd, src, src_st, T, Tcopy, in, out);
 }
 void launch_debug_prep(hipStream_t s, PairDesc* d, const float* initT, float* hist) {
   k_debug_prep<<<1, 64, 0, s>>>(d, initT, hist);

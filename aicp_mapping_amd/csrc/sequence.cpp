@@ -111,6 +111,7 @@ struct SeqSlot {
   TreeBufs tb[2];
   PinBuf pin_read, pin_par, pin_src;
   hipEvent_t ev_up = nullptr, ev_rd = nullptr, ev_ref = nullptr, ev_s3 = nullptr, ev_s2 = nullptr, ev_done = nullptr;
+  hipEvent_t ev_src = nullptr;  // recorded on stream icp once the window's last reading has stopped (early_reference)
   // early exit of the ICP loops: active counts written by the update kernels into mapped host
   // memory, one word per iteration, in two areas (debug mode's consecutive per-reading loops
   // alternate, so a loop's trailing write never lands in its successor's words)
@@ -152,7 +153,7 @@ void seq_state_free(SeqState* S) {
     for (auto& t : sl.tb) t.release_all();
     sl.g_match.reset();
     for (PinBuf* b : {&sl.pin_read, &sl.pin_par, &sl.pin_src}) release(*b);
-    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done})
+    for (hipEvent_t e : {sl.ev_up, sl.ev_rd, sl.ev_ref, sl.ev_s3, sl.ev_s2, sl.ev_done, sl.ev_src})
       if (e) (void)hipEventDestroy(e);
     if (sl.poll_host) (void)hipHostFree(sl.poll_host);
   }
@@ -330,6 +331,9 @@ struct WinRun {
   TreeCtl* ctl_w = nullptr;
   const PairDesc* src_desc = nullptr;   // the reference source's descriptor and correction
   const float* src_T = nullptr;
+  const PairState* src_state = nullptr;  // (a source in the previous window: its state, k_seq_ref_points)
+  hipEvent_t src_ev = nullptr;           // the reference waits for it instead of the previous ev_done
+  int next_src = -1;  // early_reference: the pair of this window that is the next window's source
   // S->opt.profile: ref start, matcher done, normals done, ICP start, ICP done, commit done, host at the
   // next reference's enqueue (a marker on an idle stream), its upload ready on r3, reading side
   // start and end
@@ -804,14 +808,15 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     // the source's correction must be final: from the previous window of this pass (its loop's
     // end, ev_done), or from an earlier pass (synchronised)
     const SeqSlot& ps = S->slot[(w.slot + kSlots - 1) % kSlots];
-    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, ps.ev_done, 0));
+    // (early_reference: the previous window's loop is still running, its source pair stopped)
+    if (w.index > 0) HIPC(hipStreamWaitEvent(s3, R.src_ev ? R.src_ev : ps.ev_done, 0));
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
     // debug mode, a source from an earlier pass (uploaded as given): it was registered as
     // initialT_ * its points (initialT_ as before it, kept by k_debug_prep)
     if (R.debug && w.index == 0)
       launch_transform(s3, (int)n_ref, S->initT.as<float>() + 16 * (1 + (size_t)w.src), src_pts,
                        const_cast<float4*>(src_pts));
-    launch_seq_ref_points(s3, (int)n_ref, dG, R.src_desc, R.src_T, sl.tsrc.as<float>(), src_pts,
+    launch_seq_ref_points(s3, (int)n_ref, dG, R.src_desc, R.src_state, R.src_T, sl.tsrc.as<float>(), src_pts,
                           sl.ref_raw.as<float4>());
   } else {
     if (R.tev) HIPC(hipEventRecord(R.tev[0], s3));
@@ -977,6 +982,7 @@ struct IcpLoop {
   bool stop = false;
   int wait_it = -1;  // the poll word being waited for since wait_t0 (the drained-stream check)
   std::chrono::steady_clock::time_point wait_t0;
+  bool src_done = false;  // the next window's source pair has stopped: ev_src recorded
 };
 
 // the blocks [off, off + cnt) of a block map
@@ -1051,7 +1057,7 @@ static int loop_part(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
         HIPC(hipEventCreate(&e));
         S->nn_ev.push_back(e);
       }
-    if (it == 0) launch_active_list(st, lp.np_l, lp.gd, lp.gs, al, ctr, hn_this);
+    if (it == 0) launch_active_list(st, lp.np_l, lp.gd, lp.gs, al, ctr, hn_this, nullptr, nullptr, nullptr, R.next_src);
     launch_icp_nn(st, (int)lp.reads, lp.gd, lp.gs, al, sl.read_c.as<float4>(), sl.nodes.as<uint4>(),
                   R.use_tl ? sl.tl.as<uint4>() : nullptr, nullptr, sl.bpts.as<float4>(),
                   R.use_tl ? sl.ptl.as<uint2>() : nullptr, sl.match.as<int32_t>(), sl.d2.as<float>(),
@@ -1076,6 +1082,7 @@ static int loop_part(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
   y.al = al;
   y.ctr = ctr;
   y.host_n = hn_next;
+  y.src_pair = R.next_src;
   const int ff = S->opt.select_fused_from;
   if (ff > 0 && it >= ff)  // (iteration 0 has no previous bin to guess)
     launch_icp_select_fused(st, msel, dDesc, dState, sl.d2.as<float>(), sl.sel_hist.as<uint32_t>(),
@@ -1149,7 +1156,16 @@ static int loop_poll(aicp_hip_ctx* ctx, SeqState* S, IcpLoop& q, bool& got) {
     }
   }
   got = true;
-  if (w[q.it] == 0) q.stop = true;
+  const uint32_t v = w[q.it];
+  if (v == 0) {
+    q.stop = true;
+  } else if (q.R->next_src >= 0 && !q.src_done && !(v >> 31)) {
+    // the next window's source pair has stopped: its final state was written by the update
+    // before this iteration's NN launch, the last launch on the stream so far (bit 31 of the
+    // word, active_list_body)
+    HIPC(hipEventRecord(sl.ev_src, S->s_icp));
+    q.src_done = true;
+  }
   return AICP_OK;
 }
 
@@ -1215,7 +1231,7 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     S->s_r2 = ctx->stream2;
     S->s_r3 = ctx->stream3;
     for (SeqSlot& sl : S->slot) {
-      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done})
+      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done, &sl.ev_src})
         HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
       HIPC(hipHostMalloc((void**)&sl.poll_host, 2 * kMaxPolls * 4, hipHostMallocMapped));
       HIPC(hipHostGetDevicePointer((void**)&sl.poll_dev, sl.poll_host, 0));
@@ -1338,6 +1354,9 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
         const size_t off = (size_t)w.src - pw.p0;
         runs[k].src_desc = S->slot[pw.slot].wdesc.as<PairDesc>() + off;
         runs[k].src_T = S->slot[pw.slot].woutT.as<float>() + 16 * off;
+        // its correction from its state (k_finalize's product): final before that window's loop
+        // ends once the pair has stopped (early_reference)
+        if (!debug) runs[k].src_state = S->slot[pw.slot].wstate.as<PairState>() + off;
       } else if (w.src >= 0) {  // a reading of an earlier pass: committed
         runs[k].src_desc = S->desc.as<PairDesc>() + w.src;
         runs[k].src_T = S->outT.as<float>() + 16 * (size_t)w.src;
@@ -1426,6 +1445,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       // iterations are enqueued: on the polling thread it held the poll that enqueues iteration
       // smoothLength + 1, and the device waited ~0.25 ms per window for it (r04 trace).
       std::thread up_thr;
+      std::atomic<bool> up_fin{false};
       int up_rc = AICP_OK;
       ErrSink up_err;  // the upload thread's error message (ctx->err belongs to this thread)
       auto try_upload = [&]() -> int {
@@ -1440,6 +1460,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
           int r = timed(0, [&] { return upload(&up_err, k + 1); });
           if (!r) r = timed(0, [&] { return read_side(&up_err, k + 1); });
           up_rc = r;
+          up_fin = true;
         });
         return AICP_OK;
       };
@@ -1454,6 +1475,26 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
       // one loop per window; debug mode: one per reading, in order (reading i + 1 is moved by
       // the initialT_ that reading i's correction updates)
       const int n_sub = debug ? (int)runs[k].np : 1;
+      // early_reference: the next window's reference starts once its source -- this window's last
+      // reading -- has stopped iterating, beside this window's other readings (their loop runs on)
+      runs[k].next_src = -1;
+      if (!debug && next && S->opt.early_reference && plan[k + 1].index > 0 &&
+          plan[k + 1].src == (int)(plan[k].p0 + plan[k].np - 1))
+        runs[k].next_src = (int)plan[k].np - 1;
+      bool ref_early = false;
+      // the next window's reference trees, enqueued once the source pair has stopped and the next
+      // window's upload is done (its thread joined), after this iteration's launches
+      auto try_ref_early = [&]() -> int {
+        if (ref_early || runs[k].next_src < 0 || !loops[k].src_done || !uploaded || !up_fin) return AICP_OK;
+        if (up_thr.joinable()) up_thr.join();
+        if (up_rc) {
+          ctx->err = up_err.err;
+          return up_rc;
+        }
+        ref_early = true;
+        runs[k + 1].src_ev = S->slot[plan[k].slot].ev_src;
+        return timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
+      };
       for (int sub = 0; sub < n_sub && !rc; ++sub) {
         IcpLoop& q = loops[k];
         q = IcpLoop{};
@@ -1467,6 +1508,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
             bool progress = false;
             int r = advance(q, progress);
             if (!r) r = try_upload();
+            if (!r) r = try_ref_early();
             if (r) return r;
             if (!progress) std::this_thread::yield();
           }
@@ -1480,7 +1522,7 @@ int aicp_hip_sequence_run(aicp_hip_ctx* ctx, const aicp_icp_config* cfg, const a
           ctx->err = up_err.err;
         }
       }
-      if (!rc && next) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
+      if (!rc && next && !ref_early) rc = timed(1, [&] { return win_ref_trees(ctx, S, cfg, prm, runs[k + 1]); });
       if (!rc && next) rc = timed(4, [&] { return win_ref_icp(ctx, S, cfg, prm, runs[k + 1]); });
       ++windows;
     }

@@ -149,7 +149,9 @@ typedef struct {
                                  copied or compared between calls */
   uint32_t oneshot_keep_mib;  /* device copies of a one-shot call's inputs are kept for the next
                                  call up to this size (MiB), released above it; 4096 */
-  uint32_t reserved;          /* 0 */
+  int32_t early_reference;    /* stream (non-debug): 1: the next reference starts once its source
+                                 reading's registration has stopped, while the window's other
+                                 readings still iterate; 0: once the whole window's loop ends; 1 */
   uint64_t read_order_min;    /* Morton order of a batch's readings from this many points on;
                                  200000 */
 } aicp_hip_options;

@@ -80,7 +80,8 @@ def test_context_options_defaults_and_layout(L):
     o = L.default_options().as_dict()
     assert o == dict(profile=0, nn_engine=0, overlap_path=0, normals_knn_engine=0, select_pair=-1,
                      select_fused_from=3, raw_tree_first=-1, raw_first_at=2, no_early_exit=0, tree_plan=0,
-                     tree_lvl_min=1 << 22, reference_cache=1, oneshot_keep_mib=4096, read_order_min=200000)
+                     tree_lvl_min=1 << 22, reference_cache=1, oneshot_keep_mib=4096, early_reference=1,
+                     read_order_min=200000)
     with pytest.raises(AttributeError):
         L.default_options(no_such_switch=1)
     src = "".join(open(os.path.join(ROOT, "aicp_mapping_amd", "csrc", f)).read()

@@ -291,3 +291,39 @@ def test_sequence_raw_empty_after_prefilter_ends_stream(ctx, oracle, L, mode):
     ref = oracle.sequence(st.first, st.first_origin, reads, st.origins, resolution=RES, working_mode=mode,
                           prefilter_with=True, stop=3)
     _compare(out[:3], ref, T[:3])
+
+
+def test_sequence_raw_robot_equals_prefilter_then_stream(ctx, L):
+    """Robot mode from raw clouds is the device pre-filter of every cloud followed by the stream:
+    the same corrections bit for bit as pre-filtering with aicp_hip_prefilter first; invalid
+    pre-filter parameters are refused before anything runs."""
+    st = sy.make_stream(n_readings=6, n_points=20000, seed=5, half=12.0)
+    prm = L.default_sequence_params(flags=L.AICP_RUN_OVERLAP)
+    T0, out0, d0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm,
+                                         prefilter=True)
+    kept = [ctx.prefilter(r) for r in st.readings]
+    T1, out1, d1, rc1 = ctx.sequence_run(ctx.prefilter(st.first), st.first_origin, kept, st.origins, params=prm)
+    assert (rc0, d0) == (rc1, d1) == (0, 6)
+    assert np.array_equal(T0, T1)
+    assert [o["icp"]["overlap_keys"] for o in out0] == [o["icp"]["overlap_keys"] for o in out1]
+    with pytest.raises(L.AicpError):
+        ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm,
+                         prefilter=L.default_prefilter(normal_k=25))
+
+
+@pytest.mark.parametrize("jumps", [None, {3: (0, -0.8, 0)}, {4: (0, -0.8, 0)}])
+def test_sequence_early_reference_identical(ctx, L, jumps):
+    """early_reference (the next window's reference built once its source reading has stopped,
+    beside the window's other readings) changes only the schedule: corrections, decisions, key
+    counts and iterations equal the whole-window order's bit for bit, drops and re-plans included
+    (a dropped source: reading 4 of the first window)."""
+    st = sy.make_stream(n_readings=12, n_points=8000, seed=11, half=18.0, jumps=jumps)
+    prm = L.default_sequence_params(max_correction_magnitude=0.4)
+    T0, out0, d0, rc0 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    with ctx.options(early_reference=0):
+        T1, out1, d1, rc1 = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm)
+    assert (rc0, d0) == (rc1, d1) == (0, 12)
+    assert np.array_equal(T0, T1)
+    assert out0 == out1
+    if jumps:
+        assert not all(o["accepted"] for o in out0)
