@@ -327,3 +327,19 @@ def test_sequence_early_reference_identical(ctx, L, jumps):
     assert out0 == out1
     if jumps:
         assert not all(o["accepted"] for o in out0)
+
+
+def test_sequence_raw_debug_c2_full_size(ctx, oracle, L):
+    """App's debug order at the C2 size: six raw 120k-point readings moved by initialT_ and
+    pre-filtered on the device (~100k points kept each), the fifth corrected into the reference of
+    the sixth; the oracle's App-order replay gives the same decisions, key counts, iterations and
+    corrections."""
+    st = sy.make_stream(n_readings=6, n_points=120000, seed=1, half=30.0)
+    prm = L.default_sequence_params(flags=L.AICP_RUN_OVERLAP | L.AICP_SEQ_DEBUG)
+    T, out, done, rc = ctx.sequence_run(st.first, st.first_origin, st.readings, st.origins, params=prm,
+                                        prefilter=True)
+    assert rc == 0 and done == 6
+    ref = oracle.sequence(st.first, st.first_origin, st.readings, st.origins, resolution=RES, working_mode="debug",
+                          prefilter_with=True)
+    _compare(out, ref, T)
+    assert [o["reference"] for o in out] == [-1] * 5 + [4]
