@@ -992,11 +992,12 @@ __device__ void subtree_build(const SubSeg& g, uint32_t total, float4* pts, PosT
 // waves of a block take the nodes of one level each (a node is still split by one wave with the
 // same Hoare passes, so the swaps and the resulting order are the wave builder's), and a block
 // barrier separates the levels. Far fewer dependent steps per segment than depth-first by one wave.
-// waves per block, one node each per level. 16 waves took k_tr_subtree_blk from 73 to 58 us on a
-// C2 reference but cost C5 (1024 pairs, tens of thousands of segments) 13 % of its clouds/s, and
-// the C2 stream's period did not move; 8 stays the default.
+// waves per block, one node each per level. r04 kept 8 because 16 cost C5 13 %; builds of C5's
+// size now finish with k_tr_subtree_lvl (TreeWork::lvl_min), so only the small builds (C2's
+// references) run this kernel, and 16 waves take it from 72 to 59 us there (r06, same box, C3 /
+// C4 / C5 unchanged; profiles/r06_log.md)
 #ifndef AICP_SUBWAVES
-#define AICP_SUBWAVES 8
+#define AICP_SUBWAVES 16
 #endif
 constexpr int kSubWaves = AICP_SUBWAVES;
 constexpr int kSubLevelCap = 256;  // nodes above bucket per level (<= kSubMax / (bucket + 1))
@@ -1472,12 +1473,17 @@ __global__ __launch_bounds__(kLvlThreads, 8) void k_tr_subtree_lvl(uint32_t tota
 }
 
 // ---- mid-size builder: one workgroup splits a segment of <= kMidMax points in LDS ----------------
-// The global levels stop at kMidMax points (instead of kSubMax): a workgroup of 16 waves loads the
+// The global levels stop at kMidMax points (instead of kSubMax): a workgroup of kMidWaves waves loads the
 // segment into LDS and splits its nodes above kSubMax points one after another with block-wide
 // reductions and Hoare passes (the same node rule and the same swaps as the sequential loop: the
 // k-th misplaced element from the left swaps with the k-th from the right), depth first; the
 // pieces of <= kSubMax points go to the subtree builders, leaves are emitted at once.
-constexpr int kMidThreads = 1024;
+// threads per workgroup: 512 (r06; 1024 before): a node's phases are barrier-bound, and with 8
+// waves instead of 16 a C2 segment's k_tr_mid took 63 against 76 us (256 threads: 81 us)
+#ifndef AICP_MIDTHREADS
+#define AICP_MIDTHREADS 512
+#endif
+constexpr int kMidThreads = AICP_MIDTHREADS;
 constexpr int kMidWaves = kMidThreads / 64;
 constexpr int kMidStack = 32;
 constexpr int kMidOut = 64;  // pieces of <= kSubMax points per mid segment (2 per split node > kSubMax)
