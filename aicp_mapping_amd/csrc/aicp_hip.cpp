@@ -885,7 +885,6 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
     HIPC(ensure(ctx->nrm_raw, B->total_ref * 16));
     HIPC(ensure(ctx->nbids, B->total_ref * 4 * (size_t)cfg->knn_normals));
     uint32_t* nCtr = dCtr + kKnnCtrOff;
-    HIPC(hipMemsetAsync(nCtr, 0, kPersistCtrWords * 4, s2));
     if (!launch_normals(s2, (int)R, (uint32_t)B->total_ref, ctx->rdesc_raw.as<PairDesc>(), dRstate,
                         ctx->nodes_raw.as<uint4>(), nullptr, ctx->bpts_raw.as<float4>(), ctx->nrm_raw.as<float4>(),
                         cfg->knn_normals, ctx->nbids.as<int32_t>(), nCtr, ctx->opt.normals_knn_engine))

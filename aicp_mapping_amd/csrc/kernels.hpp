@@ -27,7 +27,8 @@ void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const floa
                        const int32_t* perm, float4* bpts);
 void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st);
 // SurfaceNormal of the reference points (bucket order); ids: scratch of total_ref * knn;
-// ctr: zeroed work counters (kPersistCtrWords). engine: aicp_hip_options::normals_knn_engine.
+// ctr: kPersistCtrWords work counters (zeroed on s when the persistent engine runs). engine:
+// aicp_hip_options::normals_knn_engine.
 // Returns false if knn is unsupported.
 bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
                     const uint4* nodes, const int32_t* parent, const float4* bpts, float4* bnrm, int knn,

@@ -2965,6 +2965,9 @@ bool launch_knn_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
     }
     return true;
   }
+  // the persistent engine's work counters, zeroed here: the octet engine needs none, and a
+  // caller's memset ahead of it put a ~5 us fill kernel on the C2 reference chain for nothing
+  if (hipMemsetAsync(ctr, 0, kPersistCtrWords * 4, s) != hipSuccess) return false;
   const int g = persistent_grid((int)total_ref);
   switch (knn) {
     case 10: k_knn_ids<10><<<g, 256, 0, s>>>(n_pairs, total_ref, pd, nodes, nullptr, bpts, ids, ctr, touched); break;

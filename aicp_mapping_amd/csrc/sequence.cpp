@@ -844,15 +844,15 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   hipStream_t s2 = S->s_r2;
   HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
   uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kKnnCtrOff;
-  auto raw_build = [&]() -> int {
+  auto raw_begin = [&]() -> int {
     launch_init_state(s2, 1, dRraw, dRst);
-    int r = device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
-                               sl.bpts_raw, sl.nodes_raw);
-    if (r) return r;
-    r = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw, plan0,
+    return device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
+                              sl.bpts_raw, sl.nodes_raw);
+  };
+  auto raw_build = [&]() -> int {
+    int r = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw, plan0,
                          ctl_w, !capturable);
     if (r) return r;
-    HIPC(hipMemsetAsync(nCtr, 0, kPersistCtrWords * 4, s2));
     if (!launch_normals(s2, 1, n_ref, dRraw, dRst, sl.nodes_raw.as<uint4>(), nullptr, sl.bpts_raw.as<float4>(),
                         sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr,
                         S->opt.normals_knn_engine))
@@ -861,7 +861,7 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     return AICP_OK;
   };
   // the raw tree + SurfaceNormal as direct launches (replayed from a graph they finished 0.08 ms
-  // later on the device, r03), enqueued after the matcher tree's graph
+  // later on the device, r03)
   auto raw_enqueue = [&]() -> int { return raw_build(); };
   // ---- r3: centroid + matcher tree + treelets
   auto match_build = [&]() -> int {
@@ -897,8 +897,14 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
       HIPC(hipMemcpyAsync(ctl_w + 1, sl.tb[1].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s3));
     return AICP_OK;
   };
-  // the matcher tree, which the window's loop starts on, goes first
-  rc = match_enqueue();
+  // The raw tree's first kernels (state, zero, frames, centre, roots) go first, then the matcher
+  // tree's graph, then the raw tree's levels and SurfaceNormal: the raw tree -> kNN -> normals
+  // chain gates the loop's first reduce, the matcher tree (~0.3 ms shorter) only its first NN.
+  // Enqueued after the graph, the raw chain's first kernels waited on the host (C2 trace, r06).
+  // (The whole raw chain ahead of the graph delayed the matcher tree past the normals: C2 2529-2666
+  // against 2784-2816 clouds/s, r06.)
+  rc = raw_begin();
+  if (!rc) rc = match_enqueue();
   if (!rc) rc = raw_enqueue();
   if (rc) return rc;
 
