@@ -1237,8 +1237,12 @@ static int seq_init(aicp_hip_ctx* ctx, size_t n) {
     S->s_r2 = ctx->stream2;
     S->s_r3 = ctx->stream3;
     for (SeqSlot& sl : S->slot) {
-      for (hipEvent_t* e : {&sl.ev_up, &sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done, &sl.ev_src})
-        HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+      // the events that only order streams of this device release at device scope (no system-scope
+      // fence when they are recorded); ev_up, which the host waits on before it reuses the pinned
+      // staging, keeps the default
+      HIPC(hipEventCreateWithFlags(&sl.ev_up, hipEventDisableTiming));
+      for (hipEvent_t* e : {&sl.ev_rd, &sl.ev_ref, &sl.ev_s3, &sl.ev_s2, &sl.ev_done, &sl.ev_src})
+        HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice));
       HIPC(hipHostMalloc((void**)&sl.poll_host, 2 * kMaxPolls * 4, hipHostMallocMapped));
       HIPC(hipHostGetDevicePointer((void**)&sl.poll_dev, sl.poll_host, 0));
     }
