@@ -251,7 +251,7 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
   // readings are packed and copied (references written on the device later record it in run_batch)
   B->refs_event = pack_refs;
   if (pack_refs) {
-    if (!ctx->ev[14]) HIPC(hipEventCreate(&ctx->ev[14]));
+    if (!ctx->ev[14]) HIPC(hipEventCreateWithFlags(&ctx->ev[14], hipEventReleaseToDevice));
     HIPC(hipEventRecord(ctx->ev[14], ctx->stream));
   }
   float* sw = pack_refs ? st + 4ull * ro : st;
@@ -687,13 +687,17 @@ int run_batch(aicp_hip_ctx* ctx, aicp_hip_batch* B, const aicp_icp_config* cfg, 
   const bool hit_trees = rcache.use && rcache.hit_trees && doIcp;
   const bool hit_ovl = rcache.use && rcache.hit_ovl && doOvl;
   hipStream_t s = ctx->stream;
-  for (auto& e : ctx->ev)
-    if (!e) HIPC(hipEventCreate(&e));
+  // the events that order this context's streams release at device scope; ev[1], which the host
+  // waits on before it reads the key boxes copied to pinned memory, keeps the system-scope fence
+  for (size_t k = 0; k < sizeof(ctx->ev) / sizeof(ctx->ev[0]); ++k)
+    if (!ctx->ev[k]) HIPC(hipEventCreateWithFlags(&ctx->ev[k], k == 1 ? hipEventDefault : hipEventReleaseToDevice));
   const bool timeNN = (flags & AICP_RUN_TIME_NN) && doIcp;
   if (timeNN)
     while ((int)ctx->nn_ev.size() < 2 * cfg->max_iter) {
       hipEvent_t e;
-      HIPC(hipEventCreate(&e));
+      // timing only (the NN launch's own start / end): no system-scope fence, whose cache
+      // write-back and invalidation the elapsed time would otherwise include
+      HIPC(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
       ctx->nn_ev.push_back(e);
     }
   std::vector<PairDesc> desc = B->desc;

@@ -1060,7 +1060,9 @@ static int loop_part(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* cfg,
     if (timeNN)
       while ((int)S->nn_ev.size() < 2 * (nn_launches + 1)) {
         hipEvent_t e;
-        HIPC(hipEventCreate(&e));
+        // timing only (the NN launch's own start / end): no system-scope fence, whose cache
+        // write-back and invalidation the elapsed time would otherwise include
+        HIPC(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         S->nn_ev.push_back(e);
       }
     if (it == 0) launch_active_list(st, lp.np_l, lp.gd, lp.gs, al, ctr, hn_this, nullptr, nullptr, nullptr, R.next_src);
