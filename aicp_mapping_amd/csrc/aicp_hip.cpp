@@ -292,7 +292,8 @@ int upload_pairs(aicp_hip_ctx* ctx, const aicp_pair* pairs, size_t n, aicp_hip_b
 // dDesc with ref_off / n_ref / Tin. Writes bpts_out (bucket order, w = local id), nodes_out
 // and the desc fields mean, Tmean, Tinit, node_off, n_nodes, tree_depth.
 int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
-                       const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out, bool launch) {
+                       const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out, bool launch,
+                       int part) {
   const size_t n = (size_t)total;
   const size_t max_seg = n / 2 + P + 1;
   TCHK(ensure(bpts_out, n * 16));
@@ -351,7 +352,7 @@ int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, u
   w.max_seg = max_seg;
   T.tw = w;
   if (!launch) return AICP_OK;  // work space only (before a stream capture)
-  TCHK(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts_out.as<float4>(), bucket));
+  TCHK(launch_tree_prepare(s, (int)P, (uint32_t)n, dDesc, raw, center, w, bpts_out.as<float4>(), bucket, part));
   return AICP_OK;
 }
 

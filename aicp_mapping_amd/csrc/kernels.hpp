@@ -170,8 +170,10 @@ size_t lb_stride_words(uint32_t total);
 // w.ctl->error (bit 4)
 hipError_t launch_treelets(hipStream_t s, int n_refs, uint32_t cap, const PairDesc* rd, const uint4* nodes,
                            int bucket, uint32_t* rank, uint4* tl, uint2* link, const TreeWork& w);
+// part 1: only what does not read the points (zeroed work space; frames when center = 0); part 2:
+// the rest; 0: all
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
-                               int center, const TreeWork& w, float4* bpts, int bucket);
+                               int center, const TreeWork& w, float4* bpts, int bucket, int part = 0);
 // one level: nodes at depth `level` are split (their children get depth level + 1)
 // last: the final planned level -- children above kSubMax points also go to the subtree
 // kernel (its global-memory path) instead of a next level

@@ -2038,7 +2038,11 @@ hipError_t set_lb_force_stall(int on) {
 size_t lb_bytes(uint32_t total) { return (size_t)(2 * kFarStack + 3) * lb_stride_words(total) * 8; }
 
 hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairDesc* pd, const float4* raw,
-                               int center, const TreeWork& w, float4* bpts, int bucket) {
+                               int center, const TreeWork& w, float4* bpts, int bucket, int part) {
+  // part 1: what does not read the points (the zeroed work space; without centring also the
+  // frames), so a stream can run it before it waits for them; part 2: the rest; 0: all
+  const bool first = part != 2, rest = part != 1;
+  const bool frames_first = !center;
   ZeroJob z{};
   const size_t bytes[6] = {(size_t)n_pairs * 6 * sizeof(uint64_t), sizeof(TreeCtl), ((size_t)total + 2) * 4,
                            2 * (size_t)total, (size_t)n_pairs * 4, lb_bytes(total)};
@@ -2049,11 +2053,15 @@ hipError_t launch_tree_prepare(hipStream_t s, int n_pairs, uint32_t total, PairD
     z.n16[r] = (bytes[r] + 15) / 16;
     most = std::max<uint64_t>(most, z.n16[r]);
   }
-  k_tr_zero<<<(unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (most + 255) / 256)), 256, 0, s>>>(
-      z, n_pairs, w.seg[0]);
-  uint64_t* part = w.sums + (size_t)n_pairs * 6;  // tile partials (TreeWork::sums)
-  if (center) k_tr_sum<<<tiles_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.sums, part);
-  k_tr_frames<<<n_pairs, 64, 0, s>>>(n_pairs, total, pd, w.sums, part, center);
+  uint64_t* tpart = w.sums + (size_t)n_pairs * 6;  // tile partials (TreeWork::sums)
+  if (first) {
+    k_tr_zero<<<(unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (most + 255) / 256)), 256, 0, s>>>(
+        z, n_pairs, w.seg[0]);
+    if (frames_first) k_tr_frames<<<n_pairs, 64, 0, s>>>(n_pairs, total, pd, w.sums, tpart, center);
+  }
+  if (!rest) return hipGetLastError();
+  if (center) k_tr_sum<<<tiles_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.sums, tpart);
+  if (!frames_first) k_tr_frames<<<n_pairs, 64, 0, s>>>(n_pairs, total, pd, w.sums, tpart, center);
   k_tr_center<<<tiles_of(total), 256, 0, s>>>(n_pairs, total, pd, raw, w.W[0], w.segof[0], w.seg[0], bpts, bucket,
                                              w.mid_max);
   k_tr_roots<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, total, pd, w.seg[0], w.subs, w.mids, w.ctl, w.ev, w.valid, w.ecnt,

@@ -190,10 +190,11 @@ double ev_ms(hipEvent_t a, hipEvent_t b);
 void tree_opts(TreeBufs& T, const aicp_hip_options& o);
 
 // Centroid (center = 1) + libnabo-order kd-trees of P clouds on the device (kernels_tree.hip).
-// launch = false: allocate the work space only (nothing enqueued; before a stream capture)
+// launch = false: allocate the work space only (nothing enqueued; before a stream capture);
+// part: launch_tree_prepare's (1: the kernels that do not read the points, 2: the rest, 0: all)
 int device_trees_begin(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,
                        const float4* raw, int center, int bucket, DevBuf& bpts_out, DevBuf& nodes_out,
-                       bool launch = true);
+                       bool launch = true, int part = 0);
 // plan > 0: `plan` global levels with no host read-back; the control block is copied to
 // ctl_dst (default T.pin_ctl) at the end of the build unless copy_ctl is false
 int device_trees_end(TreeBufs& T, std::string& err, hipStream_t s, size_t P, uint64_t total, PairDesc* dDesc,

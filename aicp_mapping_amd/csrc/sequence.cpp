@@ -842,12 +842,19 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   const bool capturable = plan0 > 0 && plan1 > 0;  // (a host-polled build cannot be captured)
   // ---- r2: raw-coordinate tree + SurfaceNormal (reference as given)
   hipStream_t s2 = S->s_r2;
-  HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
   uint32_t* nCtr = sl.ctrs.as<uint32_t>() + kKnnCtrOff;
+  // the raw build's kernels that do not read the reference points (state, zeroed work space,
+  // frames: no centring here) run while s2 waits for them; they need only the window's
+  // descriptors (ev_up)
   auto raw_begin = [&]() -> int {
+    HIPC(hipStreamWaitEvent(s2, sl.ev_up, 0));
     launch_init_state(s2, 1, dRraw, dRst);
+    int r = device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
+                               sl.bpts_raw, sl.nodes_raw, true, 1);
+    if (r) return r;
+    HIPC(hipStreamWaitEvent(s2, sl.ev_ref, 0));
     return device_trees_begin(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, sl.ref_raw.as<float4>(), 0, kNormalsBucket,
-                              sl.bpts_raw, sl.nodes_raw);
+                              sl.bpts_raw, sl.nodes_raw, true, 2);
   };
   auto raw_build = [&]() -> int {
     int r = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw, plan0,
