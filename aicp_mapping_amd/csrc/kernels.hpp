@@ -26,10 +26,6 @@ hipError_t launch_read_order(hipStream_t s, BlockMap m, int n_pairs, const PairD
 void launch_gather_ref(hipStream_t s, BlockMap m, const PairDesc* pd, const float4* ref_raw,
                        const int32_t* perm, float4* bpts);
 void launch_init_state(hipStream_t s, int n_pairs, const PairDesc* pd, PairState* st);
-// SurfaceNormal from launch_knn_ids' ids (bpts: the raw tree's points, w = input id); inv
-// (nullable, launch_inv_perm) writes each normal at its point's matcher-tree position instead
-bool launch_normals_from_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
-                             const float4* bpts, int knn, const int32_t* ids, float4* bnrm, const uint32_t* inv);
 // SurfaceNormal of the reference points (bucket order); ids: scratch of total_ref * knn;
 // ctr: kPersistCtrWords work counters (zeroed on s when the persistent engine runs). engine:
 // aicp_hip_options::normals_knn_engine.
@@ -195,9 +191,6 @@ hipError_t launch_tree_finish(hipStream_t s, int n_pairs, uint32_t total, PairDe
 // pairs -> their shared reference's centroid / tree fields (+ T_refMean_dataIn), and its
 // SurfaceNormal degenerate count
 void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd);
-// inv[ref_off + input id] = the matcher tree's bucket position of that point (bpts: the matcher
-// tree's points, w = input id)
-void launch_inv_perm(hipStream_t s, int n_refs, uint32_t total, const PairDesc* rd, const float4* bpts, uint32_t* inv);
 // normals of the raw-coordinate tree's bucket order -> bnrm in the matcher tree's order
 void launch_normals_to_matcher(hipStream_t s, int n_refs, uint32_t total, const PairDesc* rd, const float4* bpts,
                                const float4* bpts_raw, const float4* nrm_raw, uint32_t* inv, float4* bnrm);

@@ -1502,8 +1502,7 @@ __global__ __launch_bounds__(256) void k_normals_from_ids(int n_pairs, uint32_t 
                                                           const PairDesc* __restrict__ pd, PairState* st,
                                                           const float4* __restrict__ bpts,
                                                           const int32_t* __restrict__ ids,
-                                                          float4* __restrict__ bnrm,
-                                                          const uint32_t* __restrict__ inv) {
+                                                          float4* __restrict__ bnrm) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= total) return;
   const int pair = pair_of_ref(pd, n_pairs, s);
@@ -1542,10 +1541,7 @@ __global__ __launch_bounds__(256) void k_normals_from_ids(int n_pairs, uint32_t 
                        c12 / kk, c02 / kk, c12 / kk, c22 / kk};
   float nrm[3];
   const bool dg = normal_from_cov(C, nrm);
-  // inv (nullable): the matcher tree's position of every input id (k_inv_perm), so the normal
-  // lands in the matcher's bucket order at once (k_scatter_normals' step)
-  const uint32_t o = inv ? inv[pd[pair].ref_off + (uint32_t)__float_as_int(bpts[s].w)] : s;
-  bnrm[o] = make_float4(nrm[0], nrm[1], nrm[2], 0.f);
+  bnrm[s] = make_float4(nrm[0], nrm[1], nrm[2], 0.f);
   if (dg) atomicAdd(&st[pair].degenerate, 1);
 }
 
@@ -2935,16 +2931,11 @@ bool launch_normals(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDe
                     int32_t* ids, uint32_t* ctr, int engine) {
   if (!total_ref) return true;
   if (!launch_knn_ids(s, n_pairs, total_ref, pd, nodes, bpts, knn, ids, ctr, nullptr, engine)) return false;
-  return launch_normals_from_ids(s, n_pairs, total_ref, pd, st, bpts, knn, ids, bnrm, nullptr);
-}
-bool launch_normals_from_ids(hipStream_t s, int n_pairs, uint32_t total_ref, const PairDesc* pd, PairState* st,
-                             const float4* bpts, int knn, const int32_t* ids, float4* bnrm, const uint32_t* inv) {
-  if (!total_ref) return true;
   const int gu = (int)((total_ref + 255) / 256);
   switch (knn) {
-    case 10: k_normals_from_ids<10><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm, inv); break;
-    case 20: k_normals_from_ids<20><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm, inv); break;
-    case 30: k_normals_from_ids<30><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm, inv); break;
+    case 10: k_normals_from_ids<10><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm); break;
+    case 20: k_normals_from_ids<20><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm); break;
+    case 30: k_normals_from_ids<30><<<gu, 256, 0, s>>>(n_pairs, total_ref, pd, st, bpts, ids, bnrm); break;
     default: return false;
   }
   return true;

@@ -2008,9 +2008,6 @@ hipError_t launch_treelets(hipStream_t s, int n_refs, uint32_t cap, const PairDe
 void launch_pairs_from_refs(hipStream_t s, int n_pairs, PairDesc* pd, const PairDesc* rd) {
   k_pairs_from_refs<<<(n_pairs + 63) / 64, 64, 0, s>>>(n_pairs, pd, rd);
 }
-void launch_inv_perm(hipStream_t s, int n_refs, uint32_t total, const PairDesc* rd, const float4* bpts, uint32_t* inv) {
-  if (total) k_inv_perm<<<grid_of(total), 256, 0, s>>>(n_refs, total, rd, bpts, inv);
-}
 void launch_normals_to_matcher(hipStream_t s, int n_refs, uint32_t total, const PairDesc* rd, const float4* bpts,
                                const float4* bpts_raw, const float4* nrm_raw, uint32_t* inv, float4* bnrm) {
   if (!total) return;

@@ -104,7 +104,7 @@ struct SeqSlot {
   DevBuf read_raw, read_s, read_c, match, d2, touch, cand, slab, ord_k0, ord_k1, ord_v0, ord_v1, ord_tmp, maps, bitmap,
       ovl, caps, sel_hist, sel_cnt, ctrs, active;
   // reference side
-  DevBuf ref_src, ref_raw, bpts, bnrm, nodes, tl, ptl, tl_rank, bpts_raw, nodes_raw, nbids,
+  DevBuf ref_src, ref_raw, bpts, bnrm, nodes, tl, ptl, tl_rank, bpts_raw, nodes_raw, nrm_raw, nbids,
       inv, rd, tsrc,  // rd: rdesc, rdesc_raw, gdesc (PairDesc) + rstate, gstate (PairState); tsrc: source T
       wdesc, wstate, woutT, isync,  // the window's readings (committed to the sequence's arrays at its end)
       sp_par, sp_cnt, sp_off, sp_keys_r, sp_keys_g, sp_tmp_r, sp_tmp_g, sp_pc;  // sorted-key overlap (sparse windows)
@@ -146,7 +146,7 @@ void seq_state_free(SeqState* S) {
                       &sl.ord_k0, &sl.ord_k1, &sl.ord_v0, &sl.ord_v1, &sl.ord_tmp, &sl.maps, &sl.bitmap, &sl.ovl,
                       &sl.caps, &sl.sel_hist, &sl.sel_cnt, &sl.ctrs, &sl.active, &sl.ref_src, &sl.ref_raw, &sl.bpts,
                       &sl.bnrm, &sl.nodes, &sl.tl, &sl.ptl, &sl.tl_rank, &sl.bpts_raw,
-                      &sl.nodes_raw, &sl.nbids, &sl.inv, &sl.rd, &sl.tsrc, &sl.wdesc, &sl.wstate,
+                      &sl.nodes_raw, &sl.nrm_raw, &sl.nbids, &sl.inv, &sl.rd, &sl.tsrc, &sl.wdesc, &sl.wstate,
                       &sl.woutT, &sl.isync, &sl.sp_par, &sl.sp_cnt, &sl.sp_off, &sl.sp_keys_r,
                       &sl.sp_keys_g, &sl.sp_tmp_r, &sl.sp_tmp_g, &sl.sp_pc})
       release(*b);
@@ -426,6 +426,7 @@ static int win_upload(C* ctx, SeqState* S, const aicp_icp_config* cfg, const aic
   HIPC(ensure(sl.ref_raw, (size_t)n_ref * 16));
   HIPC(ensure(sl.bpts, (size_t)n_ref * 16));
   HIPC(ensure(sl.bnrm, (size_t)n_ref * 16));
+  HIPC(ensure(sl.nrm_raw, (size_t)n_ref * 16));
   HIPC(ensure(sl.nbids, (size_t)n_ref * 4 * cfg->knn_normals));
   HIPC(ensure(sl.inv, (size_t)n_ref * 4));
   HIPC(ensure(sl.rd, 3 * sizeof(PairDesc) + 2 * sizeof(PairState)));
@@ -859,14 +860,9 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
     int r = device_trees_end(sl.tb[0], ctx->err, s2, 1, n_ref, dRraw, kNormalsBucket, sl.bpts_raw, sl.nodes_raw, plan0,
                          ctl_w, !capturable);
     if (r) return r;
-    if (!launch_knn_ids(s2, 1, n_ref, dRraw, sl.nodes_raw.as<uint4>(), sl.bpts_raw.as<float4>(), cfg->knn_normals,
-                        sl.nbids.as<int32_t>(), nCtr, nullptr, S->opt.normals_knn_engine))
-      FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
-    // the normals go straight into the matcher tree's order through its inverse permutation
-    // (k_inv_perm on r3 behind the matcher tree, ev_s3): no scatter kernel on this chain
-    HIPC(hipStreamWaitEvent(s2, sl.ev_s3, 0));
-    if (!launch_normals_from_ids(s2, 1, n_ref, dRraw, dRst, sl.bpts_raw.as<float4>(), cfg->knn_normals,
-                                 sl.nbids.as<int32_t>(), sl.bnrm.as<float4>(), sl.inv.as<uint32_t>()))
+    if (!launch_normals(s2, 1, n_ref, dRraw, dRst, sl.nodes_raw.as<uint4>(), nullptr, sl.bpts_raw.as<float4>(),
+                        sl.nrm_raw.as<float4>(), cfg->knn_normals, sl.nbids.as<int32_t>(), nCtr,
+                        S->opt.normals_knn_engine))
       FAIL(AICP_ERR_UNSUPPORTED, "normals knn");
     HIPC(hipGetLastError());
     return AICP_OK;
@@ -900,7 +896,6 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
       r = match_build();
     }
     if (r) return r;
-    launch_inv_perm(s3, 1, n_ref, dRdesc, sl.bpts.as<float4>(), sl.inv.as<uint32_t>());
     HIPC(hipEventRecord(sl.ev_s3, s3));
     if (R.tev) HIPC(hipEventRecord(R.tev[1], s3));
     // the build's control block for the host's check after the run, behind the event the loop
@@ -920,6 +915,10 @@ static int win_ref_trees(aicp_hip_ctx* ctx, SeqState* S, const aicp_icp_config* 
   if (!rc) rc = raw_enqueue();
   if (rc) return rc;
 
+  HIPC(hipStreamWaitEvent(s2, sl.ev_s3, 0));
+  launch_normals_to_matcher(s2, 1, n_ref, dRdesc, sl.bpts.as<float4>(), sl.bpts_raw.as<float4>(),
+                            sl.nrm_raw.as<float4>(), sl.inv.as<uint32_t>(), sl.bnrm.as<float4>());
+  HIPC(hipGetLastError());
   HIPC(hipEventRecord(sl.ev_s2, s2));
   if (R.tev) HIPC(hipEventRecord(R.tev[2], s2));
   if (capturable) HIPC(hipMemcpyAsync(ctl_w, sl.tb[0].tw.ctl, sizeof(TreeCtl), hipMemcpyDeviceToHost, s2));
